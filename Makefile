@@ -1,0 +1,51 @@
+# Build of the MI355X (gfx950) SIFT hot path.
+#   libsift_hip.so   -- HIP kernels + C ABI (include/sift_hip.h)
+#   libsift_cuda.so  -- C++ drop-in surface sift_cuda::Detector / matchBruteForce
+#                       (include/sift_cuda/*.hh), g++ only, links libsift_hip.so
+#   tools            -- C++ callers mirroring the reference's tool/ examples
+# The CPU oracle (test infrastructure) builds separately: make -C oracle.
+HIPCC    ?= /opt/rocm/bin/hipcc
+CXX      ?= g++
+ARCH     ?= gfx950
+PKG      := another-cuda-sift_amd
+SRC      := $(PKG)/csrc
+OUT      := $(PKG)/lib
+JOBS     ?= 8
+
+# -ffp-contract=off + correctly rounded f32 div/sqrt: the float operation order
+# written in the kernels is the one executed (bit-exact parity with the oracle).
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
+            -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -I$(SRC) -Wall -Wno-unused-result
+CXXFLAGS := -O2 -std=c++17 -fPIC -Iinclude -Wall -Wextra
+
+HIP_SRCS := $(SRC)/detector.hip $(SRC)/pyramid.hip $(SRC)/keypoints.hip $(SRC)/match.hip
+HIP_OBJS := $(patsubst $(SRC)/%.hip,$(OUT)/obj/%.o,$(HIP_SRCS)) $(OUT)/obj/synth_frame.o
+
+all: $(OUT)/libsift_hip.so $(OUT)/libsift_cuda.so tools
+
+$(OUT)/obj/%.o: $(SRC)/%.hip $(SRC)/sift_kernels.h $(SRC)/sift_math.h $(SRC)/sift_match.h include/sift_hip.h
+	@mkdir -p $(OUT)/obj
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OUT)/obj/synth_frame.o: $(SRC)/synth_frame.cpp include/sift_hip.h
+	@mkdir -p $(OUT)/obj
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(OUT)/libsift_hip.so: $(HIP_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HIP_OBJS) -Wl,-soname,libsift_hip.so
+
+$(OUT)/libsift_cuda.so: $(SRC)/detector_cxx.cpp $(wildcard include/sift_cuda/*.hh) $(OUT)/libsift_hip.so
+	$(CXX) $(CXXFLAGS) -shared -o $@ $(SRC)/detector_cxx.cpp -L$(OUT) -lsift_hip -Wl,-rpath,'$$ORIGIN'
+
+tools: $(OUT)/detection_example $(OUT)/extract_and_match_example
+
+$(OUT)/%: tools/%.cpp $(OUT)/libsift_cuda.so
+	$(CXX) $(CXXFLAGS) -o $@ $< -L$(OUT) -lsift_cuda -lsift_hip -Wl,-rpath,'$$ORIGIN'
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf $(OUT)
+
+.PHONY: all tools oracle clean

@@ -1,0 +1,770 @@
+// C ABI of libsift_hip.so: Detector state, buffer layout in HBM, the hipGraph
+// of the whole fixed-shape pipeline, timing hooks and the matcher handle.
+//
+// Replaces /root/reference/sift_cuda/interface/Detector.cu (8 stages, 5 CUDA
+// graphs with a host sync after each, a mid-pipeline count D2H, a 10-stream
+// pool) with ONE graph per descriptor buffer: every data-dependent size lives
+// in device counters, every launch has a fixed grid, and the only host sync
+// per frame is the final 32-byte counter readback.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "sift_hip.h"
+#include "sift_kernels.h"
+#include "sift_match.h"
+
+using namespace sift_amd;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                                    \
+    do {                                                                                                \
+        hipError_t e_ = (expr);                                                                         \
+        if (e_ != hipSuccess)                                                                           \
+            return fail(SIFT_HIP_ERR_RUNTIME, std::string(#expr) + ": " + hipGetErrorString(e_));      \
+    } while (0)
+
+// OpenCV getGaussianKernelBitExact (same arithmetic as oracle gaussianTaps).
+Taps gaussian_taps(double sigma) {
+    Taps t{};
+    int n = (int)lrint(sigma * 4 * 2 + 1) | 1;
+    if (n > kMaxTaps) n = kMaxTaps;
+    const double scale2X = -0.125 / (sigma * sigma);
+    const int n2 = (n - 1) / 2;
+    std::vector<double> values(n2 + 1);
+    double sum = 0;
+    for (int i = 0, x = 1 - n; i < n2; i++, x += 2) {
+        const double v = std::exp((double)(x * x) * scale2X);
+        values[i] = v;
+        sum += v;
+    }
+    sum *= 2.0;
+    sum += 1.0;
+    const double mul1 = 1.0 / sum;
+    for (int i = 0; i < n2; i++) {
+        const float v = (float)(values[i] * mul1);
+        t.w[i] = v;
+        t.w[n - 1 - i] = v;
+    }
+    t.w[n2] = (float)(1.0 * mul1);
+    t.n = n;
+    return t;
+}
+
+struct TimingRec {
+    int name;
+    hipEvent_t e0, e1;
+    double bytes;
+};
+
+struct TimingAgg {
+    std::string name;
+    double ms = 0, bytes = 0;
+    int launches = 0;
+};
+
+}  // namespace
+
+struct sift_hip_detector {
+    sift_hip_config cfg{};
+    int device = 0;
+    int L = 3, nOct = 0, firstOctave = 0;
+    int baseW = 0, baseH = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t evIn = nullptr, evOut = nullptr;
+    bool allocated = false;
+
+    PyrDesc pyr{};
+    Taps initTaps{};
+    std::vector<Taps> layerTaps;
+    float threshold = 1.f;
+    KeypointParams kp{};
+
+    int inPitch = 0, upPitch = 0;
+    float* dInput = nullptr;
+    float* dUp = nullptr;
+    float* dPyr = nullptr;
+    uint2* dCand = nullptr;
+    unsigned capCand = 1u << 20;
+    RefKpt* dRef = nullptr;
+    OriKpt* dOri = nullptr;
+    int* dSlot = nullptr;
+    int* dOrder = nullptr;
+    int* dFinalOrder = nullptr;
+    unsigned* dBcount = nullptr;
+    unsigned* dBoff = nullptr;
+    uint32_t* dBitmap = nullptr;
+    size_t bitmapWords = 0;
+    Counters* dCtr = nullptr;
+    Counters* hCtr = nullptr;
+    float* dKpts3[2] = {nullptr, nullptr};
+    float* dFeats4[2] = {nullptr, nullptr};
+    uint16_t* dDesc[2] = {nullptr, nullptr};
+    int cur = 0, count = 0, prevCount = 0;
+
+    hipGraphExec_t exec[2] = {nullptr, nullptr};
+    bool useGraph = true;
+
+    bool timing = false;
+    std::vector<TimingRec> trecs;
+    std::vector<TimingAgg> tagg;
+    std::vector<hipEvent_t> evPool;
+    size_t evUsed = 0;
+
+    int name_id(const char* n) {
+        for (size_t i = 0; i < tagg.size(); i++)
+            if (tagg[i].name == n) return (int)i;
+        tagg.push_back(TimingAgg{n});
+        return (int)tagg.size() - 1;
+    }
+    hipEvent_t next_event() {
+        if (evUsed == evPool.size()) {
+            hipEvent_t e;
+            (void)hipEventCreate(&e);
+            evPool.push_back(e);
+        }
+        return evPool[evUsed++];
+    }
+    template <class F>
+    void timed(const char* name, double bytes, F&& fn) {
+        if (!timing) {
+            fn();
+            return;
+        }
+        TimingRec r{name_id(name), next_event(), next_event(), bytes};
+        (void)hipEventRecord(r.e0, stream);
+        fn();
+        (void)hipEventRecord(r.e1, stream);
+        trecs.push_back(r);
+    }
+    void collect_timing() {
+        for (auto& r : trecs) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, r.e0, r.e1);
+            tagg[r.name].ms += ms;
+            tagg[r.name].bytes += r.bytes;
+            tagg[r.name].launches += 1;
+        }
+        trecs.clear();
+        evUsed = 0;
+    }
+
+    ~sift_hip_detector() {
+        if (allocated) {
+            (void)hipSetDevice(device);
+            for (auto& e : exec)
+                if (e) (void)hipGraphExecDestroy(e);
+            void* bufs[] = {dInput, dUp, dPyr, dCand, dRef, dOri, dSlot, dOrder, dFinalOrder, dBcount, dBoff,
+                            dBitmap, dCtr, dKpts3[0], dKpts3[1], dFeats4[0], dFeats4[1], dDesc[0], dDesc[1]};
+            for (void* b : bufs)
+                if (b) (void)hipFree(b);
+            if (hCtr) (void)hipHostFree(hCtr);
+            for (auto e : evPool) (void)hipEventDestroy(e);
+            if (evIn) (void)hipEventDestroy(evIn);
+            if (evOut) (void)hipEventDestroy(evOut);
+            if (stream) (void)hipStreamDestroy(stream);
+        }
+    }
+};
+
+namespace {
+
+int setup_geometry(sift_hip_detector* d) {
+    const sift_hip_config& c = d->cfg;
+    d->L = c.numOctaveLayers;
+    d->firstOctave = c.upscale ? -1 : 0;
+    d->baseW = c.upscale ? 2 * c.col_width : c.col_width;
+    d->baseH = c.upscale ? 2 * c.row_width : c.row_width;
+    int nOct = c.numOctaves;
+    if (nOct <= 0)  // [OpenCV 4.x sift.dispatch.cpp] cvRound(log2(min) - 2) - firstOctave
+        nOct = (int)lrint(std::log((double)std::min(d->baseW, d->baseH)) / std::log(2.) - 2) - d->firstOctave;
+    if (nOct < 1) nOct = 1;
+    if (nOct > kMaxOctaves) return fail(SIFT_HIP_ERR_INVALID, "too many octaves");
+    d->nOct = nOct;
+    int W = d->baseW, H = d->baseH;
+    int rowBase = 0;
+    long bitBase = 0;
+    size_t off = 0;
+    for (int o = 0; o < nOct; o++) {
+        if (o > 0) {
+            W /= 2;
+            H /= 2;
+        }
+        if (W < 1 || H < 1) return fail(SIFT_HIP_ERR_INVALID, "octave smaller than one pixel");
+        OctGeom& g = d->pyr.oct[o];
+        g.W = W;
+        g.H = H;
+        g.pitch = (W + 63) / 64 * 64;
+        g.planeStride = (long)g.pitch * H;
+        g.base = reinterpret_cast<float*>(off);  // relocated after allocation
+        g.rowBase = rowBase;
+        g.bitBase = bitBase;
+        off += (size_t)g.planeStride * (d->L + 3);
+        rowBase += d->L * H;
+        bitBase += (long)d->L * H * W;
+    }
+    d->pyr.nOct = nOct;
+    d->pyr.L = d->L;
+    d->pyr.firstOctave = d->firstOctave;
+    d->kp.numBuckets = rowBase;
+    d->bitmapWords = (size_t)(bitBase + 31) / 32;
+    return SIFT_HIP_OK;
+}
+
+void setup_taps(sift_hip_detector* d) {
+    const float sigma = (float)d->cfg.sigma;
+    const float sig_diff = d->firstOctave < 0 ? sqrtf(std::max(sigma * sigma - 0.5f * 0.5f * 4, 0.01f))
+                                              : sqrtf(std::max(sigma * sigma - 0.5f * 0.5f, 0.01f));
+    d->initTaps = gaussian_taps((double)sig_diff);
+    const int L = d->L;
+    std::vector<double> sig(L + 3);
+    sig[0] = d->cfg.sigma;
+    const double k = std::pow(2., 1. / L);
+    for (int i = 1; i < L + 3; i++) {
+        const double sig_prev = std::pow(k, (double)(i - 1)) * d->cfg.sigma;
+        const double sig_total = sig_prev * k;
+        sig[i] = std::sqrt(sig_total * sig_total - sig_prev * sig_prev);
+    }
+    d->layerTaps.resize(L + 3);
+    for (int i = 0; i < L + 3; i++) d->layerTaps[i] = gaussian_taps(sig[i]);
+    d->threshold = (float)(int)std::floor(0.5 * d->cfg.contrastThreshould / L * 255 * 1.0);
+    d->kp.contrastThreshold = (float)d->cfg.contrastThreshould;
+    d->kp.edgeThreshold = (float)d->cfg.edgeThreshould;
+    d->kp.sigma = (float)d->cfg.sigma;
+    d->kp.numFeatures = d->cfg.numFeatures;
+    d->kp.capRefined = 1u << 18;
+    d->kp.capOriented = 1u << 19;
+    d->kp.capFinal = (unsigned)(d->cfg.maxKeypoints > 0 ? d->cfg.maxKeypoints : 65536);
+}
+
+void upload_exp_tab() {
+    const double A0 = .9670371139572337719125840413672004409288e-2;
+    float tab[64];
+    for (int j = 0; j < 64; j++) tab[j] = (float)(std::exp2((double)j / 64.0) * A0);
+    upload_exp_table(tab);
+}
+
+template <class T>
+int dalloc(T** p, size_t count) {
+    if (hipMalloc((void**)p, sizeof(T) * std::max<size_t>(count, 1)) != hipSuccess)
+        return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc failed");
+    return SIFT_HIP_OK;
+}
+
+int allocate(sift_hip_detector* d) {
+    HIPCHK(hipSetDevice(d->device));
+    HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&d->evIn, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&d->evOut, hipEventDisableTiming));
+    d->allocated = true;
+    const int W = d->cfg.col_width, H = d->cfg.row_width;
+    d->inPitch = (W + 63) / 64 * 64;
+    int rc;
+    if ((rc = dalloc(&d->dInput, (size_t)d->inPitch * H))) return rc;
+    if (d->firstOctave < 0) {
+        d->upPitch = (2 * W + 63) / 64 * 64;
+        if ((rc = dalloc(&d->dUp, (size_t)d->upPitch * 2 * H))) return rc;
+    }
+    size_t pyrFloats = 0;
+    for (int o = 0; o < d->nOct; o++) pyrFloats += (size_t)d->pyr.oct[o].planeStride * (d->L + 3);
+    if ((rc = dalloc(&d->dPyr, pyrFloats))) return rc;
+    HIPCHK(hipMemset(d->dPyr, 0, sizeof(float) * pyrFloats));
+    for (int o = 0; o < d->nOct; o++)
+        d->pyr.oct[o].base = d->dPyr + reinterpret_cast<size_t>(d->pyr.oct[o].base);
+    const unsigned capO = d->kp.capOriented, capF = d->kp.capFinal;
+    if ((rc = dalloc(&d->dCand, d->capCand))) return rc;
+    if ((rc = dalloc(&d->dRef, d->kp.capRefined))) return rc;
+    if ((rc = dalloc(&d->dOri, capO))) return rc;
+    if ((rc = dalloc(&d->dSlot, capO))) return rc;
+    if ((rc = dalloc(&d->dOrder, capO))) return rc;
+    if ((rc = dalloc(&d->dFinalOrder, capF))) return rc;
+    if ((rc = dalloc(&d->dBcount, (size_t)d->kp.numBuckets))) return rc;
+    if ((rc = dalloc(&d->dBoff, (size_t)d->kp.numBuckets))) return rc;
+    if ((rc = dalloc(&d->dBitmap, d->bitmapWords))) return rc;
+    if ((rc = dalloc(&d->dCtr, 1))) return rc;
+    HIPCHK(hipHostMalloc((void**)&d->hCtr, sizeof(Counters), hipHostMallocDefault));
+    memset(d->hCtr, 0, sizeof(Counters));
+    for (int b = 0; b < 2; b++) {
+        if ((rc = dalloc(&d->dKpts3[b], (size_t)capF * 3))) return rc;
+        if ((rc = dalloc(&d->dFeats4[b], (size_t)capF * 4))) return rc;
+        if ((rc = dalloc(&d->dDesc[b], (size_t)capF * 128))) return rc;
+        HIPCHK(hipMemset(d->dDesc[b], 0, sizeof(uint16_t) * (size_t)capF * 128));
+    }
+    HIPCHK(hipMemset(d->dInput, 0, sizeof(float) * (size_t)d->inPitch * H));
+    upload_exp_tab();
+    return SIFT_HIP_OK;
+}
+
+// The first kernel reads the caller's image (host upload buffer or a device
+// pointer); it stays outside the graph so the graph never bakes a user pointer.
+void enqueue_head(sift_hip_detector* d, const float* img, int pitchFloats) {
+    const int W = d->cfg.col_width, H = d->cfg.row_width;
+    if (d->firstOctave < 0) {
+        d->timed("upsample", (double)W * H * 4 + (double)W * H * 16, [&] {
+            launch_upsample2x(img, pitchFloats, W, H, d->dUp, d->upPitch, d->stream);
+        });
+    } else {
+        const OctGeom& g = d->pyr.oct[0];
+        d->timed("blur_init", (double)W * H * 8, [&] {
+            launch_blur(img, pitchFloats, 1, W, H, g.base, g.pitch, nullptr, d->initTaps, d->stream);
+        });
+    }
+}
+
+void enqueue_body(sift_hip_detector* d, int buf) {
+    hipStream_t s = d->stream;
+    const int L = d->L;
+    d->timed("memset", 0, [&] {
+        (void)hipMemsetAsync(d->dCtr, 0, sizeof(Counters), s);
+        (void)hipMemsetAsync(d->dBcount, 0, sizeof(unsigned) * (size_t)d->kp.numBuckets, s);
+        (void)hipMemsetAsync(d->dBitmap, 0, sizeof(uint32_t) * d->bitmapWords, s);
+    });
+    if (d->firstOctave < 0) {
+        const OctGeom& g = d->pyr.oct[0];
+        d->timed("blur_init", (double)g.W * g.H * 8, [&] {
+            launch_blur(d->dUp, d->upPitch, 1, g.W, g.H, g.base, g.pitch, nullptr, d->initTaps, s);
+        });
+    }
+    static const char* blurNames[kMaxOctaves] = {"blur_o0", "blur_o1", "blur_o2", "blur_o3", "blur_o4", "blur_o5",
+                                                 "blur_o6", "blur_o7", "blur_o8", "blur_o9", "blur_o10", "blur_o11",
+                                                 "blur_o12", "blur_o13", "blur_o14", "blur_o15"};
+    for (int o = 0; o < d->nOct; o++) {
+        const OctGeom& g = d->pyr.oct[o];
+        for (int i = 1; i < L + 3; i++) {
+            float* dst = g.base + (size_t)i * g.planeStride;
+            if (i == 1 && o > 0) {
+                const OctGeom& p = d->pyr.oct[o - 1];
+                d->timed(blurNames[o], (double)g.W * g.H * 12, [&] {
+                    launch_blur(p.base + (size_t)L * p.planeStride, p.pitch, 2, g.W, g.H, dst, g.pitch, g.base,
+                                d->layerTaps[i], s);
+                });
+            } else {
+                d->timed(blurNames[o], (double)g.W * g.H * 8, [&] {
+                    launch_blur(g.base + (size_t)(i - 1) * g.planeStride, g.pitch, 1, g.W, g.H, dst, g.pitch,
+                                nullptr, d->layerTaps[i], s);
+                });
+            }
+        }
+    }
+    for (int o = 0; o < d->nOct; o++) {
+        const OctGeom& g = d->pyr.oct[o];
+        d->timed("extrema", (double)g.W * g.H * 4 * (L + 3), [&] {
+            launch_extrema(d->pyr, o, d->threshold, d->dCand, d->dCtr, d->capCand, s);
+        });
+    }
+    d->timed("refine", 0, [&] { launch_refine(d->pyr, d->dCand, d->capCand, d->dCtr, d->dBitmap, d->dRef, d->kp, s); });
+    d->timed("orientation", 0, [&] { launch_orientation(d->pyr, d->dRef, d->dCtr, d->dOri, d->kp, s); });
+    d->timed("select", 0, [&] { launch_select(d->dOri, d->dCtr, d->kp, s); });
+    d->timed("bucket_count", 0, [&] { launch_bucket_count(d->dOri, d->dCtr, d->dBcount, d->dSlot, d->kp, s); });
+    d->timed("bucket_scan", 0, [&] { launch_bucket_scan(d->dBcount, d->dBoff, d->dCtr, d->kp, s); });
+    d->timed("bucket_scatter", 0,
+             [&] { launch_bucket_scatter(d->dOri, d->dCtr, d->dBoff, d->dSlot, d->dOrder, d->kp, s); });
+    d->timed("bucket_rank", 0, [&] {
+        launch_bucket_rank(d->dOri, d->dBcount, d->dBoff, d->dOrder, d->dCtr, d->dFinalOrder, d->kp, s);
+    });
+    d->timed("descriptor", 0, [&] {
+        launch_descriptor(d->pyr, d->dOri, d->dFinalOrder, d->dCtr, d->dKpts3[buf], d->dFeats4[buf], d->dDesc[buf],
+                          d->kp, s);
+    });
+    (void)hipMemcpyAsync(d->hCtr, d->dCtr, sizeof(Counters), hipMemcpyDeviceToHost, s);
+}
+
+int build_graphs(sift_hip_detector* d) {
+    for (int b = 0; b < 2; b++) {
+        hipGraph_t g = nullptr;
+        HIPCHK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
+        enqueue_body(d, b);
+        HIPCHK(hipStreamEndCapture(d->stream, &g));
+        HIPCHK(hipGraphInstantiate(&d->exec[b], g, nullptr, nullptr, 0));
+        HIPCHK(hipGraphDestroy(g));
+    }
+    return SIFT_HIP_OK;
+}
+
+int run_frame(sift_hip_detector* d, const float* img, int pitchFloats) {
+    d->prevCount = d->count;
+    d->cur ^= 1;
+    enqueue_head(d, img, pitchFloats);
+    if (d->useGraph && !d->timing) {
+        HIPCHK(hipGraphLaunch(d->exec[d->cur], d->stream));
+    } else {
+        enqueue_body(d, d->cur);
+    }
+    return SIFT_HIP_OK;
+}
+
+int finish_frame(sift_hip_detector* d) {
+    HIPCHK(hipStreamSynchronize(d->stream));
+    if (d->timing) d->collect_timing();
+    d->count = (int)std::min<unsigned>(d->hCtr->final_n, d->kp.capFinal);
+    return SIFT_HIP_OK;
+}
+
+#define CHECK_HANDLE(h)                                                                       \
+    do {                                                                                      \
+        if (!(h)) return fail(SIFT_HIP_ERR_INVALID, "null handle");                          \
+        if (!(h)->allocated) return fail(SIFT_HIP_ERR_STATE, "sift_hip_warmup not called"); \
+        HIPCHK(hipSetDevice((h)->device));                                                    \
+    } while (0)
+
+}  // namespace
+
+extern "C" {
+
+void sift_hip_default_config(sift_hip_config* c, int w, int h) {
+    c->col_width = w;
+    c->row_width = h;
+    c->numFeatures = 5000;
+    c->numOctaveLayers = 3;
+    c->contrastThreshould = 0.04;
+    c->edgeThreshould = 10;
+    c->sigma = 1.6;
+    c->upscale = 0;
+    c->numOctaves = 0;
+    c->maxKeypoints = 0;
+}
+
+const char* sift_hip_version(void) {
+    static char buf[96];
+    int rt = 0;
+    (void)hipRuntimeGetVersion(&rt);
+    snprintf(buf, sizeof buf, "abi=%d arch=gfx950 hip=%d", SIFT_HIP_ABI_VERSION, rt);
+    return buf;
+}
+
+const char* sift_hip_last_error(void) { return g_err.c_str(); }
+
+int sift_hip_create(const sift_hip_config* cfg, int device, sift_hip_t* out) {
+    if (!cfg || !out) return fail(SIFT_HIP_ERR_INVALID, "null argument");
+    *out = nullptr;
+    if (cfg->col_width <= 0 || cfg->row_width <= 0) return fail(SIFT_HIP_ERR_INVALID, "image width or height not set");
+    if (cfg->col_width >= 65536 || cfg->row_width >= 65536)
+        return fail(SIFT_HIP_ERR_INVALID, "image dimension >= 65536 unsupported");
+    if (cfg->numOctaveLayers < 1 || cfg->numOctaveLayers > 32)
+        return fail(SIFT_HIP_ERR_INVALID, "numOctaveLayers out of range");
+    if (!(cfg->sigma > 0)) return fail(SIFT_HIP_ERR_INVALID, "sigma must be > 0");
+    auto* d = new sift_hip_detector();
+    d->cfg = *cfg;
+    if (device < 0) {
+        if (hipGetDevice(&d->device) != hipSuccess) d->device = 0;
+    } else {
+        d->device = device;
+    }
+    int rc = setup_geometry(d);
+    if (rc) {
+        delete d;
+        return rc;
+    }
+    setup_taps(d);
+    *out = d;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_destroy(sift_hip_t h) {
+    delete h;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_warmup(sift_hip_t d) {
+    if (!d) return fail(SIFT_HIP_ERR_INVALID, "null handle");
+    if (d->allocated) return SIFT_HIP_OK;
+    int rc = allocate(d);
+    if (rc) return rc;
+    rc = build_graphs(d);
+    if (rc) return rc;
+    // One blank frame through each graph: first-touch, code-object load.
+    for (int i = 0; i < 2; i++) {
+        if ((rc = run_frame(d, d->dInput, d->inPitch))) return rc;
+        if ((rc = finish_frame(d))) return rc;
+    }
+    d->count = d->prevCount = 0;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_num_octaves(sift_hip_t h, int* n) {
+    if (!h || !n) return fail(SIFT_HIP_ERR_INVALID, "null argument");
+    *n = h->nOct;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_octave_dims(sift_hip_t h, int o, int* w, int* hh, int* pitch) {
+    if (!h || o < 0 || o >= h->nOct) return fail(SIFT_HIP_ERR_INVALID, "bad octave");
+    if (w) *w = h->pyr.oct[o].W;
+    if (hh) *hh = h->pyr.oct[o].H;
+    if (pitch) *pitch = h->pyr.oct[o].pitch;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_detect(sift_hip_t d, const float* img, size_t stride) {
+    CHECK_HANDLE(d);
+    if (!img) return fail(SIFT_HIP_ERR_INVALID, "null image");
+    const int W = d->cfg.col_width, H = d->cfg.row_width;
+    if (stride == 0) stride = sizeof(float) * (size_t)W;
+    if (stride < sizeof(float) * (size_t)W) return fail(SIFT_HIP_ERR_INVALID, "row stride smaller than width");
+    HIPCHK(hipMemcpy2DAsync(d->dInput, sizeof(float) * d->inPitch, img, stride, sizeof(float) * W, H,
+                            hipMemcpyHostToDevice, d->stream));
+    int rc = run_frame(d, d->dInput, d->inPitch);
+    if (rc) return rc;
+    return finish_frame(d);
+}
+
+int sift_hip_detect_device(sift_hip_t d, const float* img, size_t stride, void* stream) {
+    CHECK_HANDLE(d);
+    if (!img) return fail(SIFT_HIP_ERR_INVALID, "null image");
+    const int W = d->cfg.col_width;
+    if (stride == 0) stride = sizeof(float) * (size_t)W;
+    if (stride % sizeof(float) || stride < sizeof(float) * (size_t)W)
+        return fail(SIFT_HIP_ERR_INVALID, "row stride must be a multiple of 4 and >= 4*width");
+    hipStream_t ext = (hipStream_t)stream;
+    if (ext) {
+        HIPCHK(hipEventRecord(d->evIn, ext));
+        HIPCHK(hipStreamWaitEvent(d->stream, d->evIn, 0));
+    }
+    int rc = run_frame(d, img, (int)(stride / sizeof(float)));
+    if (rc) return rc;
+    if (ext) {
+        HIPCHK(hipEventRecord(d->evOut, d->stream));
+        HIPCHK(hipStreamWaitEvent(ext, d->evOut, 0));
+    }
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_sync(sift_hip_t d) {
+    CHECK_HANDLE(d);
+    return finish_frame(d);
+}
+
+int sift_hip_num_keypoints(sift_hip_t d, int* n) {
+    if (!d || !n) return fail(SIFT_HIP_ERR_INVALID, "null argument");
+    *n = d->count;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_overflow_flags(sift_hip_t d, int* flags) {
+    if (!d || !flags) return fail(SIFT_HIP_ERR_INVALID, "null argument");
+    *flags = d->hCtr ? (int)d->hCtr->overflow : 0;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_results_device(sift_hip_t d, const float** k3, const float** f4, const uint16_t** desc,
+                            const uint16_t** prev, int* prevCount, int* capacity) {
+    CHECK_HANDLE(d);
+    if (k3) *k3 = d->dKpts3[d->cur];
+    if (f4) *f4 = d->dFeats4[d->cur];
+    if (desc) *desc = d->dDesc[d->cur];
+    if (prev) *prev = d->dDesc[d->cur ^ 1];
+    if (prevCount) *prevCount = d->prevCount;
+    if (capacity) *capacity = (int)d->kp.capFinal;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_copy_to_host(sift_hip_t d, float* k3, float* f4, uint16_t* desc, int cap) {
+    CHECK_HANDLE(d);
+    const int n = std::min(d->count, cap);
+    if (n > 0) {
+        if (k3)
+            HIPCHK(hipMemcpyAsync(k3, d->dKpts3[d->cur], sizeof(float) * 3 * n, hipMemcpyDeviceToHost, d->stream));
+        if (f4)
+            HIPCHK(hipMemcpyAsync(f4, d->dFeats4[d->cur], sizeof(float) * 4 * n, hipMemcpyDeviceToHost, d->stream));
+        if (desc)
+            HIPCHK(hipMemcpyAsync(desc, d->dDesc[d->cur], sizeof(uint16_t) * 128 * n, hipMemcpyDeviceToHost,
+                                  d->stream));
+    }
+    HIPCHK(hipStreamSynchronize(d->stream));
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_copy_descriptors_device(sift_hip_t d, uint16_t* dst, int cap, void* stream) {
+    CHECK_HANDLE(d);
+    const int n = std::min(d->count, cap);
+    hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+    if (n > 0) HIPCHK(hipMemcpyAsync(dst, d->dDesc[d->cur], sizeof(uint16_t) * 128 * n, hipMemcpyDeviceToDevice, s));
+    if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_set_timing(sift_hip_t d, int enable) {
+    if (!d) return fail(SIFT_HIP_ERR_INVALID, "null handle");
+    d->timing = enable != 0;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_timing_count(sift_hip_t d, int* n) {
+    if (!d || !n) return fail(SIFT_HIP_ERR_INVALID, "null argument");
+    *n = (int)d->tagg.size();
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_timing_entry(sift_hip_t d, int i, const char** name, double* ms, int* launches, double* bytes) {
+    if (!d || i < 0 || i >= (int)d->tagg.size()) return fail(SIFT_HIP_ERR_INVALID, "bad timing index");
+    if (name) *name = d->tagg[i].name.c_str();
+    if (ms) *ms = d->tagg[i].ms;
+    if (launches) *launches = d->tagg[i].launches;
+    if (bytes) *bytes = d->tagg[i].bytes;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_timing_reset(sift_hip_t d) {
+    if (!d) return fail(SIFT_HIP_ERR_INVALID, "null handle");
+    for (auto& a : d->tagg) a.ms = a.bytes = 0, a.launches = 0;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_debug_gaussian(sift_hip_t d, int o, int layer, float* out) {
+    CHECK_HANDLE(d);
+    if (o < 0 || o >= d->nOct || layer < 0 || layer >= d->L + 3 || !out)
+        return fail(SIFT_HIP_ERR_INVALID, "bad plane");
+    const OctGeom& g = d->pyr.oct[o];
+    HIPCHK(hipMemcpy2D(out, sizeof(float) * g.W, g.base + (size_t)layer * g.planeStride, sizeof(float) * g.pitch,
+                       sizeof(float) * g.W, g.H, hipMemcpyDeviceToHost));
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_debug_candidates(sift_hip_t d, int* quads, int cap, int* count) {
+    CHECK_HANDLE(d);
+    const int n = (int)std::min<unsigned>(d->hCtr->cand, d->capCand);
+    if (count) *count = (int)d->hCtr->cand;
+    const int m = std::min(n, cap);
+    if (m > 0 && quads) {
+        std::vector<uint2> tmp(m);
+        HIPCHK(hipMemcpy(tmp.data(), d->dCand, sizeof(uint2) * m, hipMemcpyDeviceToHost));
+        for (int i = 0; i < m; i++) {
+            quads[4 * i] = (int)(tmp[i].x >> 8);
+            quads[4 * i + 1] = (int)(tmp[i].x & 255);
+            quads[4 * i + 2] = (int)(tmp[i].y >> 16);
+            quads[4 * i + 3] = (int)(tmp[i].y & 0xffff);
+        }
+    }
+    return SIFT_HIP_OK;
+}
+
+// ----------------------------------------------------------------------------
+// Matcher
+// ----------------------------------------------------------------------------
+}  // extern "C"
+
+struct sift_hip_matcher {
+    int device = 0;
+    int maxQ = 0, maxT = 0, maxP = 0;
+    float4* dPart = nullptr;
+    float* dQnorm = nullptr;
+    int* dMatch = nullptr;
+    static constexpr int kMaxSplits = 256;
+    ~sift_hip_matcher() {
+        (void)hipSetDevice(device);
+        if (dPart) (void)hipFree(dPart);
+        if (dQnorm) (void)hipFree(dQnorm);
+        if (dMatch) (void)hipFree(dMatch);
+    }
+};
+
+extern "C" {
+
+int sift_hip_matcher_create(int device, int max_query, int max_train, int max_pairs, sift_hip_matcher_t* out) {
+    if (!out || max_query <= 0 || max_train <= 0 || max_pairs <= 0 || max_pairs > kMaxMatchPairs)
+        return fail(SIFT_HIP_ERR_INVALID, "bad matcher limits");
+    *out = nullptr;
+    auto* m = new sift_hip_matcher();
+    if (device < 0) {
+        if (hipGetDevice(&m->device) != hipSuccess) m->device = 0;
+    } else {
+        m->device = device;
+    }
+    m->maxQ = max_query;
+    m->maxT = max_train;
+    m->maxP = max_pairs;
+    if (hipSetDevice(m->device) != hipSuccess ||
+        hipMalloc((void**)&m->dPart, sizeof(float4) * (size_t)max_pairs * sift_hip_matcher::kMaxSplits * max_query) !=
+            hipSuccess ||
+        hipMalloc((void**)&m->dQnorm, sizeof(float) * (size_t)max_pairs * max_query) != hipSuccess ||
+        hipMalloc((void**)&m->dMatch, sizeof(int) * (size_t)max_pairs * max_query) != hipSuccess) {
+        delete m;
+        return fail(SIFT_HIP_ERR_NOMEM, "matcher allocation failed");
+    }
+    *out = m;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_matcher_destroy(sift_hip_matcher_t m) {
+    delete m;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_match_batched(sift_hip_matcher_t m, int P, const uint16_t* const* q, const int* nq,
+                           const uint16_t* const* t, const int* nt, float ratio, int ratio_on_squared, int* idx2,
+                           float* d2, int* match, void* stream) {
+    if (!m || P <= 0 || P > m->maxP || !q || !nq || !t || !nt) return fail(SIFT_HIP_ERR_INVALID, "bad batch");
+    MatchBatch b{};
+    b.P = P;
+    int off = 0, maxq = 1, maxt = 1;
+    for (int p = 0; p < P; p++) {
+        if (nq[p] < 0 || nt[p] < 0 || nq[p] > m->maxQ || nt[p] > m->maxT)
+            return fail(SIFT_HIP_ERR_INVALID, "pair size exceeds matcher limits");
+        if ((nq[p] && !q[p]) || (nt[p] && !t[p])) return fail(SIFT_HIP_ERR_INVALID, "null descriptor pointer");
+        b.pair[p] = MatchPair{q[p], t[p], nq[p], nt[p], off, 0};
+        off += nq[p];
+        maxq = std::max(maxq, nq[p]);
+        maxt = std::max(maxt, nt[p]);
+    }
+    HIPCHK(hipSetDevice(m->device));
+    const int S = std::min(match_splits(maxq, maxt, P), (int)sift_hip_matcher::kMaxSplits);
+    launch_match(b, S, m->maxQ, m->dPart, m->dQnorm, ratio, ratio_on_squared, idx2, d2, match, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_match_device(sift_hip_matcher_t m, const uint16_t* q, int nq, const uint16_t* t, int nt, float ratio,
+                          int ratio_on_squared, int* idx2, float* d2, int* match, void* stream) {
+    return sift_hip_match_batched(m, 1, &q, &nq, &t, &nt, ratio, ratio_on_squared, idx2, d2, match, stream);
+}
+
+int sift_hip_match_host(sift_hip_matcher_t m, const uint16_t* q, int nq, const uint16_t* t, int nt, float ratio,
+                        int ratio_on_squared, int* out) {
+    if (!m || !out) return fail(SIFT_HIP_ERR_INVALID, "null argument");
+    if (nq <= 0) return SIFT_HIP_OK;
+    int rc = sift_hip_match_device(m, q, nq, t, nt, ratio, ratio_on_squared, nullptr, nullptr, m->dMatch, nullptr);
+    if (rc) return rc;
+    HIPCHK(hipMemcpy(out, m->dMatch, sizeof(int) * nq, hipMemcpyDeviceToHost));
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_device_count(int* n) {
+    if (!n) return fail(SIFT_HIP_ERR_INVALID, "null argument");
+    if (hipGetDeviceCount(n) != hipSuccess) *n = 0;
+    return SIFT_HIP_OK;
+}
+int sift_hip_malloc(void** p, size_t bytes) {
+    HIPCHK(hipMalloc(p, bytes));
+    return SIFT_HIP_OK;
+}
+int sift_hip_free(void* p) {
+    HIPCHK(hipFree(p));
+    return SIFT_HIP_OK;
+}
+int sift_hip_memcpy_h2d(void* dst, const void* src, size_t bytes) {
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return SIFT_HIP_OK;
+}
+int sift_hip_memcpy_d2h(void* dst, const void* src, size_t bytes) {
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return SIFT_HIP_OK;
+}
+int sift_hip_device_sync(void) {
+    HIPCHK(hipDeviceSynchronize());
+    return SIFT_HIP_OK;
+}
+
+}  // extern "C"

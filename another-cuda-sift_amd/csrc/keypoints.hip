@@ -1,0 +1,602 @@
+// Keypoint stages for gfx950: sub-pixel refinement, orientation histogram,
+// retainBest selection, deterministic ordering and the 4x4x8 descriptor.
+//
+// Replaces /root/reference/sift_cuda/sift_func/SiftOps.cu and
+// /root/reference/sift_cuda/utils/CudaMemcpyUtils.cu.  Semantics follow OpenCV
+// 4.x; float operation order is the oracle's
+// (oracle/sift_oracle.cpp adjustLocalExtrema / calcOrientationHist /
+// calcSIFTDescriptor), so refined keypoints and angles are bit-exact.  The
+// descriptor histogram is accumulated in a different (parallel) order, so
+// descriptor bytes may differ from the oracle by +-1 (tests/test_gpu_parity.py).
+#include <hip/hip_fp16.h>
+
+#include "sift_kernels.h"
+#include "sift_math.h"
+
+namespace sift_amd {
+
+__constant__ float c_exptab[64];
+
+void upload_exp_table(const float* tab64) {
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_exptab), tab64, 64 * sizeof(float));
+}
+
+constexpr int kBorder = 5;
+constexpr int kMaxInterpSteps = 5;
+constexpr int kOriBins = 36;
+constexpr float kOriSigFctr = 1.5f;
+constexpr float kOriRadius = 3 * kOriSigFctr;
+constexpr float kOriPeakRatio = 0.8f;
+
+__device__ __forceinline__ const OctGeom& octave_geom(const PyrDesc& pyr, int o) { return pyr.oct[o]; }
+
+__device__ __forceinline__ float dog_at(const float* g, long ps, int pitch, int layer, int r, int c) {
+    const float* p = g + (size_t)r * pitch + c;
+    return p[(size_t)(layer + 1) * ps] - p[(size_t)layer * ps];
+}
+
+// ---------------------------------------------------------------------------
+// adjustLocalExtrema (OpenCV 4.x sift.simd.hpp), one thread per candidate.
+// DoG values are re-formed from the Gaussian planes (G_{l+1} - G_l: the same
+// single rounding as a stored DoG).  Accepted keypoints are de-duplicated by
+// final grid position with a bitmap (OpenCV removes the same duplicates later
+// in removeDuplicatedSorted) and compacted with an atomic.
+// Reference: SiftOps.cu:63-208 + collectKpts SiftOps.cu:210-235.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_refine(PyrDesc pyr, const uint2* __restrict__ cand, unsigned capCand,
+                                                Counters* __restrict__ ctr, uint32_t* __restrict__ bitmap,
+                                                RefKpt* __restrict__ out, KeypointParams kp) {
+    const unsigned n = min(ctr->cand, capCand);
+    const int L = pyr.L;
+    const float img_scale = 1.f / 255.f;
+    const float deriv_scale = img_scale * 0.5f;
+    const float second_deriv_scale = img_scale;
+    const float cross_deriv_scale = img_scale * 0.25f;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint2 q = cand[i];
+        const int o = (int)(q.x >> 8);
+        int layer = (int)(q.x & 255);
+        int r = (int)(q.y >> 16), c = (int)(q.y & 0xffff);
+        const OctGeom& g = octave_geom(pyr, o);
+        const float* G = g.base;
+        const long ps = g.planeStride;
+        const int pitch = g.pitch;
+
+        float xi = 0, xr = 0, xc = 0;
+        int it = 0;
+        bool ok = true;
+        for (; it < kMaxInterpSteps; it++) {
+            const float c0 = dog_at(G, ps, pitch, layer, r, c);
+            const float cl = dog_at(G, ps, pitch, layer, r, c - 1), cr = dog_at(G, ps, pitch, layer, r, c + 1);
+            const float cu = dog_at(G, ps, pitch, layer, r - 1, c), cd = dog_at(G, ps, pitch, layer, r + 1, c);
+            const float pc = dog_at(G, ps, pitch, layer - 1, r, c), nc = dog_at(G, ps, pitch, layer + 1, r, c);
+            const float dD0 = (cr - cl) * deriv_scale;
+            const float dD1 = (cd - cu) * deriv_scale;
+            const float dD2 = (nc - pc) * deriv_scale;
+            const float v2 = c0 * 2;
+            const float dxx = (cr + cl - v2) * second_deriv_scale;
+            const float dyy = (cd + cu - v2) * second_deriv_scale;
+            const float dss = (nc + pc - v2) * second_deriv_scale;
+            const float dxy = (dog_at(G, ps, pitch, layer, r + 1, c + 1) - dog_at(G, ps, pitch, layer, r + 1, c - 1) -
+                               dog_at(G, ps, pitch, layer, r - 1, c + 1) + dog_at(G, ps, pitch, layer, r - 1, c - 1)) *
+                              cross_deriv_scale;
+            const float dxs = (dog_at(G, ps, pitch, layer + 1, r, c + 1) - dog_at(G, ps, pitch, layer + 1, r, c - 1) -
+                               dog_at(G, ps, pitch, layer - 1, r, c + 1) + dog_at(G, ps, pitch, layer - 1, r, c - 1)) *
+                              cross_deriv_scale;
+            const float dys = (dog_at(G, ps, pitch, layer + 1, r + 1, c) - dog_at(G, ps, pitch, layer + 1, r - 1, c) -
+                               dog_at(G, ps, pitch, layer - 1, r + 1, c) + dog_at(G, ps, pitch, layer - 1, r - 1, c)) *
+                              cross_deriv_scale;
+            // Matx_FastSolveOp<float,3,1>: Cramer's rule, det from Matx_DetOp.
+            const float a00 = dxx, a01 = dxy, a02 = dxs, a10 = dxy, a11 = dyy, a12 = dys, a20 = dxs, a21 = dys,
+                        a22 = dss;
+            const float b0 = dD0, b1 = dD1, b2 = dD2;
+            float X0 = 0, X1 = 0, X2 = 0;
+            float d = a00 * (a11 * a22 - a21 * a12) - a01 * (a10 * a22 - a20 * a12) + a02 * (a10 * a21 - a20 * a11);
+            if (d != 0) {
+                d = 1 / d;
+                X0 = d * (b0 * (a11 * a22 - a12 * a21) - a01 * (b1 * a22 - a12 * b2) + a02 * (b1 * a21 - a11 * b2));
+                X1 = d * (a00 * (b1 * a22 - a12 * b2) - b0 * (a10 * a22 - a12 * a20) + a02 * (a10 * b2 - b1 * a20));
+                X2 = d * (a00 * (a11 * b2 - b1 * a21) - a01 * (a10 * b2 - b1 * a20) + b0 * (a10 * a21 - a11 * a20));
+            }
+            xi = -X2;
+            xr = -X1;
+            xc = -X0;
+            if (fabsf(xi) < 0.5f && fabsf(xr) < 0.5f && fabsf(xc) < 0.5f) break;
+            const float big = (float)(INT_MAX / 3);
+            if (fabsf(xi) > big || fabsf(xr) > big || fabsf(xc) > big) {
+                ok = false;
+                break;
+            }
+            c += cv_round(xc);
+            r += cv_round(xr);
+            layer += cv_round(xi);
+            if (layer < 1 || layer > L || c < kBorder || c >= g.W - kBorder || r < kBorder || r >= g.H - kBorder) {
+                ok = false;
+                break;
+            }
+        }
+        if (!ok || it >= kMaxInterpSteps) continue;
+
+        const float c0 = dog_at(G, ps, pitch, layer, r, c);
+        const float cl = dog_at(G, ps, pitch, layer, r, c - 1), cr = dog_at(G, ps, pitch, layer, r, c + 1);
+        const float cu = dog_at(G, ps, pitch, layer, r - 1, c), cd = dog_at(G, ps, pitch, layer, r + 1, c);
+        const float pc = dog_at(G, ps, pitch, layer - 1, r, c), nc = dog_at(G, ps, pitch, layer + 1, r, c);
+        const float dD0 = (cr - cl) * deriv_scale;
+        const float dD1 = (cd - cu) * deriv_scale;
+        const float dD2 = (nc - pc) * deriv_scale;
+        float t = 0.f;
+        t += dD0 * xc;
+        t += dD1 * xr;
+        t += dD2 * xi;
+        const float contr = c0 * img_scale + t * 0.5f;
+        if (fabsf(contr) * L < kp.contrastThreshold) continue;
+        const float v2 = c0 * 2.f;
+        const float dxx = (cr + cl - v2) * second_deriv_scale;
+        const float dyy = (cd + cu - v2) * second_deriv_scale;
+        const float dxy = (dog_at(G, ps, pitch, layer, r + 1, c + 1) - dog_at(G, ps, pitch, layer, r + 1, c - 1) -
+                           dog_at(G, ps, pitch, layer, r - 1, c + 1) + dog_at(G, ps, pitch, layer, r - 1, c - 1)) *
+                          cross_deriv_scale;
+        const float tr = dxx + dyy;
+        const float det = dxx * dyy - dxy * dxy;
+        const float et = kp.edgeThreshold;
+        if (det <= 0 || tr * tr * et >= (et + 1) * (et + 1) * det) continue;
+
+        // Duplicate (same final octave/layer/r/c) -> identical keypoint: keep one.
+        const long bit = g.bitBase + ((long)(layer - 1) * g.H + r) * g.W + c;
+        const uint32_t m = 1u << (bit & 31);
+        if (atomicOr(&bitmap[bit >> 5], m) & m) continue;
+
+        RefKpt k;
+        k.x = ((float)c + xc) * (float)(1 << o);
+        k.y = ((float)r + xr) * (float)(1 << o);
+        k.octave = o + (layer << 8) + ((int)rint(((double)xi + 0.5) * 255) << 16);
+        k.size = kp.sigma * pow2_via_double((layer + xi) / (float)L) * (float)(1 << o) * 2;
+        k.response = fabsf(contr);
+        k.o = o;
+        k.layer = layer;
+        k.rc = r << 16 | c;
+        const unsigned slot = atomicAdd(&ctr->refined, 1u);
+        if (slot < kp.capRefined)
+            out[slot] = k;
+        else
+            atomicOr(&ctr->overflow, 2u);
+    }
+}
+
+void launch_refine(const PyrDesc& pyr, const uint2* cand, unsigned capCand, Counters* ctr, uint32_t* bitmap,
+                   RefKpt* out, const KeypointParams& kp, hipStream_t s) {
+    hipLaunchKernelGGL(k_refine, dim3(512), dim3(256), 0, s, pyr, cand, capCand, ctr, bitmap, out, kp);
+}
+
+// ---------------------------------------------------------------------------
+// calcOrientationHist + peak search (OpenCV 4.x sift.simd.hpp), one wave64 per
+// refined keypoint, on the Gaussian plane of the refined layer.  Samples are
+// produced 64 at a time in raster order; lane b (< 36) owns histogram bin b and
+// adds the chunk's contributions in lane order, so every bin sees exactly the
+// oracle's sequential summation order (adding +0.f for non-matching samples is
+// exact).  Smoothing, max and peak interpolation use wave shuffles.
+// Reference: SiftOps.cu:237-376 (DoG plane, 32-lane LDS atomics, floor bins,
+// no interpolation, SURVEY A-9).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_orientation(PyrDesc pyr, const RefKpt* __restrict__ in,
+                                                     Counters* __restrict__ ctr, OriKpt* __restrict__ out,
+                                                     KeypointParams kp) {
+    const int lane = threadIdx.x & 63;
+    const unsigned wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const unsigned nwaves = gridDim.x * 4;
+    const unsigned n = min(ctr->refined, kp.capRefined);
+    const int fo = pyr.firstOctave;
+    for (unsigned k = wave; k < n; k += nwaves) {
+        const RefKpt kpt = in[k];
+        const int o = kpt.o, layer = kpt.layer, r = kpt.rc >> 16, c = kpt.rc & 0xffff;
+        const OctGeom& g = octave_geom(pyr, o);
+        const float* img = g.base + (size_t)layer * g.planeStride;
+        const int pitch = g.pitch, W = g.W, H = g.H;
+        const float scl_octv = kpt.size * 0.5f / (float)(1 << o);
+        const int radius = cv_round(kOriRadius * scl_octv);
+        const float sigma = kOriSigFctr * scl_octv;
+        const float expf_scale = -1.f / (2.f * sigma * sigma);
+        const int side = 2 * radius + 1, total = side * side;
+
+        float acc = 0.f;
+        for (int base = 0; base < total; base += 64) {
+            const int idx = base + lane;
+            int bin = -1;
+            float val = 0.f;
+            if (idx < total) {
+                const int i = idx / side - radius, j = idx - (idx / side) * side - radius;
+                const int y = r + i, x = c + j;
+                if (y > 0 && y < H - 1 && x > 0 && x < W - 1) {
+                    const float* p = img + (size_t)y * pitch + x;
+                    const float dx = p[1] - p[-1];
+                    const float dy = p[-pitch] - p[pitch];
+                    const float w = cv_exp32f((float)(i * i + j * j) * expf_scale, c_exptab);
+                    const float ori = cv_fast_atan2(dy, dx);
+                    const float mag = cv_magnitude(dx, dy);
+                    int b = cv_round((kOriBins / 360.f) * ori);
+                    if (b >= kOriBins) b -= kOriBins;
+                    if (b < 0) b += kOriBins;
+                    bin = b;
+                    val = w * mag;
+                }
+            }
+#pragma unroll
+            for (int l = 0; l < 64; l++) {
+                const int bl = __builtin_amdgcn_readlane(bin, l);
+                if (bl >= 0) {
+                    const float vl = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(val), l));
+                    acc = acc + (lane == bl ? vl : 0.f);
+                }
+            }
+        }
+
+        // Circular [1 4 6 4 1]/16 smoothing (SIMD body, fma form).
+        const int bl = lane < kOriBins ? lane : 0;
+        const float tm2 = __shfl(acc, (bl + kOriBins - 2) % kOriBins);
+        const float tm1 = __shfl(acc, (bl + kOriBins - 1) % kOriBins);
+        const float tp1 = __shfl(acc, (bl + 1) % kOriBins);
+        const float tp2 = __shfl(acc, (bl + 2) % kOriBins);
+        const float h = __fmaf_rn(tm2 + tp2, 1.f / 16.f, __fmaf_rn(tm1 + tp1, 4.f / 16.f, acc * (6.f / 16.f)));
+        float mx = lane < kOriBins ? h : -INFINITY;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+        const float mag_thr = (float)(mx * kOriPeakRatio);
+        const float hl = __shfl(h, (bl + kOriBins - 1) % kOriBins);
+        const float hr = __shfl(h, (bl + 1) % kOriBins);
+        const bool peak = lane < kOriBins && h > hl && h > hr && h >= mag_thr;
+        const unsigned long long mask = __ballot(peak);
+        if (!mask) continue;
+        unsigned basepos = 0;
+        if (lane == 0) basepos = atomicAdd(&ctr->oriented, (unsigned)__popcll(mask));
+        basepos = __shfl(basepos, 0);
+        if (peak) {
+            float bin = (float)lane + 0.5f * (hl - hr) / (hl - 2 * h + hr);
+            bin = bin < 0 ? kOriBins + bin : bin >= kOriBins ? bin - kOriBins : bin;
+            float angle = 360.f - (float)((360.f / kOriBins) * bin);
+            if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+            OriKpt ok;
+            ok.x = kpt.x;
+            ok.y = kpt.y;
+            ok.size = kpt.size;
+            ok.angle = angle;
+            ok.response = kpt.response;
+            ok.octave = kpt.octave;
+            if (fo < 0) {
+                const float scale = 1.f / (float)(1 << -fo);
+                ok.octave = (kpt.octave & ~255) | ((kpt.octave + fo) & 255);
+                ok.x *= scale;
+                ok.y *= scale;
+                ok.size *= scale;
+            }
+            ok.bucket = g.rowBase + (layer - 1) * H + r;
+            ok.sub = (c << 6) | lane;
+            const unsigned pos = basepos + (unsigned)__popcll(mask & ((1ull << lane) - 1ull));
+            if (pos < kp.capOriented)
+                out[pos] = ok;
+            else
+                atomicOr(&ctr->overflow, 4u);
+        }
+    }
+}
+
+void launch_orientation(const PyrDesc& pyr, const RefKpt* in, Counters* ctr, OriKpt* out, const KeypointParams& kp,
+                        hipStream_t s) {
+    hipLaunchKernelGGL(k_orientation, dim3(1024), dim3(256), 0, s, pyr, in, ctr, out, kp);
+}
+
+// ---------------------------------------------------------------------------
+// KeyPointsFilter::retainBest: response threshold = the numFeatures-th largest
+// response (positive floats order like their bit patterns), by a 4-pass 8-bit
+// MSB radix select in one workgroup.  Keeps every keypoint with response >= it,
+// which is exactly the set OpenCV's nth_element + partition keeps.
+// Reference: keeps the first numFeatures in octave order (CudaMemcpyUtils.cu:38-49).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_select(const OriKpt* __restrict__ kpts, Counters* __restrict__ ctr,
+                                                 KeypointParams kp) {
+    __shared__ unsigned hist[256];
+    __shared__ unsigned s_prefix, s_k;
+    const unsigned n = min(ctr->oriented, kp.capOriented);
+    const int tid = threadIdx.x;
+    if (kp.numFeatures <= 0 || n <= (unsigned)kp.numFeatures) {
+        if (tid == 0) ctr->thr_bits = 0u;
+        return;
+    }
+    if (tid == 0) {
+        s_prefix = 0;
+        s_k = (unsigned)kp.numFeatures;
+    }
+    unsigned pmask = 0;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        for (int i = tid; i < 256; i += 1024) hist[i] = 0;
+        __syncthreads();
+        const unsigned prefix = s_prefix;
+        for (unsigned i = tid; i < n; i += 1024) {
+            const unsigned b = __float_as_uint(kpts[i].response);
+            if ((b & pmask) == prefix) atomicAdd(&hist[(b >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            unsigned k = s_k, cum = 0;
+            int digit = 0;
+            for (int d = 255; d >= 0; d--) {
+                if (cum + hist[d] >= k) {
+                    digit = d;
+                    k -= cum;
+                    break;
+                }
+                cum += hist[d];
+            }
+            s_k = k;
+            s_prefix = prefix | ((unsigned)digit << shift);
+        }
+        pmask |= 255u << shift;
+        __syncthreads();
+    }
+    if (tid == 0) ctr->thr_bits = s_prefix;
+}
+
+void launch_select(const OriKpt* kpts, Counters* ctr, const KeypointParams& kp, hipStream_t s) {
+    hipLaunchKernelGGL(k_select, dim3(1), dim3(1024), 0, s, kpts, ctr, kp);
+}
+
+// ---------------------------------------------------------------------------
+// Deterministic output order without a comparison sort: counting sort into
+// row buckets (octave, layer, r), then rank by (c, peak) inside each bucket.
+// Atomic compaction upstream makes arrival order nondeterministic; this makes
+// the output order a pure function of the keypoint set.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_bucket_count(const OriKpt* __restrict__ kpts, const Counters* __restrict__ ctr,
+                                                      unsigned* __restrict__ bcount, int* __restrict__ slot,
+                                                      KeypointParams kp) {
+    const unsigned n = min(ctr->oriented, kp.capOriented);
+    const float thr = __uint_as_float(ctr->thr_bits);
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const OriKpt k = kpts[i];
+        slot[i] = k.response >= thr ? (int)atomicAdd(&bcount[k.bucket], 1u) : -1;
+    }
+}
+
+void launch_bucket_count(const OriKpt* kpts, const Counters* ctr, unsigned* bcount, int* slot,
+                         const KeypointParams& kp, hipStream_t s) {
+    hipLaunchKernelGGL(k_bucket_count, dim3(256), dim3(256), 0, s, kpts, ctr, bcount, slot, kp);
+}
+
+__global__ __launch_bounds__(1024) void k_bucket_scan(const unsigned* __restrict__ bcount, unsigned* __restrict__ boff,
+                                                      Counters* __restrict__ ctr, KeypointParams kp) {
+    __shared__ unsigned wsum[16];
+    __shared__ unsigned carry_s;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) carry_s = 0;
+    __syncthreads();
+    for (int base = 0; base < kp.numBuckets; base += 1024) {
+        const int i = base + tid;
+        const unsigned v = i < kp.numBuckets ? bcount[i] : 0u;
+        unsigned x = v;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const unsigned y = __shfl_up(x, off);
+            if (lane >= off) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        unsigned wpre = 0, tot = 0;
+        for (int k = 0; k < 16; k++) {
+            if (k < w) wpre += wsum[k];
+            tot += wsum[k];
+        }
+        const unsigned carry = carry_s;
+        if (i < kp.numBuckets) boff[i] = carry + wpre + x - v;
+        __syncthreads();
+        if (tid == 0) carry_s = carry + tot;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        const unsigned total = carry_s;
+        ctr->final_n = min(total, kp.capFinal);
+        if (total > kp.capFinal) atomicOr(&ctr->overflow, 8u);
+    }
+}
+
+void launch_bucket_scan(unsigned* bcount, unsigned* boff, Counters* ctr, const KeypointParams& kp, hipStream_t s) {
+    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(1024), 0, s, bcount, boff, ctr, kp);
+}
+
+__global__ __launch_bounds__(256) void k_bucket_scatter(const OriKpt* __restrict__ kpts, const Counters* __restrict__ ctr,
+                                                        const unsigned* __restrict__ boff, const int* __restrict__ slot,
+                                                        int* __restrict__ order, KeypointParams kp) {
+    const unsigned n = min(ctr->oriented, kp.capOriented);
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int s = slot[i];
+        if (s >= 0) order[boff[kpts[i].bucket] + (unsigned)s] = (int)i;
+    }
+}
+
+void launch_bucket_scatter(const OriKpt* kpts, const Counters* ctr, const unsigned* boff, const int* slot, int* order,
+                           const KeypointParams& kp, hipStream_t s) {
+    hipLaunchKernelGGL(k_bucket_scatter, dim3(256), dim3(256), 0, s, kpts, ctr, boff, slot, order, kp);
+}
+
+__global__ __launch_bounds__(256) void k_bucket_rank(const OriKpt* __restrict__ kpts, const unsigned* __restrict__ bcount,
+                                                     const unsigned* __restrict__ boff, const int* __restrict__ order,
+                                                     const Counters* __restrict__ ctr, int* __restrict__ final_order,
+                                                     KeypointParams kp) {
+    const int lane = threadIdx.x & 63;
+    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int nwaves = gridDim.x * 4;
+    const unsigned cap = kp.capFinal;
+    for (int b = wave; b < kp.numBuckets; b += nwaves) {
+        const unsigned cnt = bcount[b];
+        if (cnt == 0) continue;
+        const unsigned base = boff[b];
+        for (unsigned e0 = 0; e0 < cnt; e0 += 64) {
+            const unsigned e = e0 + lane;
+            int idx = -1, se = 0;
+            if (e < cnt) {
+                idx = order[base + e];
+                se = kpts[idx].sub;
+            }
+            unsigned rank = 0;
+            for (unsigned f0 = 0; f0 < cnt; f0 += 64) {
+                const unsigned f = f0 + lane;
+                const int sf = f < cnt ? kpts[order[base + f]].sub : 0x7fffffff;
+                const unsigned lim = min(64u, cnt - f0);
+                for (unsigned l = 0; l < lim; l++) rank += (unsigned)(__shfl(sf, (int)l) < se);
+            }
+            if (e < cnt && base + rank < cap) final_order[base + rank] = idx;
+        }
+    }
+}
+
+void launch_bucket_rank(const OriKpt* kpts, const unsigned* bcount, const unsigned* boff, const int* order,
+                        const Counters* ctr, int* final_order, const KeypointParams& kp, hipStream_t s) {
+    hipLaunchKernelGGL(k_bucket_rank, dim3(256), dim3(256), 0, s, kpts, bcount, boff, order, ctr, final_order, kp);
+}
+
+// ---------------------------------------------------------------------------
+// calcSIFTDescriptor (OpenCV 4.x sift.simd.hpp), one 256-thread workgroup per
+// keypoint.  Samples of the (2R+1)^2 window are spread over the 4 waves; each
+// wave accumulates its trilinear contributions into a private LDS histogram
+// (6 x 6 x 10 bins), the 4 copies are summed in fixed order (deterministic
+// run to run), then wrap, L2 norm, 0.2 clip, renorm and x512 round to 0..255
+// exactly as the oracle.  Output layout is the reference's (Detector.hh:54-57).
+// Reference: SiftOps.cu:454-623 (modff bins, half(x512), SURVEY A-10).
+// ---------------------------------------------------------------------------
+constexpr int kD = 4, kN = 8;
+constexpr int kHistLen = (kD + 2) * (kD + 2) * (kN + 2);  // 360
+
+__global__ __launch_bounds__(256) void k_descriptor(PyrDesc pyr, const OriKpt* __restrict__ kpts,
+                                                    const int* __restrict__ final_order,
+                                                    const Counters* __restrict__ ctr, float* __restrict__ kpts3,
+                                                    float* __restrict__ feats4, uint16_t* __restrict__ desc,
+                                                    KeypointParams kp) {
+    __shared__ float hist[4][kHistLen + 8];
+    __shared__ float raw[128];
+    __shared__ float s_nrm;
+    const int tid = threadIdx.x, w = tid >> 6;
+    const unsigned n = ctr->final_n;
+    const int fo = pyr.firstOctave;
+    for (unsigned p = blockIdx.x; p < n; p += gridDim.x) {
+        const OriKpt kpt = kpts[final_order[p]];
+        int octave = kpt.octave & 255;
+        const int layer = (kpt.octave >> 8) & 255;
+        octave = octave < 128 ? octave : (-128 | octave);
+        const float scale = octave >= 0 ? 1.f / (float)(1 << octave) : (float)(1 << -octave);
+        const float size = kpt.size * scale;
+        const float ptfx = kpt.x * scale, ptfy = kpt.y * scale;
+        const OctGeom& g = octave_geom(pyr, octave - fo);
+        const float* img = g.base + (size_t)layer * g.planeStride;
+        const int pitch = g.pitch, rows = g.H, cols = g.W;
+        float angle = 360.f - kpt.angle;
+        if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+        const float scl = size * 0.5f;
+
+        const int ptx = cv_round(ptfx), pty = cv_round(ptfy);
+        const float arg = angle * (float)(M_PI / 180);
+        float cos_t = (float)cos((double)arg);
+        float sin_t = (float)sin((double)arg);
+        const float bins_per_rad = kN / 360.f;
+        const float exp_scale = -1.f / (kD * kD * 0.5f);
+        const float hist_width = 3.f * scl;
+        int radius = cv_round(hist_width * 1.4142135623730951f * (float)(kD + 1) * 0.5f);
+        radius = min(radius, (int)sqrt((double)cols * cols + (double)rows * rows));
+        cos_t /= hist_width;
+        sin_t /= hist_width;
+
+        for (int i = tid; i < 4 * (kHistLen + 8); i += 256) (&hist[0][0])[i] = 0.f;
+        __syncthreads();
+        float* hw = hist[w];
+        const int side = 2 * radius + 1, total = side * side;
+        for (int idx = tid; idx < total; idx += 256) {
+            const int i = idx / side - radius, j = idx - (idx / side) * side - radius;
+            const float c_rot = (float)j * cos_t - (float)i * sin_t;
+            const float r_rot = (float)j * sin_t + (float)i * cos_t;
+            float rbin = r_rot + (float)(kD / 2) - 0.5f;
+            float cbin = c_rot + (float)(kD / 2) - 0.5f;
+            const int r = pty + i, c = ptx + j;
+            if (rbin > -1 && rbin < kD && cbin > -1 && cbin < kD && r > 0 && r < rows - 1 && c > 0 && c < cols - 1) {
+                const float* pp = img + (size_t)r * pitch + c;
+                const float dx = pp[1] - pp[-1];
+                const float dy = pp[-pitch] - pp[pitch];
+                const float wgt = cv_exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, c_exptab);
+                const float gori = cv_fast_atan2(dy, dx);
+                const float gmag = cv_magnitude(dx, dy);
+                float obin = (gori - angle) * bins_per_rad;
+                const float mag = gmag * wgt;
+                const int r0 = cv_floor(rbin), c0 = cv_floor(cbin);
+                int o0 = cv_floor(obin);
+                rbin -= (float)r0;
+                cbin -= (float)c0;
+                obin -= (float)o0;
+                if (o0 < 0) o0 += kN;
+                if (o0 >= kN) o0 -= kN;
+                const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+                const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
+                const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+                const float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
+                const float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
+                const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
+                const float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
+                const int hidx = ((r0 + 1) * (kD + 2) + c0 + 1) * (kN + 2) + o0;
+                atomicAdd(&hw[hidx], v_rco000);
+                atomicAdd(&hw[hidx + 1], v_rco001);
+                atomicAdd(&hw[hidx + (kN + 2)], v_rco010);
+                atomicAdd(&hw[hidx + (kN + 3)], v_rco011);
+                atomicAdd(&hw[hidx + (kD + 2) * (kN + 2)], v_rco100);
+                atomicAdd(&hw[hidx + (kD + 2) * (kN + 2) + 1], v_rco101);
+                atomicAdd(&hw[hidx + (kD + 3) * (kN + 2)], v_rco110);
+                atomicAdd(&hw[hidx + (kD + 3) * (kN + 2) + 1], v_rco111);
+            }
+        }
+        __syncthreads();
+        for (int b = tid; b < kHistLen; b += 256) hist[0][b] = ((hist[0][b] + hist[1][b]) + hist[2][b]) + hist[3][b];
+        __syncthreads();
+        if (tid < 128) {
+            const int i = tid >> 5, j = (tid >> 3) & 3, k = tid & 7;
+            const int hidx = ((i + 1) * (kD + 2) + (j + 1)) * (kN + 2);
+            float v = hist[0][hidx + k];
+            if (k < 2) v = v + hist[0][hidx + kN + k];
+            raw[tid] = v;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            float acc8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            for (int k = 0; k < 128; k++) acc8[k & 7] = __fmaf_rn(raw[k], raw[k], acc8[k & 7]);
+            const float t0 = acc8[0] + acc8[4], t1 = acc8[1] + acc8[5], t2 = acc8[2] + acc8[6], t3 = acc8[3] + acc8[7];
+            float nrm2 = (t0 + t2) + (t1 + t3);
+            const float thr = __fsqrt_rn(nrm2) * 0.2f;
+            nrm2 = 0.f;
+            for (int k = 0; k < 128; k++) {
+                const float val = fminf(raw[k], thr);
+                raw[k] = val;
+                nrm2 = nrm2 + val * val;
+            }
+            s_nrm = 512.f / fmaxf(__fsqrt_rn(nrm2), FLT_EPSILON);
+            float* k3 = kpts3 + 3 * (size_t)p;
+            k3[0] = kpt.x;
+            k3[1] = kpt.y;
+            k3[2] = (float)layer;
+            float4 f;
+            f.x = (float)kpt.octave;
+            f.y = kpt.size;
+            f.z = kpt.response;
+            f.w = kpt.angle;
+            reinterpret_cast<float4*>(feats4)[p] = f;
+        }
+        __syncthreads();
+        if (tid < 128) {
+            int v = cv_round(raw[tid] * s_nrm);
+            v = v < 0 ? 0 : (v > 255 ? 255 : v);
+            const _Float16 hv = (_Float16)(float)v;
+            desc[(size_t)p * 128 + tid] = __builtin_bit_cast(uint16_t, hv);
+        }
+        __syncthreads();
+    }
+}
+
+void launch_descriptor(const PyrDesc& pyr, const OriKpt* kpts, const int* final_order, const Counters* ctr,
+                       float* kpts3, float* feats4, uint16_t* desc, const KeypointParams& kp, hipStream_t s) {
+    hipLaunchKernelGGL(k_descriptor, dim3(2048), dim3(256), 0, s, pyr, kpts, final_order, ctr, kpts3, feats4, desc,
+                       kp);
+}
+
+}  // namespace sift_amd

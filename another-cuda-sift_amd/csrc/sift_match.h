@@ -1,0 +1,28 @@
+// Matcher launch interface (match.hip) used by detector.hip's C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sift_amd {
+
+constexpr int kMaxMatchPairs = 64;
+
+struct MatchPair {
+    const uint16_t* q;  // nq x 128 half, row-major
+    const uint16_t* t;  // nt x 128 half, row-major
+    int nq, nt;
+    int out_off;        // output row offset of this pair
+    int pad;
+};
+
+// Passed by value: lives in the kernarg segment (64 x 32 B = 2 KiB).
+struct MatchBatch {
+    MatchPair pair[kMaxMatchPairs];
+    int P;
+};
+
+int match_splits(int max_nq, int max_nt, int P);
+void launch_match(const MatchBatch& batch, int S, int nq_stride, float4* part, float* qnorm, float ratio,
+                  int ratio_on_squared, int* idx2, float* d2, int* match, hipStream_t s);
+
+}  // namespace sift_amd

@@ -1,0 +1,365 @@
+"""Python mirror of the reference's SIFT interface over libsift_hip.so (C ABI).
+
+Names follow /root/reference/sift_cuda/interface/Detector.hh:24-96 and
+/root/reference/sift_cuda/types/CudaSiftConfig.hh:3-14 (including the
+reference's field spellings), so host code and parity tests read like the
+reference's own callers (/root/reference/tool/*.cc).
+
+The compute path is the HIP library only: if libsift_hip.so is missing this
+module raises ImportError-like errors on first use; there is no CPU fallback.
+
+HIP runtime note: PyTorch wheels bundle their own libamdhip64.so.  A process that
+uses both torch and this library must `import torch` BEFORE the first call here,
+so that libsift_hip.so binds to the already-loaded runtime (one HIP runtime per
+process).  bench.py does this.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.normpath(os.path.join(_HERE, "..", "lib"))
+LIB_PATH = os.path.join(LIB_DIR, "libsift_hip.so")
+
+SIFT_HIP_OK = 0
+_lib = None
+
+
+class SiftHipError(RuntimeError):
+    pass
+
+
+class _Config(ctypes.Structure):
+    _fields_ = [
+        ("col_width", ctypes.c_int),
+        ("row_width", ctypes.c_int),
+        ("numFeatures", ctypes.c_int),
+        ("numOctaveLayers", ctypes.c_int),
+        ("contrastThreshould", ctypes.c_double),
+        ("edgeThreshould", ctypes.c_double),
+        ("sigma", ctypes.c_double),
+        ("upscale", ctypes.c_int),
+        ("numOctaves", ctypes.c_int),
+        ("maxKeypoints", ctypes.c_int),
+    ]
+
+
+def lib() -> ctypes.CDLL:
+    """Load libsift_hip.so (once).  Fails loudly when the build is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SiftHipError(f"{LIB_PATH} not found: build it with `make` (or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, ip, i, f, d, sz = ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_float, ctypes.c_double, ctypes.c_size_t
+    sigs = {
+        "sift_hip_default_config": (None, [ctypes.POINTER(_Config), i, i]),
+        "sift_hip_version": (ctypes.c_char_p, []),
+        "sift_hip_last_error": (ctypes.c_char_p, []),
+        "sift_hip_create": (i, [ctypes.POINTER(_Config), i, ctypes.POINTER(vp)]),
+        "sift_hip_destroy": (i, [vp]),
+        "sift_hip_warmup": (i, [vp]),
+        "sift_hip_num_octaves": (i, [vp, ip]),
+        "sift_hip_octave_dims": (i, [vp, i, ip, ip, ip]),
+        "sift_hip_detect": (i, [vp, vp, sz]),
+        "sift_hip_detect_device": (i, [vp, vp, sz, vp]),
+        "sift_hip_sync": (i, [vp]),
+        "sift_hip_num_keypoints": (i, [vp, ip]),
+        "sift_hip_overflow_flags": (i, [vp, ip]),
+        "sift_hip_results_device": (i, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), ip, ip]),
+        "sift_hip_copy_to_host": (i, [vp, vp, vp, vp, i]),
+        "sift_hip_copy_descriptors_device": (i, [vp, vp, i, vp]),
+        "sift_hip_set_timing": (i, [vp, i]),
+        "sift_hip_timing_count": (i, [vp, ip]),
+        "sift_hip_timing_entry": (i, [vp, i, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(d), ip, ctypes.POINTER(d)]),
+        "sift_hip_timing_reset": (i, [vp]),
+        "sift_hip_debug_gaussian": (i, [vp, i, i, vp]),
+        "sift_hip_debug_candidates": (i, [vp, vp, i, ip]),
+        "sift_hip_matcher_create": (i, [i, i, i, i, ctypes.POINTER(vp)]),
+        "sift_hip_matcher_destroy": (i, [vp]),
+        "sift_hip_match_device": (i, [vp, vp, i, vp, i, f, i, vp, vp, vp, vp]),
+        "sift_hip_match_batched": (i, [vp, i, vp, vp, vp, vp, f, i, vp, vp, vp, vp]),
+        "sift_hip_match_host": (i, [vp, vp, i, vp, i, f, i, vp]),
+        "sift_synth_frame": (i, [ctypes.c_uint, i, i, vp]),
+        "sift_hip_device_count": (i, [ip]),
+        "sift_hip_malloc": (i, [ctypes.POINTER(vp), sz]),
+        "sift_hip_free": (i, [vp]),
+        "sift_hip_memcpy_h2d": (i, [vp, vp, sz]),
+        "sift_hip_memcpy_d2h": (i, [vp, vp, sz]),
+        "sift_hip_device_sync": (i, []),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != SIFT_HIP_OK:
+        msg = lib().sift_hip_last_error().decode(errors="replace")
+        raise SiftHipError(f"{what} failed ({rc}): {msg}")
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def version() -> str:
+    return lib().sift_hip_version().decode()
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    lib().sift_hip_device_count(ctypes.byref(n))
+    return n.value
+
+
+def synth_frame(index: int, width: int, height: int) -> np.ndarray:
+    """Deterministic synthetic frame: float32 HxW, integers 0..255."""
+    out = np.empty((height, width), np.float32)
+    _check(lib().sift_synth_frame(index, width, height, _ptr(out)), "sift_synth_frame")
+    return out
+
+
+@dataclass
+class CudaSiftConfig:
+    """/root/reference/sift_cuda/types/CudaSiftConfig.hh:3-14 (+ numOctaves, maxKeypoints)."""
+
+    col_width: int = 0
+    row_width: int = 0
+    numFeatures: int = 5000
+    numOctaveLayers: int = 3
+    contrastThreshould: float = 0.04
+    edgeThreshould: float = 10.0
+    sigma: float = 1.6
+    upscale: bool = False
+    numOctaves: int = 0
+    maxKeypoints: int = 0
+
+    def _abi(self) -> _Config:
+        c = _Config()
+        for name, _ in _Config._fields_:
+            setattr(c, name, int(getattr(self, name)) if name == "upscale" else getattr(self, name))
+        return c
+
+
+class DeviceBuffer:
+    """Non-owning device array view (stands in for thrust::device_vector)."""
+
+    def __init__(self, ptr: int, size: int):
+        self.ptr, self._size = int(ptr or 0), int(size)
+
+    def data(self) -> int:
+        return self.ptr
+
+    def size(self) -> int:
+        return self._size
+
+
+class Detector:
+    """sift_cuda::Detector (Detector.hh:24-96) over the C ABI."""
+
+    def __init__(self, config: CudaSiftConfig, device: int = -1):
+        self.config = config
+        self._h = ctypes.c_void_p()
+        _check(lib().sift_hip_create(ctypes.byref(config._abi()), device, ctypes.byref(self._h)), "sift_hip_create")
+        n = ctypes.c_int()
+        lib().sift_hip_num_octaves(self._h, ctypes.byref(n))
+        self.nOctaves = n.value
+        self.total_size = 0
+        self.prev_size = 0
+        self.final_kpts = np.zeros((0, 3), np.float32)
+        self.final_features = np.zeros((0, 4), np.float32)
+        self.descriptors = np.zeros((0, 128), np.float16)
+        self.device_kpts = self.device_features = self.device_descriptor = self.prev_descriptor = DeviceBuffer(0, 0)
+        self._ready = False
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and h.value and _lib is not None:
+            _lib.sift_hip_destroy(h)
+            self._h = None
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._h
+
+    def gpuWarmUpAndAllocate(self) -> bool:
+        if not self._ready:
+            _check(lib().sift_hip_warmup(self._h), "gpuWarmUpAndAllocate")
+            self._ready = True
+            self._refresh()
+        return True
+
+    def octave_dims(self, o: int):
+        w, h, p = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(lib().sift_hip_octave_dims(self._h, o, ctypes.byref(w), ctypes.byref(h), ctypes.byref(p)), "octave_dims")
+        return w.value, h.value, p.value
+
+    def _refresh(self) -> None:
+        k3, f4, d, pd = (ctypes.c_void_p() for _ in range(4))
+        pc, cap = ctypes.c_int(), ctypes.c_int()
+        _check(lib().sift_hip_results_device(self._h, ctypes.byref(k3), ctypes.byref(f4), ctypes.byref(d),
+                                             ctypes.byref(pd), ctypes.byref(pc), ctypes.byref(cap)), "results")
+        self.device_kpts = DeviceBuffer(k3.value, cap.value)
+        self.device_features = DeviceBuffer(f4.value, cap.value)
+        self.device_descriptor = DeviceBuffer(d.value, cap.value * 128)
+        self.prev_descriptor = DeviceBuffer(pd.value, cap.value * 128)
+        self.prev_size = pc.value
+        n = ctypes.c_int()
+        lib().sift_hip_num_keypoints(self._h, ctypes.byref(n))
+        self.total_size = n.value
+
+    def detectAndCompute(self, image: np.ndarray) -> None:
+        """Detector.cu:133-233.  `image`: float32 (rows, cols) 0..255."""
+        self.gpuWarmUpAndAllocate()
+        img = np.ascontiguousarray(image, dtype=np.float32)
+        if img.shape != (self.config.row_width, self.config.col_width):
+            raise SiftHipError(f"image shape {img.shape} != configured {(self.config.row_width, self.config.col_width)}")
+        _check(lib().sift_hip_detect(self._h, _ptr(img), img.strides[0]), "detectAndCompute")
+        self._refresh()
+
+    def detectAndComputeDevice(self, dev_ptr: int, row_stride_bytes: int, stream: Optional[int] = None, sync: bool = True) -> None:
+        self.gpuWarmUpAndAllocate()
+        _check(lib().sift_hip_detect_device(self._h, dev_ptr, row_stride_bytes, stream), "detectAndComputeDevice")
+        if sync:
+            self.sync()
+
+    def sync(self) -> None:
+        _check(lib().sift_hip_sync(self._h), "sync")
+        self._refresh()
+
+    def copyToHost(self, descriptor: bool = True) -> None:
+        """Detector.cu:606-634."""
+        n = self.total_size
+        k3 = np.zeros((n, 3), np.float32)
+        f4 = np.zeros((n, 4), np.float32)
+        d = np.zeros((n, 128), np.uint16) if descriptor else None
+        _check(lib().sift_hip_copy_to_host(self._h, _ptr(k3), _ptr(f4), _ptr(d) if d is not None else None, n), "copyToHost")
+        self.final_kpts, self.final_features = k3, f4
+        if d is not None:
+            self.descriptors = d.view(np.float16)
+
+    def overflow_flags(self) -> int:
+        v = ctypes.c_int()
+        lib().sift_hip_overflow_flags(self._h, ctypes.byref(v))
+        return v.value
+
+    # --- parity/debug helpers -------------------------------------------------
+    def debug_gaussian(self, octave: int, layer: int) -> np.ndarray:
+        w, h, _ = self.octave_dims(octave)
+        out = np.empty((h, w), np.float32)
+        _check(lib().sift_hip_debug_gaussian(self._h, octave, layer, _ptr(out)), "debug_gaussian")
+        return out
+
+    def debug_candidates(self, cap: int = 1 << 20) -> np.ndarray:
+        q = np.zeros((cap, 4), np.int32)
+        cnt = ctypes.c_int()
+        _check(lib().sift_hip_debug_candidates(self._h, _ptr(q), cap, ctypes.byref(cnt)), "debug_candidates")
+        return q[: min(cnt.value, cap)]
+
+    # --- stage timing (roofline) ---------------------------------------------
+    def set_timing(self, enable: bool) -> None:
+        _check(lib().sift_hip_set_timing(self._h, int(enable)), "set_timing")
+
+    def timing(self) -> dict:
+        n = ctypes.c_int()
+        lib().sift_hip_timing_count(self._h, ctypes.byref(n))
+        out = {}
+        for k in range(n.value):
+            name, ms, nl, by = ctypes.c_char_p(), ctypes.c_double(), ctypes.c_int(), ctypes.c_double()
+            _check(lib().sift_hip_timing_entry(self._h, k, ctypes.byref(name), ctypes.byref(ms), ctypes.byref(nl), ctypes.byref(by)), "timing")
+            out[name.value.decode()] = {"ms": ms.value, "launches": nl.value, "bytes": by.value}
+        return out
+
+    def timing_reset(self) -> None:
+        lib().sift_hip_timing_reset(self._h)
+
+
+class Matcher:
+    """Brute-force L2 matcher (replaces Match.cu:8-177) with preallocated scratch."""
+
+    def __init__(self, max_query: int, max_train: int, max_pairs: int = 1, device: int = -1):
+        self._m = ctypes.c_void_p()
+        self.max_query, self.max_train, self.max_pairs = max_query, max_train, max_pairs
+        _check(lib().sift_hip_matcher_create(device, max_query, max_train, max_pairs, ctypes.byref(self._m)), "matcher_create")
+
+    def __del__(self):
+        m = getattr(self, "_m", None)
+        if m and m.value and _lib is not None:
+            _lib.sift_hip_matcher_destroy(m)
+            self._m = None
+
+    def match_device(self, q_ptr: int, nq: int, t_ptr: int, nt: int, ratio: float = 0.8, ratio_on_squared: bool = False,
+                     idx2_ptr: int = 0, d2_ptr: int = 0, match_ptr: int = 0, stream: Optional[int] = None) -> None:
+        _check(lib().sift_hip_match_device(self._m, q_ptr, nq, t_ptr, nt, ratio, int(ratio_on_squared),
+                                           idx2_ptr or None, d2_ptr or None, match_ptr or None, stream), "match_device")
+
+    def match_batched(self, q_ptrs: Sequence[int], nqs: Sequence[int], t_ptrs: Sequence[int], nts: Sequence[int],
+                      ratio: float = 0.8, ratio_on_squared: bool = False, idx2_ptr: int = 0, d2_ptr: int = 0,
+                      match_ptr: int = 0, stream: Optional[int] = None) -> None:
+        P = len(q_ptrs)
+        qa = (ctypes.c_void_p * P)(*q_ptrs)
+        ta = (ctypes.c_void_p * P)(*t_ptrs)
+        na = (ctypes.c_int * P)(*nqs)
+        ma = (ctypes.c_int * P)(*nts)
+        _check(lib().sift_hip_match_batched(self._m, P, qa, na, ta, ma, ratio, int(ratio_on_squared),
+                                            idx2_ptr or None, d2_ptr or None, match_ptr or None, stream), "match_batched")
+
+    def match_host(self, q_ptr: int, nq: int, t_ptr: int, nt: int, ratio: float = 0.8, ratio_on_squared: bool = True) -> np.ndarray:
+        out = np.full(max(nq, 0), -1, np.int32)
+        _check(lib().sift_hip_match_host(self._m, q_ptr, nq, t_ptr, nt, ratio, int(ratio_on_squared), _ptr(out)), "match_host")
+        return out
+
+
+_default_matcher: Optional[Matcher] = None
+
+
+def matchBruteForce(des: DeviceBuffer, num_des: int, src: DeviceBuffer, num_src: int) -> np.ndarray:
+    """Match.cuh:9-14: nearest src row per des row if d1^2 < 0.8 d2^2, else -1."""
+    global _default_matcher
+    if _default_matcher is None or num_des > _default_matcher.max_query or num_src > _default_matcher.max_train:
+        mq = max(num_des, _default_matcher.max_query if _default_matcher else 0, 1)
+        mt = max(num_src, _default_matcher.max_train if _default_matcher else 0, 1)
+        _default_matcher = Matcher(mq, mt)
+    if num_des <= 0:
+        return np.zeros(0, np.int32)
+    return _default_matcher.match_host(des.data(), num_des, src.data(), num_src, 0.8, True)
+
+
+class DeviceArray:
+    """Minimal owning device allocation for callers without torch (tests)."""
+
+    def __init__(self, nbytes: int):
+        self.ptr = ctypes.c_void_p()
+        self.nbytes = nbytes
+        _check(lib().sift_hip_malloc(ctypes.byref(self.ptr), max(nbytes, 1)), "malloc")
+
+    @classmethod
+    def from_numpy(cls, a: np.ndarray) -> "DeviceArray":
+        a = np.ascontiguousarray(a)
+        d = cls(a.nbytes)
+        _check(lib().sift_hip_memcpy_h2d(d.ptr, _ptr(a), a.nbytes), "h2d")
+        return d
+
+    def to_numpy(self, dtype, shape) -> np.ndarray:
+        out = np.empty(shape, dtype)
+        _check(lib().sift_hip_memcpy_d2h(_ptr(out), self.ptr, out.nbytes), "d2h")
+        return out
+
+    @property
+    def value(self) -> int:
+        return self.ptr.value
+
+    def __del__(self):
+        if getattr(self, "ptr", None) is not None and self.ptr.value and _lib is not None:
+            _lib.sift_hip_free(self.ptr)
+            self.ptr = None

@@ -1,0 +1,68 @@
+// Drop-in for /root/reference/sift_cuda/interface/Detector.hh:24-96.
+// Same class name, constructor, public methods and public result members;
+// device members are non-owning DeviceBuffer views, host members std::vector.
+// No HIP/CUDA header is included: everything goes through include/sift_hip.h.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "sift_cuda/CudaSiftConfig.hh"
+#include "sift_cuda/HostImage.hh"
+#include "sift_cuda/Types.hh"
+
+struct sift_hip_detector;
+
+namespace sift_cuda {
+
+class Detector {
+public:
+    explicit Detector(const CudaSiftConfig& config);
+    ~Detector();
+    Detector(const Detector&) = delete;
+    Detector& operator=(const Detector&) = delete;
+
+    // Detector.cu:17-39: allocate, capture the pipeline graph, warm up.
+    // Returns false when the image size is unset (as the reference does).
+    bool gpuWarmUpAndAllocate();
+
+    // Detector.cu:133-233: synchronous; results valid until the next call.
+    void detectAndCompute(const Imagef& image);
+    // Extra: image already in device memory (fp32, row stride in bytes).
+    void detectAndComputeDevice(const float* device_image, size_t row_stride_bytes, void* hip_stream = nullptr);
+
+    // Detector.cu:606-634: copies total_size results (+ descriptors) to host.
+    void copyToHost(bool descriptor);
+
+    // Detector.hh:48-51 debug snapshot switch: accepted, snapshots not produced.
+    void setDataGen(const std::string& path) { m_debug_path = path; }
+
+    int numOctaves() const { return m_nOctaves; }
+    sift_hip_detector* handle() const { return m_handle; }
+
+    // Results (Detector.hh:53-62).
+    DeviceBuffer<Float3> device_kpts;      // {x, y, layer}
+    DeviceBuffer<Float4> device_features;  // {octave (packed, as float), size, response, angle}
+    DeviceBuffer<Half> device_descriptor;  // 128 per keypoint, values 0..255
+    DeviceBuffer<Half> prev_descriptor;    // previous frame's descriptors
+    std::vector<Float3> final_kpts{};
+    std::vector<Float4> final_features{};
+    std::vector<Half> descriptors{};
+    int max_kpts = 5000;
+    int total_size{0};
+
+private:
+    void refreshViews();
+    CudaSiftConfig m_config{};
+    sift_hip_detector* m_handle{nullptr};
+    bool m_initialized{false};
+    int m_nOctaves{0};
+    std::string m_debug_path;
+};
+
+// Match.cuh:9-14: for each of the num_des rows of `des`, the index of its
+// nearest row of `src` if it passes Lowe's test on squared distances
+// (d1^2 < 0.8 d2^2, the reference's Match.cu:172 convention), else -1.
+std::vector<int> matchBruteForce(const DeviceBuffer<Half>& des, int num_des, const DeviceBuffer<Half>& src,
+                                 int num_src);
+
+}  // namespace sift_cuda

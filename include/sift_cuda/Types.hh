@@ -1,0 +1,61 @@
+// Host-side element types of the drop-in surface.  The reference exposes CUDA's
+// float3 / float4 / half (Detector.hh:54-60); these PODs have the same layout
+// and member names so caller code like `kpts[i].x` or `(float)desc[k]` compiles
+// unchanged, without pulling HIP headers into the caller.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+
+namespace sift_cuda {
+
+struct Float3 {
+    float x, y, z;
+};
+struct Float4 {
+    float x, y, z, w;
+};
+
+// IEEE binary16 storage; SIFT descriptor values are integers 0..255, exact here.
+struct Half {
+    uint16_t bits{0};
+    operator float() const {
+        const uint32_t s = (bits & 0x8000u) << 16, e = (bits >> 10) & 0x1f, m = bits & 0x3ffu;
+        uint32_t f;
+        if (e == 0) {
+            if (m == 0) {
+                f = s;
+            } else {  // subnormal
+                int sh = 0;
+                uint32_t mm = m;
+                while (!(mm & 0x400u)) { mm <<= 1; sh++; }
+                f = s | ((uint32_t)(113 - sh) << 23) | ((mm & 0x3ffu) << 13);
+            }
+        } else if (e == 31) {
+            f = s | 0x7f800000u | (m << 13);
+        } else {
+            f = s | ((e + 112) << 23) | (m << 13);
+        }
+        float out;
+        std::memcpy(&out, &f, 4);
+        return out;
+    }
+};
+static_assert(sizeof(Float3) == 12 && sizeof(Float4) == 16 && sizeof(Half) == 2, "layout");
+
+// Non-owning view of a device array owned by a Detector (stands in for the
+// reference's thrust::device_vector members; data()/size() as there).
+template <class T>
+class DeviceBuffer {
+public:
+    DeviceBuffer() = default;
+    DeviceBuffer(T* p, size_t n) : ptr_(p), n_(n) {}
+    T* data() const { return ptr_; }
+    size_t size() const { return n_; }
+
+private:
+    T* ptr_{nullptr};
+    size_t n_{0};
+};
+
+}  // namespace sift_cuda

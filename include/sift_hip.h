@@ -1,0 +1,167 @@
+/*
+ * sift_hip.h -- C ABI of the MI355X SIFT hot path (libsift_hip.so).
+ *
+ * Plain C types only: no HIP, torch or C++ types cross this boundary.  Device
+ * memory is owned by the handle; device pointers handed out are valid until the
+ * next sift_hip_detect* call on the same handle (the reference's contract for
+ * Detector::device_* members, /root/reference/sift_cuda/interface/Detector.hh:54-57).
+ * Streams are passed as `void*` (a hipStream_t; NULL = the handle's own stream).
+ * Every function returns 0 (SIFT_HIP_OK) or a negative error; the message of the
+ * last error on the calling thread is in sift_hip_last_error().
+ *
+ * Each entry point names the reference interface it replaces.  The C++ surface
+ * sift_cuda::Detector / CudaSiftConfig / matchBruteForce in include/sift_cuda/ is
+ * a thin wrapper over this ABI.
+ */
+#ifndef SIFT_HIP_H
+#define SIFT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SIFT_HIP_OK 0
+#define SIFT_HIP_ERR_INVALID (-1)   /* bad argument / size mismatch        */
+#define SIFT_HIP_ERR_RUNTIME (-2)   /* HIP runtime error                   */
+#define SIFT_HIP_ERR_STATE   (-3)   /* call out of order (e.g. no warmup)  */
+#define SIFT_HIP_ERR_NOMEM   (-4)   /* device allocation failed            */
+
+#define SIFT_HIP_ABI_VERSION 1
+
+typedef struct sift_hip_detector* sift_hip_t;
+typedef struct sift_hip_matcher* sift_hip_matcher_t;
+
+/* Mirrors CudaSiftConfig (/root/reference/sift_cuda/types/CudaSiftConfig.hh:3-14),
+ * field for field including the reference's spellings, plus defaulted extras. */
+typedef struct {
+    int    col_width;           /* image width  (CudaSiftConfig.hh:4)            */
+    int    row_width;           /* image height (CudaSiftConfig.hh:5)            */
+    int    numFeatures;         /* retainBest count, 0 = keep all (.hh:6)        */
+    int    numOctaveLayers;     /* (.hh:7)                                      */
+    double contrastThreshould;  /* (.hh:8)                                      */
+    double edgeThreshould;      /* (.hh:9)                                      */
+    double sigma;               /* (.hh:10)                                     */
+    int    upscale;             /* 1 = double the base image = OpenCV default   */
+                                /* firstOctave -1 (.hh:12, broken there)        */
+    int    numOctaves;          /* extra: 0 = auto (OpenCV formula)             */
+    int    maxKeypoints;        /* extra: result capacity, 0 = 65536            */
+} sift_hip_config;
+
+/* Fills the reference defaults (CudaSiftConfig.hh:6-12) for a w x h image. */
+void sift_hip_default_config(sift_hip_config* cfg, int w, int h);
+
+/* Library / build info: "abi=<n> arch=gfx950 hip=<ver>". */
+const char* sift_hip_version(void);
+const char* sift_hip_last_error(void);
+
+/* --- Detector (replaces sift_cuda::Detector, Detector.hh:24-96) ------------ */
+
+/* Detector::Detector(const CudaSiftConfig&) (Detector.hh:26-29).  device < 0
+ * binds to the calling thread's current HIP device like the reference. */
+int sift_hip_create(const sift_hip_config* cfg, int device, sift_hip_t* out);
+int sift_hip_destroy(sift_hip_t h);
+
+/* Detector::gpuWarmUpAndAllocate() (Detector.cu:17-39): allocate every buffer,
+ * build the hipGraph of the whole pipeline and run it once on a blank frame. */
+int sift_hip_warmup(sift_hip_t h);
+
+/* Octave count and per-octave geometry chosen for this configuration. */
+int sift_hip_num_octaves(sift_hip_t h, int* n);
+int sift_hip_octave_dims(sift_hip_t h, int octave, int* w, int* hgt, int* pitch_floats);
+
+/* Detector::detectAndCompute(const Imagef&) (Detector.cu:133-233): uploads the
+ * fp32 host image (row stride in bytes, 0 = packed) and runs the pipeline;
+ * returns when results are ready.  Keypoint count via sift_hip_num_keypoints. */
+int sift_hip_detect(sift_hip_t h, const float* host_img, size_t row_stride_bytes);
+
+/* Same, for an image already in device memory (HBM-resident input); enqueued on
+ * `stream` (NULL = internal) and NOT synchronised: call sift_hip_sync. */
+int sift_hip_detect_device(sift_hip_t h, const float* dev_img, size_t row_stride_bytes, void* stream);
+int sift_hip_sync(sift_hip_t h);
+
+/* Detector::total_size (Detector.hh:62, Detector.cu:584-604). */
+int sift_hip_num_keypoints(sift_hip_t h, int* n);
+/* Non-zero when a capacity (candidates / keypoints / results) overflowed. */
+int sift_hip_overflow_flags(sift_hip_t h, int* flags);
+
+/* Device result arrays (Detector.hh:54-57): kpts = float3 {x, y, layer}
+ * per keypoint, features = float4 {octave packed as float, size, response,
+ * angle}, descriptors = 128 x IEEE half (values 0..255) per keypoint.
+ * prev_desc = the previous frame's descriptors (Detector.cu:136-141). */
+int sift_hip_results_device(sift_hip_t h, const float** kpts3, const float** feats4,
+                            const uint16_t** desc, const uint16_t** prev_desc,
+                            int* prev_count, int* capacity);
+
+/* Detector::copyToHost(bool descriptor) (Detector.cu:606-634).  Copies
+ * min(count, cap) results; desc may be NULL. */
+int sift_hip_copy_to_host(sift_hip_t h, float* kpts3, float* feats4, uint16_t* desc, int cap);
+
+/* Device-to-device copy of this frame's descriptors (e.g. into a torch tensor
+ * for an RCCL all-gather).  Copies min(count, cap) rows, pads nothing. */
+int sift_hip_copy_descriptors_device(sift_hip_t h, uint16_t* dst, int cap, void* stream);
+
+/* Stage timing for roofline reporting: when enabled, the next detect calls run
+ * un-graphed with HIP events around every kernel; names are stable strings. */
+int sift_hip_set_timing(sift_hip_t h, int enable);
+int sift_hip_timing_count(sift_hip_t h, int* n);
+int sift_hip_timing_entry(sift_hip_t h, int i, const char** name, double* total_ms,
+                          int* launches, double* algo_bytes);
+int sift_hip_timing_reset(sift_hip_t h);
+
+/* Debug/parity accessors (tests): Gaussian plane (octave, layer) as w*h floats;
+ * pre-refinement candidates as (octave, layer, r, c) int quadruples. */
+int sift_hip_debug_gaussian(sift_hip_t h, int octave, int layer, float* out);
+int sift_hip_debug_candidates(sift_hip_t h, int* quads, int cap, int* count);
+
+/* --- Brute-force matcher (replaces sift_cuda::matchBruteForce, Match.cuh:9-25) */
+
+/* Scratch for up to max_query x max_train per pair and max_pairs pairs. */
+int sift_hip_matcher_create(int device, int max_query, int max_train, int max_pairs,
+                            sift_hip_matcher_t* out);
+int sift_hip_matcher_destroy(sift_hip_matcher_t m);
+
+/* Top-2 L2 neighbours of each query row in train, 128-D half descriptors in
+ * device memory.  Outputs (device, may be NULL): idx2[2*i+{0,1}] (-1 if none),
+ * d2[2*i+{0,1}] squared L2 distance (exact for integer descriptors).
+ * match[i] = idx2[2i] if d2[2i] < ratio^2 * d2[2i+1] (ratio on distances,
+ * ratio_on_squared = 0) or d2[2i] < ratio * d2[2i+1] (ratio_on_squared = 1, the
+ * reference's Match.cu:172 convention), else -1; a query with one train row
+ * matches it.  Enqueued on `stream`. */
+int sift_hip_match_device(sift_hip_matcher_t m, const uint16_t* query, int nq,
+                          const uint16_t* train, int nt, float ratio, int ratio_on_squared,
+                          int* idx2, float* d2, int* match, void* stream);
+
+/* P independent (query_p, train_p) pairs in ONE launch (8-way cross-GPU match).
+ * Arrays of P device pointers / counts live in host memory; outputs are packed
+ * per pair at offset sum_{q<p} nq[q]. */
+int sift_hip_match_batched(sift_hip_matcher_t m, int P, const uint16_t* const* query,
+                           const int* nq, const uint16_t* const* train, const int* nt,
+                           float ratio, int ratio_on_squared, int* idx2, float* d2,
+                           int* match, void* stream);
+
+/* matchBruteForce(des, num_des, src, num_src) (Match.cu:8-33): synchronous,
+ * result to host memory out[nq]. */
+int sift_hip_match_host(sift_hip_matcher_t m, const uint16_t* query, int nq,
+                        const uint16_t* train, int nt, float ratio, int ratio_on_squared,
+                        int* out);
+
+/* --- Utilities -------------------------------------------------------------- */
+
+/* Deterministic synthetic frame, fp32 0..255 integers. */
+int sift_synth_frame(unsigned frame_index, int w, int h, float* out);
+
+/* Device helpers for callers without a HIP toolchain (ctypes tests/bench). */
+int sift_hip_device_count(int* n);
+int sift_hip_malloc(void** p, size_t bytes);
+int sift_hip_free(void* p);
+int sift_hip_memcpy_h2d(void* dst, const void* src, size_t bytes);
+int sift_hip_memcpy_d2h(void* dst, const void* src, size_t bytes);
+int sift_hip_device_sync(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,156 @@
+"""ctypes binding of the CPU oracle (oracle/_build/libsift_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, always as the checker / baseline, never as the
+thing measured or shipped.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_LIB = os.path.join(ORACLE_DIR, "_build", "libsift_oracle.so")
+
+
+class Params(ctypes.Structure):
+    _fields_ = [
+        ("nfeatures", ctypes.c_int),
+        ("nOctaveLayers", ctypes.c_int),
+        ("contrastThreshold", ctypes.c_double),
+        ("edgeThreshold", ctypes.c_double),
+        ("sigma", ctypes.c_double),
+        ("firstOctave", ctypes.c_int),
+        ("nOctaves", ctypes.c_int),
+    ]
+
+
+class Kpt(ctypes.Structure):
+    _fields_ = [
+        ("x", ctypes.c_float),
+        ("y", ctypes.c_float),
+        ("size", ctypes.c_float),
+        ("angle", ctypes.c_float),
+        ("response", ctypes.c_float),
+        ("octave", ctypes.c_int),
+    ]
+
+
+KPT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"), ("octave", "<i4")])
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_LIB):
+            subprocess.run(["make", "-C", ORACLE_DIR], check=True, capture_output=True)
+        L = ctypes.CDLL(ORACLE_LIB)
+        vp, i, l, d = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_double
+        P = ctypes.POINTER(Params)
+        L.sift_oracle_default_params.argtypes = [P]
+        L.sift_oracle_gaussian_taps.argtypes = [d, vp, i]
+        L.sift_oracle_gaussian_taps.restype = i
+        L.sift_oracle_num_octaves.argtypes = [i, i, P]
+        L.sift_oracle_num_octaves.restype = i
+        L.sift_oracle_octave_dims.argtypes = [i, i, P, i, ctypes.POINTER(i), ctypes.POINTER(i)]
+        L.sift_oracle_gaussian_pyramid.argtypes = [vp, i, i, P, vp]
+        L.sift_oracle_gaussian_pyramid.restype = l
+        L.sift_oracle_extrema.argtypes = [vp, i, i, P, vp, l]
+        L.sift_oracle_extrema.restype = l
+        L.sift_oracle_detect_and_compute.argtypes = [vp, i, i, P, i, vp, vp, l]
+        L.sift_oracle_detect_and_compute.restype = l
+        L.sift_oracle_compute_descriptors.argtypes = [vp, i, i, P, vp, l, vp]
+        L.sift_oracle_knn2.argtypes = [vp, l, vp, l, i, vp, vp]
+        _lib = L
+    return _lib
+
+
+def params(nfeatures=0, nOctaveLayers=3, contrastThreshold=0.04, edgeThreshold=10.0, sigma=1.6, firstOctave=-1, nOctaves=0) -> Params:
+    p = Params()
+    lib().sift_oracle_default_params(ctypes.byref(p))
+    p.nfeatures, p.nOctaveLayers, p.contrastThreshold = nfeatures, nOctaveLayers, contrastThreshold
+    p.edgeThreshold, p.sigma, p.firstOctave, p.nOctaves = edgeThreshold, sigma, firstOctave, nOctaves
+    return p
+
+
+def from_config(cfg) -> Params:
+    """Oracle parameters equivalent to a sift_amd.CudaSiftConfig."""
+    return params(cfg.numFeatures, cfg.numOctaveLayers, cfg.contrastThreshould, cfg.edgeThreshould, cfg.sigma,
+                  -1 if cfg.upscale else 0, cfg.numOctaves)
+
+
+def gaussian_taps(sigma: float) -> np.ndarray:
+    buf = np.zeros(128, np.float32)
+    n = lib().sift_oracle_gaussian_taps(sigma, buf.ctypes.data, 128)
+    return buf[:n].copy()
+
+
+def num_octaves(w: int, h: int, p: Params) -> int:
+    return lib().sift_oracle_num_octaves(w, h, ctypes.byref(p))
+
+
+def octave_dims(w: int, h: int, p: Params, o: int):
+    ow, oh = ctypes.c_int(), ctypes.c_int()
+    lib().sift_oracle_octave_dims(w, h, ctypes.byref(p), o, ctypes.byref(ow), ctypes.byref(oh))
+    return ow.value, oh.value
+
+
+def gaussian_pyramid(img: np.ndarray, p: Params):
+    """List (per octave) of arrays (L+3, oh, ow)."""
+    img = np.ascontiguousarray(img, np.float32)
+    h, w = img.shape
+    n = lib().sift_oracle_gaussian_pyramid(img.ctypes.data, w, h, ctypes.byref(p), None)
+    buf = np.zeros(n, np.float32)
+    lib().sift_oracle_gaussian_pyramid(img.ctypes.data, w, h, ctypes.byref(p), buf.ctypes.data)
+    out, off = [], 0
+    L = p.nOctaveLayers
+    for o in range(num_octaves(w, h, p)):
+        ow, oh = octave_dims(w, h, p, o)
+        cnt = ow * oh * (L + 3)
+        out.append(buf[off:off + cnt].reshape(L + 3, oh, ow))
+        off += cnt
+    return out
+
+
+def extrema(img: np.ndarray, p: Params) -> np.ndarray:
+    img = np.ascontiguousarray(img, np.float32)
+    h, w = img.shape
+    n = lib().sift_oracle_extrema(img.ctypes.data, w, h, ctypes.byref(p), None, 0)
+    q = np.zeros((max(n, 1), 4), np.int32)
+    lib().sift_oracle_extrema(img.ctypes.data, w, h, ctypes.byref(p), q.ctypes.data, n)
+    return q[:n]
+
+
+def detect_and_compute(img: np.ndarray, p: Params, threads: int = 0, cap: int = 1 << 20):
+    """(keypoints structured array, descriptors float32 (n,128) of 0..255 integers)."""
+    img = np.ascontiguousarray(img, np.float32)
+    h, w = img.shape
+    kp = np.zeros(cap, KPT_DTYPE)
+    desc = np.zeros((cap, 128), np.float32)
+    n = lib().sift_oracle_detect_and_compute(img.ctypes.data, w, h, ctypes.byref(p), threads, kp.ctypes.data, desc.ctypes.data, cap)
+    n = min(n, cap)
+    return kp[:n].copy(), desc[:n].copy()
+
+
+def compute_descriptors(img: np.ndarray, p: Params, kpts: np.ndarray) -> np.ndarray:
+    img = np.ascontiguousarray(img, np.float32)
+    h, w = img.shape
+    k = np.ascontiguousarray(kpts.astype(KPT_DTYPE))
+    desc = np.zeros((len(k), 128), np.float32)
+    lib().sift_oracle_compute_descriptors(img.ctypes.data, w, h, ctypes.byref(p), k.ctypes.data, len(k), desc.ctypes.data)
+    return desc
+
+
+def knn2(query: np.ndarray, train: np.ndarray, threads: int = 0):
+    q = np.ascontiguousarray(query, np.float32)
+    t = np.ascontiguousarray(train, np.float32)
+    idx = np.zeros((len(q), 2), np.int32)
+    dist = np.zeros((len(q), 2), np.float32)
+    lib().sift_oracle_knn2(q.ctypes.data, len(q), t.ctypes.data, len(t), threads, idx.ctypes.data, dist.ctypes.data)
+    return idx, dist

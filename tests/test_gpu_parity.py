@@ -1,0 +1,223 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bar (tests/README in DESIGN.md "Parity"):
+  * Gaussian planes, 3x3x3 candidates, keypoints (x, y, size, angle, response,
+    packed octave): bit-exact, compared as sets (both sides sorted).
+  * Descriptors: |gpu - oracle| <= 1 per element (the 360-bin trilinear histogram
+    is summed in a different order), and >= 99.5 % of elements exact.
+  * Matcher: top-2 indices and squared distances exact (integer descriptors).
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def make_detector(sift, w, h, **kw):
+    cfg = sift.CudaSiftConfig(col_width=w, row_width=h, **kw)
+    det = sift.Detector(cfg)
+    det.gpuWarmUpAndAllocate()
+    return cfg, det
+
+
+def gpu_keypoints(det):
+    det.copyToHost(True)
+    k, f = det.final_kpts, det.final_features
+    out = np.zeros(det.total_size, [("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"), ("octave", "<i4")])
+    out["x"], out["y"], out["size"] = k[:, 0], k[:, 1], f[:, 1]
+    out["angle"], out["response"], out["octave"] = f[:, 3], f[:, 2], f[:, 0].astype(np.int64).astype(np.int32)
+    return out, det.descriptors.astype(np.float32), k[:, 2]
+
+
+def sort_keys(k):
+    return np.lexsort((k["octave"], k["response"], k["angle"], k["size"], k["y"], k["x"]))
+
+
+def assert_same_keypoints(gk, ok):
+    assert len(gk) == len(ok), f"keypoint count gpu={len(gk)} oracle={len(ok)}"
+    gs, os_ = gk[sort_keys(gk)], ok[sort_keys(ok)]
+    for f in ("x", "y", "size", "angle", "response"):
+        a, b = gs[f].view(np.uint32), os_[f].view(np.uint32)
+        bad = np.nonzero(a != b)[0]
+        assert len(bad) == 0, f"field {f}: {len(bad)} mismatches, first gpu={gs[bad[:3]]} oracle={os_[bad[:3]]}"
+    assert np.array_equal(gs["octave"], os_["octave"])
+
+
+CONFIGS = [
+    # (w, h, upscale, numOctaves, numFeatures, frame)
+    (256, 256, False, 0, 0, 1),
+    (257, 191, True, 0, 0, 2),       # ragged, doubled base (OpenCV default firstOctave -1)
+    (752, 480, False, 3, 5000, 0),   # BASELINE C2 shape family: 3 octaves
+    (640, 360, True, 0, 300, 3),     # retainBest active
+]
+
+
+@pytest.mark.parametrize("w,h,upscale,nOct,nfeat,frame", CONFIGS)
+def test_pyramid_bitexact(sift, oracle, w, h, upscale, nOct, nfeat, frame):
+    img = sift.synth_frame(frame, w, h)
+    cfg, det = make_detector(sift, w, h, upscale=upscale, numOctaves=nOct, numFeatures=nfeat)
+    det.detectAndCompute(img)
+    pyr = oracle.gaussian_pyramid(img, oracle.from_config(cfg))
+    assert det.nOctaves == len(pyr)
+    for o, planes in enumerate(pyr):
+        for layer in range(planes.shape[0]):
+            g = det.debug_gaussian(o, layer)
+            assert g.shape == planes[layer].shape
+            bad = np.count_nonzero(g.view(np.uint32) != planes[layer].view(np.uint32))
+            assert bad == 0, f"octave {o} layer {layer}: {bad} pixels differ (max |d| {np.abs(g - planes[layer]).max()})"
+
+
+@pytest.mark.parametrize("w,h,upscale,nOct,nfeat,frame", CONFIGS)
+def test_candidates_exact(sift, oracle, w, h, upscale, nOct, nfeat, frame):
+    img = sift.synth_frame(frame, w, h)
+    cfg, det = make_detector(sift, w, h, upscale=upscale, numOctaves=nOct, numFeatures=nfeat)
+    det.detectAndCompute(img)
+    g = det.debug_candidates()
+    o = oracle.extrema(img, oracle.from_config(cfg))
+    g = g[np.lexsort(g.T[::-1])]
+    o = o[np.lexsort(o.T[::-1])]
+    assert g.shape == o.shape, f"candidates gpu={len(g)} oracle={len(o)}"
+    assert np.array_equal(g, o)
+
+
+@pytest.mark.parametrize("w,h,upscale,nOct,nfeat,frame", CONFIGS)
+def test_keypoints_and_descriptors(sift, oracle, w, h, upscale, nOct, nfeat, frame):
+    img = sift.synth_frame(frame, w, h)
+    cfg, det = make_detector(sift, w, h, upscale=upscale, numOctaves=nOct, numFeatures=nfeat)
+    det.detectAndCompute(img)
+    assert det.overflow_flags() == 0
+    gk, gd, layer = gpu_keypoints(det)
+    ok, od = oracle.detect_and_compute(img, oracle.from_config(cfg))
+    assert len(ok) > 20, "fixture too small to be meaningful"
+    assert_same_keypoints(gk, ok)
+    assert np.array_equal(layer.astype(np.int32), (gk["octave"] >> 8) & 255)
+    gi, oi = sort_keys(gk), sort_keys(ok)
+    diff = np.abs(gd[gi] - od[oi])
+    assert diff.max() <= 1.0, f"descriptor max |diff| {diff.max()}"
+    assert (diff == 0).mean() >= 0.995, f"exact fraction {(diff == 0).mean()}"
+    assert gd.min() >= 0 and gd.max() <= 255 and np.all(gd == np.round(gd))
+
+
+def test_output_order_deterministic(sift):
+    w, h = 640, 480
+    img = sift.synth_frame(11, w, h)
+    _, det = make_detector(sift, w, h, upscale=True)
+    runs = []
+    for _ in range(3):
+        det.detectAndCompute(img)
+        k, d, _ = gpu_keypoints(det)
+        runs.append((k.copy(), d.copy()))
+    for k, d in runs[1:]:
+        assert np.array_equal(k, runs[0][0]) and np.array_equal(d, runs[0][1])
+
+
+def test_prev_descriptor_is_previous_frame(sift):
+    w, h = 320, 240
+    _, det = make_detector(sift, w, h)
+    det.detectAndCompute(sift.synth_frame(4, w, h))
+    det.copyToHost(True)
+    first, n1 = det.descriptors.copy(), det.total_size
+    det.detectAndCompute(sift.synth_frame(5, w, h))
+    assert det.prev_size == n1
+    prev = sift.DeviceArray(0)
+    got = np.empty((n1, 128), np.uint16)
+    sift._check(sift.lib().sift_hip_memcpy_d2h(got.ctypes.data, det.prev_descriptor.data(), got.nbytes), "d2h")
+    assert np.array_equal(got.view(np.float16), first)
+    del prev
+
+
+def test_blank_and_tiny_images(sift, oracle):
+    for (w, h, up) in [(64, 48, False), (33, 17, True), (128, 128, False)]:
+        img = np.full((h, w), 128.0, np.float32)
+        cfg, det = make_detector(sift, w, h, upscale=up)
+        det.detectAndCompute(img)
+        assert det.total_size == 0
+        img = sift.synth_frame(9, w, h)
+        det.detectAndCompute(img)
+        gk, _, _ = gpu_keypoints(det)
+        ok, _ = oracle.detect_and_compute(img, oracle.from_config(cfg))
+        assert_same_keypoints(gk, ok)
+
+
+def test_size_mismatch_rejected(sift):
+    _, det = make_detector(sift, 64, 64)
+    with pytest.raises(sift.SiftHipError):
+        det.detectAndCompute(np.zeros((65, 64), np.float32))
+
+
+def _half_rows(a):
+    return np.ascontiguousarray(a.astype(np.float16))
+
+
+@pytest.mark.parametrize("nq,nt", [(1, 1), (37, 5), (2000, 2000), (513, 1999), (64, 3000)])
+def test_matcher_exact(sift, oracle, nq, nt):
+    rng = np.random.default_rng(nq * 7919 + nt)
+    q = rng.integers(0, 256, (nq, 128)).astype(np.float32)
+    t = rng.integers(0, 256, (nt, 128)).astype(np.float32)
+    if nt > 4:
+        t[3] = t[1]  # exact tie: lower index must win
+        q[0] = t[1]
+    dq, dt = sift.DeviceArray.from_numpy(_half_rows(q)), sift.DeviceArray.from_numpy(_half_rows(t))
+    idx2, d2, mt = sift.DeviceArray(nq * 8), sift.DeviceArray(nq * 8), sift.DeviceArray(nq * 4)
+    m = sift.Matcher(nq, nt)
+    m.match_device(dq.value, nq, dt.value, nt, 0.8, False, idx2.value, d2.value, mt.value)
+    gi = idx2.to_numpy(np.int32, (nq, 2))
+    gd = d2.to_numpy(np.float32, (nq, 2))
+    gm = mt.to_numpy(np.int32, (nq,))
+    oi, od = oracle.knn2(q, t)
+    assert np.array_equal(gi, oi)
+    valid = oi >= 0
+    assert np.array_equal(np.sqrt(gd[valid]).astype(np.float32), od[valid])
+    exp = np.where(oi[:, 1] < 0, oi[:, 0], np.where(od[:, 0] < 0.8 * od[:, 1], oi[:, 0], -1))
+    assert np.array_equal(gm, exp)
+
+
+def test_match_batched_equals_pairs(sift, oracle):
+    rng = np.random.default_rng(5)
+    sets = [rng.integers(0, 256, (n, 128)).astype(np.float32) for n in (300, 257, 64, 500)]
+    dev = [sift.DeviceArray.from_numpy(_half_rows(s)) for s in sets]
+    pairs = [(i, j) for i in range(4) for j in range(4) if i != j]
+    nq = [len(sets[i]) for i, _ in pairs]
+    tot = sum(nq)
+    idx2 = sift.DeviceArray(tot * 8)
+    m = sift.Matcher(max(nq), 500, max_pairs=len(pairs))
+    m.match_batched([dev[i].value for i, _ in pairs], nq, [dev[j].value for _, j in pairs], [len(sets[j]) for _, j in pairs],
+                    idx2_ptr=idx2.value)
+    gi = idx2.to_numpy(np.int32, (tot, 2))
+    off = 0
+    for (i, j), n in zip(pairs, nq):
+        oi, _ = oracle.knn2(sets[i], sets[j])
+        assert np.array_equal(gi[off:off + n], oi), (i, j)
+        off += n
+
+
+def test_match_brute_force_dropin(sift):
+    """Reference call pattern: match prev_descriptor against device_descriptor."""
+    w, h = 400, 300
+    big = sift.synth_frame(21, w + 8, h + 8)
+    _, det = make_detector(sift, w, h, numFeatures=2000)
+    det.detectAndCompute(big[:h, :w])
+    det.copyToHost(False)
+    k0, n0 = det.final_kpts.copy(), det.total_size
+    det.detectAndCompute(big[4:4 + h, 6:6 + w])
+    det.copyToHost(False)
+    m = sift.matchBruteForce(det.prev_descriptor, n0, det.device_descriptor, det.total_size)
+    good = m >= 0
+    assert good.sum() > 0.3 * n0
+    d = k0[good, :2] - det.final_kpts[m[good], :2] - np.array([6, 4], np.float32)
+    assert (np.abs(d).max(axis=1) < 1.5).mean() > 0.9
+
+
+def test_cpp_tools(sift):
+    lib = os.path.join(ROOT, "another-cuda-sift_amd", "lib")
+    r = subprocess.run([os.path.join(lib, "detection_example"), "--width", "752", "--height", "480", "--iters", "3"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "keypoints" in r.stdout
+    r = subprocess.run([os.path.join(lib, "extract_and_match_example"), "--frames", "3"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr

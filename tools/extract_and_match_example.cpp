@@ -1,0 +1,63 @@
+// Mirrors /root/reference/tool/extract_and_match_example.cc:38-105: detect on
+// consecutive frames and match each frame against the previous one through
+// Detector::prev_descriptor + matchBruteForce.  Frames: a synthetic frame and
+// copies shifted by (k*dx, k*dy) pixels, so good matches must agree with the shift.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+
+#include "sift_cuda/Detector.hh"
+#include "sift_hip.h"
+
+int main(int argc, char** argv) {
+    int W = 752, H = 480, frames = 4, dx = 3, dy = 2;
+    for (int i = 1; i < argc; i++) {
+        std::string a = argv[i];
+        if (a == "--width" && i + 1 < argc) W = std::atoi(argv[++i]);
+        else if (a == "--height" && i + 1 < argc) H = std::atoi(argv[++i]);
+        else if (a == "--frames" && i + 1 < argc) frames = std::atoi(argv[++i]);
+    }
+    const int PW = W + frames * dx, PH = H + frames * dy;
+    std::vector<float> big((size_t)PW * PH);
+    sift_synth_frame(7, PW, PH, big.data());
+
+    CudaSiftConfig config;
+    config.upscale = false;
+    config.numFeatures = 2000;
+    config.col_width = W;
+    config.row_width = H;
+    sift_cuda::Detector detector(config);
+    detector.gpuWarmUpAndAllocate();
+    int prev_size = 0;
+    std::vector<sift_cuda::Float3> prev_kpts;
+    int failures = 0;
+    for (int f = 0; f < frames; f++) {
+        Imagef img(H, W);
+        for (int y = 0; y < H; y++)
+            for (int x = 0; x < W; x++) img.at(y, x) = big[(size_t)(y + f * dy) * PW + x + f * dx];
+        detector.detectAndCompute(img);
+        detector.copyToHost(false);
+        const int curr_size = detector.total_size;
+        if (f > 0) {
+            const auto matches = sift_cuda::matchBruteForce(detector.prev_descriptor, prev_size,
+                                                            detector.device_descriptor, curr_size);
+            int good = 0, consistent = 0;
+            for (int i = 0; i < prev_size; i++) {
+                if (matches[i] < 0) continue;
+                good++;
+                const auto& a = prev_kpts[i];
+                const auto& b = detector.final_kpts[matches[i]];
+                if (std::fabs((a.x - dx) - b.x) < 1.5f && std::fabs((a.y - dy) - b.y) < 1.5f) consistent++;
+            }
+            std::printf("frame %d: %d kpts, %d matches, %d consistent with the (%d,%d) shift\n", f, curr_size, good,
+                        consistent, -dx, -dy);
+            if (good == 0 || consistent * 10 < good * 8) failures++;
+        } else {
+            std::printf("frame 0: %d kpts\n", curr_size);
+        }
+        prev_size = curr_size;
+        prev_kpts = detector.final_kpts;
+    }
+    return failures ? 2 : 0;
+}
