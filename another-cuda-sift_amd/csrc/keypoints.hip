@@ -563,14 +563,14 @@ __global__ __launch_bounds__(256) void k_descriptor(PyrDesc pyr, const OriKpt* _
             for (int k = 0; k < 128; k++) acc8[k & 7] = __fmaf_rn(raw[k], raw[k], acc8[k & 7]);
             const float t0 = acc8[0] + acc8[4], t1 = acc8[1] + acc8[5], t2 = acc8[2] + acc8[6], t3 = acc8[3] + acc8[7];
             float nrm2 = (t0 + t2) + (t1 + t3);
-            const float thr = __fsqrt_rn(nrm2) * 0.2f;
+            const float thr = __builtin_sqrtf(nrm2) * 0.2f;
             nrm2 = 0.f;
             for (int k = 0; k < 128; k++) {
                 const float val = fminf(raw[k], thr);
                 raw[k] = val;
                 nrm2 = nrm2 + val * val;
             }
-            s_nrm = 512.f / fmaxf(__fsqrt_rn(nrm2), FLT_EPSILON);
+            s_nrm = 512.f / fmaxf(__builtin_sqrtf(nrm2), FLT_EPSILON);
             float* k3 = kpts3 + 3 * (size_t)p;
             k3[0] = kpt.x;
             k3[1] = kpt.y;

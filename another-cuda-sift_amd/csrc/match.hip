@@ -191,7 +191,7 @@ __global__ __launch_bounds__(256) void k_match_merge(MatchBatch batch, int S, in
             else if (ratio_on_squared)
                 m = e1 < ratio * e2 ? i1 : -1;
             else
-                m = __fsqrt_rn(e1) < ratio * __fsqrt_rn(e2) ? i1 : -1;
+                m = __builtin_sqrtf(e1) < ratio * __builtin_sqrtf(e2) ? i1 : -1;
         }
         match[o] = m;
     }

@@ -60,8 +60,9 @@ __device__ __forceinline__ float cv_fast_atan2(float y, float x) {
     return a;
 }
 
-// hal::magnitude32f SIMD body.
-__device__ __forceinline__ float cv_magnitude(float x, float y) { return __fsqrt_rn(__fmaf_rn(x, x, y * y)); }
+// hal::magnitude32f SIMD body.  NB: __fsqrt_rn lowers to a bare v_sqrt_f32
+// (~1 ulp) on gfx950; __builtin_sqrtf is the correctly rounded expansion.
+__device__ __forceinline__ float cv_magnitude(float x, float y) { return __builtin_sqrtf(__fmaf_rn(x, x, y * y)); }
 
 __device__ __forceinline__ int cv_round(float v) { return (int)__builtin_rintf(v); }
 __device__ __forceinline__ int cv_floor(float v) { return (int)floorf(v); }
