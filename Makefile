@@ -18,7 +18,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
             -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -I$(SRC) -Wall -Wno-unused-result
 CXXFLAGS := -O2 -std=c++17 -fPIC -Iinclude -Wall -Wextra
 
-HIP_SRCS := $(SRC)/detector.hip $(SRC)/pyramid.hip $(SRC)/keypoints.hip $(SRC)/match.hip
+HIP_SRCS := $(SRC)/detector.hip $(SRC)/pyramid.hip $(SRC)/keypoints.hip $(SRC)/descriptor.hip $(SRC)/match.hip
 HIP_OBJS := $(patsubst $(SRC)/%.hip,$(OUT)/obj/%.o,$(HIP_SRCS)) $(OUT)/obj/synth_frame.o
 
 all: $(OUT)/libsift_hip.so $(OUT)/libsift_cuda.so tools

@@ -248,6 +248,14 @@ void setup_taps(sift_hip_detector* d) {
     d->kp.capRefined = 1u << 18;
     d->kp.capOriented = 1u << 19;
     d->kp.capFinal = (unsigned)(d->cfg.maxKeypoints > 0 ? d->cfg.maxKeypoints : 65536);
+    // LDS patch bounds: scl_octv = sigma * 2^((layer + xi) / L) <= sigma * 2^((L + 0.5) / L).
+    // Larger radii (not reachable from accepted keypoints) fall back to HBM reads.
+    const double sclMax = d->cfg.sigma * std::pow(2.0, (L + 0.5) / L);
+    d->kp.oriRmax = (int)lrint(4.5 * sclMax) + 1;
+    d->kp.descRmax = std::min((int)lrint(3.0 * sclMax * 1.4142135623730951 * 2.5) + 1, 60);
+    // Valid descriptor samples lie in a rotated square of side 5 * hist_width.
+    const double hw = 3.0 * sclMax;
+    d->kp.descNrec = std::min((int)std::ceil((5.0 * hw + 3.0) * (5.0 * hw + 3.0)), 8192);
 }
 
 void upload_exp_tab() {
@@ -255,6 +263,7 @@ void upload_exp_tab() {
     float tab[64];
     for (int j = 0; j < 64; j++) tab[j] = (float)(std::exp2((double)j / 64.0) * A0);
     upload_exp_table(tab);
+    upload_exp_table_desc(tab);
 }
 
 template <class T>

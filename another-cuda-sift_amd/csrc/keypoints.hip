@@ -30,6 +30,33 @@ constexpr float kOriPeakRatio = 0.8f;
 
 __device__ __forceinline__ const OctGeom& octave_geom(const PyrDesc& pyr, int o) { return pyr.oct[o]; }
 
+// Copy a ps x ps window (origin py0, px0) of a plane into LDS, zero outside the
+// image.  Each of the nt participating lanes has U independent loads in flight
+// before its first LDS store: one memory latency per U elements, not per element.
+template <int U>
+__device__ __forceinline__ void stage_patch(float* patch, const float* img, int pitch, int W, int H, int py0, int px0,
+                                            int ps, int t, int nt) {
+    const int total = ps * ps;
+    for (int base = t; base < total; base += nt * U) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int idx = base + nt * u;
+            const int yy = py0 + idx / ps, xx = px0 + idx % ps;
+            const bool in = idx < total && yy >= 0 && yy < H && xx >= 0 && xx < W;
+            // Unconditional load from a clamped address, then select: a guarded
+            // load would make hipcc branch + vmcnt(0) per element (serial latency).
+            const float x = img[(size_t)min(max(yy, 0), H - 1) * pitch + min(max(xx, 0), W - 1)];
+            v[u] = in ? x : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int idx = base + nt * u;
+            if (idx < total) patch[idx] = v[u];
+        }
+    }
+}
+
 __device__ __forceinline__ float dog_at(const float* g, long ps, int pitch, int layer, int r, int c) {
     const float* p = g + (size_t)r * pitch + c;
     return p[(size_t)(layer + 1) * ps] - p[(size_t)layer * ps];
@@ -170,18 +197,23 @@ void launch_refine(const PyrDesc& pyr, const uint2* cand, unsigned capCand, Coun
 
 // ---------------------------------------------------------------------------
 // calcOrientationHist + peak search (OpenCV 4.x sift.simd.hpp), one wave64 per
-// refined keypoint, on the Gaussian plane of the refined layer.  Samples are
-// produced 64 at a time in raster order; lane b (< 36) owns histogram bin b and
-// adds the chunk's contributions in lane order, so every bin sees exactly the
-// oracle's sequential summation order (adding +0.f for non-matching samples is
-// exact).  Smoothing, max and peak interpolation use wave shuffles.
+// refined keypoint, on the Gaussian plane of the refined layer.  The wave first
+// stages its (2R+3)^2 patch in LDS (one burst of independent loads), then
+// produces samples 64 at a time in raster order; lane b (< 36) owns histogram
+// bin b and adds the chunk's contributions in lane order, so every bin sees
+// exactly the oracle's sequential summation order (adding +0.f for
+// non-matching samples is exact).  Smoothing, max and peak interpolation use
+// wave shuffles.  Radii above the host-computed bound read HBM directly.
 // Reference: SiftOps.cu:237-376 (DoG plane, 32-lane LDS atomics, floor bins,
 // no interpolation, SURVEY A-9).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_orientation(PyrDesc pyr, const RefKpt* __restrict__ in,
                                                      Counters* __restrict__ ctr, OriKpt* __restrict__ out,
                                                      KeypointParams kp) {
+    extern __shared__ float lds_ori[];
     const int lane = threadIdx.x & 63;
+    const int PSMAX = 2 * kp.oriRmax + 3;
+    float* patch = lds_ori + (threadIdx.x >> 6) * PSMAX * PSMAX;
     const unsigned wave = blockIdx.x * 4 + (threadIdx.x >> 6);
     const unsigned nwaves = gridDim.x * 4;
     const unsigned n = min(ctr->refined, kp.capRefined);
@@ -197,6 +229,14 @@ __global__ __launch_bounds__(256) void k_orientation(PyrDesc pyr, const RefKpt* 
         const float sigma = kOriSigFctr * scl_octv;
         const float expf_scale = -1.f / (2.f * sigma * sigma);
         const int side = 2 * radius + 1, total = side * side;
+        const bool staged = radius <= kp.oriRmax;
+        const int ps = side + 2, py0 = r - radius - 1, px0 = c - radius - 1;
+        if (staged) {
+            stage_patch<8>(patch, img, pitch, W, H, py0, px0, ps, lane, 64);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
 
         float acc = 0.f;
         for (int base = 0; base < total; base += 64) {
@@ -207,9 +247,16 @@ __global__ __launch_bounds__(256) void k_orientation(PyrDesc pyr, const RefKpt* 
                 const int i = idx / side - radius, j = idx - (idx / side) * side - radius;
                 const int y = r + i, x = c + j;
                 if (y > 0 && y < H - 1 && x > 0 && x < W - 1) {
-                    const float* p = img + (size_t)y * pitch + x;
-                    const float dx = p[1] - p[-1];
-                    const float dy = p[-pitch] - p[pitch];
+                    float dx, dy;
+                    if (staged) {
+                        const float* p = patch + (y - py0) * ps + (x - px0);
+                        dx = p[1] - p[-1];
+                        dy = p[-ps] - p[ps];
+                    } else {
+                        const float* p = img + (size_t)y * pitch + x;
+                        dx = p[1] - p[-1];
+                        dy = p[-pitch] - p[pitch];
+                    }
                     const float w = cv_exp32f((float)(i * i + j * j) * expf_scale, c_exptab);
                     const float ori = cv_fast_atan2(dy, dx);
                     const float mag = cv_magnitude(dx, dy);
@@ -229,6 +276,8 @@ __global__ __launch_bounds__(256) void k_orientation(PyrDesc pyr, const RefKpt* 
                 }
             }
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
 
         // Circular [1 4 6 4 1]/16 smoothing (SIMD body, fma form).
         const int bl = lane < kOriBins ? lane : 0;
@@ -281,7 +330,8 @@ __global__ __launch_bounds__(256) void k_orientation(PyrDesc pyr, const RefKpt* 
 
 void launch_orientation(const PyrDesc& pyr, const RefKpt* in, Counters* ctr, OriKpt* out, const KeypointParams& kp,
                         hipStream_t s) {
-    hipLaunchKernelGGL(k_orientation, dim3(1024), dim3(256), 0, s, pyr, in, ctr, out, kp);
+    const int ps = 2 * kp.oriRmax + 3;
+    hipLaunchKernelGGL(k_orientation, dim3(1024), dim3(256), sizeof(float) * 4 * ps * ps, s, pyr, in, ctr, out, kp);
 }
 
 // ---------------------------------------------------------------------------
@@ -452,26 +502,34 @@ void launch_bucket_rank(const OriKpt* kpts, const unsigned* bcount, const unsign
     hipLaunchKernelGGL(k_bucket_rank, dim3(256), dim3(256), 0, s, kpts, bcount, boff, order, ctr, final_order, kp);
 }
 
+#if 0  // superseded by descriptor.hip (LDS float atomics were the bottleneck)
 // ---------------------------------------------------------------------------
 // calcSIFTDescriptor (OpenCV 4.x sift.simd.hpp), one 256-thread workgroup per
-// keypoint.  Samples of the (2R+1)^2 window are spread over the 4 waves; each
-// wave accumulates its trilinear contributions into a private LDS histogram
-// (6 x 6 x 10 bins), the 4 copies are summed in fixed order (deterministic
-// run to run), then wrap, L2 norm, 0.2 clip, renorm and x512 round to 0..255
-// exactly as the oracle.  Output layout is the reference's (Detector.hh:54-57).
-// Reference: SiftOps.cu:454-623 (modff bins, half(x512), SURVEY A-10).
+// keypoint.  The (2R+3)^2 patch around the keypoint is staged in LDS first.
+// Each thread walks a contiguous run of the (2R+1)^2 raster (so the 64 lanes of
+// a wave sit ~R/4 rows apart and their LDS atomics rarely collide); each wave
+// accumulates its trilinear contributions into a private LDS histogram (6 x 6
+// x 10 bins), the 4 copies are summed in fixed order (deterministic run to
+// run), then wrap, L2 norm (8 fma lanes + v_reduce_sum order), 0.2 clip,
+// renorm and x512 round to 0..255 exactly as the oracle.  Output layout is the
+// reference's (Detector.hh:54-57).
+// Reference: SiftOps.cu:454-623 (modff bins, half(x512), serial lane-0
+// normalisation, SURVEY A-10).
 // ---------------------------------------------------------------------------
 constexpr int kD = 4, kN = 8;
 constexpr int kHistLen = (kD + 2) * (kD + 2) * (kN + 2);  // 360
+constexpr int kHistStride = kHistLen + 8;
 
 __global__ __launch_bounds__(256) void k_descriptor(PyrDesc pyr, const OriKpt* __restrict__ kpts,
                                                     const int* __restrict__ final_order,
                                                     const Counters* __restrict__ ctr, float* __restrict__ kpts3,
                                                     float* __restrict__ feats4, uint16_t* __restrict__ desc,
                                                     KeypointParams kp) {
-    __shared__ float hist[4][kHistLen + 8];
-    __shared__ float raw[128];
-    __shared__ float s_nrm;
+    extern __shared__ float lds_desc[];
+    float* hist = lds_desc;                       // 4 x kHistStride
+    float* raw = hist + 4 * kHistStride;          // 128
+    float* nacc = raw + 128;                      // 8 + 1
+    float* patch = nacc + 16;                     // (2Rmax+3)^2
     const int tid = threadIdx.x, w = tid >> 6;
     const unsigned n = ctr->final_n;
     const int fo = pyr.firstOctave;
@@ -501,22 +559,35 @@ __global__ __launch_bounds__(256) void k_descriptor(PyrDesc pyr, const OriKpt* _
         radius = min(radius, (int)sqrt((double)cols * cols + (double)rows * rows));
         cos_t /= hist_width;
         sin_t /= hist_width;
-
-        for (int i = tid; i < 4 * (kHistLen + 8); i += 256) (&hist[0][0])[i] = 0.f;
-        __syncthreads();
-        float* hw = hist[w];
         const int side = 2 * radius + 1, total = side * side;
-        for (int idx = tid; idx < total; idx += 256) {
-            const int i = idx / side - radius, j = idx - (idx / side) * side - radius;
+        const bool staged = radius <= kp.descRmax;
+        const int ps = side + 2, py0 = pty - radius - 1, px0 = ptx - radius - 1;
+
+        for (int i = tid; i < 4 * kHistStride; i += 256) hist[i] = 0.f;
+        if (staged) stage_patch<16>(patch, img, pitch, cols, rows, py0, px0, ps, tid, 256);
+        __syncthreads();
+
+        float* hw = hist + w * kHistStride;
+        const int run = (total + 255) / 256;
+        const int k0 = tid * run, k1 = min(k0 + run, total);
+        int i = k0 / side - radius, j = k0 - (k0 / side) * side - radius;
+        for (int k = k0; k < k1; k++) {
             const float c_rot = (float)j * cos_t - (float)i * sin_t;
             const float r_rot = (float)j * sin_t + (float)i * cos_t;
             float rbin = r_rot + (float)(kD / 2) - 0.5f;
             float cbin = c_rot + (float)(kD / 2) - 0.5f;
             const int r = pty + i, c = ptx + j;
             if (rbin > -1 && rbin < kD && cbin > -1 && cbin < kD && r > 0 && r < rows - 1 && c > 0 && c < cols - 1) {
-                const float* pp = img + (size_t)r * pitch + c;
-                const float dx = pp[1] - pp[-1];
-                const float dy = pp[-pitch] - pp[pitch];
+                float dx, dy;
+                if (staged) {
+                    const float* pp = patch + (r - py0) * ps + (c - px0);
+                    dx = pp[1] - pp[-1];
+                    dy = pp[-ps] - pp[ps];
+                } else {
+                    const float* pp = img + (size_t)r * pitch + c;
+                    dx = pp[1] - pp[-1];
+                    dy = pp[-pitch] - pp[pitch];
+                }
                 const float wgt = cv_exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, c_exptab);
                 const float gori = cv_fast_atan2(dy, dx);
                 const float gmag = cv_magnitude(dx, dy);
@@ -546,31 +617,50 @@ __global__ __launch_bounds__(256) void k_descriptor(PyrDesc pyr, const OriKpt* _
                 atomicAdd(&hw[hidx + (kD + 3) * (kN + 2)], v_rco110);
                 atomicAdd(&hw[hidx + (kD + 3) * (kN + 2) + 1], v_rco111);
             }
+            if (++j > radius) {
+                j = -radius;
+                i++;
+            }
         }
         __syncthreads();
-        for (int b = tid; b < kHistLen; b += 256) hist[0][b] = ((hist[0][b] + hist[1][b]) + hist[2][b]) + hist[3][b];
-        __syncthreads();
         if (tid < 128) {
-            const int i = tid >> 5, j = (tid >> 3) & 3, k = tid & 7;
-            const int hidx = ((i + 1) * (kD + 2) + (j + 1)) * (kN + 2);
-            float v = hist[0][hidx + k];
-            if (k < 2) v = v + hist[0][hidx + kN + k];
+            // wrap the two extra orientation bins into bins 0 and 1, sum the 4 copies in fixed order
+            const int ii = tid >> 5, jj = (tid >> 3) & 3, kk = tid & 7;
+            const int hidx = ((ii + 1) * (kD + 2) + (jj + 1)) * (kN + 2) + kk;
+            float v = ((hist[hidx] + hist[kHistStride + hidx]) + hist[2 * kHistStride + hidx]) + hist[3 * kHistStride + hidx];
+            if (kk < 2) {
+                const int h2 = hidx + kN;
+                const float e = ((hist[h2] + hist[kHistStride + h2]) + hist[2 * kHistStride + h2]) + hist[3 * kHistStride + h2];
+                v = v + e;
+            }
             raw[tid] = v;
         }
         __syncthreads();
+        if (tid < 8) {
+            float a = 0.f;
+#pragma unroll
+            for (int q = 0; q < 16; q++) a = __fmaf_rn(raw[tid + 8 * q], raw[tid + 8 * q], a);
+            nacc[tid] = a;
+        }
+        __syncthreads();
         if (tid == 0) {
-            float acc8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            for (int k = 0; k < 128; k++) acc8[k & 7] = __fmaf_rn(raw[k], raw[k], acc8[k & 7]);
-            const float t0 = acc8[0] + acc8[4], t1 = acc8[1] + acc8[5], t2 = acc8[2] + acc8[6], t3 = acc8[3] + acc8[7];
+            const float t0 = nacc[0] + nacc[4], t1 = nacc[1] + nacc[5], t2 = nacc[2] + nacc[6], t3 = nacc[3] + nacc[7];
             float nrm2 = (t0 + t2) + (t1 + t3);
             const float thr = __builtin_sqrtf(nrm2) * 0.2f;
             nrm2 = 0.f;
-            for (int k = 0; k < 128; k++) {
-                const float val = fminf(raw[k], thr);
-                raw[k] = val;
-                nrm2 = nrm2 + val * val;
+#pragma unroll 1
+            for (int q0 = 0; q0 < 128; q0 += 8) {
+                float vals[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) vals[u] = raw[q0 + u];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const float val = fminf(vals[u], thr);
+                    raw[q0 + u] = val;
+                    nrm2 = nrm2 + val * val;
+                }
             }
-            s_nrm = 512.f / fmaxf(__builtin_sqrtf(nrm2), FLT_EPSILON);
+            nacc[8] = 512.f / fmaxf(__builtin_sqrtf(nrm2), FLT_EPSILON);
             float* k3 = kpts3 + 3 * (size_t)p;
             k3[0] = kpt.x;
             k3[1] = kpt.y;
@@ -584,7 +674,7 @@ __global__ __launch_bounds__(256) void k_descriptor(PyrDesc pyr, const OriKpt* _
         }
         __syncthreads();
         if (tid < 128) {
-            int v = cv_round(raw[tid] * s_nrm);
+            int v = cv_round(raw[tid] * nacc[8]);
             v = v < 0 ? 0 : (v > 255 ? 255 : v);
             const _Float16 hv = (_Float16)(float)v;
             desc[(size_t)p * 128 + tid] = __builtin_bit_cast(uint16_t, hv);
@@ -595,8 +685,12 @@ __global__ __launch_bounds__(256) void k_descriptor(PyrDesc pyr, const OriKpt* _
 
 void launch_descriptor(const PyrDesc& pyr, const OriKpt* kpts, const int* final_order, const Counters* ctr,
                        float* kpts3, float* feats4, uint16_t* desc, const KeypointParams& kp, hipStream_t s) {
-    hipLaunchKernelGGL(k_descriptor, dim3(2048), dim3(256), 0, s, pyr, kpts, final_order, ctr, kpts3, feats4, desc,
+    const int ps = 2 * kp.descRmax + 3;
+    const size_t lds = sizeof(float) * (4 * kHistStride + 128 + 16 + (size_t)ps * ps);
+    hipLaunchKernelGGL(k_descriptor, dim3(2048), dim3(256), lds, s, pyr, kpts, final_order, ctr, kpts3, feats4, desc,
                        kp);
 }
+
+#endif
 
 }  // namespace sift_amd

@@ -4,6 +4,9 @@
 // Semantics follow OpenCV 4.x; the float
 // operation order is the oracle's (oracle/sift_oracle.cpp gaussianBlur /
 // upsample2x / isExtremum), so planes and candidate lists are bit-exact.
+#include <array>
+#include <utility>
+
 #include "sift_kernels.h"
 #include "sift_math.h"
 
@@ -47,77 +50,140 @@ void launch_upsample2x(const float* src, int spitch, int W, int H, float* dst, i
 }
 
 // ---------------------------------------------------------------------------
-// Separable Gaussian blur, one 64 x 32 output tile per 256-thread workgroup.
-// The (32+2r) x (64+2r) input tile (reflect-101 borders, optional stride-2
-// read = INTER_NEAREST octave decimation fused in) is staged once in LDS; the
-// row pass writes a (32+2r) x 64 LDS tile; the column pass writes HBM.
-// Row:    s = 0; s = fma(in[x-r+k], w[k], s), k = 0..n-1   (n > 5)
-//         s = in[x]*w[r]; s = fma(in[x-k]+in[x+k], w[r+k], s)   (n <= 5)
-// Column: s = fma(mid[y], w[r], 0); s = fma(mid[y+k]+mid[y-k], w[r+k], s)
+// Separable Gaussian blur, one 64 x 32 output tile per 256-thread workgroup,
+// instantiated per radius R (taps 2R+1) so every tap loop is fully unrolled.
+// The (32+2R) x (64+2R) input tile (reflect-101 borders, optional stride-2
+// read = INTER_NEAREST octave decimation fused in) is staged once in LDS.
+// Row pass: 16 threads per row, each keeps a (2R+4)-float register window
+// (ds_read_b128) and runs 4 independent fma chains (4 adjacent outputs).
+// Column pass: one column per lane, 8 rows per thread, (2R+8)-float window.
+// Row:    s = 0; s = fma(in[x-R+k], w[k], s), k = 0..2R          (2R+1 > 5)
+//         s = in[x]*w[R]; s = fma(in[x-k]+in[x+k], w[R+k], s)      (2R+1 <= 5)
+// Column: s = fma(mid[y], w[R], 0); s = fma(mid[y+k]+mid[y-k], w[R+k], s)
 // Reference: Filter.cu:8-51 (no LDS, vertical first, modulo per tap).
 // ---------------------------------------------------------------------------
 constexpr int BLUR_TW = 64;
 constexpr int BLUR_TH = 32;
 
+template <int R>
 __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, int spitch, int sstep, int W, int H,
                                               float* __restrict__ dst, int dpitch, float* __restrict__ copy_out,
                                               Taps taps) {
-    extern __shared__ float lds[];
-    const int n = taps.n, r = n >> 1;
-    const int IW = BLUR_TW + 2 * r, IH = BLUR_TH + 2 * r;
-    float* in = lds;
-    float* mid = lds + IH * IW;
+    constexpr int IW = (BLUR_TW + 2 * R + 3) & ~3;  // row stride, multiple of 4 floats
+    constexpr int IH = BLUR_TH + 2 * R;
+    constexpr int NW = (2 * R + 4 + 3) / 4;          // float4 reads per row window
+    __shared__ __attribute__((aligned(16))) float in[IH * IW + 4];
+    __shared__ __attribute__((aligned(16))) float mid[IH * BLUR_TW];
     const int x0 = blockIdx.x * BLUR_TW, y0 = blockIdx.y * BLUR_TH;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
-    for (int ly = tid >> 6; ly < IH; ly += 4) {
-        const int gy = reflect101(y0 - r + ly, H);
-        const float* srow = src + (size_t)gy * sstep * spitch;
-        for (int lx = tid & 63; lx < IW; lx += 64) {
-            const int gx = reflect101(x0 - r + lx, W);
-            in[ly * IW + lx] = srow[(size_t)gx * sstep];
+    // Stage the input tile: every thread issues all of its loads before its
+    // first LDS store (one memory latency per workgroup, not one per row).
+    {
+        constexpr int RW = BLUR_TW + 2 * R;
+        constexpr int TOTAL = IH * RW;
+        constexpr int PER = (TOTAL + 255) / 256;
+        const bool single = W > R + 1 && H > R + 1;  // one reflection suffices
+        float v[PER];
+#pragma unroll
+        for (int u = 0; u < PER; u++) {
+            const int idx = tid + 256 * u;
+            const int ly = min(idx / RW, IH - 1), lx = idx - (idx / RW) * RW;
+            int gy = y0 - R + ly, gx = x0 - R + lx;
+            if (single) {
+                // One bounce is exact for every input of an in-image output
+                // (|offset| <= R < len); tile positions past the image edge feed
+                // only discarded outputs, so clamping them just keeps the read
+                // in bounds.
+                gy = gy < 0 ? -gy : (gy >= H ? 2 * H - 2 - gy : gy);
+                gx = gx < 0 ? -gx : (gx >= W ? 2 * W - 2 - gx : gx);
+                gy = min(max(gy, 0), H - 1);
+                gx = min(max(gx, 0), W - 1);
+            } else {
+                gy = reflect101(gy, H);
+                gx = reflect101(gx, W);
+            }
+            v[u] = src[((size_t)gy * spitch + gx) * sstep];  // always in bounds; unused if idx >= TOTAL
+        }
+#pragma unroll
+        for (int u = 0; u < PER; u++) {
+            const int idx = tid + 256 * u;
+            const int ly = idx / RW, lx = idx - (idx / RW) * RW;
+            if (idx < TOTAL) in[ly * IW + lx] = v[u];
         }
     }
     __syncthreads();
 
-    if (n > 5) {
-        for (int i = tid; i < IH * BLUR_TW; i += 256) {
-            const int ly = i >> 6, lx = i & 63;
-            const float* p = in + ly * IW + lx;
-            float s = 0.f;
-            for (int k = 0; k < n; k++) s = __fmaf_rn(p[k], taps.w[k], s);
-            mid[i] = s;
-        }
-    } else {
-        for (int i = tid; i < IH * BLUR_TW; i += 256) {
-            const int ly = i >> 6, lx = i & 63;
-            const float* p = in + ly * IW + lx + r;
-            float s = p[0] * taps.w[r];
-            for (int k = 1; k <= r; k++) s = __fmaf_rn(p[-k] + p[k], taps.w[r + k], s);
-            mid[i] = s;
+    {
+        const int xq = (tid & 15) * 4;
+        for (int ly = tid >> 4; ly < IH; ly += 16) {
+            float win[4 * NW];
+            const float4* p = reinterpret_cast<const float4*>(in + ly * IW + xq);
+#pragma unroll
+            for (int v = 0; v < NW; v++) {
+                const float4 f = p[v];
+                win[4 * v] = f.x;
+                win[4 * v + 1] = f.y;
+                win[4 * v + 2] = f.z;
+                win[4 * v + 3] = f.w;
+            }
+            float s[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if constexpr (2 * R + 1 > 5) {
+                    s[q] = 0.f;
+#pragma unroll
+                    for (int k = 0; k <= 2 * R; k++) s[q] = __fmaf_rn(win[q + k], taps.w[k], s[q]);
+                } else {
+                    s[q] = win[q + R] * taps.w[R];
+#pragma unroll
+                    for (int k = 1; k <= R; k++) s[q] = __fmaf_rn(win[q + R - k] + win[q + R + k], taps.w[R + k], s[q]);
+                }
+            }
+            *reinterpret_cast<float4*>(mid + ly * BLUR_TW + xq) = make_float4(s[0], s[1], s[2], s[3]);
         }
     }
     __syncthreads();
 
-    for (int i = tid; i < BLUR_TH * BLUR_TW; i += 256) {
-        const int ly = i >> 6, lx = i & 63;
-        const int gy = y0 + ly, gx = x0 + lx;
-        if (gy < H && gx < W) {
-            const float* p = mid + (ly + r) * BLUR_TW + lx;
-            float s = __fmaf_rn(p[0], taps.w[r], 0.f);
-            for (int k = 1; k <= r; k++) s = __fmaf_rn(p[k * BLUR_TW] + p[-k * BLUR_TW], taps.w[r + k], s);
-            dst[(size_t)gy * dpitch + gx] = s;
-            if (copy_out) copy_out[(size_t)gy * dpitch + gx] = in[(ly + r) * IW + lx + r];
+    {
+        const int lx = lane, yb = wave * 8;
+        float win[8 + 2 * R];
+#pragma unroll
+        for (int j = 0; j < 8 + 2 * R; j++) win[j] = mid[(yb + j) * BLUR_TW + lx];
+        const int gx = x0 + lx;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            float s = __fmaf_rn(win[q + R], taps.w[R], 0.f);
+#pragma unroll
+            for (int k = 1; k <= R; k++) s = __fmaf_rn(win[q + R + k] + win[q + R - k], taps.w[R + k], s);
+            const int gy = y0 + yb + q;
+            if (gy < H && gx < W) {
+                dst[(size_t)gy * dpitch + gx] = s;
+                if (copy_out) copy_out[(size_t)gy * dpitch + gx] = in[(yb + q + R) * IW + lx + R];
+            }
         }
     }
 }
 
+using BlurLaunch = void (*)(dim3, hipStream_t, const float*, int, int, int, int, float*, int, float*, const Taps&);
+
+template <int R>
+void blur_launch_r(dim3 grid, hipStream_t s, const float* src, int spitch, int sstep, int W, int H, float* dst,
+                   int dpitch, float* copy_out, const Taps& taps) {
+    hipLaunchKernelGGL(k_blur<R>, grid, dim3(256), 0, s, src, spitch, sstep, W, H, dst, dpitch, copy_out, taps);
+}
+
+template <int... Rs>
+constexpr std::array<BlurLaunch, sizeof...(Rs)> blur_table(std::integer_sequence<int, Rs...>) {
+    return {&blur_launch_r<Rs + 1>...};
+}
+static const std::array<BlurLaunch, kMaxTaps / 2> kBlurTable = blur_table(std::make_integer_sequence<int, kMaxTaps / 2>{});
+
 void launch_blur(const float* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, float* copy_out,
                  const Taps& taps, hipStream_t s) {
-    const int r = taps.n >> 1;
-    const size_t lds = sizeof(float) * ((size_t)(BLUR_TH + 2 * r) * (BLUR_TW + 2 * r) + (size_t)(BLUR_TH + 2 * r) * BLUR_TW);
+    const int r = taps.n >> 1;  // 1 .. kMaxTaps/2 (taps.n >= 3 by construction)
     dim3 grid((W + BLUR_TW - 1) / BLUR_TW, (H + BLUR_TH - 1) / BLUR_TH);
-    hipLaunchKernelGGL(k_blur, grid, dim3(256), lds, s, src, spitch, sstep, W, H, dst, dpitch, copy_out, taps);
+    kBlurTable[r - 1](grid, s, src, spitch, sstep, W, H, dst, dpitch, copy_out, taps);
 }
 
 // ---------------------------------------------------------------------------
@@ -132,28 +198,62 @@ constexpr int EX_TW = 64;
 constexpr int EX_TH = 16;
 constexpr int EX_SW = EX_TW + 2;
 constexpr int EX_SH = EX_TH + 2;
+constexpr int EX_LIST = 512;  // per-workgroup candidate list (LDS)
 
-__global__ __launch_bounds__(256) void k_extrema(OctGeom g, int L, int o, float thr, uint2* __restrict__ cand,
+// LT = compile-time layer count (1..6), or 0 for the generic runtime-L path.
+template <int LT>
+__global__ __launch_bounds__(256) void k_extrema(OctGeom g, int Lrt, int o, float thr, uint2* __restrict__ cand,
                                                  Counters* __restrict__ ctr, unsigned cap) {
     extern __shared__ float dog[];  // (L+2) planes of EX_SH x EX_SW
+    const int L = LT > 0 ? LT : Lrt;
     const int tid = threadIdx.x;
     const int x0 = blockIdx.x * EX_TW, y0 = blockIdx.y * EX_TH;
     const int W = g.W, H = g.H, pitch = g.pitch;
-    const int PS = EX_SH * EX_SW;
+    constexpr int PS = EX_SH * EX_SW;
+    constexpr int PER = (PS + 255) / 256;
+    __shared__ unsigned s_cnt, s_base;
+    __shared__ uint2 s_list[EX_LIST];
+    if (tid == 0) s_cnt = 0;
 
-    for (int i = tid; i < PS; i += 256) {
-        const int ly = i / EX_SW, lx = i - ly * EX_SW;
-        const int gy = y0 - 1 + ly, gx = x0 - 1 + lx;
-        if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
-            const float* p = g.base + (size_t)gy * pitch + gx;
-            float prev = p[0];
-            for (int d = 0; d < L + 2; d++) {
-                const float next = p[(size_t)(d + 1) * g.planeStride];
-                dog[d * PS + i] = next - prev;
-                prev = next;
+    if constexpr (LT > 0) {
+        // All (L+3) x PER loads of this thread in flight at once, then DoG -> LDS.
+        float v[PER][LT + 3];
+#pragma unroll
+        for (int u = 0; u < PER; u++) {
+            const int i = tid + 256 * u;
+            const int ly = i / EX_SW, lx = i - ly * EX_SW;
+            const int gy = y0 - 1 + ly, gx = x0 - 1 + lx;
+            const bool in = i < PS && gy >= 0 && gy < H && gx >= 0 && gx < W;
+            const float* p = g.base + (size_t)min(max(gy, 0), H - 1) * pitch + min(max(gx, 0), W - 1);
+#pragma unroll
+            for (int d = 0; d < LT + 3; d++) {
+                const float x = p[(size_t)d * g.planeStride];  // unconditional (clamped) load
+                v[u][d] = in ? x : 0.f;
             }
-        } else {
-            for (int d = 0; d < L + 2; d++) dog[d * PS + i] = 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < PER; u++) {
+            const int i = tid + 256 * u;
+            if (i < PS) {
+#pragma unroll
+                for (int d = 0; d < LT + 2; d++) dog[d * PS + i] = v[u][d + 1] - v[u][d];
+            }
+        }
+    } else {
+        for (int i = tid; i < PS; i += 256) {
+            const int ly = i / EX_SW, lx = i - ly * EX_SW;
+            const int gy = y0 - 1 + ly, gx = x0 - 1 + lx;
+            if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+                const float* p = g.base + (size_t)gy * pitch + gx;
+                float prev = p[0];
+                for (int d = 0; d < L + 2; d++) {
+                    const float next = p[(size_t)(d + 1) * g.planeStride];
+                    dog[d * PS + i] = next - prev;
+                    prev = next;
+                }
+            } else {
+                for (int d = 0; d < L + 2; d++) dog[d * PS + i] = 0.f;
+            }
         }
     }
     __syncthreads();
@@ -193,20 +293,38 @@ __global__ __launch_bounds__(256) void k_extrema(OctGeom g, int L, int o, float 
                 }
             }
         }
+        // Hits go to a workgroup-local LDS list (wave ballot + one LDS atomic
+        // per wave); the list is flushed with ONE global atomic per workgroup.
         const unsigned long long mask = __ballot(hit);
         if (mask) {
-            const int cnt = __popcll(mask);
             unsigned basepos = 0;
-            if (lane == 0) basepos = atomicAdd(&ctr->cand, (unsigned)cnt);
+            if (lane == 0) basepos = atomicAdd(&s_cnt, (unsigned)__popcll(mask));
             basepos = __shfl(basepos, 0);
             if (hit) {
                 const unsigned pos = basepos + (unsigned)__popcll(mask & ((1ull << lane) - 1ull));
-                if (pos < cap)
-                    cand[pos] = make_uint2((unsigned)(o << 8 | layer), (unsigned)(r << 16 | c));
-                else
-                    atomicOr(&ctr->overflow, 1u);
+                const uint2 q = make_uint2((unsigned)(o << 8 | layer), (unsigned)(r << 16 | c));
+                if (pos < EX_LIST) {
+                    s_list[pos] = q;
+                } else {  // plateau-heavy tile: spill straight to the global list
+                    const unsigned gp = atomicAdd(&ctr->cand, 1u);
+                    if (gp < cap)
+                        cand[gp] = q;
+                    else
+                        atomicOr(&ctr->overflow, 1u);
+                }
             }
         }
+    }
+    __syncthreads();
+    const unsigned nl = min(s_cnt, (unsigned)EX_LIST);
+    if (tid == 0) s_base = nl ? atomicAdd(&ctr->cand, nl) : 0u;
+    __syncthreads();
+    for (unsigned k = tid; k < nl; k += 256) {
+        const unsigned pos = s_base + k;
+        if (pos < cap)
+            cand[pos] = s_list[k];
+        else
+            atomicOr(&ctr->overflow, 1u);
     }
 }
 
@@ -215,7 +333,18 @@ void launch_extrema(const PyrDesc& pyr, int o, float threshold, uint2* cand, Cou
     const OctGeom& g = pyr.oct[o];
     dim3 grid((g.W + EX_TW - 1) / EX_TW, (g.H + EX_TH - 1) / EX_TH);
     const size_t lds = sizeof(float) * (size_t)(pyr.L + 2) * EX_SH * EX_SW;
-    hipLaunchKernelGGL(k_extrema, grid, dim3(256), lds, s, g, pyr.L, o, threshold, cand, ctr, cap);
+    switch (pyr.L) {
+#define SIFT_EX_CASE(LV) \
+    case LV: hipLaunchKernelGGL(k_extrema<LV>, grid, dim3(256), lds, s, g, pyr.L, o, threshold, cand, ctr, cap); break;
+        SIFT_EX_CASE(1)
+        SIFT_EX_CASE(2)
+        SIFT_EX_CASE(3)
+        SIFT_EX_CASE(4)
+        SIFT_EX_CASE(5)
+        SIFT_EX_CASE(6)
+#undef SIFT_EX_CASE
+        default: hipLaunchKernelGGL(k_extrema<0>, grid, dim3(256), lds, s, g, pyr.L, o, threshold, cand, ctr, cap);
+    }
 }
 
 }  // namespace sift_amd

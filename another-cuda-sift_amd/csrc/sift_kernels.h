@@ -72,6 +72,8 @@ struct KeypointParams {
     int numFeatures;
     unsigned capRefined, capOriented, capFinal;
     int numBuckets;
+    int oriRmax, descRmax;  // LDS patch bounds for orientation / descriptor radii
+    int descNrec;           // LDS record bound of the descriptor's counting sort
 };
 void launch_refine(const PyrDesc& pyr, const uint2* cand, unsigned capCand, Counters* ctr, uint32_t* bitmap,
                    RefKpt* out, const KeypointParams& kp, hipStream_t s);
@@ -90,5 +92,6 @@ void launch_descriptor(const PyrDesc& pyr, const OriKpt* kpts, const int* final_
 
 // Exp table (OpenCV expTab_f) uploaded once per device.
 void upload_exp_table(const float* tab64);
+void upload_exp_table_desc(const float* tab64);
 
 }  // namespace sift_amd

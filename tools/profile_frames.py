@@ -1,0 +1,28 @@
+"""Run the C2 workload for a few frames (no torch) -- a small target for rocprofv3."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "another-cuda-sift_amd"))
+import sift_amd as sift  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--frames", type=int, default=10)
+ap.add_argument("--width", type=int, default=1920)
+ap.add_argument("--height", type=int, default=1200)
+ap.add_argument("--octaves", type=int, default=3)
+ap.add_argument("--upscale", action="store_true")
+ap.add_argument("--eager", action="store_true", help="timing mode: un-graphed launches")
+a = ap.parse_args()
+cfg = sift.CudaSiftConfig(col_width=a.width, row_width=a.height, numOctaves=a.octaves, upscale=a.upscale)
+det = sift.Detector(cfg, device=0)
+det.gpuWarmUpAndAllocate()
+det.set_timing(a.eager)
+img = sift.synth_frame(0, a.width, a.height)
+for _ in range(a.frames):
+    det.detectAndCompute(img)
+print("keypoints", det.total_size)
+if a.eager:
+    for k, v in sorted(det.timing().items(), key=lambda kv: -kv[1]["ms"]):
+        print(f"{k:16s} {v['ms'] / a.frames * 1e3:9.2f} us/frame  launches/frame {v['launches'] / a.frames:.0f}")
