@@ -4,27 +4,32 @@
 // per keypoint, 8 shared-memory float atomics per sample, modff bins, serial
 // lane-0 normalisation, half(x512) output).
 //
-// One 256-thread workgroup per keypoint.  Eight LDS float atomics per sample
-// saturate the CU's LDS pipe on gfx950 (~30 cycles per ds_add_f32 wave
-// instruction, measured: SQ_WAIT_INST_LDS ~40 % of wave cycles), so the
-// trilinear histogram is built without per-sample atomics:
-//   A  classify every sample of the (2R+1)^2 window, count it into its base
-//      bucket (r0, c0, o0) -- 25 spatial base cells x 8 orientation bins; all
-//      samples of a bucket feed the SAME 8 histogram bins;
-//   B  exclusive scan of the 200 bucket counts;
-//   C  recompute each sample (gradient, fastAtan2, magnitude, exp32f weight:
-//      the oracle's operation order) and scatter a 12-byte record into its
-//      bucket (counting sort in LDS);
-//   E  every thread walks an equal slice of the bucket-ordered records, forms
-//      the 8 trilinear contributions exactly as OpenCV does, accumulates them in
-//      registers and flushes once per bucket run with 8 ds_add_u64.
-// Sums are kept in 32.32 fixed point: integer addition is associative, so the
-// histogram is bit-identical for any thread/record order (deterministic) and is
-// the correctly rounded exact sum of the float contributions.  OpenCV sums the
-// same float contributions sequentially, so descriptor bytes can differ from the
-// oracle by +-1 where a float rounding lands on a .5 boundary (tests bound this).
-// Then wrap, L2 norm (8 fma lanes + v_reduce_sum order), 0.2 clip, renorm and
-// x512 rounding to 0..255 are the oracle's exact float operations.
+// One wavefront (64-thread workgroup) per keypoint, ~20 keypoints in flight
+// per CU, so memory latency of one keypoint hides behind the others' ALU work:
+//   * k_bucket_rank already computed the keypoint's window (DescJob), read
+//     here with scalar loads;
+//   * only samples inside the rotated 4x4-cell square are enumerated: per row
+//     a conservative j-interval, a prefix sum over rows, and each lane takes a
+//     contiguous run of the enumerated samples (the oracle's exact per-sample
+//     test is still applied, so the set of samples is unchanged);
+//   * gradients are read straight from the Gaussian plane (L1/L2 resident:
+//     neighbouring keypoints share it) with bounds-checked buffer loads, four
+//     samples' loads in flight per lane;
+//   * each sample is computed exactly as the oracle (fastAtan2, magnitude,
+//     exp32f weight, cvFloor bins, trilinear split in OpenCV's operation
+//     order) and its 8 contributions go to the LDS histogram as 4 ds_add_u64,
+//     each carrying the orientation pair (o0, o0+1) as two u32 words.
+// The histogram is fixed point (scale 2^S per keypoint, chosen from the
+// frame's pixel range so no bin can reach 2^31): on gfx950 an LDS f32 atomic
+// costs ~193 cycles per wave instruction against ~9 for u32 and ~17 for u64
+// (tools/lds_atomic_bench.hip), and integer addition is
+// associative, so the histogram is identical for any lane schedule
+// (deterministic) and equals the exact sum of the rounded contributions.
+// OpenCV sums the same float contributions sequentially in float, so
+// descriptor bytes can differ from the oracle by +-1 where that rounding lands
+// on a .5 boundary (tests bound the rate).  L2 norm (8 fma lanes +
+// v_reduce_sum order), 0.2 clip, sequential renorm and x512 rounding are the
+// oracle's float operations.
 #include <hip/hip_runtime.h>
 
 #include "sift_kernels.h"
@@ -39,18 +44,13 @@ void upload_exp_table_desc(const float* tab64) {
 }
 
 constexpr int kD = 4, kN = 8;
-constexpr int kHistLen = (kD + 2) * (kD + 2) * (kN + 2);  // 360
-constexpr int kBuckets = 25 * 8;                           // base cell (r0+1, c0+1) x o0
+constexpr int kCells = (kD + 2) * (kD + 2);  // 36 spatial cells incl. the border ring
+constexpr int kMaxRows = kDescMaxRows;       // enumerated windows: side = 2R+1 <= kMaxRows
+constexpr int kGroup = 4;                    // samples whose loads are in flight together
 
 struct DescGeom {
-    float cos_t, sin_t, angle, bins_per_rad, exp_scale;
-    int ptx, pty, radius, rows, cols;
-};
-
-struct DescRec {
-    unsigned key;  // bucket << 16 | (i + R) << 8 | (j + R)
-    float mag;     // |grad| * gaussian weight
-    float obf;     // fractional orientation bin
+    float cos_t, sin_t, exp_scale;
+    int ptx, pty, rows, cols;
 };
 
 // Rotated-grid coordinates of window sample (i, j) and its validity: the
@@ -64,16 +64,6 @@ __device__ __forceinline__ bool desc_sample(const DescGeom& G, int i, int j, flo
     const int r = G.pty + i, c = G.ptx + j;
     return rbin > -1 && rbin < kD && cbin > -1 && cbin < kD && r > 0 && r < G.rows - 1 && c > 0 && c < G.cols - 1;
 }
-
-// Exact 32.32 fixed-point image of a non-negative float < 2^31 (bits below
-// 2^-32 are dropped).
-__device__ __forceinline__ long long to_fx(float v) {
-    const float hi = floorf(v);
-    const unsigned lo = (unsigned)((v - hi) * 4294967296.0f);
-    return ((long long)(int)hi << 32) | (long long)lo;
-}
-
-__device__ __forceinline__ float from_fx(long long x) { return (float)((double)x * 2.3283064365386962890625e-10); }
 
 // The 8 contributions of one sample, OpenCV's order and names (v_rco[r][c][o]).
 __device__ __forceinline__ void trilinear(float mag, float rbf, float cbf, float obf, float v[8]) {
@@ -90,257 +80,278 @@ __device__ __forceinline__ void trilinear(float mag, float rbf, float cbf, float
     v[0] = v_rc00 - v[1];
 }
 
-// Histogram offsets of v_rco000..111 from the base index ((r0+1)*6 + c0+1)*10 + o0.
-__device__ __forceinline__ int tri_off(int q) {
-    return (q & 4 ? (kD + 2) * (kN + 2) : 0) + (q & 2 ? (kN + 2) : 0) + (q & 1);
+// Shrink [lo, hi] to a superset of the integers j with -1 < j*s + b < kD
+// (margin 1e-4 in bin units and one sample each side, so float rounding of the
+// exact per-sample test can never fall outside the enumerated range).
+__device__ __forceinline__ void clip_interval(int& lo, int& hi, double s, double b, int R) {
+    constexpr double lb = -1.0 - 1e-4, ub = kD + 1e-4;
+    if (fabs(s) < 1e-12) {
+        if (b <= lb || b >= ub) hi = lo - 1;
+        return;
+    }
+    double x1 = (lb - b) / s, x2 = (ub - b) / s;
+    if (x1 > x2) {
+        const double t = x1;
+        x1 = x2;
+        x2 = t;
+    }
+    x1 = fmax(x1, (double)(-R - 2));
+    x2 = fmin(x2, (double)(R + 2));
+    lo = max(lo, (int)floor(x1) - 1);
+    hi = min(hi, (int)ceil(x2) + 1);
 }
 
-__device__ __forceinline__ int bucket_base_index(int b) {
-    const int cell = b >> 3, o0 = b & 7;
-    return ((cell / 5) * (kD + 2) + (cell % 5)) * (kN + 2) + o0;
+// DescJob read with scalar loads from the constant address space: every field
+// is uniform and lives in SGPRs.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+struct JobWords {
+    u32x4 w[4];
+};
+
+__device__ __forceinline__ DescJob load_job(const DescJob* jobs, unsigned p) {
+    const __attribute__((address_space(4))) u32x4* c = (const __attribute__((address_space(4))) u32x4*)(jobs + p);
+    JobWords r;
+#pragma unroll
+    for (int i = 0; i < 4; i++) r.w[i] = c[i];
+    return __builtin_bit_cast(DescJob, r);
 }
 
-__global__ __launch_bounds__(256) void k_descriptor(PyrDesc pyr, const OriKpt* __restrict__ kpts,
-                                                    const int* __restrict__ final_order,
-                                                    const Counters* __restrict__ ctr, float* __restrict__ kpts3,
-                                                    float* __restrict__ feats4, uint16_t* __restrict__ desc,
-                                                    KeypointParams kp) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    long long* hist = reinterpret_cast<long long*>(lds_raw);  // kHistLen
-    int* bcount = reinterpret_cast<int*>(hist + kHistLen);     // kBuckets
-    int* bstart = bcount + kBuckets;                           // kBuckets + 8
-    int* bcur = bstart + kBuckets + 8;                         // kBuckets
-    float* raw = reinterpret_cast<float*>(bcur + kBuckets);    // 128
-    float* nacc = raw + 128;                                   // 16
-    DescRec* recs = reinterpret_cast<DescRec*>(nacc + 16);     // kp.descNrec
+__global__ __launch_bounds__(64) void k_descriptor(const DescJob* __restrict__ jobs, const Counters* __restrict__ ctr,
+                                                   const unsigned* __restrict__ range_keys,
+                                                   uint16_t* __restrict__ desc) {
+    // Two u32 fixed-point histograms so that each sample's orientation pair
+    // (o0, o0+1) is one naturally aligned ds_add_u64 (low word o0, high word
+    // o0+1): even o0 -> histE[cell*8 + o], odd o0 -> histO[cell*10 + 1 + o]
+    // (slot 9 = orientation 8, wrapped into 0 at the end).  The per-keypoint
+    // scale keeps every bin below 2^31, so no carry crosses the word boundary.
+    __shared__ __attribute__((aligned(16))) unsigned histE[kCells * 8 + kCells * 10];
+    unsigned* histO = histE + kCells * 8;
+    __shared__ __attribute__((aligned(16))) float sq[128];
+    __shared__ int rowpre[kMaxRows + 4], rowlo[kMaxRows];
+    __shared__ float s_exptab[64];
 
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int lane = threadIdx.x;
+    s_exptab[lane] = c_exptab_d[lane];
     const unsigned n = ctr->final_n;
-    const int fo = pyr.firstOctave;
+    // Pixel range of the frame; it bounds every Gaussian plane (convex blurs).
+    unsigned kmax = 0, knmn = 0;
+    for (int i = lane; i < kRangeSlots; i += 64) {
+        kmax = max(kmax, range_keys[2 * i]);
+        knmn = max(knmn, range_keys[2 * i + 1]);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        kmax = max(kmax, (unsigned)__shfl_xor((int)kmax, off));
+        knmn = max(knmn, (unsigned)__shfl_xor((int)knmn, off));
+    }
+    const float range = (decode_range_key(kmax) + decode_range_key(knmn)) * 1.001f;
+    const float bins_per_rad = kN / 360.f;
+
     for (unsigned p = blockIdx.x; p < n; p += gridDim.x) {
-        const OriKpt kpt = kpts[final_order[p]];
-        // unpackOctave + calcDescriptorsComputer (sift.dispatch.cpp).
-        int octave = kpt.octave & 255;
-        const int layer = (kpt.octave >> 8) & 255;
-        octave = octave < 128 ? octave : (-128 | octave);
-        const float scale = octave >= 0 ? 1.f / (float)(1 << octave) : (float)(1 << -octave);
-        const float size = kpt.size * scale;
-        const float ptfx = kpt.x * scale, ptfy = kpt.y * scale;
-        const OctGeom& g = pyr.oct[octave - fo];
-        const float* img = g.base + (size_t)layer * g.planeStride;
-        const int pitch = g.pitch;
-        float angle = 360.f - kpt.angle;
-        if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
-        const float scl = size * 0.5f;
-
+        const DescJob jb = load_job(jobs, p);
         DescGeom G;
-        G.rows = g.H;
-        G.cols = g.W;
-        G.ptx = cv_round(ptfx);
-        G.pty = cv_round(ptfy);
-        const float arg = angle * (float)(M_PI / 180);
-        float cos_t = (float)cos((double)arg);
-        float sin_t = (float)sin((double)arg);
-        G.bins_per_rad = kN / 360.f;
+        G.cos_t = jb.cos_t;
+        G.sin_t = jb.sin_t;
         G.exp_scale = -1.f / (kD * kD * 0.5f);
-        const float hist_width = 3.f * scl;
-        int radius = cv_round(hist_width * 1.4142135623730951f * (float)(kD + 1) * 0.5f);
-        radius = min(radius, (int)sqrt((double)G.cols * G.cols + (double)G.rows * G.rows));
-        radius = min(radius, 120);  // record packing bound; unreachable for accepted keypoints
-        G.cos_t = cos_t / hist_width;
-        G.sin_t = sin_t / hist_width;
-        G.angle = angle;
-        G.radius = radius;
-        const int side = 2 * radius + 1, total = side * side;
+        G.ptx = jb.ptx;
+        G.pty = jb.pty;
+        G.rows = jb.rows;
+        G.cols = jb.cols;
+        const int radius = jb.radius, side = 2 * radius + 1;
+        const bool enumerated = side <= kMaxRows;
+        const __amdgpu_buffer_rsrc_t rsrc =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(jb.img), 0, jb.rows * jb.pitch * 4, 0x00020000);
 
-        for (int i = tid; i < kHistLen; i += 256) hist[i] = 0;
-        for (int i = tid; i < kBuckets; i += 256) {
-            bcount[i] = 0;
-            bcur[i] = 0;
-        }
-        __syncthreads();
-
-        // A: count samples per base bucket.
-        for (int k = tid; k < total; k += 256) {
-            const int i = k / side - radius, j = k - (k / side) * side - radius;
-            float rbin, cbin, c_rot, r_rot;
-            if (desc_sample(G, i, j, rbin, cbin, c_rot, r_rot)) {
-                const float* pp = img + (size_t)(G.pty + i) * pitch + (G.ptx + j);
-                const float dx = pp[1] - pp[-1], dy = pp[-pitch] - pp[pitch];
-                const float obin = (cv_fast_atan2(dy, dx) - angle) * G.bins_per_rad;
-                int o0 = cv_floor(obin);
-                if (o0 < 0) o0 += kN;
-                if (o0 >= kN) o0 -= kN;
-                const int b = ((cv_floor(rbin) + 1) * 5 + (cv_floor(cbin) + 1)) * 8 + o0;
-                atomicAdd(&bcount[b], 1);
+        for (int i = lane; i < kCells * 18; i += 64) histE[i] = 0u;
+        if (enumerated) {
+            for (int t = lane; t < side; t += 64) {
+                const int i = t - radius, r = G.pty + i;
+                int lo = max(-radius, 1 - G.ptx), hi = min(radius, G.cols - 2 - G.ptx);
+                if (r <= 0 || r >= G.rows - 1) hi = lo - 1;
+                clip_interval(lo, hi, (double)G.sin_t, (double)i * G.cos_t + (kD / 2 - 0.5), radius);
+                clip_interval(lo, hi, (double)G.cos_t, -(double)i * G.sin_t + (kD / 2 - 0.5), radius);
+                rowlo[t] = lo;
+                rowpre[t + 1] = max(hi - lo + 1, 0);
             }
-        }
-        __syncthreads();
-
-        // B: exclusive scan of the bucket counts (wave 0, 4 buckets per lane).
-        if (tid < 64) {
-            int c4[4], s = 0;
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int b = lane * 4 + u;
-                c4[u] = b < kBuckets ? bcount[b] : 0;
-                s += c4[u];
-            }
-            int x = s;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const int y = __shfl_up(x, off);
-                if (lane >= off) x += y;
-            }
-            int run = x - s;
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int b = lane * 4 + u;
-                if (b < kBuckets) bstart[b] = run;
-                run += c4[u];
-            }
-            if (lane == 63) bstart[kBuckets] = x;
-        }
-        __syncthreads();
-        const int nrec = bstart[kBuckets];
-        const bool useRecs = nrec <= kp.descNrec;
-
-        // C: full sample, scatter a record into its bucket (or, past the LDS
-        // bound, add its 8 fixed-point contributions directly: same sums).
-        for (int k = tid; k < total; k += 256) {
-            const int i = k / side - radius, j = k - (k / side) * side - radius;
-            float rbin, cbin, c_rot, r_rot;
-            if (desc_sample(G, i, j, rbin, cbin, c_rot, r_rot)) {
-                const float* pp = img + (size_t)(G.pty + i) * pitch + (G.ptx + j);
-                const float dx = pp[1] - pp[-1], dy = pp[-pitch] - pp[pitch];
-                const float wgt = cv_exp32f((c_rot * c_rot + r_rot * r_rot) * G.exp_scale, c_exptab_d);
-                const float gori = cv_fast_atan2(dy, dx);
-                const float gmag = cv_magnitude(dx, dy);
-                float obin = (gori - angle) * G.bins_per_rad;
-                const float mag = gmag * wgt;
-                const int r0 = cv_floor(rbin), c0 = cv_floor(cbin);
-                int o0 = cv_floor(obin);
-                obin -= (float)o0;
-                if (o0 < 0) o0 += kN;
-                if (o0 >= kN) o0 -= kN;
-                const int b = ((r0 + 1) * 5 + (c0 + 1)) * 8 + o0;
-                if (useRecs) {
-                    const int slot = bstart[b] + atomicAdd(&bcur[b], 1);
-                    DescRec rec;
-                    rec.key = (unsigned)b << 16 | (unsigned)(i + radius) << 8 | (unsigned)(j + radius);
-                    rec.mag = mag;
-                    rec.obf = obin;
-                    recs[slot] = rec;
-                } else {
-                    float v[8];
-                    trilinear(mag, rbin - (float)r0, cbin - (float)c0, obin, v);
-                    const int base = bucket_base_index(b);
-#pragma unroll
-                    for (int q = 0; q < 8; q++) atomicAdd((unsigned long long*)&hist[base + tri_off(q)],
-                                                          (unsigned long long)to_fx(v[q]));
+            if (lane == 0) rowpre[0] = 0;
+            lds_barrier();
+            {  // inclusive scan of row counts (entries 2l+1, 2l+2 of rowpre per lane)
+                const int a = 2 * lane + 1 <= side ? rowpre[2 * lane + 1] : 0;
+                const int b = 2 * lane + 2 <= side ? rowpre[2 * lane + 2] : 0;
+                int sum = a + b;
+                for (int off = 1; off < 64; off <<= 1) {
+                    const int t = __shfl_up(sum, off);
+                    if (lane >= off) sum += t;
                 }
+                if (2 * lane + 1 <= side) rowpre[2 * lane + 1] = sum - b;
+                if (2 * lane + 2 <= side) rowpre[2 * lane + 2] = sum;
             }
         }
-        __syncthreads();
+        // Fixed-point scale 2^S with every bin < 2^31: a contribution is at most
+        // the gradient magnitude <= sqrt(2) * range, and a bin collects samples
+        // from a 2x2-cell rotated square of side 2*hist_width, i.e. at most
+        // (2*sqrt(2)*hist_width + 2)^2 samples.
+        const float nb = 2.8285f * jb.hist_width + 2.f;
+        int e;
+        (void)frexpf(nb * nb * 1.4143f * range + 1.f, &e);
+        const int S = min(31 - e, 40);
+        const float fxs = ldexpf(1.f, S);
+        lds_barrier();
 
-        // E: balanced walk over the bucket-ordered records, register
-        // accumulation, one 8-atomic flush per bucket run.
-        if (useRecs) {
-            const int chunk = (nrec + 255) / 256;
-            const int e0 = min(nrec, tid * chunk), e1 = min(nrec, e0 + chunk);
-            int curb = -1;
-            long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            for (int e = e0; e < e1; e++) {
-                const DescRec rec = recs[e];
-                const int b = (int)(rec.key >> 16);
-                if (b != curb) {
-                    if (curb >= 0) {
-                        const int base = bucket_base_index(curb);
+        // One sample from its four neighbours (l, r, u, d).
+        auto accumulate = [&](int i, int j, float l, float r, float u, float d) {
+            float rbin, cbin, c_rot, r_rot;
+            if (!desc_sample(G, i, j, rbin, cbin, c_rot, r_rot)) return;
+            const float dx = r - l, dy = u - d;
+            const float wgt = cv_exp32f((c_rot * c_rot + r_rot * r_rot) * G.exp_scale, s_exptab);
+            const float gori = cv_fast_atan2(dy, dx);
+            const float gmag = cv_magnitude(dx, dy);
+            float obin = (gori - jb.angle) * bins_per_rad;
+            const float mag = gmag * wgt;
+            const int r0 = cv_floor(rbin), c0 = cv_floor(cbin);
+            int o0 = cv_floor(obin);
+            rbin -= (float)r0;
+            cbin -= (float)c0;
+            obin -= (float)o0;
+            if (o0 < 0) o0 += kN;
+            if (o0 >= kN) o0 -= kN;
+            const int cell = (r0 + 1) * (kD + 2) + c0 + 1;
+            const bool odd = o0 & 1;
+            const int stride = odd ? 10 : 8;  // dwords per cell
+            unsigned* hb = odd ? histO + cell * 10 + 1 + o0 : histE + cell * 8 + o0;
+            float v[8];
+            trilinear(mag, rbin, cbin, obin, v);
 #pragma unroll
-                        for (int q = 0; q < 8; q++) {
-                            atomicAdd((unsigned long long*)&hist[base + tri_off(q)], (unsigned long long)acc[q]);
-                            acc[q] = 0;
+            for (int q = 0; q < 8; q += 2) {
+                const int off = (q & 4 ? (kD + 2) * stride : 0) + (q & 2 ? stride : 0);
+                const unsigned lo = (unsigned)__builtin_rintf(v[q] * fxs);
+                const unsigned hi = (unsigned)__builtin_rintf(v[q + 1] * fxs);
+                atomicAdd(reinterpret_cast<unsigned long long*>(hb + off),
+                          ((unsigned long long)hi << 32) | (unsigned long long)lo);
+            }
+        };
+        // Gradient loads of up to kGroup samples, then their accumulation.
+        // Samples outside the plane read 0 (buffer range check) and are
+        // rejected by desc_sample.
+        auto group = [&](const int (&gi)[kGroup], const int (&gj)[kGroup], int cnt) {
+            float l[kGroup], r[kGroup], u[kGroup], d[kGroup];
+#pragma unroll
+            for (int t = 0; t < kGroup; t++) {
+                const unsigned o = (unsigned)((G.pty + gi[t]) * jb.pitch + G.ptx + gj[t]) * 4u;
+                l[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o - 4u, 0, 0));
+                r[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o + 4u, 0, 0));
+                u[t] = __builtin_bit_cast(float,
+                                          __builtin_amdgcn_raw_buffer_load_b32(rsrc, o - 4u * jb.pitch, 0, 0));
+                d[t] = __builtin_bit_cast(float,
+                                          __builtin_amdgcn_raw_buffer_load_b32(rsrc, o + 4u * jb.pitch, 0, 0));
+            }
+#pragma unroll
+            for (int t = 0; t < kGroup; t++)
+                if (t < cnt) accumulate(gi[t], gj[t], l[t], r[t], u[t], d[t]);
+        };
+
+        if (enumerated) {
+            const int N = rowpre[side];
+            const int run = (N + 63) / 64;
+            const int k0 = min(N, lane * run), k1 = min(N, k0 + run);
+            if (k0 < k1) {
+                int lo = 0, hi = side - 1;  // last row with rowpre[row] <= k0 (non-empty)
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (rowpre[mid] <= k0) lo = mid;
+                    else hi = mid - 1;
+                }
+                int row = lo;
+                int j = rowlo[row] + (k0 - rowpre[row]);
+                int jend = rowlo[row] + (rowpre[row + 1] - rowpre[row]) - 1;
+                for (int q = k0; q < k1; q += kGroup) {
+                    int gi[kGroup], gj[kGroup];
+#pragma unroll
+                    for (int t = 0; t < kGroup; t++) {
+                        gi[t] = row - radius;
+                        gj[t] = j;
+                        if (q + t + 1 < k1 && ++j > jend) {
+                            do row++;
+                            while (rowpre[row + 1] == rowpre[row]);
+                            j = rowlo[row];
+                            jend = j + (rowpre[row + 1] - rowpre[row]) - 1;
                         }
                     }
-                    curb = b;
+                    group(gi, gj, k1 - q);
                 }
-                const int i = (int)((rec.key >> 8) & 255u) - radius, j = (int)(rec.key & 255u) - radius;
-                float rbin, cbin, c_rot, r_rot;
-                desc_sample(G, i, j, rbin, cbin, c_rot, r_rot);
-                float v[8];
-                trilinear(rec.mag, rbin - (float)cv_floor(rbin), cbin - (float)cv_floor(cbin), rec.obf, v);
-#pragma unroll
-                for (int q = 0; q < 8; q++) acc[q] += to_fx(v[q]);
             }
-            if (curb >= 0) {
-                const int base = bucket_base_index(curb);
+        } else {  // huge window: the full raster, rejected samples included
+            const int total = side * side;
+            for (int q0 = lane * kGroup; q0 < total; q0 += 64 * kGroup) {
+                int gi[kGroup], gj[kGroup];
 #pragma unroll
-                for (int q = 0; q < 8; q++)
-                    atomicAdd((unsigned long long*)&hist[base + tri_off(q)], (unsigned long long)acc[q]);
+                for (int t = 0; t < kGroup; t++) {
+                    const int q = min(q0 + t, total - 1);
+                    gi[t] = q / side - radius;
+                    gj[t] = q % side - radius;
+                }
+                group(gi, gj, total - q0);
             }
         }
-        __syncthreads();
+        lds_barrier();
 
-        // Wrap bins 8,9 into 0,1 (bin 9 never receives a contribution).
-        if (tid < 128) {
-            const int ii = tid >> 5, jj = (tid >> 3) & 3, kk = tid & 7;
-            const int hidx = ((ii + 1) * (kD + 2) + (jj + 1)) * (kN + 2) + kk;
-            float v = from_fx(hist[hidx]);
-            if (kk < 2) v = v + from_fx(hist[hidx + kN]);
-            raw[tid] = v;
+        // Wrap, L2 norm (8 fma lanes, then v_reduce_sum's pairing), 0.2 clip.
+        const float inv = ldexpf(1.f, -S);
+        float val[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int t = lane + 64 * h;
+            const int ii = t >> 5, jj = (t >> 3) & 3, kk = t & 7;
+            const int cell = (ii + 1) * (kD + 2) + (jj + 1);
+            unsigned long long hv = (unsigned long long)histE[cell * 8 + kk] + histO[cell * 10 + 1 + kk];
+            if (kk == 0) hv += histO[cell * 10 + 9];
+            val[h] = (float)((double)hv * (double)inv);
         }
-        __syncthreads();
-        if (tid < 8) {
-            float a = 0.f;
+        sq[lane] = val[0];
+        sq[lane + 64] = val[1];
+        lds_barrier();
+        float a = 0.f;
+        if (lane < 8) {
 #pragma unroll
-            for (int q = 0; q < 16; q++) a = __fmaf_rn(raw[tid + 8 * q], raw[tid + 8 * q], a);
-            nacc[tid] = a;
+            for (int q = 0; q < 16; q++) a = __fmaf_rn(sq[lane + 8 * q], sq[lane + 8 * q], a);
         }
-        __syncthreads();
-        if (tid == 0) {
-            const float t0 = nacc[0] + nacc[4], t1 = nacc[1] + nacc[5], t2 = nacc[2] + nacc[6], t3 = nacc[3] + nacc[7];
-            float nrm2 = (t0 + t2) + (t1 + t3);
-            const float thr = __builtin_sqrtf(nrm2) * 0.2f;
-            nrm2 = 0.f;
-#pragma unroll 1
-            for (int q0 = 0; q0 < 128; q0 += 8) {
-                float vals[8];
-#pragma unroll
-                for (int u = 0; u < 8; u++) vals[u] = raw[q0 + u];
-#pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const float val = fminf(vals[u], thr);
-                    raw[q0 + u] = val;
-                    nrm2 = nrm2 + val * val;
-                }
+        const float n0 = __shfl(a, 0), n1 = __shfl(a, 1), n2 = __shfl(a, 2), n3 = __shfl(a, 3);
+        const float n4 = __shfl(a, 4), n5 = __shfl(a, 5), n6 = __shfl(a, 6), n7 = __shfl(a, 7);
+        const float t0 = n0 + n4, t1 = n1 + n5, t2 = n2 + n6, t3 = n3 + n7;
+        const float thr = __builtin_sqrtf((t0 + t2) + (t1 + t3)) * 0.2f;
+        val[0] = fminf(val[0], thr);
+        val[1] = fminf(val[1], thr);
+        lds_barrier();
+        sq[lane] = val[0] * val[0];
+        sq[lane + 64] = val[1] * val[1];
+        lds_barrier();
+        float nrm2 = 0.f;  // sequential over k = 0..127, the oracle's order
+        if (lane == 0) {
+#pragma unroll 4
+            for (int q = 0; q < 128; q += 4) {
+                const float4 s4 = *reinterpret_cast<const float4*>(sq + q);
+                nrm2 = nrm2 + s4.x;
+                nrm2 = nrm2 + s4.y;
+                nrm2 = nrm2 + s4.z;
+                nrm2 = nrm2 + s4.w;
             }
-            nacc[8] = 512.f / fmaxf(__builtin_sqrtf(nrm2), FLT_EPSILON);
-            float* k3 = kpts3 + 3 * (size_t)p;
-            k3[0] = kpt.x;
-            k3[1] = kpt.y;
-            k3[2] = (float)layer;
-            reinterpret_cast<float4*>(feats4)[p] = make_float4((float)kpt.octave, kpt.size, kpt.response, kpt.angle);
         }
-        __syncthreads();
-        if (tid < 128) {
-            int v = cv_round(raw[tid] * nacc[8]);
+        nrm2 = __shfl(nrm2, 0);
+        const float scale = 512.f / fmaxf(__builtin_sqrtf(nrm2), FLT_EPSILON);
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            int v = cv_round(val[h] * scale);
             v = v < 0 ? 0 : (v > 255 ? 255 : v);
             const _Float16 hv = (_Float16)(float)v;
-            desc[(size_t)p * 128 + tid] = __builtin_bit_cast(uint16_t, hv);
+            desc[(size_t)p * 128 + lane + 64 * h] = __builtin_bit_cast(uint16_t, hv);
         }
-        __syncthreads();
+        lds_barrier();  // sq / histograms are rewritten by the next keypoint
     }
 }
 
-size_t descriptor_lds_bytes(const KeypointParams& kp) {
-    return sizeof(long long) * kHistLen + sizeof(int) * (3 * kBuckets + 8) + sizeof(float) * (128 + 16) +
-           sizeof(DescRec) * (size_t)kp.descNrec;
-}
-
-void launch_descriptor(const PyrDesc& pyr, const OriKpt* kpts, const int* final_order, const Counters* ctr,
-                       float* kpts3, float* feats4, uint16_t* desc, const KeypointParams& kp, hipStream_t s) {
-    hipLaunchKernelGGL(k_descriptor, dim3(2048), dim3(256), descriptor_lds_bytes(kp), s, pyr, kpts, final_order, ctr,
-                       kpts3, feats4, desc, kp);
+void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned* range_keys, uint16_t* desc,
+                       const KeypointParams& kp, hipStream_t s) {
+    (void)kp;
+    hipLaunchKernelGGL(k_descriptor, dim3(8192), dim3(64), 0, s, jobs, ctr, range_keys, desc);
 }
 
 }  // namespace sift_amd

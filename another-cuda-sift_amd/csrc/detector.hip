@@ -103,7 +103,8 @@ struct sift_hip_detector {
     OriKpt* dOri = nullptr;
     int* dSlot = nullptr;
     int* dOrder = nullptr;
-    int* dFinalOrder = nullptr;
+    DescJob* dJobs = nullptr;  // per final keypoint, written by k_bucket_rank
+    unsigned* dRange = nullptr;  // 2 * kRangeSlots pixel-range keys (initial blur -> descriptor)
     unsigned* dBcount = nullptr;
     unsigned* dBoff = nullptr;
     uint32_t* dBitmap = nullptr;
@@ -167,7 +168,7 @@ struct sift_hip_detector {
             (void)hipSetDevice(device);
             for (auto& e : exec)
                 if (e) (void)hipGraphExecDestroy(e);
-            void* bufs[] = {dInput, dUp, dPyr, dCand, dRef, dOri, dSlot, dOrder, dFinalOrder, dBcount, dBoff,
+            void* bufs[] = {dInput, dUp, dPyr, dCand, dRef, dOri, dSlot, dOrder, dJobs, dRange, dBcount, dBoff,
                             dBitmap, dCtr, dKpts3[0], dKpts3[1], dFeats4[0], dFeats4[1], dDesc[0], dDesc[1]};
             for (void* b : bufs)
                 if (b) (void)hipFree(b);
@@ -299,7 +300,8 @@ int allocate(sift_hip_detector* d) {
     if ((rc = dalloc(&d->dOri, capO))) return rc;
     if ((rc = dalloc(&d->dSlot, capO))) return rc;
     if ((rc = dalloc(&d->dOrder, capO))) return rc;
-    if ((rc = dalloc(&d->dFinalOrder, capF))) return rc;
+    if ((rc = dalloc(&d->dJobs, capF))) return rc;
+    if ((rc = dalloc(&d->dRange, 2 * kRangeSlots))) return rc;
     if ((rc = dalloc(&d->dBcount, (size_t)d->kp.numBuckets))) return rc;
     if ((rc = dalloc(&d->dBoff, (size_t)d->kp.numBuckets))) return rc;
     if ((rc = dalloc(&d->dBitmap, d->bitmapWords))) return rc;
@@ -321,6 +323,11 @@ int allocate(sift_hip_detector* d) {
 // pointer); it stays outside the graph so the graph never bakes a user pointer.
 void enqueue_head(sift_hip_detector* d, const float* img, int pitchFloats) {
     const int W = d->cfg.col_width, H = d->cfg.row_width;
+    // Counters first: the initial blur accumulates the frame's pixel range.
+    d->timed("memset", 0, [&] {
+        (void)hipMemsetAsync(d->dCtr, 0, sizeof(Counters), d->stream);
+        (void)hipMemsetAsync(d->dRange, 0, sizeof(unsigned) * 2 * kRangeSlots, d->stream);
+    });
     if (d->firstOctave < 0) {
         d->timed("upsample", (double)W * H * 4 + (double)W * H * 16, [&] {
             launch_upsample2x(img, pitchFloats, W, H, d->dUp, d->upPitch, d->stream);
@@ -328,7 +335,7 @@ void enqueue_head(sift_hip_detector* d, const float* img, int pitchFloats) {
     } else {
         const OctGeom& g = d->pyr.oct[0];
         d->timed("blur_init", (double)W * H * 8, [&] {
-            launch_blur(img, pitchFloats, 1, W, H, g.base, g.pitch, nullptr, d->initTaps, d->stream);
+            launch_blur(img, pitchFloats, 1, W, H, g.base, g.pitch, nullptr, d->initTaps, d->stream, d->dRange);
         });
     }
 }
@@ -337,14 +344,13 @@ void enqueue_body(sift_hip_detector* d, int buf) {
     hipStream_t s = d->stream;
     const int L = d->L;
     d->timed("memset", 0, [&] {
-        (void)hipMemsetAsync(d->dCtr, 0, sizeof(Counters), s);
         (void)hipMemsetAsync(d->dBcount, 0, sizeof(unsigned) * (size_t)d->kp.numBuckets, s);
         (void)hipMemsetAsync(d->dBitmap, 0, sizeof(uint32_t) * d->bitmapWords, s);
     });
     if (d->firstOctave < 0) {
         const OctGeom& g = d->pyr.oct[0];
         d->timed("blur_init", (double)g.W * g.H * 8, [&] {
-            launch_blur(d->dUp, d->upPitch, 1, g.W, g.H, g.base, g.pitch, nullptr, d->initTaps, s);
+            launch_blur(d->dUp, d->upPitch, 1, g.W, g.H, g.base, g.pitch, nullptr, d->initTaps, s, d->dRange);
         });
     }
     static const char* blurNames[kMaxOctaves] = {"blur_o0", "blur_o1", "blur_o2", "blur_o3", "blur_o4", "blur_o5",
@@ -382,12 +388,10 @@ void enqueue_body(sift_hip_detector* d, int buf) {
     d->timed("bucket_scatter", 0,
              [&] { launch_bucket_scatter(d->dOri, d->dCtr, d->dBoff, d->dSlot, d->dOrder, d->kp, s); });
     d->timed("bucket_rank", 0, [&] {
-        launch_bucket_rank(d->dOri, d->dBcount, d->dBoff, d->dOrder, d->dCtr, d->dFinalOrder, d->kp, s);
+        launch_bucket_rank(d->pyr, d->dOri, d->dBcount, d->dBoff, d->dOrder, d->dCtr, d->dJobs, d->dKpts3[buf],
+                           d->dFeats4[buf], d->kp, s);
     });
-    d->timed("descriptor", 0, [&] {
-        launch_descriptor(d->pyr, d->dOri, d->dFinalOrder, d->dCtr, d->dKpts3[buf], d->dFeats4[buf], d->dDesc[buf],
-                          d->kp, s);
-    });
+    d->timed("descriptor", 0, [&] { launch_descriptor(d->dJobs, d->dCtr, d->dRange, d->dDesc[buf], d->kp, s); });
     (void)hipMemcpyAsync(d->hCtr, d->dCtr, sizeof(Counters), hipMemcpyDeviceToHost, s);
 }
 

@@ -466,9 +466,48 @@ void launch_bucket_scatter(const OriKpt* kpts, const Counters* ctr, const unsign
     hipLaunchKernelGGL(k_bucket_scatter, dim3(256), dim3(256), 0, s, kpts, ctr, boff, slot, order, kp);
 }
 
-__global__ __launch_bounds__(256) void k_bucket_rank(const OriKpt* __restrict__ kpts, const unsigned* __restrict__ bcount,
+// Descriptor job of one final keypoint: calcDescriptorsComputer (unpackOctave,
+// octave scale, angle flip 360 - angle) and the head of calcSIFTDescriptor
+// (cos/sin / hist_width, radius clamped to the image diagonal), computed once
+// per keypoint here so the descriptor workgroup starts from scalar loads.
+__device__ DescJob make_desc_job(const PyrDesc& pyr, const OriKpt& kpt) {
+    DescJob j;
+    int octave = kpt.octave & 255;
+    const int layer = (kpt.octave >> 8) & 255;
+    octave = octave < 128 ? octave : (-128 | octave);
+    const float scale = octave >= 0 ? 1.f / (float)(1 << octave) : (float)(1 << -octave);
+    const float size = kpt.size * scale;
+    const float ptfx = kpt.x * scale, ptfy = kpt.y * scale;
+    const OctGeom& g = pyr.oct[octave - pyr.firstOctave];
+    j.img = g.base + (size_t)layer * g.planeStride;
+    j.pitch = g.pitch;
+    j.rows = g.H;
+    j.cols = g.W;
+    float angle = 360.f - kpt.angle;
+    if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+    j.angle = angle;
+    const float scl = size * 0.5f;
+    j.ptx = cv_round(ptfx);
+    j.pty = cv_round(ptfy);
+    j.hist_width = 3.f * scl;
+    int radius = cv_round(j.hist_width * 1.4142135623730951f * (float)(4 + 1) * 0.5f);
+    radius = min(radius, (int)sqrt((double)g.W * g.W + (double)g.H * g.H));
+    j.radius = radius;
+    const float arg = angle * (float)(M_PI / 180);  // cosf/sinf via double
+    j.cos_t = (float)cos((double)arg) / j.hist_width;
+    j.sin_t = (float)sin((double)arg) / j.hist_width;
+    j.pad[0] = j.pad[1] = j.pad[2] = j.pad[3] = 0;
+    return j;
+}
+
+// Final order inside each row bucket (rank by sub key), then write the
+// keypoint's outputs (reference layout Detector.hh:54-57: float3 {x, y,
+// layer}, float4 {packed octave, size, response, angle}) and its descriptor job.
+__global__ __launch_bounds__(256) void k_bucket_rank(PyrDesc pyr, const OriKpt* __restrict__ kpts,
+                                                     const unsigned* __restrict__ bcount,
                                                      const unsigned* __restrict__ boff, const int* __restrict__ order,
-                                                     const Counters* __restrict__ ctr, int* __restrict__ final_order,
+                                                     const Counters* __restrict__ ctr, DescJob* __restrict__ jobs,
+                                                     float* __restrict__ kpts3, float* __restrict__ feats4,
                                                      KeypointParams kp) {
     const int lane = threadIdx.x & 63;
     const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -492,205 +531,24 @@ __global__ __launch_bounds__(256) void k_bucket_rank(const OriKpt* __restrict__ 
                 const unsigned lim = min(64u, cnt - f0);
                 for (unsigned l = 0; l < lim; l++) rank += (unsigned)(__shfl(sf, (int)l) < se);
             }
-            if (e < cnt && base + rank < cap) final_order[base + rank] = idx;
+            const unsigned pos = base + rank;
+            if (e < cnt && pos < cap) {
+                const OriKpt k = kpts[idx];
+                jobs[pos] = make_desc_job(pyr, k);
+                kpts3[3 * (size_t)pos + 0] = k.x;
+                kpts3[3 * (size_t)pos + 1] = k.y;
+                kpts3[3 * (size_t)pos + 2] = (float)((k.octave >> 8) & 255);
+                reinterpret_cast<float4*>(feats4)[pos] = make_float4((float)k.octave, k.size, k.response, k.angle);
+            }
         }
     }
 }
 
-void launch_bucket_rank(const OriKpt* kpts, const unsigned* bcount, const unsigned* boff, const int* order,
-                        const Counters* ctr, int* final_order, const KeypointParams& kp, hipStream_t s) {
-    hipLaunchKernelGGL(k_bucket_rank, dim3(256), dim3(256), 0, s, kpts, bcount, boff, order, ctr, final_order, kp);
+void launch_bucket_rank(const PyrDesc& pyr, const OriKpt* kpts, const unsigned* bcount, const unsigned* boff,
+                        const int* order, const Counters* ctr, DescJob* jobs, float* kpts3, float* feats4,
+                        const KeypointParams& kp, hipStream_t s) {
+    hipLaunchKernelGGL(k_bucket_rank, dim3(256), dim3(256), 0, s, pyr, kpts, bcount, boff, order, ctr, jobs, kpts3,
+                       feats4, kp);
 }
-
-#if 0  // superseded by descriptor.hip (LDS float atomics were the bottleneck)
-// ---------------------------------------------------------------------------
-// calcSIFTDescriptor (OpenCV 4.x sift.simd.hpp), one 256-thread workgroup per
-// keypoint.  The (2R+3)^2 patch around the keypoint is staged in LDS first.
-// Each thread walks a contiguous run of the (2R+1)^2 raster (so the 64 lanes of
-// a wave sit ~R/4 rows apart and their LDS atomics rarely collide); each wave
-// accumulates its trilinear contributions into a private LDS histogram (6 x 6
-// x 10 bins), the 4 copies are summed in fixed order (deterministic run to
-// run), then wrap, L2 norm (8 fma lanes + v_reduce_sum order), 0.2 clip,
-// renorm and x512 round to 0..255 exactly as the oracle.  Output layout is the
-// reference's (Detector.hh:54-57).
-// Reference: SiftOps.cu:454-623 (modff bins, half(x512), serial lane-0
-// normalisation, SURVEY A-10).
-// ---------------------------------------------------------------------------
-constexpr int kD = 4, kN = 8;
-constexpr int kHistLen = (kD + 2) * (kD + 2) * (kN + 2);  // 360
-constexpr int kHistStride = kHistLen + 8;
-
-__global__ __launch_bounds__(256) void k_descriptor(PyrDesc pyr, const OriKpt* __restrict__ kpts,
-                                                    const int* __restrict__ final_order,
-                                                    const Counters* __restrict__ ctr, float* __restrict__ kpts3,
-                                                    float* __restrict__ feats4, uint16_t* __restrict__ desc,
-                                                    KeypointParams kp) {
-    extern __shared__ float lds_desc[];
-    float* hist = lds_desc;                       // 4 x kHistStride
-    float* raw = hist + 4 * kHistStride;          // 128
-    float* nacc = raw + 128;                      // 8 + 1
-    float* patch = nacc + 16;                     // (2Rmax+3)^2
-    const int tid = threadIdx.x, w = tid >> 6;
-    const unsigned n = ctr->final_n;
-    const int fo = pyr.firstOctave;
-    for (unsigned p = blockIdx.x; p < n; p += gridDim.x) {
-        const OriKpt kpt = kpts[final_order[p]];
-        int octave = kpt.octave & 255;
-        const int layer = (kpt.octave >> 8) & 255;
-        octave = octave < 128 ? octave : (-128 | octave);
-        const float scale = octave >= 0 ? 1.f / (float)(1 << octave) : (float)(1 << -octave);
-        const float size = kpt.size * scale;
-        const float ptfx = kpt.x * scale, ptfy = kpt.y * scale;
-        const OctGeom& g = octave_geom(pyr, octave - fo);
-        const float* img = g.base + (size_t)layer * g.planeStride;
-        const int pitch = g.pitch, rows = g.H, cols = g.W;
-        float angle = 360.f - kpt.angle;
-        if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
-        const float scl = size * 0.5f;
-
-        const int ptx = cv_round(ptfx), pty = cv_round(ptfy);
-        const float arg = angle * (float)(M_PI / 180);
-        float cos_t = (float)cos((double)arg);
-        float sin_t = (float)sin((double)arg);
-        const float bins_per_rad = kN / 360.f;
-        const float exp_scale = -1.f / (kD * kD * 0.5f);
-        const float hist_width = 3.f * scl;
-        int radius = cv_round(hist_width * 1.4142135623730951f * (float)(kD + 1) * 0.5f);
-        radius = min(radius, (int)sqrt((double)cols * cols + (double)rows * rows));
-        cos_t /= hist_width;
-        sin_t /= hist_width;
-        const int side = 2 * radius + 1, total = side * side;
-        const bool staged = radius <= kp.descRmax;
-        const int ps = side + 2, py0 = pty - radius - 1, px0 = ptx - radius - 1;
-
-        for (int i = tid; i < 4 * kHistStride; i += 256) hist[i] = 0.f;
-        if (staged) stage_patch<16>(patch, img, pitch, cols, rows, py0, px0, ps, tid, 256);
-        __syncthreads();
-
-        float* hw = hist + w * kHistStride;
-        const int run = (total + 255) / 256;
-        const int k0 = tid * run, k1 = min(k0 + run, total);
-        int i = k0 / side - radius, j = k0 - (k0 / side) * side - radius;
-        for (int k = k0; k < k1; k++) {
-            const float c_rot = (float)j * cos_t - (float)i * sin_t;
-            const float r_rot = (float)j * sin_t + (float)i * cos_t;
-            float rbin = r_rot + (float)(kD / 2) - 0.5f;
-            float cbin = c_rot + (float)(kD / 2) - 0.5f;
-            const int r = pty + i, c = ptx + j;
-            if (rbin > -1 && rbin < kD && cbin > -1 && cbin < kD && r > 0 && r < rows - 1 && c > 0 && c < cols - 1) {
-                float dx, dy;
-                if (staged) {
-                    const float* pp = patch + (r - py0) * ps + (c - px0);
-                    dx = pp[1] - pp[-1];
-                    dy = pp[-ps] - pp[ps];
-                } else {
-                    const float* pp = img + (size_t)r * pitch + c;
-                    dx = pp[1] - pp[-1];
-                    dy = pp[-pitch] - pp[pitch];
-                }
-                const float wgt = cv_exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, c_exptab);
-                const float gori = cv_fast_atan2(dy, dx);
-                const float gmag = cv_magnitude(dx, dy);
-                float obin = (gori - angle) * bins_per_rad;
-                const float mag = gmag * wgt;
-                const int r0 = cv_floor(rbin), c0 = cv_floor(cbin);
-                int o0 = cv_floor(obin);
-                rbin -= (float)r0;
-                cbin -= (float)c0;
-                obin -= (float)o0;
-                if (o0 < 0) o0 += kN;
-                if (o0 >= kN) o0 -= kN;
-                const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
-                const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
-                const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
-                const float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
-                const float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
-                const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
-                const float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
-                const int hidx = ((r0 + 1) * (kD + 2) + c0 + 1) * (kN + 2) + o0;
-                atomicAdd(&hw[hidx], v_rco000);
-                atomicAdd(&hw[hidx + 1], v_rco001);
-                atomicAdd(&hw[hidx + (kN + 2)], v_rco010);
-                atomicAdd(&hw[hidx + (kN + 3)], v_rco011);
-                atomicAdd(&hw[hidx + (kD + 2) * (kN + 2)], v_rco100);
-                atomicAdd(&hw[hidx + (kD + 2) * (kN + 2) + 1], v_rco101);
-                atomicAdd(&hw[hidx + (kD + 3) * (kN + 2)], v_rco110);
-                atomicAdd(&hw[hidx + (kD + 3) * (kN + 2) + 1], v_rco111);
-            }
-            if (++j > radius) {
-                j = -radius;
-                i++;
-            }
-        }
-        __syncthreads();
-        if (tid < 128) {
-            // wrap the two extra orientation bins into bins 0 and 1, sum the 4 copies in fixed order
-            const int ii = tid >> 5, jj = (tid >> 3) & 3, kk = tid & 7;
-            const int hidx = ((ii + 1) * (kD + 2) + (jj + 1)) * (kN + 2) + kk;
-            float v = ((hist[hidx] + hist[kHistStride + hidx]) + hist[2 * kHistStride + hidx]) + hist[3 * kHistStride + hidx];
-            if (kk < 2) {
-                const int h2 = hidx + kN;
-                const float e = ((hist[h2] + hist[kHistStride + h2]) + hist[2 * kHistStride + h2]) + hist[3 * kHistStride + h2];
-                v = v + e;
-            }
-            raw[tid] = v;
-        }
-        __syncthreads();
-        if (tid < 8) {
-            float a = 0.f;
-#pragma unroll
-            for (int q = 0; q < 16; q++) a = __fmaf_rn(raw[tid + 8 * q], raw[tid + 8 * q], a);
-            nacc[tid] = a;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            const float t0 = nacc[0] + nacc[4], t1 = nacc[1] + nacc[5], t2 = nacc[2] + nacc[6], t3 = nacc[3] + nacc[7];
-            float nrm2 = (t0 + t2) + (t1 + t3);
-            const float thr = __builtin_sqrtf(nrm2) * 0.2f;
-            nrm2 = 0.f;
-#pragma unroll 1
-            for (int q0 = 0; q0 < 128; q0 += 8) {
-                float vals[8];
-#pragma unroll
-                for (int u = 0; u < 8; u++) vals[u] = raw[q0 + u];
-#pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const float val = fminf(vals[u], thr);
-                    raw[q0 + u] = val;
-                    nrm2 = nrm2 + val * val;
-                }
-            }
-            nacc[8] = 512.f / fmaxf(__builtin_sqrtf(nrm2), FLT_EPSILON);
-            float* k3 = kpts3 + 3 * (size_t)p;
-            k3[0] = kpt.x;
-            k3[1] = kpt.y;
-            k3[2] = (float)layer;
-            float4 f;
-            f.x = (float)kpt.octave;
-            f.y = kpt.size;
-            f.z = kpt.response;
-            f.w = kpt.angle;
-            reinterpret_cast<float4*>(feats4)[p] = f;
-        }
-        __syncthreads();
-        if (tid < 128) {
-            int v = cv_round(raw[tid] * nacc[8]);
-            v = v < 0 ? 0 : (v > 255 ? 255 : v);
-            const _Float16 hv = (_Float16)(float)v;
-            desc[(size_t)p * 128 + tid] = __builtin_bit_cast(uint16_t, hv);
-        }
-        __syncthreads();
-    }
-}
-
-void launch_descriptor(const PyrDesc& pyr, const OriKpt* kpts, const int* final_order, const Counters* ctr,
-                       float* kpts3, float* feats4, uint16_t* desc, const KeypointParams& kp, hipStream_t s) {
-    const int ps = 2 * kp.descRmax + 3;
-    const size_t lds = sizeof(float) * (4 * kHistStride + 128 + 16 + (size_t)ps * ps);
-    hipLaunchKernelGGL(k_descriptor, dim3(2048), dim3(256), lds, s, pyr, kpts, final_order, ctr, kpts3, feats4, desc,
-                       kp);
-}
-
-#endif
 
 }  // namespace sift_amd

@@ -68,7 +68,7 @@ constexpr int BLUR_TH = 32;
 template <int R>
 __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, int spitch, int sstep, int W, int H,
                                               float* __restrict__ dst, int dpitch, float* __restrict__ copy_out,
-                                              Taps taps) {
+                                              Taps taps, unsigned* __restrict__ range_keys) {
     constexpr int IW = (BLUR_TW + 2 * R + 3) & ~3;  // row stride, multiple of 4 floats
     constexpr int IH = BLUR_TH + 2 * R;
     constexpr int NW = (2 * R + 4 + 3) / 4;          // float4 reads per row window
@@ -151,6 +151,7 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, int
 #pragma unroll
         for (int j = 0; j < 8 + 2 * R; j++) win[j] = mid[(yb + j) * BLUR_TW + lx];
         const int gx = x0 + lx;
+        float mx = -FLT_MAX, nmn = -FLT_MAX;
 #pragma unroll
         for (int q = 0; q < 8; q++) {
             float s = __fmaf_rn(win[q + R], taps.w[R], 0.f);
@@ -160,17 +161,41 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, int
             if (gy < H && gx < W) {
                 dst[(size_t)gy * dpitch + gx] = s;
                 if (copy_out) copy_out[(size_t)gy * dpitch + gx] = in[(yb + q + R) * IW + lx + R];
+                mx = fmaxf(mx, s);
+                nmn = fmaxf(nmn, -s);
+            }
+        }
+        // Pixel range of the plane (requested for octave 0 / plane 0 only: every
+        // later plane is a convex combination of it).  The descriptor sizes its
+        // fixed-point histogram scale from it.
+        if (range_keys) {
+            for (int off = 32; off > 0; off >>= 1) {
+                mx = fmaxf(mx, __shfl_xor(mx, off));
+                nmn = fmaxf(nmn, __shfl_xor(nmn, off));
+            }
+            __syncthreads();  // reuse `mid` for the per-wave partials
+            if (lane == 0) {
+                mid[wave] = mx;
+                mid[4 + wave] = nmn;
+            }
+            __syncthreads();
+            if (tid == 0) {  // spread over kRangeSlots address pairs: no single hot atomic
+                unsigned* slot = range_keys + 2 * ((blockIdx.y * gridDim.x + blockIdx.x) % kRangeSlots);
+                atomicMax(slot, range_key(fmaxf(fmaxf(mid[0], mid[1]), fmaxf(mid[2], mid[3]))));
+                atomicMax(slot + 1, range_key(fmaxf(fmaxf(mid[4], mid[5]), fmaxf(mid[6], mid[7]))));
             }
         }
     }
 }
 
-using BlurLaunch = void (*)(dim3, hipStream_t, const float*, int, int, int, int, float*, int, float*, const Taps&);
+using BlurLaunch = void (*)(dim3, hipStream_t, const float*, int, int, int, int, float*, int, float*, const Taps&,
+                            unsigned*);
 
 template <int R>
 void blur_launch_r(dim3 grid, hipStream_t s, const float* src, int spitch, int sstep, int W, int H, float* dst,
-                   int dpitch, float* copy_out, const Taps& taps) {
-    hipLaunchKernelGGL(k_blur<R>, grid, dim3(256), 0, s, src, spitch, sstep, W, H, dst, dpitch, copy_out, taps);
+                   int dpitch, float* copy_out, const Taps& taps, unsigned* range_keys) {
+    hipLaunchKernelGGL(k_blur<R>, grid, dim3(256), 0, s, src, spitch, sstep, W, H, dst, dpitch, copy_out, taps,
+                       range_keys);
 }
 
 template <int... Rs>
@@ -180,10 +205,10 @@ constexpr std::array<BlurLaunch, sizeof...(Rs)> blur_table(std::integer_sequence
 static const std::array<BlurLaunch, kMaxTaps / 2> kBlurTable = blur_table(std::make_integer_sequence<int, kMaxTaps / 2>{});
 
 void launch_blur(const float* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, float* copy_out,
-                 const Taps& taps, hipStream_t s) {
+                 const Taps& taps, hipStream_t s, unsigned* range_keys) {
     const int r = taps.n >> 1;  // 1 .. kMaxTaps/2 (taps.n >= 3 by construction)
     dim3 grid((W + BLUR_TW - 1) / BLUR_TW, (H + BLUR_TH - 1) / BLUR_TH);
-    kBlurTable[r - 1](grid, s, src, spitch, sstep, W, H, dst, dpitch, copy_out, taps);
+    kBlurTable[r - 1](grid, s, src, spitch, sstep, W, H, dst, dpitch, copy_out, taps, range_keys);
 }
 
 // ---------------------------------------------------------------------------

@@ -62,8 +62,13 @@ struct Counters {
 
 // --- launch wrappers (implemented in pyramid.hip / keypoints.hip / match.hip) --
 void launch_upsample2x(const float* src, int spitch, int W, int H, float* dst, int dpitch, hipStream_t s);
+// Pixel range of octave 0 / plane 0 (every later plane is a convex combination
+// of it), accumulated by the initial blur as kRangeSlots pairs of
+// order-preserving keys {max(v), max(-v)} (atomicMax spread over slots).
+constexpr int kRangeSlots = 256;
+// range_keys (nullable): 2 * kRangeSlots keys, zeroed before the launch.
 void launch_blur(const float* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, float* copy_out,
-                 const Taps& taps, hipStream_t s);
+                 const Taps& taps, hipStream_t s, unsigned* range_keys = nullptr);
 void launch_extrema(const PyrDesc& pyr, int o, float threshold, uint2* cand, Counters* ctr, unsigned cap,
                     hipStream_t s);
 
@@ -85,10 +90,36 @@ void launch_bucket_count(const OriKpt* kpts, const Counters* ctr, unsigned* bcou
 void launch_bucket_scan(unsigned* bcount, unsigned* boff, Counters* ctr, const KeypointParams& kp, hipStream_t s);
 void launch_bucket_scatter(const OriKpt* kpts, const Counters* ctr, const unsigned* boff, const int* slot,
                            int* order, const KeypointParams& kp, hipStream_t s);
-void launch_bucket_rank(const OriKpt* kpts, const unsigned* bcount, const unsigned* boff, const int* order,
-                        const Counters* ctr, int* final_order, const KeypointParams& kp, hipStream_t s);
-void launch_descriptor(const PyrDesc& pyr, const OriKpt* kpts, const int* final_order, const Counters* ctr,
-                       float* kpts3, float* feats4, uint16_t* desc, const KeypointParams& kp, hipStream_t s);
+// One final keypoint's descriptor window (written by k_bucket_rank, read with
+// scalar loads by k_descriptor).  64 bytes.
+constexpr int kDescMaxRows = 128;  // enumerated windows: 2 * radius + 1 <= kDescMaxRows
+struct DescJob {
+    const float* img;        // Gaussian plane (octave, layer) of the keypoint
+    float cos_t, sin_t;      // cos/sin(angle) / hist_width
+    float angle;             // 360 - kpt.angle (0 when that is 360)
+    float hist_width;        // 3 * scl
+    int ptx, pty;            // rounded keypoint position in the octave
+    int rows, cols, pitch;   // plane geometry
+    int radius;              // window radius (clamped to the plane diagonal)
+    int pad[4];
+};
+static_assert(sizeof(DescJob) == 64, "DescJob is one 64-byte scalar load");
+
+void launch_bucket_rank(const PyrDesc& pyr, const OriKpt* kpts, const unsigned* bcount, const unsigned* boff,
+                        const int* order, const Counters* ctr, DescJob* jobs, float* kpts3, float* feats4,
+                        const KeypointParams& kp, hipStream_t s);
+void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned* range_keys, uint16_t* desc,
+                       const KeypointParams& kp, hipStream_t s);
+
+// Order-preserving unsigned key of a float (0 is below every key), so that
+// atomicMax over keys is a float max with a zeroed counter as the identity.
+__device__ __forceinline__ unsigned range_key(float f) {
+    const unsigned u = __float_as_uint(f);
+    return u & 0x80000000u ? ~u : u | 0x80000000u;
+}
+__device__ __forceinline__ float decode_range_key(unsigned u) {
+    return __uint_as_float(u & 0x80000000u ? u & 0x7fffffffu : ~u);
+}
 
 // Exp table (OpenCV expTab_f) uploaded once per device.
 void upload_exp_table(const float* tab64);

@@ -76,4 +76,13 @@ __device__ __forceinline__ int reflect101(int p, int len) {
     return p;
 }
 
+// Workgroup barrier ordering LDS only.  __syncthreads() also fences global
+// memory, i.e. waits for every outstanding global load (vmcnt(0)) -- which
+// would drain loads deliberately issued ahead across the barrier.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 }  // namespace sift_amd

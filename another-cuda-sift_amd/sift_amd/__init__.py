@@ -24,7 +24,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.normpath(os.path.join(_HERE, "..", "lib"))
-LIB_PATH = os.path.join(LIB_DIR, "libsift_hip.so")
+# SIFT_HIP_LIB: alternative build of the same library (kernel A/B experiments).
+LIB_PATH = os.environ.get("SIFT_HIP_LIB") or os.path.join(LIB_DIR, "libsift_hip.so")
 
 SIFT_HIP_OK = 0
 _lib = None
