@@ -32,6 +32,7 @@ import torch.distributed as dist  # noqa: E402
 import numpy as np  # noqa: E402
 
 import sift_amd as sift  # noqa: E402
+from sift_amd import multi  # noqa: E402
 
 METRIC = "detectAndCompute Mpix/s + 2kx2k 128-D match ms at 1/2/4/8 MI355X"
 W, H = 1920, 1200
@@ -205,18 +206,17 @@ def main():
     c5 = None
     if world > 1:
         mine = sets[rank % 2].contiguous()
-        gathered = torch.empty((world, nq, 128), dtype=torch.int16, device=dev)
         for _ in range(5):
-            dist.all_gather_into_tensor(gathered, mine)
+            gathered, counts = multi.all_gather_sets(mine, nq, world)
         torch.cuda.synchronize()
         ag0, ag1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ag0.record()
         for _ in range(20):
-            dist.all_gather_into_tensor(gathered, mine)
+            gathered, counts = multi.all_gather_sets(mine, nq, world)
         ag1.record()
         torch.cuda.synchronize()
         ag_us = max_over_ranks(ag0.elapsed_time(ag1) / 20 * 1e3)
-        peers = [j for j in range(world) if j != rank]
+        peers = [j for _, j in multi.peer_pairs(rank, world)]
         P = len(peers)
         bi = torch.empty((P * nq, 2), dtype=torch.int32, device=dev)
         bm = sift.Matcher(nq, nq, max_pairs=P, device=local)
@@ -236,7 +236,7 @@ def main():
         torch.cuda.synchronize()
         c5 = {"allgather_us": round(ag_us, 2), "pairs_per_gpu": P,
               "batched_match_ms": round(max_over_ranks(m0.elapsed_time(m1) / 50), 4),
-              "collective": "RCCL all_gather_into_tensor (torch.distributed nccl backend)"}
+              "collective": "RCCL all_gather_into_tensor (torch.distributed nccl backend), sift_amd/multi.py"}
 
     # ---- CPU baseline: the oracle on the host cores (rank 0, N=1 only) -------
     cpu = None

@@ -54,6 +54,9 @@ CONFIGS = [
     (257, 191, True, 0, 0, 2),       # ragged, doubled base (OpenCV default firstOctave -1)
     (752, 480, False, 3, 5000, 0),   # BASELINE C2 shape family: 3 octaves
     (640, 360, True, 0, 300, 3),     # retainBest active
+    (1920, 1200, False, 3, 5000, 0),  # BASELINE C2 (the bench workload), full size
+    (1600, 900, False, 0, 5000, 4),   # BASELINE C4 frame shape, auto octaves
+    (1920, 1200, True, 0, 0, 7),      # OpenCV defaults (doubled base, keep all) at full HD
 ]
 
 
