@@ -62,6 +62,7 @@ void launch_upsample2x(const float* src, int spitch, int W, int H, float* dst, i
 // Column: s = fma(mid[y], w[R], 0); s = fma(mid[y+k]+mid[y-k], w[R+k], s)
 // Reference: Filter.cu:8-51 (no LDS, vertical first, modulo per tap).
 // ---------------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int BLUR_TW = 64;
 constexpr int BLUR_TH = 32;
 
@@ -74,7 +75,8 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, int
     constexpr int NW = (2 * R + 4 + 3) / 4;          // float4 reads per row window
     __shared__ __attribute__((aligned(16))) float in[IH * IW + 4];
     __shared__ __attribute__((aligned(16))) float mid[IH * BLUR_TW];
-    const int x0 = blockIdx.x * BLUR_TW, y0 = blockIdx.y * BLUR_TH;
+    const int tile = xcd_tile(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+    const int x0 = (tile % gridDim.x) * BLUR_TW, y0 = (tile / gridDim.x) * BLUR_TH;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
     // Stage the input tile: every thread issues all of its loads before its
@@ -115,17 +117,28 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, int
     __syncthreads();
 
     {
-        const int xq = (tid & 15) * 4;
-        for (int ly = tid >> 4; ly < IH; ly += 16) {
+        // ds_read_b128 serves a wave in four 16-lane groups {0-3,12-15,20-27},
+        // {4-11,16-19,28-31} (+32): give each group one row's 16 float4 blocks
+        // so every group covers the 64 banks exactly once (conflict-free for
+        // any row pitch).
+        const int l = lane & 31;
+        const bool grpB = (l >= 4 && l < 12) || (l >= 16 && l < 20) || l >= 28;
+        const int blk = grpB ? (l < 12 ? l - 4 : (l < 20 ? l - 8 : l - 16)) : (l < 4 ? l : (l < 16 ? l - 8 : l - 12));
+        const int xq = blk * 4;
+        for (int ly = wave * 4 + (lane >> 5) * 2 + (grpB ? 1 : 0); ly < IH; ly += 16) {
             float win[4 * NW];
-            const float4* p = reinterpret_cast<const float4*>(in + ly * IW + xq);
+            const f32x4* p = reinterpret_cast<const f32x4*>(in + ly * IW + xq);
 #pragma unroll
             for (int v = 0; v < NW; v++) {
-                const float4 f = p[v];
-                win[4 * v] = f.x;
-                win[4 * v + 1] = f.y;
-                win[4 * v + 2] = f.z;
-                win[4 * v + 3] = f.w;
+                f32x4 f = p[v];
+                // Opaque use of all four lanes: otherwise the compiler narrows
+                // the partly used last vector and splits the row into
+                // misaligned ds_read2_b32/b64 pieces (bank conflicts).
+                __asm__ volatile("" : "+v"(f));
+                win[4 * v] = f[0];
+                win[4 * v + 1] = f[1];
+                win[4 * v + 2] = f[2];
+                win[4 * v + 3] = f[3];
             }
             float s[4];
 #pragma unroll
@@ -232,7 +245,8 @@ __global__ __launch_bounds__(256) void k_extrema(OctGeom g, int Lrt, int o, floa
     extern __shared__ float dog[];  // (L+2) planes of EX_SH x EX_SW
     const int L = LT > 0 ? LT : Lrt;
     const int tid = threadIdx.x;
-    const int x0 = blockIdx.x * EX_TW, y0 = blockIdx.y * EX_TH;
+    const int tile = xcd_tile(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+    const int x0 = (tile % gridDim.x) * EX_TW, y0 = (tile / gridDim.x) * EX_TH;
     const int W = g.W, H = g.H, pitch = g.pitch;
     constexpr int PS = EX_SH * EX_SW;
     constexpr int PER = (PS + 255) / 256;
@@ -353,23 +367,153 @@ __global__ __launch_bounds__(256) void k_extrema(OctGeom g, int Lrt, int o, floa
     }
 }
 
+// Register-streaming variant for L = 1..6 (the common case).  One wave per
+// 62-column x EX2_TH-row strip: lane = column (lanes 0 and 63 only feed their
+// neighbours), rows stream top to bottom.  Per row: the L+3 Gaussian values
+// (one buffer address, plane offset in SGPR), the L+2 DoG values, each DoG
+// plane's horizontal 3-max/3-min through DPP wave shifts + v_max3/v_min3, then
+// the vertical 3-max/min over a 3-row ring and the 3-plane max/min per layer.
+// "v >= all 26 neighbours" is exactly "v >= max of the 3x3x3 block" (the block
+// contains v), so the test is OpenCV's, with ~4x fewer instructions than 26
+// LDS compares and no LDS staging.
+constexpr int EX2_TH = 8;              // output rows per wave
+constexpr int EX2_COLS = 62;           // output columns per wave (64 lanes - 2 halo)
+
+__device__ __forceinline__ float dpp_from_left(float v) {  // lane i <- lane i-1
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float dpp_from_right(float v) {  // lane i <- lane i+1
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
+
+template <int LT>
+__global__ __launch_bounds__(256) void k_extrema_rows(OctGeom g, int o, float thr, uint2* __restrict__ cand,
+                                                      Counters* __restrict__ ctr, unsigned cap) {
+    constexpr int NG = LT + 3, ND = LT + 2;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tile = xcd_tile(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+    const int x0 = (tile % gridDim.x) * EX2_COLS, y0 = ((tile / gridDim.x) * 4 + wave) * EX2_TH;
+    const int W = g.W, H = g.H, pitch = g.pitch;
+    const int x = x0 - 1 + lane;
+    const bool colOK = lane >= 1 && lane <= EX2_COLS && x >= 5 && x < W - 5;
+    const int xc = min(max(x, 0), W - 1);
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        g.base, 0, (int)min((long)NG * g.planeStride * 4, 0x7fffffffL), 0x00020000);
+    __shared__ unsigned s_cnt, s_base;
+    __shared__ uint2 s_list[EX_LIST];
+    if (tid == 0) s_cnt = 0;
+    __syncthreads();
+
+    auto load_row = [&](int y, float (&gv)[NG]) {
+        const unsigned off = (unsigned)(min(max(y, 0), H - 1) * pitch + xc) * 4u;
+#pragma unroll
+        for (int d = 0; d < NG; d++)
+            gv[d] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                  rsrc, off, (int)((long)d * g.planeStride * 4), 0));
+    };
+    // Per ring slot: horizontal max/min of every DoG plane, centre DoG of layers.
+    float hmx[3][ND], hmn[3][ND], dc[3][LT];
+    auto push_row = [&](const float (&gv)[NG], float (&mx)[ND], float (&mn)[ND], float (&c)[LT]) {
+#pragma unroll
+        for (int d = 0; d < ND; d++) {
+            const float v = gv[d + 1] - gv[d];
+            const float l = dpp_from_left(v), r = dpp_from_right(v);
+            mx[d] = fmaxf(fmaxf(v, l), r);
+            mn[d] = fminf(fminf(v, l), r);
+            if (d >= 1 && d <= LT) c[d - 1] = v;
+        }
+    };
+    auto emit = [&](bool hit, int layer, int r) {
+        const unsigned long long mask = __ballot(hit);
+        if (!mask) return;
+        unsigned basepos = 0;
+        if (lane == 0) basepos = atomicAdd(&s_cnt, (unsigned)__popcll(mask));
+        basepos = __shfl(basepos, 0);
+        if (hit) {
+            const unsigned pos = basepos + (unsigned)__popcll(mask & ((1ull << lane) - 1ull));
+            const uint2 q = make_uint2((unsigned)(o << 8 | layer), (unsigned)(r << 16 | x));
+            if (pos < EX_LIST) {
+                s_list[pos] = q;
+            } else {  // plateau-heavy tile: spill straight to the global list
+                const unsigned gp = atomicAdd(&ctr->cand, 1u);
+                if (gp < cap)
+                    cand[gp] = q;
+                else
+                    atomicOr(&ctr->overflow, 1u);
+            }
+        }
+    };
+    // Test row r (ring slot B = centre, A above, C below).
+    auto test_row = [&](int r, int A, int B, int C) {
+        if (r < 5 || r >= H - 5) return;  // wave-uniform
+        float vmx[ND], vmn[ND];
+#pragma unroll
+        for (int d = 0; d < ND; d++) {
+            vmx[d] = fmaxf(fmaxf(hmx[A][d], hmx[B][d]), hmx[C][d]);
+            vmn[d] = fminf(fminf(hmn[A][d], hmn[B][d]), hmn[C][d]);
+        }
+#pragma unroll
+        for (int l = 1; l <= LT; l++) {
+            const float v = dc[B][l - 1];
+            const float M = fmaxf(fmaxf(vmx[l - 1], vmx[l]), vmx[l + 1]);
+            const float m = fminf(fminf(vmn[l - 1], vmn[l]), vmn[l + 1]);
+            const bool hit = colOK && fabsf(v) > thr && ((v > 0 && v >= M) || (v < 0 && v <= m));
+            emit(hit, l, r);
+        }
+    };
+
+    if (y0 < H) {
+        float ga[NG], gb[NG];
+        load_row(y0 - 1, ga);
+        load_row(y0, gb);
+        push_row(ga, hmx[0], hmn[0], dc[0]);
+        load_row(y0 + 1, ga);
+        push_row(gb, hmx[1], hmn[1], dc[1]);
+        // Steady state: row y0 + k + 1 enters slot (k + 2) % 3, row y0 + k is tested.
+#pragma unroll
+        for (int k = 0; k < EX2_TH; k++) {
+            const int A = k % 3, B = (k + 1) % 3, C = (k + 2) % 3;
+            float (&cur)[NG] = (k & 1) ? gb : ga;
+            float (&nxt)[NG] = (k & 1) ? ga : gb;
+            if (k + 1 < EX2_TH) load_row(y0 + k + 2, nxt);  // one row ahead in flight
+            push_row(cur, hmx[C], hmn[C], dc[C]);
+            if (y0 + k < H) test_row(y0 + k, A, B, C);
+        }
+    }
+    __syncthreads();
+    const unsigned nl = min(s_cnt, (unsigned)EX_LIST);
+    if (tid == 0) s_base = nl ? atomicAdd(&ctr->cand, nl) : 0u;
+    __syncthreads();
+    for (unsigned k = tid; k < nl; k += 256) {
+        const unsigned pos = s_base + k;
+        if (pos < cap)
+            cand[pos] = s_list[k];
+        else
+            atomicOr(&ctr->overflow, 1u);
+    }
+}
+
 void launch_extrema(const PyrDesc& pyr, int o, float threshold, uint2* cand, Counters* ctr, unsigned cap,
                     hipStream_t s) {
     const OctGeom& g = pyr.oct[o];
+    if (pyr.L >= 1 && pyr.L <= 6) {
+        dim3 grid((g.W + EX2_COLS - 1) / EX2_COLS, (g.H + 4 * EX2_TH - 1) / (4 * EX2_TH));
+        switch (pyr.L) {
+#define SIFT_EX_CASE(LV) \
+    case LV: hipLaunchKernelGGL(k_extrema_rows<LV>, grid, dim3(256), 0, s, g, o, threshold, cand, ctr, cap); break;
+            SIFT_EX_CASE(1)
+            SIFT_EX_CASE(2)
+            SIFT_EX_CASE(3)
+            SIFT_EX_CASE(4)
+            SIFT_EX_CASE(5)
+            SIFT_EX_CASE(6)
+#undef SIFT_EX_CASE
+        }
+        return;
+    }
     dim3 grid((g.W + EX_TW - 1) / EX_TW, (g.H + EX_TH - 1) / EX_TH);
     const size_t lds = sizeof(float) * (size_t)(pyr.L + 2) * EX_SH * EX_SW;
-    switch (pyr.L) {
-#define SIFT_EX_CASE(LV) \
-    case LV: hipLaunchKernelGGL(k_extrema<LV>, grid, dim3(256), lds, s, g, pyr.L, o, threshold, cand, ctr, cap); break;
-        SIFT_EX_CASE(1)
-        SIFT_EX_CASE(2)
-        SIFT_EX_CASE(3)
-        SIFT_EX_CASE(4)
-        SIFT_EX_CASE(5)
-        SIFT_EX_CASE(6)
-#undef SIFT_EX_CASE
-        default: hipLaunchKernelGGL(k_extrema<0>, grid, dim3(256), lds, s, g, pyr.L, o, threshold, cand, ctr, cap);
-    }
+    hipLaunchKernelGGL(k_extrema<0>, grid, dim3(256), lds, s, g, pyr.L, o, threshold, cand, ctr, cap);
 }
 
 }  // namespace sift_amd

@@ -76,6 +76,16 @@ __device__ __forceinline__ int reflect101(int p, int len) {
     return p;
 }
 
+// XCD-aware tile order.  Workgroups are dispatched round-robin over the 8
+// XCDs (linear id b -> XCD b % 8) and each XCD has its own 4 MiB L2, so a
+// raster tile order scatters neighbouring tiles -- whose halos overlap --
+// over all eight L2s.  This bijection gives XCD k a contiguous run of tiles in
+// raster order, so halo re-reads mostly hit the L2 that loaded them.
+__device__ __forceinline__ int xcd_tile(int b, int ntiles) {
+    const int q = ntiles >> 3, rem = ntiles & 7, k = b & 7, i = b >> 3;
+    return k * q + min(k, rem) + i;
+}
+
 // Workgroup barrier ordering LDS only.  __syncthreads() also fences global
 // memory, i.e. waits for every outstanding global load (vmcnt(0)) -- which
 // would drain loads deliberately issued ahead across the barrier.
