@@ -30,33 +30,6 @@ constexpr float kOriPeakRatio = 0.8f;
 
 __device__ __forceinline__ const OctGeom& octave_geom(const PyrDesc& pyr, int o) { return pyr.oct[o]; }
 
-// Copy a ps x ps window (origin py0, px0) of a plane into LDS, zero outside the
-// image.  Each of the nt participating lanes has U independent loads in flight
-// before its first LDS store: one memory latency per U elements, not per element.
-template <int U>
-__device__ __forceinline__ void stage_patch(float* patch, const float* img, int pitch, int W, int H, int py0, int px0,
-                                            int ps, int t, int nt) {
-    const int total = ps * ps;
-    for (int base = t; base < total; base += nt * U) {
-        float v[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int idx = base + nt * u;
-            const int yy = py0 + idx / ps, xx = px0 + idx % ps;
-            const bool in = idx < total && yy >= 0 && yy < H && xx >= 0 && xx < W;
-            // Unconditional load from a clamped address, then select: a guarded
-            // load would make hipcc branch + vmcnt(0) per element (serial latency).
-            const float x = img[(size_t)min(max(yy, 0), H - 1) * pitch + min(max(xx, 0), W - 1)];
-            v[u] = in ? x : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int idx = base + nt * u;
-            if (idx < total) patch[idx] = v[u];
-        }
-    }
-}
-
 __device__ __forceinline__ float dog_at(const float* g, long ps, int pitch, int layer, int r, int c) {
     const float* p = g + (size_t)r * pitch + c;
     return p[(size_t)(layer + 1) * ps] - p[(size_t)layer * ps];
@@ -196,30 +169,46 @@ void launch_refine(const PyrDesc& pyr, const uint2* cand, unsigned capCand, Coun
 }
 
 // ---------------------------------------------------------------------------
-// calcOrientationHist + peak search (OpenCV 4.x sift.simd.hpp), one wave64 per
-// refined keypoint, on the Gaussian plane of the refined layer.  The wave first
-// stages its (2R+3)^2 patch in LDS (one burst of independent loads), then
-// produces samples 64 at a time in raster order; lane b (< 36) owns histogram
-// bin b and adds the chunk's contributions in lane order, so every bin sees
-// exactly the oracle's sequential summation order (adding +0.f for
-// non-matching samples is exact).  Smoothing, max and peak interpolation use
-// wave shuffles.  Radii above the host-computed bound read HBM directly.
+// calcOrientationHist + peak search (OpenCV 4.x sift.simd.hpp), one wave64
+// (a 64-thread workgroup) per refined keypoint, on the Gaussian plane of the
+// refined layer.  OpenCV sums each of the 36 bins sequentially in float over
+// the window's samples in raster order, so that order is kept exactly:
+// samples are produced 64 at a time in raster order (lane = sample; gradients
+// by bounds-checked buffer loads straight from the plane); six ballots group
+// the chunk's lanes by bin, a scan over the 36 group sizes packs the chunk's
+// values bin by bin (lane order inside a bin) into a 64-entry LDS buffer, and
+// lane b (< 36) adds its bin's values to its running sum in that order --
+// OpenCV's sequential sum, carried in a register across chunks.  <1 KB of LDS
+// per keypoint.  Smoothing, max and peak interpolation use wave shuffles.
 // Reference: SiftOps.cu:237-376 (DoG plane, 32-lane LDS atomics, floor bins,
 // no interpolation, SURVEY A-9).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_orientation(PyrDesc pyr, const RefKpt* __restrict__ in,
-                                                     Counters* __restrict__ ctr, OriKpt* __restrict__ out,
-                                                     KeypointParams kp) {
-    extern __shared__ float lds_ori[];
-    const int lane = threadIdx.x & 63;
-    const int PSMAX = 2 * kp.oriRmax + 3;
-    float* patch = lds_ori + (threadIdx.x >> 6) * PSMAX * PSMAX;
-    const unsigned wave = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const unsigned nwaves = gridDim.x * 4;
+typedef unsigned u32x4_k __attribute__((ext_vector_type(4)));
+struct RefWords {
+    u32x4_k w[2];
+};
+
+__device__ __forceinline__ RefKpt load_ref(const RefKpt* in, unsigned k) {  // scalar (constant address space)
+    const __attribute__((address_space(4))) u32x4_k* c = (const __attribute__((address_space(4))) u32x4_k*)(in + k);
+    RefWords r;
+    r.w[0] = c[0];
+    r.w[1] = c[1];
+    return __builtin_bit_cast(RefKpt, r);
+}
+
+__global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* __restrict__ in,
+                                                    Counters* __restrict__ ctr, OriKpt* __restrict__ out,
+                                                    KeypointParams kp) {
+    __shared__ float chunk[64];
+    __shared__ int ccnt[kOriBins + 4], coff[kOriBins + 4];
+    __shared__ float s_exptab[64];
+    const int lane = threadIdx.x;
+    s_exptab[lane] = c_exptab[lane];
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
     const unsigned n = min(ctr->refined, kp.capRefined);
     const int fo = pyr.firstOctave;
-    for (unsigned k = wave; k < n; k += nwaves) {
-        const RefKpt kpt = in[k];
+    for (unsigned k = blockIdx.x; k < n; k += gridDim.x) {
+        const RefKpt kpt = load_ref(in, k);
         const int o = kpt.o, layer = kpt.layer, r = kpt.rc >> 16, c = kpt.rc & 0xffff;
         const OctGeom& g = octave_geom(pyr, o);
         const float* img = g.base + (size_t)layer * g.planeStride;
@@ -229,55 +218,55 @@ __global__ __launch_bounds__(256) void k_orientation(PyrDesc pyr, const RefKpt* 
         const float sigma = kOriSigFctr * scl_octv;
         const float expf_scale = -1.f / (2.f * sigma * sigma);
         const int side = 2 * radius + 1, total = side * side;
-        const bool staged = radius <= kp.oriRmax;
-        const int ps = side + 2, py0 = r - radius - 1, px0 = c - radius - 1;
-        if (staged) {
-            stage_patch<8>(patch, img, pitch, W, H, py0, px0, ps, lane, 64);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
+        const unsigned mside = (unsigned)(4294967296.0 / side) + 1u;  // idx / side == umulhi(idx, mside)
+        const __amdgpu_buffer_rsrc_t rsrc =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(img), 0, H * pitch * 4, 0x00020000);
 
-        float acc = 0.f;
+        float acc = 0.f;  // temphist[lane] for lane < 36
         for (int base = 0; base < total; base += 64) {
             const int idx = base + lane;
-            int bin = -1;
-            float val = 0.f;
-            if (idx < total) {
-                const int i = idx / side - radius, j = idx - (idx / side) * side - radius;
-                const int y = r + i, x = c + j;
-                if (y > 0 && y < H - 1 && x > 0 && x < W - 1) {
-                    float dx, dy;
-                    if (staged) {
-                        const float* p = patch + (y - py0) * ps + (x - px0);
-                        dx = p[1] - p[-1];
-                        dy = p[-ps] - p[ps];
-                    } else {
-                        const float* p = img + (size_t)y * pitch + x;
-                        dx = p[1] - p[-1];
-                        dy = p[-pitch] - p[pitch];
-                    }
-                    const float w = cv_exp32f((float)(i * i + j * j) * expf_scale, c_exptab);
-                    const float ori = cv_fast_atan2(dy, dx);
-                    const float mag = cv_magnitude(dx, dy);
-                    int b = cv_round((kOriBins / 360.f) * ori);
-                    if (b >= kOriBins) b -= kOriBins;
-                    if (b < 0) b += kOriBins;
-                    bin = b;
-                    val = w * mag;
-                }
-            }
+            const int i = (int)__umulhi((unsigned)idx, mside), j = idx - i * side;
+            const int y = r + i - radius, x = c + j - radius;
+            const bool valid = idx < total && y > 0 && y < H - 1 && x > 0 && x < W - 1;
+            const unsigned o0 = valid ? (unsigned)(y * pitch + x) * 4u : 0x80000000u;
+            const float xl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o0 - 4u, 0, 0));
+            const float xr = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o0 + 4u, 0, 0));
+            const float yu = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o0 - 4u * pitch, 0, 0));
+            const float yd = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o0 + 4u * pitch, 0, 0));
+            const int ii = i - radius, jj = j - radius;
+            const float dx = xr - xl, dy = yu - yd;
+            const float w = cv_exp32f((float)(ii * ii + jj * jj) * expf_scale, s_exptab);
+            const float ori = cv_fast_atan2(dy, dx);
+            const float mag = cv_magnitude(dx, dy);
+            int bin = cv_round((kOriBins / 360.f) * ori);
+            if (bin >= kOriBins) bin -= kOriBins;
+            if (bin < 0) bin += kOriBins;
+            // Lanes holding a sample of the same bin: six ballots on its bits.
+            unsigned long long eq = __ballot(valid);
 #pragma unroll
-            for (int l = 0; l < 64; l++) {
-                const int bl = __builtin_amdgcn_readlane(bin, l);
-                if (bl >= 0) {
-                    const float vl = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(val), l));
-                    acc = acc + (lane == bl ? vl : 0.f);
-                }
+            for (int bit = 0; bit < 6; bit++) {
+                const unsigned long long m = __ballot((bin >> bit) & 1);
+                eq &= ((bin >> bit) & 1) ? m : ~m;
             }
+            const int rank = __popcll(eq & lt_mask);
+            if (lane < kOriBins) ccnt[lane] = 0;
+            lds_barrier();
+            if (valid && rank == 0) ccnt[bin] = __popcll(eq);  // one leader per bin present
+            lds_barrier();
+            const int cb = lane < kOriBins ? ccnt[lane] : 0;
+            int incl = cb;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int t = __shfl_up(incl, d);
+                if (lane >= d) incl += t;
+            }
+            if (lane < kOriBins) coff[lane] = incl - cb;
+            lds_barrier();
+            if (valid) chunk[coff[bin] + rank] = w * mag;
+            lds_barrier();
+            for (int t = incl - cb; t < incl; t++) acc = acc + chunk[t];  // lanes >= 36: cb = 0
+            lds_barrier();  // chunk / ccnt are rewritten by the next 64 samples
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
 
         // Circular [1 4 6 4 1]/16 smoothing (SIMD body, fma form).
         const int bl = lane < kOriBins ? lane : 0;
@@ -288,7 +277,7 @@ __global__ __launch_bounds__(256) void k_orientation(PyrDesc pyr, const RefKpt* 
         const float h = __fmaf_rn(tm2 + tp2, 1.f / 16.f, __fmaf_rn(tm1 + tp1, 4.f / 16.f, acc * (6.f / 16.f)));
         float mx = lane < kOriBins ? h : -INFINITY;
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+        for (int d = 32; d > 0; d >>= 1) mx = fmaxf(mx, __shfl_xor(mx, d));
         const float mag_thr = (float)(mx * kOriPeakRatio);
         const float hl = __shfl(h, (bl + kOriBins - 1) % kOriBins);
         const float hr = __shfl(h, (bl + 1) % kOriBins);
@@ -319,7 +308,7 @@ __global__ __launch_bounds__(256) void k_orientation(PyrDesc pyr, const RefKpt* 
             }
             ok.bucket = g.rowBase + (layer - 1) * H + r;
             ok.sub = (c << 6) | lane;
-            const unsigned pos = basepos + (unsigned)__popcll(mask & ((1ull << lane) - 1ull));
+            const unsigned pos = basepos + (unsigned)__popcll(mask & lt_mask);
             if (pos < kp.capOriented)
                 out[pos] = ok;
             else
@@ -330,8 +319,7 @@ __global__ __launch_bounds__(256) void k_orientation(PyrDesc pyr, const RefKpt* 
 
 void launch_orientation(const PyrDesc& pyr, const RefKpt* in, Counters* ctr, OriKpt* out, const KeypointParams& kp,
                         hipStream_t s) {
-    const int ps = 2 * kp.oriRmax + 3;
-    hipLaunchKernelGGL(k_orientation, dim3(1024), dim3(256), sizeof(float) * 4 * ps * ps, s, pyr, in, ctr, out, kp);
+    hipLaunchKernelGGL(k_orientation, dim3(8192), dim3(64), 0, s, pyr, in, ctr, out, kp);
 }
 
 // ---------------------------------------------------------------------------

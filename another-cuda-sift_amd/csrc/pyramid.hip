@@ -63,6 +63,14 @@ void launch_upsample2x(const float* src, int spitch, int W, int H, float* dst, i
 // Reference: Filter.cu:8-51 (no LDS, vertical first, modulo per tap).
 // ---------------------------------------------------------------------------
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// (a.y, b.x) in one v_pk_mov_b32 (the compiler otherwise emits two v_mov).
+__device__ __forceinline__ f32x2 pk_mov_hi_lo(f32x2 a, f32x2 b) {
+    f32x2 r;
+    __asm__("v_pk_mov_b32 %0, %1, %2 op_sel:[1,0]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 constexpr int BLUR_TW = 64;
 constexpr int BLUR_TH = 32;
 
@@ -79,39 +87,46 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, int
     const int x0 = (tile % gridDim.x) * BLUR_TW, y0 = (tile / gridDim.x) * BLUR_TH;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
-    // Stage the input tile: every thread issues all of its loads before its
-    // first LDS store (one memory latency per workgroup, not one per row).
+    // Stage the input tile row by row: wave w takes rows w, w+4, ...; lane l
+    // columns l and 64+l.  A row's source offset is wave-uniform (SGPR,
+    // reflected in scalar code) and a lane's column offset is the same for
+    // every row, so a staging load costs no vector address arithmetic.  All
+    // loads are issued before the first LDS store.
     {
-        constexpr int RW = BLUR_TW + 2 * R;
-        constexpr int TOTAL = IH * RW;
-        constexpr int PER = (TOTAL + 255) / 256;
+        constexpr int RW = BLUR_TW + 2 * R;  // <= 128: two column chunks
+        constexpr int RPW = (IH + 3) / 4;    // rows per wave
+        const int wv = __builtin_amdgcn_readfirstlane(wave);
         const bool single = W > R + 1 && H > R + 1;  // one reflection suffices
-        float v[PER];
-#pragma unroll
-        for (int u = 0; u < PER; u++) {
-            const int idx = tid + 256 * u;
-            const int ly = min(idx / RW, IH - 1), lx = idx - (idx / RW) * RW;
-            int gy = y0 - R + ly, gx = x0 - R + lx;
+        auto refl = [&](int p, int len) {
             if (single) {
                 // One bounce is exact for every input of an in-image output
                 // (|offset| <= R < len); tile positions past the image edge feed
                 // only discarded outputs, so clamping them just keeps the read
                 // in bounds.
-                gy = gy < 0 ? -gy : (gy >= H ? 2 * H - 2 - gy : gy);
-                gx = gx < 0 ? -gx : (gx >= W ? 2 * W - 2 - gx : gx);
-                gy = min(max(gy, 0), H - 1);
-                gx = min(max(gx, 0), W - 1);
-            } else {
-                gy = reflect101(gy, H);
-                gx = reflect101(gx, W);
+                p = p < 0 ? -p : (p >= len ? 2 * len - 2 - p : p);
+                return min(max(p, 0), len - 1);
             }
-            v[u] = src[((size_t)gy * spitch + gx) * sstep];  // always in bounds; unused if idx >= TOTAL
+            return reflect101(p, len);
+        };
+        const int gx0 = refl(x0 - R + lane, W), gx1 = refl(x0 - R + 64 + min(lane, RW - 65), W);
+        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(src), 0, (int)min((long)spitch * sstep * H * 4, 0x7fffffffL), 0x00020000);
+        const unsigned c0 = (unsigned)(gx0 * sstep) * 4u, c1 = (unsigned)(gx1 * sstep) * 4u;
+        float v0[RPW], v1[RPW];
+#pragma unroll
+        for (int i = 0; i < RPW; i++) {
+            const int ly = min(wv + 4 * i, IH - 1);
+            const int roff = __builtin_amdgcn_readfirstlane(refl(y0 - R + ly, H) * spitch * sstep * 4);
+            v0[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, c0, roff, 0));
+            v1[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, c1, roff, 0));
         }
 #pragma unroll
-        for (int u = 0; u < PER; u++) {
-            const int idx = tid + 256 * u;
-            const int ly = idx / RW, lx = idx - (idx / RW) * RW;
-            if (idx < TOTAL) in[ly * IW + lx] = v[u];
+        for (int i = 0; i < RPW; i++) {
+            const int ly = wv + 4 * i;
+            if (ly < IH) {
+                in[ly * IW + lane] = v0[i];
+                if (lane < RW - 64) in[ly * IW + 64 + lane] = v1[i];
+            }
         }
     }
     __syncthreads();
@@ -140,36 +155,64 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, int
                 win[4 * v + 2] = f[2];
                 win[4 * v + 3] = f[3];
             }
-            float s[4];
+            // Packed FP32: outputs (q, q+1) for q = 0, 2 share one v_pk_fma_f32
+            // per tap (each lane an IEEE fma, so the chain is OpenCV's).  Their
+            // operand (win[q+k], win[q+k+1]) is an even-aligned pair for even
+            // q+k and an odd-aligned pair (built once per window) otherwise.
+            f32x2 pe[2 * NW], po[2 * NW - 1];
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
+            for (int j = 0; j < 2 * NW; j++) pe[j] = (f32x2){win[2 * j], win[2 * j + 1]};
+#pragma unroll
+            for (int j = 0; j < 2 * NW - 1; j++) po[j] = pk_mov_hi_lo(pe[j], pe[j + 1]);
+            auto pr = [&](int i) -> f32x2 { return (i & 1) ? po[i >> 1] : pe[i >> 1]; };  // (win[i], win[i+1])
+            f32x2 s2[2];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int q = 2 * h;
                 if constexpr (2 * R + 1 > 5) {
-                    s[q] = 0.f;
+                    f32x2 a = {0.f, 0.f};
 #pragma unroll
-                    for (int k = 0; k <= 2 * R; k++) s[q] = __fmaf_rn(win[q + k], taps.w[k], s[q]);
+                    for (int k = 0; k <= 2 * R; k++) a = __builtin_elementwise_fma(pr(q + k), (f32x2)taps.w[k], a);
+                    s2[h] = a;
                 } else {
-                    s[q] = win[q + R] * taps.w[R];
+                    f32x2 a = pr(q + R) * (f32x2)taps.w[R];
 #pragma unroll
-                    for (int k = 1; k <= R; k++) s[q] = __fmaf_rn(win[q + R - k] + win[q + R + k], taps.w[R + k], s[q]);
+                    for (int k = 1; k <= R; k++)
+                        a = __builtin_elementwise_fma(pr(q + R - k) + pr(q + R + k), (f32x2)taps.w[R + k], a);
+                    s2[h] = a;
                 }
             }
-            *reinterpret_cast<float4*>(mid + ly * BLUR_TW + xq) = make_float4(s[0], s[1], s[2], s[3]);
+            *reinterpret_cast<float4*>(mid + ly * BLUR_TW + xq) = make_float4(s2[0][0], s2[0][1], s2[1][0], s2[1][1]);
         }
     }
     __syncthreads();
 
     {
         const int lx = lane, yb = wave * 8;
-        float win[8 + 2 * R];
+        // Column pairs (c[i], c[i+4]), one ds_read2st64_b32 each: output rows
+        // (q, q+4) share every v_pk_add/v_pk_fma_f32 and no pair is assembled
+        // from two loads.
+        // (volatile: every element is loaded twice, into both pairs it belongs
+        // to, instead of being loaded once and copied with v_mov.)
+        const volatile __attribute__((address_space(3))) float* vmid =
+            (const volatile __attribute__((address_space(3))) float*)(mid + yb * BLUR_TW + lx);
+        f32x2 cp[4 + 2 * R];
 #pragma unroll
-        for (int j = 0; j < 8 + 2 * R; j++) win[j] = mid[(yb + j) * BLUR_TW + lx];
+        for (int j = 0; j < 4 + 2 * R; j++) cp[j] = (f32x2){vmid[j * BLUR_TW], vmid[(j + 4) * BLUR_TW]};
         const int gx = x0 + lx;
         float mx = -FLT_MAX, nmn = -FLT_MAX;
+        float out[8];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            f32x2 a = __builtin_elementwise_fma(cp[q + R], (f32x2)taps.w[R], (f32x2){0.f, 0.f});
+#pragma unroll
+            for (int k = 1; k <= R; k++) a = __builtin_elementwise_fma(cp[q + R + k] + cp[q + R - k], (f32x2)taps.w[R + k], a);
+            out[q] = a[0];
+            out[q + 4] = a[1];
+        }
 #pragma unroll
         for (int q = 0; q < 8; q++) {
-            float s = __fmaf_rn(win[q + R], taps.w[R], 0.f);
-#pragma unroll
-            for (int k = 1; k <= R; k++) s = __fmaf_rn(win[q + R + k] + win[q + R - k], taps.w[R + k], s);
+            const float s = out[q];
             const int gy = y0 + yb + q;
             if (gy < H && gx < W) {
                 dst[(size_t)gy * dpitch + gx] = s;

@@ -44,6 +44,17 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 FP16_MFMA_PEAK_TFLOPS = 2500.0  # dense
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -52,8 +63,8 @@ def parse():
     ap.add_argument("--streams", type=int, default=3, help="detectors (HIP streams) frames rotate over")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-oracle sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-csv", default=os.environ.get("SIFT_BENCH_TRAFFIC_CSV", ""),
-                    help="rocprofv3 --pmc counter_collection.csv with FETCH_SIZE/WRITE_SIZE of the same run")
+    ap.add_argument("--traffic-summary", default=os.path.join(ROOT, "profiles", "round1", "pmc_summary.json"),
+                    help="PMC summary (tools/pmc_summary.py) with FETCH_SIZE/WRITE_SIZE of this code")
     return ap.parse_args()
 
 
@@ -63,28 +74,29 @@ def make_config(**kw):
     return sift.CudaSiftConfig(**cfg)
 
 
-def pmc_traffic(csv_path, kernel_substr):
-    """Per-launch HBM bytes of a kernel from a rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE csv.
+def pmc_traffic(summary_path, kernel_prefix, grids):
+    """HBM bytes per launch of a kernel family from a committed PMC summary
+    (tools/pmc.sh + tools/pmc_summary.py on the same code).
 
-    MI355X_MICROARCH.md §HBM: FETCH_SIZE reads 1/2 of wide streaming read bytes on
-    gfx950 (doubled here); WRITE_SIZE is exact for 16-B streaming stores; both KiB.
-    """
-    import csv
-
-    fetch, write, n = 0.0, 0.0, set()
-    with open(csv_path) as f:
-        for row in csv.DictReader(f):
-            if kernel_substr not in row.get("Kernel_Name", ""):
-                continue
-            name, val = row.get("Counter_Name", ""), float(row.get("Counter_Value", 0))
-            n.add(row.get("Dispatch_Id"))
-            if name == "FETCH_SIZE":
-                fetch += val
-            elif name == "WRITE_SIZE":
-                write += val
-    if not n:
+    MI355X_MICROARCH.md HBM section + our calibration (tools/hbm_calib.hip, in
+    the summary): FETCH_SIZE counts 1/2 of the bytes read, WRITE_SIZE is exact;
+    both in KiB.  `grids` selects the launches of the bench workload (grid size
+    in threads, one per pyramid octave)."""
+    try:
+        with open(summary_path) as f:
+            summ = json.load(f)
+    except (OSError, ValueError):
         return None
-    return (2.0 * fetch + write) * 1024.0 / len(n)
+    cal = summ.get("calibration_counter_over_true_bytes", {})
+    fetch_scale = 1.0 / cal.get("copy4:FETCH_SIZE", 0.5)
+    write_scale = 1.0 / cal.get("copy4:WRITE_SIZE", 1.0)
+    tot, n = 0.0, 0
+    for k in summ.get("kernels", []):
+        if k["kernel"].split("<")[0].endswith(kernel_prefix) and k["grid_size"] in grids \
+                and "FETCH_SIZE" in k and "WRITE_SIZE" in k:
+            tot += (k["FETCH_SIZE"] * fetch_scale + k["WRITE_SIZE"] * write_scale) * 1024 * k["dispatches"]
+            n += k["dispatches"]
+    return {"bytes_per_launch": round(tot / n), "launches": n, "source": os.path.relpath(summary_path, ROOT)} if n else None
 
 
 def main():
@@ -127,6 +139,7 @@ def main():
     for d in dets:
         d.sync()
     kcount = det.total_size
+    sum_px = sum(det.octave_dims(o)[0] * det.octave_dims(o)[1] for o in range(det.nOctaves))
     barrier()
     t0 = time.perf_counter()
     for s in range(a.steps):
@@ -168,14 +181,17 @@ def main():
     total_ms = sum(v["ms"] for v in timing.values())
     dom = max(timing, key=lambda k: timing[k]["ms"])
     stages = {k: round(v["ms"] / nt * 1e3, 2) for k, v in sorted(timing.items(), key=lambda kv: -kv[1]["ms"])}
-    blur = timing.get("blur_o0")
-    roof_name = "blur_o0"
-    per_launch_bytes = blur["bytes"] / blur["launches"]
-    per_launch_s = blur["ms"] / blur["launches"] / 1e3
+    # k_blur: the kernel with the largest share of frame time (all launches).
+    blurs = [v for k, v in timing.items() if k.startswith("blur_")]
+    blur_launches = sum(v["launches"] for v in blurs)
+    per_launch_bytes = sum(v["bytes"] for v in blurs) / blur_launches
+    per_launch_s = sum(v["ms"] for v in blurs) / blur_launches / 1e3
     achieved = per_launch_bytes / per_launch_s / 1e9
-    traffic = None
-    if a.traffic_csv and os.path.exists(a.traffic_csv):
-        traffic = pmc_traffic(a.traffic_csv, "k_blur")
+    grids = set()
+    for o in range(det.nOctaves):
+        ow, oh, _ = det.octave_dims(o)
+        grids.add(((ow + 63) // 64) * ((oh + 31) // 32) * 256)
+    traffic = pmc_traffic(a.traffic_summary, "k_blur", grids)
 
     # ---- C3: 2000 x 2000 x 128 match -----------------------------------------
     det2 = sift.Detector(make_config(numOctaves=0), device=local)
@@ -278,7 +294,23 @@ def main():
         dt = time.perf_counter() - t
         cpu = {"value": round(n * W * H / 1e6 / dt, 2), "unit": "Mpix/s", "cores": threads, "kind": "port",
                "sample": f"{n} frames of the C2 workload (1920x1200, 3 octaves, numFeatures 5000) in {dt:.1f}s, "
-                         f"oracle/sift_oracle.cpp OpenMP {threads} threads"}
+                         f"oracle/sift_oracle.cpp OpenMP {threads} threads",
+               "cpu_model": cpu_model()}
+        try:  # OpenCV itself, when the box has it (secondary)
+            import cv2
+
+            cv2.setNumThreads(threads)
+            sift_cv = cv2.SIFT_create(nfeatures=5000, nOctaveLayers=3)
+            u8 = imgs[0].astype(np.uint8)
+            sift_cv.detectAndCompute(u8, None)
+            m, t = 0, time.perf_counter()
+            while time.perf_counter() - t < 5.0 or m < 3:
+                sift_cv.detectAndCompute(imgs[m % nframes].astype(np.uint8), None)
+                m += 1
+            cpu["opencv"] = {"version": cv2.__version__, "value": round(m * W * H / 1e6 / (time.perf_counter() - t), 2),
+                             "note": "cv2.SIFT_create defaults (firstOctave -1), not the C2 octave count"}
+        except ImportError:
+            cpu["opencv"] = "cv2 not importable on this box"
 
     if rank == 0:
         line = {
@@ -303,17 +335,19 @@ def main():
                 "keypoints_per_frame": kcount,
             },
             "roofline": {
-                "kernel": "k_blur (octave 0, 5 launches/frame)",
+                "kernel": f"k_blur (all {blur_launches // nt} launches/frame, eager HIP-event timing)",
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
+                "traffic": traffic["bytes_per_launch"] if traffic else None,
+                "traffic_source": traffic,
                 "algo_bytes_per_launch": per_launch_bytes,
                 "avg_launch_us": round(per_launch_s * 1e6, 3),
             },
             "cpu_baseline": cpu,
+            "pipeline_hbm_frac": round(88.0 * sum_px / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             "sync_ms_per_frame": round(sync_ms, 4),
             "single_stream": {"value": round(single_value, 2), "ms_per_frame": round(single / n1 * 1e3, 4)},
             "stage_us_per_frame_eager": stages,
