@@ -37,12 +37,6 @@
 
 namespace sift_amd {
 
-__constant__ float c_exptab_d[64];
-
-void upload_exp_table_desc(const float* tab64) {
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_exptab_d), tab64, 64 * sizeof(float));
-}
-
 constexpr int kD = 4, kN = 8;
 constexpr int kCells = (kD + 2) * (kD + 2);  // 36 spatial cells incl. the border ring
 constexpr int kMaxRows = kDescMaxRows;       // enumerated windows: side = 2R+1 <= kMaxRows
@@ -101,6 +95,32 @@ __device__ __forceinline__ void clip_interval(int& lo, int& hi, double s, double
     hi = min(hi, (int)ceil(x2) + 1);
 }
 
+// Sample math with native gfx950 instructions (v_rcp_f32, v_sqrt_f32,
+// v_exp_f32; ~1 ulp) instead of the correctly rounded / table forms the
+// orientation and pyramid need for bit-exact keypoints.  Every operation is
+// continuous in its inputs here (trilinear split, magnitude weights), so ulp
+// differences move a descriptor entry by ~1e-7 relative and flip its rounding
+// only at a .5 boundary: inside the |diff| <= 1 bar, at the same rate as the
+// summation-order difference.  The fastAtan2 polynomial itself is kept.
+__device__ __forceinline__ float desc_atan2(float y, float x) {
+    const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
+    const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
+    const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
+    const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float c = fminf(ax, ay) * __builtin_amdgcn_rcpf(fmaxf(ax, ay) + (float)DBL_EPSILON);
+    const float cc = c * c;
+    float a = __fmaf_rn(__fmaf_rn(__fmaf_rn(cc, p7, p5), cc, p3), cc, p1) * c;
+    if (!(ax >= ay)) a = 90.f - a;
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+__device__ __forceinline__ float desc_magnitude(float x, float y) {
+    return __builtin_amdgcn_sqrtf(__fmaf_rn(x, x, y * y));
+}
+__device__ __forceinline__ float desc_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
+
 // DescJob read with scalar loads from the constant address space: every field
 // is uniform and lives in SGPRs.
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -128,10 +148,8 @@ __global__ __launch_bounds__(64) void k_descriptor(const DescJob* __restrict__ j
     unsigned* histO = histE + kCells * 8;
     __shared__ __attribute__((aligned(16))) float sq[128];
     __shared__ int rowpre[kMaxRows + 4], rowlo[kMaxRows];
-    __shared__ float s_exptab[64];
 
     const int lane = threadIdx.x;
-    s_exptab[lane] = c_exptab_d[lane];
     const unsigned n = ctr->final_n;
     // Pixel range of the frame; it bounds every Gaussian plane (convex blurs).
     unsigned kmax = 0, knmn = 0;
@@ -198,22 +216,26 @@ __global__ __launch_bounds__(64) void k_descriptor(const DescJob* __restrict__ j
         lds_barrier();
 
         // One sample from its four neighbours (l, r, u, d).
-        auto accumulate = [&](int i, int j, float l, float r, float u, float d) {
+        // One sample from its four neighbours (l, r, u, d).  Branch-free so
+        // that the kGroup samples of a group interleave (ILP): a rejected
+        // sample keeps in-range bin indices and adds zeros.
+        auto accumulate = [&](int i, int j, bool in, float l, float r, float u, float d) {
             float rbin, cbin, c_rot, r_rot;
-            if (!desc_sample(G, i, j, rbin, cbin, c_rot, r_rot)) return;
+            const bool valid = desc_sample(G, i, j, rbin, cbin, c_rot, r_rot) && in;
             const float dx = r - l, dy = u - d;
-            const float wgt = cv_exp32f((c_rot * c_rot + r_rot * r_rot) * G.exp_scale, s_exptab);
-            const float gori = cv_fast_atan2(dy, dx);
-            const float gmag = cv_magnitude(dx, dy);
+            const float wgt = desc_exp((c_rot * c_rot + r_rot * r_rot) * G.exp_scale);
+            const float gori = desc_atan2(dy, dx);
+            const float gmag = desc_magnitude(dx, dy);
             float obin = (gori - jb.angle) * bins_per_rad;
-            const float mag = gmag * wgt;
-            const int r0 = cv_floor(rbin), c0 = cv_floor(cbin);
+            const float mag = valid ? gmag * wgt : 0.f;
+            const int r0 = min(max(cv_floor(rbin), -1), kD - 1), c0 = min(max(cv_floor(cbin), -1), kD - 1);
             int o0 = cv_floor(obin);
             rbin -= (float)r0;
             cbin -= (float)c0;
             obin -= (float)o0;
             if (o0 < 0) o0 += kN;
             if (o0 >= kN) o0 -= kN;
+            o0 &= kN - 1;  // no-op for valid samples (o0 in [0, 8) already)
             const int cell = (r0 + 1) * (kD + 2) + c0 + 1;
             const bool odd = o0 & 1;
             const int stride = odd ? 10 : 8;  // dwords per cell
@@ -223,8 +245,8 @@ __global__ __launch_bounds__(64) void k_descriptor(const DescJob* __restrict__ j
 #pragma unroll
             for (int q = 0; q < 8; q += 2) {
                 const int off = (q & 4 ? (kD + 2) * stride : 0) + (q & 2 ? stride : 0);
-                const unsigned lo = (unsigned)__builtin_rintf(v[q] * fxs);
-                const unsigned hi = (unsigned)__builtin_rintf(v[q + 1] * fxs);
+                const unsigned lo = (unsigned)(v[q] * fxs);  // truncation: < 2^-S per contribution
+                const unsigned hi = (unsigned)(v[q + 1] * fxs);
                 atomicAdd(reinterpret_cast<unsigned long long*>(hb + off),
                           ((unsigned long long)hi << 32) | (unsigned long long)lo);
             }
@@ -245,8 +267,7 @@ __global__ __launch_bounds__(64) void k_descriptor(const DescJob* __restrict__ j
                                           __builtin_amdgcn_raw_buffer_load_b32(rsrc, o + 4u * jb.pitch, 0, 0));
             }
 #pragma unroll
-            for (int t = 0; t < kGroup; t++)
-                if (t < cnt) accumulate(gi[t], gj[t], l[t], r[t], u[t], d[t]);
+            for (int t = 0; t < kGroup; t++) accumulate(gi[t], gj[t], t < cnt, l[t], r[t], u[t], d[t]);
         };
 
         if (enumerated) {

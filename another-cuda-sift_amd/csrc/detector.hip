@@ -264,7 +264,6 @@ void upload_exp_tab() {
     float tab[64];
     for (int j = 0; j < 64; j++) tab[j] = (float)(std::exp2((double)j / 64.0) * A0);
     upload_exp_table(tab);
-    upload_exp_table_desc(tab);
 }
 
 template <class T>

@@ -200,7 +200,8 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
                                                     Counters* __restrict__ ctr, OriKpt* __restrict__ out,
                                                     KeypointParams kp) {
     __shared__ float chunk[64];
-    __shared__ int ccnt[kOriBins + 4], coff[kOriBins + 4];
+    __shared__ __attribute__((aligned(16))) int ccnt[kOriBins + 4];
+    __shared__ int coff[kOriBins + 4];
     __shared__ float s_exptab[64];
     const int lane = threadIdx.x;
     s_exptab[lane] = c_exptab[lane];
@@ -222,17 +223,35 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
         const __amdgpu_buffer_rsrc_t rsrc =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(img), 0, H * pitch * 4, 0x00020000);
 
-        float acc = 0.f;  // temphist[lane] for lane < 36
-        for (int base = 0; base < total; base += 64) {
+        // Chunk geometry + its four gradient loads; the next chunk's loads are
+        // issued before this chunk is processed (one chunk of latency hidden).
+        struct Fetch {
+            int i, j;
+            bool valid;
+            float xl, xr, yu, yd;
+        };
+        auto fetch = [&](int base) {
+            Fetch f;
             const int idx = base + lane;
-            const int i = (int)__umulhi((unsigned)idx, mside), j = idx - i * side;
-            const int y = r + i - radius, x = c + j - radius;
-            const bool valid = idx < total && y > 0 && y < H - 1 && x > 0 && x < W - 1;
-            const unsigned o0 = valid ? (unsigned)(y * pitch + x) * 4u : 0x80000000u;
-            const float xl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o0 - 4u, 0, 0));
-            const float xr = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o0 + 4u, 0, 0));
-            const float yu = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o0 - 4u * pitch, 0, 0));
-            const float yd = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o0 + 4u * pitch, 0, 0));
+            f.i = (int)__umulhi((unsigned)idx, mside);
+            f.j = idx - f.i * side;
+            const int y = r + f.i - radius, x = c + f.j - radius;
+            f.valid = idx < total && y > 0 && y < H - 1 && x > 0 && x < W - 1;
+            const unsigned o0 = f.valid ? (unsigned)(y * pitch + x) * 4u : 0x80000000u;
+            f.xl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o0 - 4u, 0, 0));
+            f.xr = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o0 + 4u, 0, 0));
+            f.yu = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o0 - 4u * pitch, 0, 0));
+            f.yd = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o0 + 4u * pitch, 0, 0));
+            return f;
+        };
+        float acc = 0.f;  // temphist[lane] for lane < 36
+        Fetch nxt = fetch(0);
+        for (int base = 0; base < total; base += 64) {
+            const Fetch cur = nxt;
+            if (base + 64 < total) nxt = fetch(base + 64);
+            const int i = cur.i, j = cur.j;
+            const bool valid = cur.valid;
+            const float xl = cur.xl, xr = cur.xr, yu = cur.yu, yd = cur.yd;
             const int ii = i - radius, jj = j - radius;
             const float dx = xr - xl, dy = yu - yd;
             const float w = cv_exp32f((float)(ii * ii + jj * jj) * expf_scale, s_exptab);
@@ -264,7 +283,16 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
             lds_barrier();
             if (valid) chunk[coff[bin] + rank] = w * mag;
             lds_barrier();
-            for (int t = incl - cb; t < incl; t++) acc = acc + chunk[t];  // lanes >= 36: cb = 0
+            // Lane b (< 36; others have cb = 0) adds its bin's values in order,
+            // four LDS reads in flight at a time.
+            for (int t0 = incl - cb; t0 < incl; t0 += 4) {
+                const float v0 = chunk[t0], v1 = chunk[min(t0 + 1, 63)], v2 = chunk[min(t0 + 2, 63)],
+                            v3 = chunk[min(t0 + 3, 63)];
+                acc = acc + v0;
+                if (t0 + 1 < incl) acc = acc + v1;
+                if (t0 + 2 < incl) acc = acc + v2;
+                if (t0 + 3 < incl) acc = acc + v3;
+            }
             lds_barrier();  // chunk / ccnt are rewritten by the next 64 samples
         }
 

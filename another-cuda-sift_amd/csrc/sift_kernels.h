@@ -123,6 +123,5 @@ __device__ __forceinline__ float decode_range_key(unsigned u) {
 
 // Exp table (OpenCV expTab_f) uploaded once per device.
 void upload_exp_table(const float* tab64);
-void upload_exp_table_desc(const float* tab64);
 
 }  // namespace sift_amd
