@@ -300,11 +300,17 @@ int allocate(sift_hip_detector* d) {
     if ((rc = dalloc(&d->dSlot, capO))) return rc;
     if ((rc = dalloc(&d->dOrder, capO))) return rc;
     if ((rc = dalloc(&d->dJobs, capF))) return rc;
-    if ((rc = dalloc(&d->dRange, 2 * kRangeSlots))) return rc;
+    if ((rc = dalloc(&d->dRange, 2 * 2 * kRangeSlots))) return rc;  // one set per frame buffer
     if ((rc = dalloc(&d->dBcount, (size_t)d->kp.numBuckets))) return rc;
     if ((rc = dalloc(&d->dBoff, (size_t)d->kp.numBuckets))) return rc;
     if ((rc = dalloc(&d->dBitmap, d->bitmapWords))) return rc;
     if ((rc = dalloc(&d->dCtr, 1))) return rc;
+    // Zeroed once here; afterwards the kernels keep them zero for the next
+    // frame (first blur: counters, k_select: range keys, k_bucket_rank: bucket
+    // counts), so the frame graph has a single memset node (dedupe bitmap).
+    HIPCHK(hipMemset(d->dCtr, 0, sizeof(Counters)));
+    HIPCHK(hipMemset(d->dRange, 0, sizeof(unsigned) * 2 * 2 * kRangeSlots));
+    HIPCHK(hipMemset(d->dBcount, 0, sizeof(unsigned) * (size_t)d->kp.numBuckets));
     HIPCHK(hipHostMalloc((void**)&d->hCtr, sizeof(Counters), hipHostMallocDefault));
     memset(d->hCtr, 0, sizeof(Counters));
     for (int b = 0; b < 2; b++) {
@@ -320,13 +326,13 @@ int allocate(sift_hip_detector* d) {
 
 // The first kernel reads the caller's image (host upload buffer or a device
 // pointer); it stays outside the graph so the graph never bakes a user pointer.
+// Pixel-range keys of frame buffer b (the frame in flight uses b = cur; the
+// other set is zeroed by k_select for the next frame).
+unsigned* range_keys(sift_hip_detector* d, int b) { return d->dRange + (size_t)b * 2 * kRangeSlots; }
+
 void enqueue_head(sift_hip_detector* d, const float* img, int pitchFloats) {
     const int W = d->cfg.col_width, H = d->cfg.row_width;
     // Counters first: the initial blur accumulates the frame's pixel range.
-    d->timed("memset", 0, [&] {
-        (void)hipMemsetAsync(d->dCtr, 0, sizeof(Counters), d->stream);
-        (void)hipMemsetAsync(d->dRange, 0, sizeof(unsigned) * 2 * kRangeSlots, d->stream);
-    });
     if (d->firstOctave < 0) {
         d->timed("upsample", (double)W * H * 4 + (double)W * H * 16, [&] {
             launch_upsample2x(img, pitchFloats, W, H, d->dUp, d->upPitch, d->stream);
@@ -334,7 +340,8 @@ void enqueue_head(sift_hip_detector* d, const float* img, int pitchFloats) {
     } else {
         const OctGeom& g = d->pyr.oct[0];
         d->timed("blur_init", (double)W * H * 8, [&] {
-            launch_blur(img, pitchFloats, 1, W, H, g.base, g.pitch, nullptr, d->initTaps, d->stream, d->dRange);
+            launch_blur(img, pitchFloats, 1, W, H, g.base, g.pitch, nullptr, d->initTaps, d->stream, range_keys(d, d->cur),
+                        d->dCtr);
         });
     }
 }
@@ -343,13 +350,13 @@ void enqueue_body(sift_hip_detector* d, int buf) {
     hipStream_t s = d->stream;
     const int L = d->L;
     d->timed("memset", 0, [&] {
-        (void)hipMemsetAsync(d->dBcount, 0, sizeof(unsigned) * (size_t)d->kp.numBuckets, s);
         (void)hipMemsetAsync(d->dBitmap, 0, sizeof(uint32_t) * d->bitmapWords, s);
     });
     if (d->firstOctave < 0) {
         const OctGeom& g = d->pyr.oct[0];
         d->timed("blur_init", (double)g.W * g.H * 8, [&] {
-            launch_blur(d->dUp, d->upPitch, 1, g.W, g.H, g.base, g.pitch, nullptr, d->initTaps, s, d->dRange);
+            launch_blur(d->dUp, d->upPitch, 1, g.W, g.H, g.base, g.pitch, nullptr, d->initTaps, s, range_keys(d, buf),
+                        d->dCtr);
         });
     }
     static const char* blurNames[kMaxOctaves] = {"blur_o0", "blur_o1", "blur_o2", "blur_o3", "blur_o4", "blur_o5",
@@ -381,7 +388,7 @@ void enqueue_body(sift_hip_detector* d, int buf) {
     }
     d->timed("refine", 0, [&] { launch_refine(d->pyr, d->dCand, d->capCand, d->dCtr, d->dBitmap, d->dRef, d->kp, s); });
     d->timed("orientation", 0, [&] { launch_orientation(d->pyr, d->dRef, d->dCtr, d->dOri, d->kp, s); });
-    d->timed("select", 0, [&] { launch_select(d->dOri, d->dCtr, d->kp, s); });
+    d->timed("select", 0, [&] { launch_select(d->dOri, d->dCtr, range_keys(d, buf ^ 1), d->kp, s); });
     d->timed("bucket_count", 0, [&] { launch_bucket_count(d->dOri, d->dCtr, d->dBcount, d->dSlot, d->kp, s); });
     d->timed("bucket_scan", 0, [&] { launch_bucket_scan(d->dBcount, d->dBoff, d->dCtr, d->kp, s); });
     d->timed("bucket_scatter", 0,
@@ -390,7 +397,7 @@ void enqueue_body(sift_hip_detector* d, int buf) {
         launch_bucket_rank(d->pyr, d->dOri, d->dBcount, d->dBoff, d->dOrder, d->dCtr, d->dJobs, d->dKpts3[buf],
                            d->dFeats4[buf], d->kp, s);
     });
-    d->timed("descriptor", 0, [&] { launch_descriptor(d->dJobs, d->dCtr, d->dRange, d->dDesc[buf], d->kp, s); });
+    d->timed("descriptor", 0, [&] { launch_descriptor(d->dJobs, d->dCtr, range_keys(d, buf), d->dDesc[buf], d->kp, s); });
     (void)hipMemcpyAsync(d->hCtr, d->dCtr, sizeof(Counters), hipMemcpyDeviceToHost, s);
 }
 

@@ -358,11 +358,12 @@ void launch_orientation(const PyrDesc& pyr, const RefKpt* in, Counters* ctr, Ori
 // Reference: keeps the first numFeatures in octave order (CudaMemcpyUtils.cu:38-49).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(1024) void k_select(const OriKpt* __restrict__ kpts, Counters* __restrict__ ctr,
-                                                 KeypointParams kp) {
+                                                 unsigned* __restrict__ zero_range, KeypointParams kp) {
     __shared__ unsigned hist[256];
     __shared__ unsigned s_prefix, s_k;
     const unsigned n = min(ctr->oriented, kp.capOriented);
     const int tid = threadIdx.x;
+    for (int i = tid; i < 2 * kRangeSlots; i += 1024) zero_range[i] = 0u;  // next frame's range keys
     if (kp.numFeatures <= 0 || n <= (unsigned)kp.numFeatures) {
         if (tid == 0) ctr->thr_bits = 0u;
         return;
@@ -401,8 +402,8 @@ __global__ __launch_bounds__(1024) void k_select(const OriKpt* __restrict__ kpts
     if (tid == 0) ctr->thr_bits = s_prefix;
 }
 
-void launch_select(const OriKpt* kpts, Counters* ctr, const KeypointParams& kp, hipStream_t s) {
-    hipLaunchKernelGGL(k_select, dim3(1), dim3(1024), 0, s, kpts, ctr, kp);
+void launch_select(const OriKpt* kpts, Counters* ctr, unsigned* zero_range, const KeypointParams& kp, hipStream_t s) {
+    hipLaunchKernelGGL(k_select, dim3(1), dim3(1024), 0, s, kpts, ctr, zero_range, kp);
 }
 
 // ---------------------------------------------------------------------------
@@ -520,7 +521,7 @@ __device__ DescJob make_desc_job(const PyrDesc& pyr, const OriKpt& kpt) {
 // keypoint's outputs (reference layout Detector.hh:54-57: float3 {x, y,
 // layer}, float4 {packed octave, size, response, angle}) and its descriptor job.
 __global__ __launch_bounds__(256) void k_bucket_rank(PyrDesc pyr, const OriKpt* __restrict__ kpts,
-                                                     const unsigned* __restrict__ bcount,
+                                                     unsigned* __restrict__ bcount,
                                                      const unsigned* __restrict__ boff, const int* __restrict__ order,
                                                      const Counters* __restrict__ ctr, DescJob* __restrict__ jobs,
                                                      float* __restrict__ kpts3, float* __restrict__ feats4,
@@ -557,10 +558,11 @@ __global__ __launch_bounds__(256) void k_bucket_rank(PyrDesc pyr, const OriKpt* 
                 reinterpret_cast<float4*>(feats4)[pos] = make_float4((float)k.octave, k.size, k.response, k.angle);
             }
         }
+        if (lane == 0) bcount[b] = 0u;  // zero for the next frame (no memset node)
     }
 }
 
-void launch_bucket_rank(const PyrDesc& pyr, const OriKpt* kpts, const unsigned* bcount, const unsigned* boff,
+void launch_bucket_rank(const PyrDesc& pyr, const OriKpt* kpts, unsigned* bcount, const unsigned* boff,
                         const int* order, const Counters* ctr, DescJob* jobs, float* kpts3, float* feats4,
                         const KeypointParams& kp, hipStream_t s) {
     hipLaunchKernelGGL(k_bucket_rank, dim3(256), dim3(256), 0, s, pyr, kpts, bcount, boff, order, ctr, jobs, kpts3,

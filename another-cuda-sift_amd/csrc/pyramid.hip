@@ -77,7 +77,8 @@ constexpr int BLUR_TH = 32;
 template <int R>
 __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, int spitch, int sstep, int W, int H,
                                               float* __restrict__ dst, int dpitch, float* __restrict__ copy_out,
-                                              Taps taps, unsigned* __restrict__ range_keys) {
+                                              Taps taps, unsigned* __restrict__ range_keys,
+                                              Counters* __restrict__ zero_ctr) {
     constexpr int IW = (BLUR_TW + 2 * R + 3) & ~3;  // row stride, multiple of 4 floats
     constexpr int IH = BLUR_TH + 2 * R;
     constexpr int NW = (2 * R + 4 + 3) / 4;          // float4 reads per row window
@@ -86,6 +87,8 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, int
     const int tile = xcd_tile(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
     const int x0 = (tile % gridDim.x) * BLUR_TW, y0 = (tile / gridDim.x) * BLUR_TH;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // The frame's first blur also zeroes the frame counters (no memset node).
+    if (zero_ctr && tile == 0 && tid < (int)(sizeof(Counters) / 4)) reinterpret_cast<unsigned*>(zero_ctr)[tid] = 0u;
 
     // Stage the input tile row by row: wave w takes rows w, w+4, ...; lane l
     // columns l and 64+l.  A row's source offset is wave-uniform (SGPR,
@@ -245,13 +248,13 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, int
 }
 
 using BlurLaunch = void (*)(dim3, hipStream_t, const float*, int, int, int, int, float*, int, float*, const Taps&,
-                            unsigned*);
+                            unsigned*, Counters*);
 
 template <int R>
 void blur_launch_r(dim3 grid, hipStream_t s, const float* src, int spitch, int sstep, int W, int H, float* dst,
-                   int dpitch, float* copy_out, const Taps& taps, unsigned* range_keys) {
+                   int dpitch, float* copy_out, const Taps& taps, unsigned* range_keys, Counters* zero_ctr) {
     hipLaunchKernelGGL(k_blur<R>, grid, dim3(256), 0, s, src, spitch, sstep, W, H, dst, dpitch, copy_out, taps,
-                       range_keys);
+                       range_keys, zero_ctr);
 }
 
 template <int... Rs>
@@ -261,10 +264,10 @@ constexpr std::array<BlurLaunch, sizeof...(Rs)> blur_table(std::integer_sequence
 static const std::array<BlurLaunch, kMaxTaps / 2> kBlurTable = blur_table(std::make_integer_sequence<int, kMaxTaps / 2>{});
 
 void launch_blur(const float* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, float* copy_out,
-                 const Taps& taps, hipStream_t s, unsigned* range_keys) {
+                 const Taps& taps, hipStream_t s, unsigned* range_keys, Counters* zero_ctr) {
     const int r = taps.n >> 1;  // 1 .. kMaxTaps/2 (taps.n >= 3 by construction)
     dim3 grid((W + BLUR_TW - 1) / BLUR_TW, (H + BLUR_TH - 1) / BLUR_TH);
-    kBlurTable[r - 1](grid, s, src, spitch, sstep, W, H, dst, dpitch, copy_out, taps, range_keys);
+    kBlurTable[r - 1](grid, s, src, spitch, sstep, W, H, dst, dpitch, copy_out, taps, range_keys, zero_ctr);
 }
 
 // ---------------------------------------------------------------------------

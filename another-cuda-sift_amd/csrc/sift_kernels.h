@@ -67,8 +67,9 @@ void launch_upsample2x(const float* src, int spitch, int W, int H, float* dst, i
 // order-preserving keys {max(v), max(-v)} (atomicMax spread over slots).
 constexpr int kRangeSlots = 256;
 // range_keys (nullable): 2 * kRangeSlots keys, zeroed before the launch.
+// zero_ctr (nullable): counters to zero (the frame's first blur).
 void launch_blur(const float* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, float* copy_out,
-                 const Taps& taps, hipStream_t s, unsigned* range_keys = nullptr);
+                 const Taps& taps, hipStream_t s, unsigned* range_keys = nullptr, Counters* zero_ctr = nullptr);
 void launch_extrema(const PyrDesc& pyr, int o, float threshold, uint2* cand, Counters* ctr, unsigned cap,
                     hipStream_t s);
 
@@ -84,7 +85,9 @@ void launch_refine(const PyrDesc& pyr, const uint2* cand, unsigned capCand, Coun
                    RefKpt* out, const KeypointParams& kp, hipStream_t s);
 void launch_orientation(const PyrDesc& pyr, const RefKpt* in, Counters* ctr, OriKpt* out, const KeypointParams& kp,
                         hipStream_t s);
-void launch_select(const OriKpt* kpts, Counters* ctr, const KeypointParams& kp, hipStream_t s);
+// zero_range: the other frame buffer's 2 * kRangeSlots range keys (zeroed here
+// for the next frame, so no memset node is needed).
+void launch_select(const OriKpt* kpts, Counters* ctr, unsigned* zero_range, const KeypointParams& kp, hipStream_t s);
 void launch_bucket_count(const OriKpt* kpts, const Counters* ctr, unsigned* bcount, int* slot,
                          const KeypointParams& kp, hipStream_t s);
 void launch_bucket_scan(unsigned* bcount, unsigned* boff, Counters* ctr, const KeypointParams& kp, hipStream_t s);
@@ -105,7 +108,7 @@ struct DescJob {
 };
 static_assert(sizeof(DescJob) == 64, "DescJob is one 64-byte scalar load");
 
-void launch_bucket_rank(const PyrDesc& pyr, const OriKpt* kpts, const unsigned* bcount, const unsigned* boff,
+void launch_bucket_rank(const PyrDesc& pyr, const OriKpt* kpts, unsigned* bcount, const unsigned* boff,
                         const int* order, const Counters* ctr, DescJob* jobs, float* kpts3, float* feats4,
                         const KeypointParams& kp, hipStream_t s);
 void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned* range_keys, uint16_t* desc,
