@@ -82,8 +82,12 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, int
     constexpr int IW = (BLUR_TW + 2 * R + 3) & ~3;  // row stride, multiple of 4 floats
     constexpr int IH = BLUR_TH + 2 * R;
     constexpr int NW = (2 * R + 4 + 3) / 4;          // float4 reads per row window
+    // Row-pass results (`mid`, pitch IW) overwrite their own input row of
+    // `in` in place: a row is read and written only by the same 16 lanes of
+    // one wave, whose LDS reads complete before its writes (in-order LDS per
+    // wave), so one tile of LDS serves both passes (more workgroups per CU).
     __shared__ __attribute__((aligned(16))) float in[IH * IW + 4];
-    __shared__ __attribute__((aligned(16))) float mid[IH * BLUR_TW];
+    float* const mid = in;
     const int tile = xcd_tile(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
     const int x0 = (tile % gridDim.x) * BLUR_TW, y0 = (tile / gridDim.x) * BLUR_TH;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -129,6 +133,17 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, int
             if (ly < IH) {
                 in[ly * IW + lane] = v0[i];
                 if (lane < RW - 64) in[ly * IW + 64 + lane] = v1[i];
+            }
+        }
+        if (copy_out) {  // decimated base plane of this octave = the tile's interior inputs
+#pragma unroll
+            for (int i = 0; i < RPW; i++) {
+                const int ly = wv + 4 * i, gy = y0 - R + ly;
+                if (ly >= R && ly < R + BLUR_TH && gy < H) {
+                    float* row = copy_out + (size_t)gy * dpitch + x0 - R;
+                    if (lane >= R && x0 - R + lane < W) row[lane] = v0[i];
+                    if (lane < R && x0 + 64 + lane - R < W) row[64 + lane] = v1[i];
+                }
             }
         }
     }
@@ -185,7 +200,7 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, int
                     s2[h] = a;
                 }
             }
-            *reinterpret_cast<float4*>(mid + ly * BLUR_TW + xq) = make_float4(s2[0][0], s2[0][1], s2[1][0], s2[1][1]);
+            *reinterpret_cast<float4*>(mid + ly * IW + xq) = make_float4(s2[0][0], s2[0][1], s2[1][0], s2[1][1]);
         }
     }
     __syncthreads();
@@ -198,10 +213,10 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, int
         // (volatile: every element is loaded twice, into both pairs it belongs
         // to, instead of being loaded once and copied with v_mov.)
         const volatile __attribute__((address_space(3))) float* vmid =
-            (const volatile __attribute__((address_space(3))) float*)(mid + yb * BLUR_TW + lx);
+            (const volatile __attribute__((address_space(3))) float*)(mid + yb * IW + lx);
         f32x2 cp[4 + 2 * R];
 #pragma unroll
-        for (int j = 0; j < 4 + 2 * R; j++) cp[j] = (f32x2){vmid[j * BLUR_TW], vmid[(j + 4) * BLUR_TW]};
+        for (int j = 0; j < 4 + 2 * R; j++) cp[j] = (f32x2){vmid[j * IW], vmid[(j + 4) * IW]};
         const int gx = x0 + lx;
         float mx = -FLT_MAX, nmn = -FLT_MAX;
         float out[8];
@@ -219,7 +234,6 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, int
             const int gy = y0 + yb + q;
             if (gy < H && gx < W) {
                 dst[(size_t)gy * dpitch + gx] = s;
-                if (copy_out) copy_out[(size_t)gy * dpitch + gx] = in[(yb + q + R) * IW + lx + R];
                 mx = fmaxf(mx, s);
                 nmn = fmaxf(nmn, -s);
             }
