@@ -4,8 +4,9 @@
 // per keypoint, 8 shared-memory float atomics per sample, modff bins, serial
 // lane-0 normalisation, half(x512) output).
 //
-// One wavefront (64-thread workgroup) per keypoint, ~20 keypoints in flight
-// per CU, so memory latency of one keypoint hides behind the others' ALU work:
+// Two wavefronts (a 128-thread workgroup) per keypoint, ~10 keypoints in
+// flight per CU, so memory latency of one keypoint hides behind the others'
+// ALU work:
 //   * k_bucket_rank already computed the keypoint's window (DescJob), read
 //     here with scalar loads;
 //   * only samples inside the rotated 4x4-cell square are enumerated: per row
@@ -41,6 +42,8 @@ constexpr int kD = 4, kN = 8;
 constexpr int kCells = (kD + 2) * (kD + 2);  // 36 spatial cells incl. the border ring
 constexpr int kMaxRows = kDescMaxRows;       // enumerated windows: side = 2R+1 <= kMaxRows
 constexpr int kGroup = 4;                    // samples whose loads are in flight together
+constexpr int kDT = 128;                     // threads (2 waves) per keypoint
+constexpr int kPer = 128 / kDT;              // descriptor entries per thread in the epilogue
 
 struct DescGeom {
     float cos_t, sin_t, exp_scale;
@@ -136,7 +139,7 @@ __device__ __forceinline__ DescJob load_job(const DescJob* jobs, unsigned p) {
     return __builtin_bit_cast(DescJob, r);
 }
 
-__global__ __launch_bounds__(64) void k_descriptor(const DescJob* __restrict__ jobs, const Counters* __restrict__ ctr,
+__global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ jobs, const Counters* __restrict__ ctr,
                                                    const unsigned* __restrict__ range_keys,
                                                    uint16_t* __restrict__ desc) {
     // Two u32 fixed-point histograms so that each sample's orientation pair
@@ -148,8 +151,9 @@ __global__ __launch_bounds__(64) void k_descriptor(const DescJob* __restrict__ j
     unsigned* histO = histE + kCells * 8;
     __shared__ __attribute__((aligned(16))) float sq[128];
     __shared__ int rowpre[kMaxRows + 4], rowlo[kMaxRows];
+    __shared__ float s_norm[12];
 
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
     const unsigned n = ctr->final_n;
     // Pixel range of the frame; it bounds every Gaussian plane (convex blurs).
     unsigned kmax = 0, knmn = 0;
@@ -179,9 +183,9 @@ __global__ __launch_bounds__(64) void k_descriptor(const DescJob* __restrict__ j
         const __amdgpu_buffer_rsrc_t rsrc =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(jb.img), 0, jb.rows * jb.pitch * 4, 0x00020000);
 
-        for (int i = lane; i < kCells * 18; i += 64) histE[i] = 0u;
+        for (int i = tid; i < kCells * 18; i += kDT) histE[i] = 0u;
         if (enumerated) {
-            for (int t = lane; t < side; t += 64) {
+            for (int t = tid; t < side; t += kDT) {
                 const int i = t - radius, r = G.pty + i;
                 int lo = max(-radius, 1 - G.ptx), hi = min(radius, G.cols - 2 - G.ptx);
                 if (r <= 0 || r >= G.rows - 1) hi = lo - 1;
@@ -190,9 +194,9 @@ __global__ __launch_bounds__(64) void k_descriptor(const DescJob* __restrict__ j
                 rowlo[t] = lo;
                 rowpre[t + 1] = max(hi - lo + 1, 0);
             }
-            if (lane == 0) rowpre[0] = 0;
+            if (tid == 0) rowpre[0] = 0;
             lds_barrier();
-            {  // inclusive scan of row counts (entries 2l+1, 2l+2 of rowpre per lane)
+            if (tid < 64) {  // inclusive scan of row counts (entries 2l+1, 2l+2 of rowpre per lane)
                 const int a = 2 * lane + 1 <= side ? rowpre[2 * lane + 1] : 0;
                 const int b = 2 * lane + 2 <= side ? rowpre[2 * lane + 2] : 0;
                 int sum = a + b;
@@ -272,8 +276,8 @@ __global__ __launch_bounds__(64) void k_descriptor(const DescJob* __restrict__ j
 
         if (enumerated) {
             const int N = rowpre[side];
-            const int run = (N + 63) / 64;
-            const int k0 = min(N, lane * run), k1 = min(N, k0 + run);
+            const int run = (N + kDT - 1) / kDT;
+            const int k0 = min(N, tid * run), k1 = min(N, k0 + run);
             if (k0 < k1) {
                 int lo = 0, hi = side - 1;  // last row with rowpre[row] <= k0 (non-empty)
                 while (lo < hi) {
@@ -302,7 +306,7 @@ __global__ __launch_bounds__(64) void k_descriptor(const DescJob* __restrict__ j
             }
         } else {  // huge window: the full raster, rejected samples included
             const int total = side * side;
-            for (int q0 = lane * kGroup; q0 < total; q0 += 64 * kGroup) {
+            for (int q0 = tid * kGroup; q0 < total; q0 += kDT * kGroup) {
                 int gi[kGroup], gj[kGroup];
 #pragma unroll
                 for (int t = 0; t < kGroup; t++) {
@@ -317,36 +321,36 @@ __global__ __launch_bounds__(64) void k_descriptor(const DescJob* __restrict__ j
 
         // Wrap, L2 norm (8 fma lanes, then v_reduce_sum's pairing), 0.2 clip.
         const float inv = ldexpf(1.f, -S);
-        float val[2];
+        float val[kPer];
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const int t = lane + 64 * h;
+        for (int h = 0; h < kPer; h++) {
+            const int t = tid + kDT * h;
             const int ii = t >> 5, jj = (t >> 3) & 3, kk = t & 7;
             const int cell = (ii + 1) * (kD + 2) + (jj + 1);
             unsigned long long hv = (unsigned long long)histE[cell * 8 + kk] + histO[cell * 10 + 1 + kk];
             if (kk == 0) hv += histO[cell * 10 + 9];
             val[h] = (float)((double)hv * (double)inv);
+            sq[t] = val[h];
         }
-        sq[lane] = val[0];
-        sq[lane + 64] = val[1];
         lds_barrier();
-        float a = 0.f;
-        if (lane < 8) {
+        if (tid < 8) {
+            float a = 0.f;
 #pragma unroll
-            for (int q = 0; q < 16; q++) a = __fmaf_rn(sq[lane + 8 * q], sq[lane + 8 * q], a);
+            for (int q = 0; q < 16; q++) a = __fmaf_rn(sq[tid + 8 * q], sq[tid + 8 * q], a);
+            s_norm[tid] = a;
         }
-        const float n0 = __shfl(a, 0), n1 = __shfl(a, 1), n2 = __shfl(a, 2), n3 = __shfl(a, 3);
-        const float n4 = __shfl(a, 4), n5 = __shfl(a, 5), n6 = __shfl(a, 6), n7 = __shfl(a, 7);
-        const float t0 = n0 + n4, t1 = n1 + n5, t2 = n2 + n6, t3 = n3 + n7;
+        lds_barrier();
+        const float t0 = s_norm[0] + s_norm[4], t1 = s_norm[1] + s_norm[5], t2 = s_norm[2] + s_norm[6],
+                    t3 = s_norm[3] + s_norm[7];
         const float thr = __builtin_sqrtf((t0 + t2) + (t1 + t3)) * 0.2f;
-        val[0] = fminf(val[0], thr);
-        val[1] = fminf(val[1], thr);
+#pragma unroll
+        for (int h = 0; h < kPer; h++) {
+            val[h] = fminf(val[h], thr);
+            sq[tid + kDT * h] = val[h] * val[h];
+        }
         lds_barrier();
-        sq[lane] = val[0] * val[0];
-        sq[lane + 64] = val[1] * val[1];
-        lds_barrier();
-        float nrm2 = 0.f;  // sequential over k = 0..127, the oracle's order
-        if (lane == 0) {
+        if (tid == 0) {
+            float nrm2 = 0.f;  // sequential over k = 0..127, the oracle's order
 #pragma unroll 4
             for (int q = 0; q < 128; q += 4) {
                 const float4 s4 = *reinterpret_cast<const float4*>(sq + q);
@@ -355,15 +359,16 @@ __global__ __launch_bounds__(64) void k_descriptor(const DescJob* __restrict__ j
                 nrm2 = nrm2 + s4.z;
                 nrm2 = nrm2 + s4.w;
             }
+            s_norm[8] = 512.f / fmaxf(__builtin_sqrtf(nrm2), FLT_EPSILON);
         }
-        nrm2 = __shfl(nrm2, 0);
-        const float scale = 512.f / fmaxf(__builtin_sqrtf(nrm2), FLT_EPSILON);
+        lds_barrier();
+        const float scale = s_norm[8];
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
+        for (int h = 0; h < kPer; h++) {
             int v = cv_round(val[h] * scale);
             v = v < 0 ? 0 : (v > 255 ? 255 : v);
             const _Float16 hv = (_Float16)(float)v;
-            desc[(size_t)p * 128 + lane + 64 * h] = __builtin_bit_cast(uint16_t, hv);
+            desc[(size_t)p * 128 + tid + kDT * h] = __builtin_bit_cast(uint16_t, hv);
         }
         lds_barrier();  // sq / histograms are rewritten by the next keypoint
     }
@@ -372,7 +377,7 @@ __global__ __launch_bounds__(64) void k_descriptor(const DescJob* __restrict__ j
 void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned* range_keys, uint16_t* desc,
                        const KeypointParams& kp, hipStream_t s) {
     (void)kp;
-    hipLaunchKernelGGL(k_descriptor, dim3(8192), dim3(64), 0, s, jobs, ctr, range_keys, desc);
+    hipLaunchKernelGGL(k_descriptor, dim3(8192), dim3(kDT), 0, s, jobs, ctr, range_keys, desc);
 }
 
 }  // namespace sift_amd
