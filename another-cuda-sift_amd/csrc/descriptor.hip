@@ -42,8 +42,8 @@ constexpr int kD = 4, kN = 8;
 constexpr int kCells = (kD + 2) * (kD + 2);  // 36 spatial cells incl. the border ring
 constexpr int kMaxRows = kDescMaxRows;       // enumerated windows: side = 2R+1 <= kMaxRows
 constexpr int kGroup = 4;                    // samples whose loads are in flight together
-constexpr int kDT = 128;                     // threads (2 waves) per keypoint
-constexpr int kPer = 128 / kDT;              // descriptor entries per thread in the epilogue
+constexpr int kDT = 256;                     // threads (4 waves) per keypoint
+constexpr int kPer = kDT >= 128 ? 1 : 128 / kDT;  // descriptor entries per thread in the epilogue
 
 struct DescGeom {
     float cos_t, sin_t, exp_scale;
@@ -324,13 +324,13 @@ __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ 
         float val[kPer];
 #pragma unroll
         for (int h = 0; h < kPer; h++) {
-            const int t = tid + kDT * h;
+            const int t = min(tid + kDT * h, 127);  // threads past 128 mirror entry 127 (never stored)
             const int ii = t >> 5, jj = (t >> 3) & 3, kk = t & 7;
             const int cell = (ii + 1) * (kD + 2) + (jj + 1);
             unsigned long long hv = (unsigned long long)histE[cell * 8 + kk] + histO[cell * 10 + 1 + kk];
             if (kk == 0) hv += histO[cell * 10 + 9];
             val[h] = (float)((double)hv * (double)inv);
-            sq[t] = val[h];
+            if (tid + kDT * h < 128) sq[t] = val[h];
         }
         lds_barrier();
         if (tid < 8) {
@@ -346,7 +346,7 @@ __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ 
 #pragma unroll
         for (int h = 0; h < kPer; h++) {
             val[h] = fminf(val[h], thr);
-            sq[tid + kDT * h] = val[h] * val[h];
+            if (tid + kDT * h < 128) sq[tid + kDT * h] = val[h] * val[h];
         }
         lds_barrier();
         if (tid == 0) {
@@ -368,7 +368,7 @@ __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ 
             int v = cv_round(val[h] * scale);
             v = v < 0 ? 0 : (v > 255 ? 255 : v);
             const _Float16 hv = (_Float16)(float)v;
-            desc[(size_t)p * 128 + tid + kDT * h] = __builtin_bit_cast(uint16_t, hv);
+            if (tid + kDT * h < 128) desc[(size_t)p * 128 + tid + kDT * h] = __builtin_bit_cast(uint16_t, hv);
         }
         lds_barrier();  // sq / histograms are rewritten by the next keypoint
     }
