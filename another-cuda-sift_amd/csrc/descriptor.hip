@@ -231,7 +231,8 @@ __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ 
             const float gori = desc_atan2(dy, dx);
             const float gmag = desc_magnitude(dx, dy);
             float obin = (gori - jb.angle) * bins_per_rad;
-            const float mag = valid ? gmag * wgt : 0.f;
+            // x 2^S (exact): the trilinear parts come out in fixed-point units.
+            const float mag = valid ? gmag * wgt * fxs : 0.f;
             const int r0 = min(max(cv_floor(rbin), -1), kD - 1), c0 = min(max(cv_floor(cbin), -1), kD - 1);
             int o0 = cv_floor(obin);
             rbin -= (float)r0;
@@ -249,8 +250,8 @@ __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ 
 #pragma unroll
             for (int q = 0; q < 8; q += 2) {
                 const int off = (q & 4 ? (kD + 2) * stride : 0) + (q & 2 ? stride : 0);
-                const unsigned lo = (unsigned)(v[q] * fxs);  // truncation: < 2^-S per contribution
-                const unsigned hi = (unsigned)(v[q + 1] * fxs);
+                const unsigned lo = (unsigned)v[q];  // truncation: < 2^-S per contribution
+                const unsigned hi = (unsigned)v[q + 1];
                 atomicAdd(reinterpret_cast<unsigned long long*>(hb + off),
                           ((unsigned long long)hi << 32) | (unsigned long long)lo);
             }

@@ -141,6 +141,9 @@ struct sift_hip_detector {
     }
     template <class F>
     void timed(const char* name, double bytes, F&& fn) {
+#ifdef SIFT_SKIP_STAGES  // cost A/B builds only (tools/stage_ab.sh): results are wrong
+        if (strstr(SIFT_SKIP_STAGES, name)) return;
+#endif
         if (!timing) {
             fn();
             return;

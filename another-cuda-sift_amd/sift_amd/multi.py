@@ -40,14 +40,16 @@ def all_gather_sets(local: torch.Tensor, count: int, world: int, group=None) -> 
     counts = [torch.empty_like(cnt) for _ in range(world)]
     dist.all_gather(counts, cnt, group=group)
     local = local.contiguous()
+    # 16-bit descriptor bits travel as int32 (NCCL/RCCL and gloo have no int16).
+    wide = local.view(torch.int32) if local.dtype in (torch.int16, torch.float16) else local
     if dist.get_backend(group) == "nccl":
-        out = torch.empty((world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
-        dist.all_gather_into_tensor(out, local, group=group)
-    else:  # gloo (CPU tests): no 16-bit integer support, move the bits as int32
-        wide = local.view(torch.int32) if local.dtype in (torch.int16, torch.float16) else local
+        out = torch.empty((world,) + tuple(wide.shape), dtype=wide.dtype, device=wide.device)
+        dist.all_gather_into_tensor(out, wide, group=group)
+    else:  # gloo (CPU tests)
         parts = [torch.empty_like(wide) for _ in range(world)]
         dist.all_gather(parts, wide, group=group)
-        out = torch.stack(parts).view(local.dtype)
+        out = torch.stack(parts)
+    out = out.view(local.dtype)
     return out, [int(c.item()) for c in counts]
 
 

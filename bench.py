@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL) on the 8-GPU node; gloo to rehearse N > 1 on one GPU")
     ap.add_argument("--streams", type=int, default=3, help="detectors (HIP streams) frames rotate over")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-oracle sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -104,10 +106,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local % max(torch.cuda.device_count(), 1)  # one rank per GPU on the driver's node
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:  # gloo: exercises the N > 1 logic where RCCL cannot run (several ranks on one GPU)
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
+    cdev = dev if a.dist_backend == "nccl" else torch.device("cpu")  # collectives' tensors
 
     def barrier():
         if world > 1:
@@ -117,7 +124,7 @@ def main():
     def max_over_ranks(x):
         if world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        t = torch.tensor([x], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -161,6 +168,30 @@ def main():
     det.sync()
     single = max_over_ranks(time.perf_counter() - t)
     single_value = world * n1 * W * H / 1e6 / single
+
+    # ---- C4: 256 synthetic 1600x900 frames sharded per image over the ranks -------
+    W4, H4, N4 = 1600, 900, 256
+    mine4 = multi.frame_shard(N4, rank, world)
+    dets4 = [sift.Detector(make_config(col_width=W4, row_width=H4, numOctaves=0), device=local)
+             for _ in range(a.streams)]
+    for d in dets4:
+        d.gpuWarmUpAndAllocate()
+    frames4 = [torch.from_numpy(sift.synth_frame(i, W4, H4)).to(dev) for i in mine4[:4]]
+    for s, _ in enumerate(mine4[:6]):
+        dets4[s % a.streams].detectAndComputeDevice(frames4[s % len(frames4)].data_ptr(), W4 * 4, sync=False)
+    for d in dets4:
+        d.sync()
+    barrier()
+    t = time.perf_counter()
+    for s, _ in enumerate(mine4):
+        dets4[s % a.streams].detectAndComputeDevice(frames4[s % len(frames4)].data_ptr(), W4 * 4, sync=False)
+    for d in dets4:
+        d.sync()
+    t4 = max_over_ranks(time.perf_counter() - t)
+    c4 = {"frames": N4, "frame": f"{W4}x{H4}", "octaves": "auto", "value": round(N4 * W4 * H4 / 1e6 / t4, 2),
+          "unit": "Mpix/s", "ms_total": round(t4 * 1e3, 3), "frames_per_rank": len(mine4),
+          "note": "frame i on rank i mod N (no collective); 4 distinct synthetic frames per rank cycled"}
+    del dets4, frames4
 
     # Synchronous per-frame latency (reference semantics: detectAndCompute blocks).
     lat = []
@@ -241,16 +272,20 @@ def main():
     n_matches = int((out_m >= 0).sum().item())
 
     # ---- C5: 8-way (world-way) all-gather + pairwise match -------------------
-    c5 = None
-    if world > 1:
+    def run_c5():
         mine = sets[rank % 2].contiguous()
+
+        def gather():
+            g, c = multi.all_gather_sets(mine.to(cdev), nq, world)
+            return g.to(dev), c
+
         for _ in range(5):
-            gathered, counts = multi.all_gather_sets(mine, nq, world)
+            gathered, counts = gather()
         torch.cuda.synchronize()
         ag0, ag1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ag0.record()
         for _ in range(20):
-            gathered, counts = multi.all_gather_sets(mine, nq, world)
+            gathered, counts = gather()
         ag1.record()
         torch.cuda.synchronize()
         ag_us = max_over_ranks(ag0.elapsed_time(ag1) / 20 * 1e3)
@@ -272,9 +307,16 @@ def main():
             batched()
         m1.record()
         torch.cuda.synchronize()
-        c5 = {"allgather_us": round(ag_us, 2), "pairs_per_gpu": P,
+        return {"allgather_us": round(ag_us, 2), "pairs_per_gpu": P,
               "batched_match_ms": round(max_over_ranks(m0.elapsed_time(m1) / 50), 4),
-              "collective": "RCCL all_gather_into_tensor (torch.distributed nccl backend), sift_amd/multi.py"}
+              "collective": f"all_gather ({a.dist_backend}; nccl = RCCL all_gather_into_tensor), sift_amd/multi.py"}
+
+    c5 = None
+    if world > 1:
+        try:
+            c5 = run_c5()
+        except Exception as e:  # keep the C2 line even if the C5 side measurement fails
+            c5 = {"error": repr(e)[:300]}
 
     # ---- CPU baseline: the oracle on the host cores (rank 0, N=1 only) -------
     cpu = None
@@ -356,6 +398,7 @@ def main():
             "match_2k": {"ms": round(match_ms, 4), "ms_sync_host": round(match_sync_ms, 4),
                          "tflops": round(flops / match_ms / 1e9, 2), "mfma_frac": round(flops / match_ms / 1e9 / FP16_MFMA_PEAK_TFLOPS, 5),
                          "matches": n_matches, "ratio": 0.8},
+            "c4_256_frames_1600x900": c4,
             "c5_allgather_match": c5,
             "ref_published": {"detect_1920x1200_ms": 3.1, "match_2k_ms": "just under 1", "hardware": "RTX 4070 Super",
                               "note": "reference readme.md:11-15; config not stated (tool default upscale=false, auto octaves)"},
