@@ -141,7 +141,7 @@ __device__ __forceinline__ DescJob load_job(const DescJob* jobs, unsigned p) {
 
 __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ jobs, const Counters* __restrict__ ctr,
                                                    const unsigned* __restrict__ range_keys,
-                                                   uint16_t* __restrict__ desc) {
+                                                   uint16_t* __restrict__ desc, Counters* __restrict__ host_ctr) {
     // Two u32 fixed-point histograms so that each sample's orientation pair
     // (o0, o0+1) is one naturally aligned ds_add_u64 (low word o0, high word
     // o0+1): even o0 -> histE[cell*8 + o], odd o0 -> histO[cell*10 + 1 + o]
@@ -155,6 +155,10 @@ __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ 
 
     const int tid = threadIdx.x, lane = tid & 63;
     const unsigned n = ctr->final_n;
+    // The frame's counters are final before this (last) kernel starts: hand
+    // them to the host's pinned copy directly (no D2H copy node in the graph).
+    if (blockIdx.x == 0 && tid < (int)(sizeof(Counters) / 4))
+        reinterpret_cast<unsigned*>(host_ctr)[tid] = reinterpret_cast<const unsigned*>(ctr)[tid];
     // Pixel range of the frame; it bounds every Gaussian plane (convex blurs).
     unsigned kmax = 0, knmn = 0;
     for (int i = lane; i < kRangeSlots; i += 64) {
@@ -376,9 +380,9 @@ __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ 
 }
 
 void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned* range_keys, uint16_t* desc,
-                       const KeypointParams& kp, hipStream_t s) {
+                       Counters* host_ctr, const KeypointParams& kp, hipStream_t s) {
     (void)kp;
-    hipLaunchKernelGGL(k_descriptor, dim3(8192), dim3(kDT), 0, s, jobs, ctr, range_keys, desc);
+    hipLaunchKernelGGL(k_descriptor, dim3(8192), dim3(kDT), 0, s, jobs, ctr, range_keys, desc, host_ctr);
 }
 
 }  // namespace sift_amd

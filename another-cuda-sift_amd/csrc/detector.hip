@@ -110,7 +110,8 @@ struct sift_hip_detector {
     uint32_t* dBitmap = nullptr;
     size_t bitmapWords = 0;
     Counters* dCtr = nullptr;
-    Counters* hCtr = nullptr;
+    Counters* hCtr = nullptr;     // pinned host copy of the counters (written by k_descriptor)
+    Counters* hCtrDev = nullptr;  // its device-side address
     float* dKpts3[2] = {nullptr, nullptr};
     float* dFeats4[2] = {nullptr, nullptr};
     uint16_t* dDesc[2] = {nullptr, nullptr};
@@ -310,12 +311,14 @@ int allocate(sift_hip_detector* d) {
     if ((rc = dalloc(&d->dCtr, 1))) return rc;
     // Zeroed once here; afterwards the kernels keep them zero for the next
     // frame (first blur: counters, k_select: range keys, k_bucket_rank: bucket
-    // counts), so the frame graph has a single memset node (dedupe bitmap).
+    // counts, k_orientation: dedupe bits), so the frame graph has no memset node.
     HIPCHK(hipMemset(d->dCtr, 0, sizeof(Counters)));
     HIPCHK(hipMemset(d->dRange, 0, sizeof(unsigned) * 2 * 2 * kRangeSlots));
     HIPCHK(hipMemset(d->dBcount, 0, sizeof(unsigned) * (size_t)d->kp.numBuckets));
-    HIPCHK(hipHostMalloc((void**)&d->hCtr, sizeof(Counters), hipHostMallocDefault));
+    HIPCHK(hipMemset(d->dBitmap, 0, sizeof(uint32_t) * d->bitmapWords));
+    HIPCHK(hipHostMalloc((void**)&d->hCtr, sizeof(Counters), hipHostMallocMapped | hipHostMallocCoherent));
     memset(d->hCtr, 0, sizeof(Counters));
+    HIPCHK(hipHostGetDevicePointer((void**)&d->hCtrDev, d->hCtr, 0));
     for (int b = 0; b < 2; b++) {
         if ((rc = dalloc(&d->dKpts3[b], (size_t)capF * 3))) return rc;
         if ((rc = dalloc(&d->dFeats4[b], (size_t)capF * 4))) return rc;
@@ -352,9 +355,6 @@ void enqueue_head(sift_hip_detector* d, const float* img, int pitchFloats) {
 void enqueue_body(sift_hip_detector* d, int buf) {
     hipStream_t s = d->stream;
     const int L = d->L;
-    d->timed("memset", 0, [&] {
-        (void)hipMemsetAsync(d->dBitmap, 0, sizeof(uint32_t) * d->bitmapWords, s);
-    });
     if (d->firstOctave < 0) {
         const OctGeom& g = d->pyr.oct[0];
         d->timed("blur_init", (double)g.W * g.H * 8, [&] {
@@ -390,7 +390,7 @@ void enqueue_body(sift_hip_detector* d, int buf) {
         });
     }
     d->timed("refine", 0, [&] { launch_refine(d->pyr, d->dCand, d->capCand, d->dCtr, d->dBitmap, d->dRef, d->kp, s); });
-    d->timed("orientation", 0, [&] { launch_orientation(d->pyr, d->dRef, d->dCtr, d->dOri, d->kp, s); });
+    d->timed("orientation", 0, [&] { launch_orientation(d->pyr, d->dRef, d->dCtr, d->dOri, d->dBitmap, d->kp, s); });
     d->timed("select", 0, [&] { launch_select(d->dOri, d->dCtr, range_keys(d, buf ^ 1), d->kp, s); });
     d->timed("bucket_count", 0, [&] { launch_bucket_count(d->dOri, d->dCtr, d->dBcount, d->dSlot, d->kp, s); });
     d->timed("bucket_scan", 0, [&] { launch_bucket_scan(d->dBcount, d->dBoff, d->dCtr, d->kp, s); });
@@ -400,8 +400,7 @@ void enqueue_body(sift_hip_detector* d, int buf) {
         launch_bucket_rank(d->pyr, d->dOri, d->dBcount, d->dBoff, d->dOrder, d->dCtr, d->dJobs, d->dKpts3[buf],
                            d->dFeats4[buf], d->kp, s);
     });
-    d->timed("descriptor", 0, [&] { launch_descriptor(d->dJobs, d->dCtr, range_keys(d, buf), d->dDesc[buf], d->kp, s); });
-    (void)hipMemcpyAsync(d->hCtr, d->dCtr, sizeof(Counters), hipMemcpyDeviceToHost, s);
+    d->timed("descriptor", 0, [&] { launch_descriptor(d->dJobs, d->dCtr, range_keys(d, buf), d->dDesc[buf], d->hCtrDev, d->kp, s); });
 }
 
 int build_graphs(sift_hip_detector* d) {

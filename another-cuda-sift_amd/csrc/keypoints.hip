@@ -156,10 +156,12 @@ __global__ __launch_bounds__(256) void k_refine(PyrDesc pyr, const uint2* __rest
         k.layer = layer;
         k.rc = r << 16 | c;
         const unsigned slot = atomicAdd(&ctr->refined, 1u);
-        if (slot < kp.capRefined)
+        if (slot < kp.capRefined) {
             out[slot] = k;
-        else
+        } else {
             atomicOr(&ctr->overflow, 2u);
+            atomicAnd(&bitmap[bit >> 5], ~m);  // every set bit belongs to a stored keypoint
+        }
     }
 }
 
@@ -198,7 +200,7 @@ __device__ __forceinline__ RefKpt load_ref(const RefKpt* in, unsigned k) {  // s
 
 __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* __restrict__ in,
                                                     Counters* __restrict__ ctr, OriKpt* __restrict__ out,
-                                                    KeypointParams kp) {
+                                                    uint32_t* __restrict__ bitmap, KeypointParams kp) {
     __shared__ float chunk[64];
     __shared__ __attribute__((aligned(16))) int ccnt[kOriBins + 4];
     __shared__ int coff[kOriBins + 4];
@@ -212,6 +214,10 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
         const RefKpt kpt = load_ref(in, k);
         const int o = kpt.o, layer = kpt.layer, r = kpt.rc >> 16, c = kpt.rc & 0xffff;
         const OctGeom& g = octave_geom(pyr, o);
+        if (lane == 0) {  // clear the keypoint's dedupe bit for the next frame (no memset node)
+            const long bit = g.bitBase + ((long)(layer - 1) * g.H + r) * g.W + c;
+            atomicAnd(&bitmap[bit >> 5], ~(1u << (bit & 31)));
+        }
         const float* img = g.base + (size_t)layer * g.planeStride;
         const int pitch = g.pitch, W = g.W, H = g.H;
         const float scl_octv = kpt.size * 0.5f / (float)(1 << o);
@@ -345,9 +351,9 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
     }
 }
 
-void launch_orientation(const PyrDesc& pyr, const RefKpt* in, Counters* ctr, OriKpt* out, const KeypointParams& kp,
-                        hipStream_t s) {
-    hipLaunchKernelGGL(k_orientation, dim3(8192), dim3(64), 0, s, pyr, in, ctr, out, kp);
+void launch_orientation(const PyrDesc& pyr, const RefKpt* in, Counters* ctr, OriKpt* out, uint32_t* bitmap,
+                        const KeypointParams& kp, hipStream_t s) {
+    hipLaunchKernelGGL(k_orientation, dim3(8192), dim3(64), 0, s, pyr, in, ctr, out, bitmap, kp);
 }
 
 // ---------------------------------------------------------------------------

@@ -523,20 +523,18 @@ __global__ __launch_bounds__(256) void k_extrema_rows(OctGeom g, int o, float th
     };
 
     if (y0 < H) {
-        float ga[NG], gb[NG];
-        load_row(y0 - 1, ga);
-        load_row(y0, gb);
-        push_row(ga, hmx[0], hmn[0], dc[0]);
-        load_row(y0 + 1, ga);
-        push_row(gb, hmx[1], hmn[1], dc[1]);
-        // Steady state: row y0 + k + 1 enters slot (k + 2) % 3, row y0 + k is tested.
+        // All EX2_TH + 2 rows' loads in flight at once (one memory latency per
+        // strip), then the rows stream through the 3-row ring.
+        float gr[EX2_TH + 2][NG];
+#pragma unroll
+        for (int k = 0; k < EX2_TH + 2; k++) load_row(y0 - 1 + k, gr[k]);
+        push_row(gr[0], hmx[0], hmn[0], dc[0]);
+        push_row(gr[1], hmx[1], hmn[1], dc[1]);
+        // Row y0 + k + 1 enters slot (k + 2) % 3, row y0 + k is tested.
 #pragma unroll
         for (int k = 0; k < EX2_TH; k++) {
             const int A = k % 3, B = (k + 1) % 3, C = (k + 2) % 3;
-            float (&cur)[NG] = (k & 1) ? gb : ga;
-            float (&nxt)[NG] = (k & 1) ? ga : gb;
-            if (k + 1 < EX2_TH) load_row(y0 + k + 2, nxt);  // one row ahead in flight
-            push_row(cur, hmx[C], hmn[C], dc[C]);
+            push_row(gr[k + 2], hmx[C], hmn[C], dc[C]);
             if (y0 + k < H) test_row(y0 + k, A, B, C);
         }
     }

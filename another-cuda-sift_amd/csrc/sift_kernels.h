@@ -83,8 +83,10 @@ struct KeypointParams {
 };
 void launch_refine(const PyrDesc& pyr, const uint2* cand, unsigned capCand, Counters* ctr, uint32_t* bitmap,
                    RefKpt* out, const KeypointParams& kp, hipStream_t s);
-void launch_orientation(const PyrDesc& pyr, const RefKpt* in, Counters* ctr, OriKpt* out, const KeypointParams& kp,
-                        hipStream_t s);
+// Also clears each refined keypoint's dedupe bit (k_refine set it), so the
+// bitmap is zero again for the next frame without a memset.
+void launch_orientation(const PyrDesc& pyr, const RefKpt* in, Counters* ctr, OriKpt* out, uint32_t* bitmap,
+                        const KeypointParams& kp, hipStream_t s);
 // zero_range: the other frame buffer's 2 * kRangeSlots range keys (zeroed here
 // for the next frame, so no memset node is needed).
 void launch_select(const OriKpt* kpts, Counters* ctr, unsigned* zero_range, const KeypointParams& kp, hipStream_t s);
@@ -111,8 +113,9 @@ static_assert(sizeof(DescJob) == 64, "DescJob is one 64-byte scalar load");
 void launch_bucket_rank(const PyrDesc& pyr, const OriKpt* kpts, unsigned* bcount, const unsigned* boff,
                         const int* order, const Counters* ctr, DescJob* jobs, float* kpts3, float* feats4,
                         const KeypointParams& kp, hipStream_t s);
+// host_ctr: device-mapped pinned host memory receiving the frame's counters.
 void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned* range_keys, uint16_t* desc,
-                       const KeypointParams& kp, hipStream_t s);
+                       Counters* host_ctr, const KeypointParams& kp, hipStream_t s);
 
 // Order-preserving unsigned key of a float (0 is below every key), so that
 // atomicMax over keys is a float max with a zeroed counter as the identity.
