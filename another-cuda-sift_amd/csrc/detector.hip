@@ -84,8 +84,26 @@ struct sift_hip_detector {
     int L = 3, nOct = 0, firstOctave = 0;
     int baseW = 0, baseH = 0;
     hipStream_t stream = nullptr;
+    // Frame uploads and result downloads.  Created on first use: a stream
+    // holds a hardware queue, and device-input callers (several detectors per
+    // GPU, one stream each) need none.
+    hipStream_t copyStream = nullptr;
     hipEvent_t evIn = nullptr, evOut = nullptr;
     bool allocated = false;
+
+    // Frames are numbered in submission order.  Frame f writes results slot
+    // f % kSlots; `current` is the frame the result accessors expose (its
+    // predecessor's descriptors are prev_descriptor).  At most two frames may
+    // be in flight past `current`, so frames current-1 .. current+2 never
+    // share a slot.
+    static constexpr int kSlots = 4;
+    static constexpr int kInSlots = 2;  // upload ring (pinned staging + device)
+    long long submitted = 0, current = -1, firstFrame = 0, uploads = 0;
+    int slot_of(long long f) const { return (int)(f & (kSlots - 1)); }
+    hipEvent_t evFrame[kSlots] = {};                     // recorded after each frame's last kernel
+    void* dIn[kInSlots] = {};                            // uploaded frames (f32 or u8)
+    void* hStage[kInSlots] = {};                         // pinned staging
+    hipEvent_t evUp[kInSlots] = {}, evRead[kInSlots] = {};  // upload done / first kernel done
 
     PyrDesc pyr{};
     Taps initTaps{};
@@ -94,7 +112,7 @@ struct sift_hip_detector {
     KeypointParams kp{};
 
     int inPitch = 0, upPitch = 0;
-    float* dInput = nullptr;
+    float* dInput = nullptr;  // blank warm-up frame; f32 scratch for 8-bit frames at other init radii
     float* dUp = nullptr;
     float* dPyr = nullptr;
     uint2* dCand = nullptr;
@@ -110,14 +128,14 @@ struct sift_hip_detector {
     uint32_t* dBitmap = nullptr;
     size_t bitmapWords = 0;
     Counters* dCtr = nullptr;
-    Counters* hCtr = nullptr;     // pinned host copy of the counters (written by k_descriptor)
-    Counters* hCtrDev = nullptr;  // its device-side address
-    float* dKpts3[2] = {nullptr, nullptr};
-    float* dFeats4[2] = {nullptr, nullptr};
-    uint16_t* dDesc[2] = {nullptr, nullptr};
-    int cur = 0, count = 0, prevCount = 0;
+    Counters* hCtr = nullptr;     // kSlots pinned host copies of the counters (written by k_descriptor)
+    Counters* hCtrDev = nullptr;  // their device-side address
+    float* dKpts3[kSlots] = {};
+    float* dFeats4[kSlots] = {};
+    uint16_t* dDesc[kSlots] = {};
+    int cur = 0, count = 0, prevCount = 0;  // slot_of(current) and the counts of current, current - 1
 
-    hipGraphExec_t exec[2] = {nullptr, nullptr};
+    hipGraphExec_t exec[kSlots] = {};
     bool useGraph = true;
 
     bool timing = false;
@@ -173,14 +191,26 @@ struct sift_hip_detector {
             for (auto& e : exec)
                 if (e) (void)hipGraphExecDestroy(e);
             void* bufs[] = {dInput, dUp, dPyr, dCand, dRef, dOri, dSlot, dOrder, dJobs, dRange, dBcount, dBoff,
-                            dBitmap, dCtr, dKpts3[0], dKpts3[1], dFeats4[0], dFeats4[1], dDesc[0], dDesc[1]};
+                            dBitmap, dCtr};
             for (void* b : bufs)
                 if (b) (void)hipFree(b);
+            for (int k = 0; k < kSlots; k++) {
+                for (void* b : {(void*)dKpts3[k], (void*)dFeats4[k], (void*)dDesc[k]})
+                    if (b) (void)hipFree(b);
+                if (evFrame[k]) (void)hipEventDestroy(evFrame[k]);
+            }
+            for (int k = 0; k < kInSlots; k++) {
+                if (dIn[k]) (void)hipFree(dIn[k]);
+                if (hStage[k]) (void)hipHostFree(hStage[k]);
+                if (evUp[k]) (void)hipEventDestroy(evUp[k]);
+                if (evRead[k]) (void)hipEventDestroy(evRead[k]);
+            }
             if (hCtr) (void)hipHostFree(hCtr);
             for (auto e : evPool) (void)hipEventDestroy(e);
             if (evIn) (void)hipEventDestroy(evIn);
             if (evOut) (void)hipEventDestroy(evOut);
-            if (stream) (void)hipStreamDestroy(stream);
+            for (hipStream_t st : {stream, copyStream})
+                if (st) (void)hipStreamDestroy(st);
         }
     }
 };
@@ -280,13 +310,28 @@ int dalloc(T** p, size_t count) {
 int allocate(sift_hip_detector* d) {
     HIPCHK(hipSetDevice(d->device));
     HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+    d->allocated = true;
     HIPCHK(hipEventCreateWithFlags(&d->evIn, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&d->evOut, hipEventDisableTiming));
-    d->allocated = true;
     const int W = d->cfg.col_width, H = d->cfg.row_width;
     d->inPitch = (W + 63) / 64 * 64;
     int rc;
     if ((rc = dalloc(&d->dInput, (size_t)d->inPitch * H))) return rc;
+    // Upload ring: sized for f32 rows of pitch inPitch (an 8-bit frame uses
+    // the first quarter with a byte pitch of inPitch).
+    const size_t inBytes = sizeof(float) * (size_t)d->inPitch * H;
+    for (int k = 0; k < d->kInSlots; k++) {
+        if (hipMalloc(&d->dIn[k], inBytes) != hipSuccess) return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc failed");
+        HIPCHK(hipHostMalloc(&d->hStage[k], inBytes, hipHostMallocDefault));
+        HIPCHK(hipEventCreateWithFlags(&d->evUp[k], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&d->evRead[k], hipEventDisableTiming));
+        HIPCHK(hipEventRecord(d->evUp[k], d->stream));
+        HIPCHK(hipEventRecord(d->evRead[k], d->stream));
+    }
+    for (int k = 0; k < d->kSlots; k++) {
+        HIPCHK(hipEventCreateWithFlags(&d->evFrame[k], hipEventDisableTiming));
+        HIPCHK(hipEventRecord(d->evFrame[k], d->stream));
+    }
     if (d->firstOctave < 0) {
         d->upPitch = (2 * W + 63) / 64 * 64;
         if ((rc = dalloc(&d->dUp, (size_t)d->upPitch * 2 * H))) return rc;
@@ -316,10 +361,10 @@ int allocate(sift_hip_detector* d) {
     HIPCHK(hipMemset(d->dRange, 0, sizeof(unsigned) * 2 * 2 * kRangeSlots));
     HIPCHK(hipMemset(d->dBcount, 0, sizeof(unsigned) * (size_t)d->kp.numBuckets));
     HIPCHK(hipMemset(d->dBitmap, 0, sizeof(uint32_t) * d->bitmapWords));
-    HIPCHK(hipHostMalloc((void**)&d->hCtr, sizeof(Counters), hipHostMallocMapped | hipHostMallocCoherent));
-    memset(d->hCtr, 0, sizeof(Counters));
+    HIPCHK(hipHostMalloc((void**)&d->hCtr, sizeof(Counters) * d->kSlots, hipHostMallocMapped | hipHostMallocCoherent));
+    memset(d->hCtr, 0, sizeof(Counters) * d->kSlots);
     HIPCHK(hipHostGetDevicePointer((void**)&d->hCtrDev, d->hCtr, 0));
-    for (int b = 0; b < 2; b++) {
+    for (int b = 0; b < d->kSlots; b++) {
         if ((rc = dalloc(&d->dKpts3[b], (size_t)capF * 3))) return rc;
         if ((rc = dalloc(&d->dFeats4[b], (size_t)capF * 4))) return rc;
         if ((rc = dalloc(&d->dDesc[b], (size_t)capF * 128))) return rc;
@@ -330,36 +375,51 @@ int allocate(sift_hip_detector* d) {
     return SIFT_HIP_OK;
 }
 
-// The first kernel reads the caller's image (host upload buffer or a device
+// The first kernel reads the caller's image (upload ring slot or a device
 // pointer); it stays outside the graph so the graph never bakes a user pointer.
-// Pixel-range keys of frame buffer b (the frame in flight uses b = cur; the
-// other set is zeroed by k_select for the next frame).
-unsigned* range_keys(sift_hip_detector* d, int b) { return d->dRange + (size_t)b * 2 * kRangeSlots; }
+// Pixel-range keys by frame parity p (frame f uses p = f & 1; k_select zeroes
+// the other set for the next frame).
+unsigned* range_keys(sift_hip_detector* d, int p) { return d->dRange + (size_t)p * 2 * kRangeSlots; }
 
-void enqueue_head(sift_hip_detector* d, const float* img, int pitchFloats) {
+// pitch in elements of the frame's format (bytes for SIFT_HIP_U8).
+void enqueue_head(sift_hip_detector* d, const void* img, int pitch, int fmt, int parity) {
     const int W = d->cfg.col_width, H = d->cfg.row_width;
+    const bool u8 = fmt == SIFT_HIP_U8;
+    const double inB = (double)W * H * (u8 ? 1 : 4);
     // Counters first: the initial blur accumulates the frame's pixel range.
     if (d->firstOctave < 0) {
-        d->timed("upsample", (double)W * H * 4 + (double)W * H * 16, [&] {
-            launch_upsample2x(img, pitchFloats, W, H, d->dUp, d->upPitch, d->stream);
+        d->timed("upsample", inB + (double)W * H * 16, [&] {
+            if (u8)
+                launch_upsample2x_u8((const uint8_t*)img, pitch, W, H, d->dUp, d->upPitch, d->stream);
+            else
+                launch_upsample2x((const float*)img, pitch, W, H, d->dUp, d->upPitch, d->stream);
         });
     } else {
         const OctGeom& g = d->pyr.oct[0];
-        d->timed("blur_init", (double)W * H * 8, [&] {
-            launch_blur(img, pitchFloats, 1, W, H, g.base, g.pitch, nullptr, d->initTaps, d->stream, range_keys(d, d->cur),
-                        d->dCtr);
+        d->timed("blur_init", inB + (double)W * H * 4, [&] {
+            if (u8) {
+                if (launch_blur_u8((const uint8_t*)img, pitch, W, H, g.base, g.pitch, d->initTaps, d->stream,
+                                   range_keys(d, parity), d->dCtr))
+                    return;
+                launch_u8_to_f32((const uint8_t*)img, pitch, W, H, d->dInput, d->inPitch, d->stream);
+                img = d->dInput;
+                pitch = d->inPitch;
+            }
+            launch_blur((const float*)img, pitch, 1, W, H, g.base, g.pitch, nullptr, d->initTaps, d->stream,
+                        range_keys(d, parity), d->dCtr);
         });
     }
 }
 
-void enqueue_body(sift_hip_detector* d, int buf) {
+void enqueue_body(sift_hip_detector* d, int slot) {
     hipStream_t s = d->stream;
     const int L = d->L;
+    const int parity = slot & 1;  // kSlots is even, so slot parity = frame parity
     if (d->firstOctave < 0) {
         const OctGeom& g = d->pyr.oct[0];
         d->timed("blur_init", (double)g.W * g.H * 8, [&] {
-            launch_blur(d->dUp, d->upPitch, 1, g.W, g.H, g.base, g.pitch, nullptr, d->initTaps, s, range_keys(d, buf),
-                        d->dCtr);
+            launch_blur(d->dUp, d->upPitch, 1, g.W, g.H, g.base, g.pitch, nullptr, d->initTaps, s,
+                        range_keys(d, parity), d->dCtr);
         });
     }
     static const char* blurNames[kMaxOctaves] = {"blur_o0", "blur_o1", "blur_o2", "blur_o3", "blur_o4", "blur_o5",
@@ -391,20 +451,22 @@ void enqueue_body(sift_hip_detector* d, int buf) {
     }
     d->timed("refine", 0, [&] { launch_refine(d->pyr, d->dCand, d->capCand, d->dCtr, d->dBitmap, d->dRef, d->kp, s); });
     d->timed("orientation", 0, [&] { launch_orientation(d->pyr, d->dRef, d->dCtr, d->dOri, d->dBitmap, d->kp, s); });
-    d->timed("select", 0, [&] { launch_select(d->dOri, d->dCtr, range_keys(d, buf ^ 1), d->kp, s); });
+    d->timed("select", 0, [&] { launch_select(d->dOri, d->dCtr, range_keys(d, parity ^ 1), d->kp, s); });
     d->timed("bucket_count", 0, [&] { launch_bucket_count(d->dOri, d->dCtr, d->dBcount, d->dSlot, d->kp, s); });
     d->timed("bucket_scan", 0, [&] { launch_bucket_scan(d->dBcount, d->dBoff, d->dCtr, d->kp, s); });
     d->timed("bucket_scatter", 0,
              [&] { launch_bucket_scatter(d->dOri, d->dCtr, d->dBoff, d->dSlot, d->dOrder, d->kp, s); });
     d->timed("bucket_rank", 0, [&] {
-        launch_bucket_rank(d->pyr, d->dOri, d->dBcount, d->dBoff, d->dOrder, d->dCtr, d->dJobs, d->dKpts3[buf],
-                           d->dFeats4[buf], d->kp, s);
+        launch_bucket_rank(d->pyr, d->dOri, d->dBcount, d->dBoff, d->dOrder, d->dCtr, d->dJobs, d->dKpts3[slot],
+                           d->dFeats4[slot], d->kp, s);
     });
-    d->timed("descriptor", 0, [&] { launch_descriptor(d->dJobs, d->dCtr, range_keys(d, buf), d->dDesc[buf], d->hCtrDev, d->kp, s); });
+    d->timed("descriptor", 0, [&] {
+        launch_descriptor(d->dJobs, d->dCtr, range_keys(d, parity), d->dDesc[slot], d->hCtrDev + slot, d->kp, s);
+    });
 }
 
 int build_graphs(sift_hip_detector* d) {
-    for (int b = 0; b < 2; b++) {
+    for (int b = 0; b < d->kSlots; b++) {
         hipGraph_t g = nullptr;
         HIPCHK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
         enqueue_body(d, b);
@@ -415,22 +477,100 @@ int build_graphs(sift_hip_detector* d) {
     return SIFT_HIP_OK;
 }
 
-int run_frame(sift_hip_detector* d, const float* img, int pitchFloats) {
-    d->prevCount = d->count;
-    d->cur ^= 1;
-    enqueue_head(d, img, pitchFloats);
+// Enqueues frame d->submitted on d->stream; `consumed` (nullable) is recorded
+// once the frame's input has been read.
+int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEvent_t consumed) {
+    const long long f = d->submitted;
+    const int slot = d->slot_of(f);
+    enqueue_head(d, img, pitch, fmt, slot & 1);
+    if (consumed) HIPCHK(hipEventRecord(consumed, d->stream));
     if (d->useGraph && !d->timing) {
-        HIPCHK(hipGraphLaunch(d->exec[d->cur], d->stream));
+        HIPCHK(hipGraphLaunch(d->exec[slot], d->stream));
     } else {
-        enqueue_body(d, d->cur);
+        enqueue_body(d, slot);
     }
+    HIPCHK(hipEventRecord(d->evFrame[slot], d->stream));
+    d->submitted = f + 1;
     return SIFT_HIP_OK;
+}
+
+// Exposes frame f through the result accessors.  Its counts are read once the
+// frame is complete (complete_counts).
+void make_current(sift_hip_detector* d, long long f) {
+    d->current = f;
+    d->cur = d->slot_of(f);
+}
+
+void complete_counts(sift_hip_detector* d) {
+    const long long f = d->current;
+    auto n = [&](long long g) {
+        return g < d->firstFrame ? 0 : (int)std::min<unsigned>(d->hCtr[d->slot_of(g)].final_n, d->kp.capFinal);
+    };
+    d->count = n(f);
+    d->prevCount = n(f - 1);
 }
 
 int finish_frame(sift_hip_detector* d) {
     HIPCHK(hipStreamSynchronize(d->stream));
     if (d->timing) d->collect_timing();
-    d->count = (int)std::min<unsigned>(d->hCtr->final_n, d->kp.capFinal);
+    if (d->submitted > 0) {
+        make_current(d, d->submitted - 1);
+        complete_counts(d);
+    }
+    return SIFT_HIP_OK;
+}
+
+int copy_stream(sift_hip_detector* d, hipStream_t* s) {
+    if (!d->copyStream) HIPCHK(hipStreamCreateWithFlags(&d->copyStream, hipStreamNonBlocking));
+    *s = d->copyStream;
+    return SIFT_HIP_OK;
+}
+
+int format_size(int fmt) { return fmt == SIFT_HIP_U8 ? 1 : (fmt == SIFT_HIP_F32 ? 4 : 0); }
+
+// Host frame -> pinned staging (the caller's buffer is free on return) ->
+// device upload ring on copyStream (overlapping the frames in flight) ->
+// pipeline on d->stream.
+int submit_host(sift_hip_detector* d, const void* img, size_t stride, int fmt, long long* ticket) {
+    const int es = format_size(fmt);
+    if (!es) return fail(SIFT_HIP_ERR_INVALID, "unknown pixel format");
+    if (!img) return fail(SIFT_HIP_ERR_INVALID, "null image");
+    const int W = d->cfg.col_width, H = d->cfg.row_width;
+    const size_t rowB = (size_t)es * W, pitchB = (size_t)es * d->inPitch;
+    if (stride == 0) stride = rowB;
+    if (stride < rowB) return fail(SIFT_HIP_ERR_INVALID, "row stride smaller than width");
+    if (d->submitted > d->current + 2)
+        return fail(SIFT_HIP_ERR_STATE, "two frames already in flight past the current one: sift_hip_wait first");
+    hipStream_t cs;
+    if (int rc = copy_stream(d, &cs)) return rc;
+    const int k = (int)(d->uploads & (d->kInSlots - 1));
+    HIPCHK(hipEventSynchronize(d->evUp[k]));  // staging slot k no longer being read
+    char* dst = (char*)d->hStage[k];
+    const char* src = (const char*)img;
+    if (stride == pitchB) {
+        memcpy(dst, src, pitchB * (H - 1) + rowB);
+    } else {
+        for (int y = 0; y < H; y++) memcpy(dst + pitchB * y, src + stride * y, rowB);
+    }
+    HIPCHK(hipStreamWaitEvent(cs, d->evRead[k], 0));  // device slot k read by its last frame
+    HIPCHK(hipMemcpyAsync(d->dIn[k], d->hStage[k], pitchB * H, hipMemcpyHostToDevice, cs));
+    HIPCHK(hipEventRecord(d->evUp[k], cs));
+    HIPCHK(hipStreamWaitEvent(d->stream, d->evUp[k], 0));
+    d->uploads++;
+    const long long f = d->submitted;
+    int rc = run_frame(d, d->dIn[k], d->inPitch, fmt, d->evRead[k]);
+    if (rc) return rc;
+    if (ticket) *ticket = f;
+    return SIFT_HIP_OK;
+}
+
+int wait_frame(sift_hip_detector* d, long long f) {
+    if (f < d->firstFrame || f >= d->submitted) return fail(SIFT_HIP_ERR_INVALID, "unknown frame ticket");
+    if (f < d->submitted - (d->kSlots - 1)) return fail(SIFT_HIP_ERR_STATE, "frame results already recycled");
+    HIPCHK(hipEventSynchronize(d->evFrame[d->slot_of(f)]));
+    if (d->timing && f == d->submitted - 1) d->collect_timing();
+    make_current(d, f);
+    complete_counts(d);
     return SIFT_HIP_OK;
 }
 
@@ -507,10 +647,11 @@ int sift_hip_warmup(sift_hip_t d) {
     rc = build_graphs(d);
     if (rc) return rc;
     // One blank frame through each graph: first-touch, code-object load.
-    for (int i = 0; i < 2; i++) {
-        if ((rc = run_frame(d, d->dInput, d->inPitch))) return rc;
+    for (int i = 0; i < d->kSlots; i++) {
+        if ((rc = run_frame(d, d->dInput, d->inPitch, SIFT_HIP_F32, nullptr))) return rc;
         if ((rc = finish_frame(d))) return rc;
     }
+    d->firstFrame = d->submitted;
     d->count = d->prevCount = 0;
     return SIFT_HIP_OK;
 }
@@ -531,36 +672,59 @@ int sift_hip_octave_dims(sift_hip_t h, int o, int* w, int* hh, int* pitch) {
 
 int sift_hip_detect(sift_hip_t d, const float* img, size_t stride) {
     CHECK_HANDLE(d);
-    if (!img) return fail(SIFT_HIP_ERR_INVALID, "null image");
-    const int W = d->cfg.col_width, H = d->cfg.row_width;
-    if (stride == 0) stride = sizeof(float) * (size_t)W;
-    if (stride < sizeof(float) * (size_t)W) return fail(SIFT_HIP_ERR_INVALID, "row stride smaller than width");
-    HIPCHK(hipMemcpy2DAsync(d->dInput, sizeof(float) * d->inPitch, img, stride, sizeof(float) * W, H,
-                            hipMemcpyHostToDevice, d->stream));
-    int rc = run_frame(d, d->dInput, d->inPitch);
-    if (rc) return rc;
-    return finish_frame(d);
+    long long f = 0;
+    int rc = submit_host(d, img, stride, SIFT_HIP_F32, &f);
+    return rc ? rc : wait_frame(d, f);
 }
 
-int sift_hip_detect_device(sift_hip_t d, const float* img, size_t stride, void* stream) {
+int sift_hip_detect_u8(sift_hip_t d, const uint8_t* img, size_t stride) {
+    CHECK_HANDLE(d);
+    long long f = 0;
+    int rc = submit_host(d, img, stride, SIFT_HIP_U8, &f);
+    return rc ? rc : wait_frame(d, f);
+}
+
+int sift_hip_submit(sift_hip_t d, const void* img, size_t stride, int format, long long* ticket) {
+    CHECK_HANDLE(d);
+    return submit_host(d, img, stride, format, ticket);
+}
+
+int sift_hip_wait(sift_hip_t d, long long ticket) {
+    CHECK_HANDLE(d);
+    return wait_frame(d, ticket);
+}
+
+int sift_hip_detect_device_fmt(sift_hip_t d, const void* img, size_t stride, int format, void* stream) {
     CHECK_HANDLE(d);
     if (!img) return fail(SIFT_HIP_ERR_INVALID, "null image");
+    const int es = format_size(format);
+    if (!es) return fail(SIFT_HIP_ERR_INVALID, "unknown pixel format");
     const int W = d->cfg.col_width;
-    if (stride == 0) stride = sizeof(float) * (size_t)W;
-    if (stride % sizeof(float) || stride < sizeof(float) * (size_t)W)
-        return fail(SIFT_HIP_ERR_INVALID, "row stride must be a multiple of 4 and >= 4*width");
+    if (stride == 0) stride = (size_t)es * W;
+    if (stride % es || stride < (size_t)es * W)
+        return fail(SIFT_HIP_ERR_INVALID, "row stride must be a multiple of the pixel size and >= width");
+    if (d->submitted > d->current + 2)
+        return fail(SIFT_HIP_ERR_STATE, "two frames already in flight past the current one: sift_hip_wait first");
     hipStream_t ext = (hipStream_t)stream;
     if (ext) {
         HIPCHK(hipEventRecord(d->evIn, ext));
         HIPCHK(hipStreamWaitEvent(d->stream, d->evIn, 0));
     }
-    int rc = run_frame(d, img, (int)(stride / sizeof(float)));
+    const long long f = d->submitted;
+    int rc = run_frame(d, img, (int)(stride / es), format, nullptr);
     if (rc) return rc;
+    // Device-ordered consumers see this frame's buffers at once; counts
+    // follow at sift_hip_sync / sift_hip_wait.
+    make_current(d, f);
     if (ext) {
         HIPCHK(hipEventRecord(d->evOut, d->stream));
         HIPCHK(hipStreamWaitEvent(ext, d->evOut, 0));
     }
     return SIFT_HIP_OK;
+}
+
+int sift_hip_detect_device(sift_hip_t d, const float* img, size_t stride, void* stream) {
+    return sift_hip_detect_device_fmt(d, img, stride, SIFT_HIP_F32, stream);
 }
 
 int sift_hip_sync(sift_hip_t d) {
@@ -576,7 +740,7 @@ int sift_hip_num_keypoints(sift_hip_t d, int* n) {
 
 int sift_hip_overflow_flags(sift_hip_t d, int* flags) {
     if (!d || !flags) return fail(SIFT_HIP_ERR_INVALID, "null argument");
-    *flags = d->hCtr ? (int)d->hCtr->overflow : 0;
+    *flags = d->hCtr ? (int)d->hCtr[d->cur].overflow : 0;
     return SIFT_HIP_OK;
 }
 
@@ -586,7 +750,7 @@ int sift_hip_results_device(sift_hip_t d, const float** k3, const float** f4, co
     if (k3) *k3 = d->dKpts3[d->cur];
     if (f4) *f4 = d->dFeats4[d->cur];
     if (desc) *desc = d->dDesc[d->cur];
-    if (prev) *prev = d->dDesc[d->cur ^ 1];
+    if (prev) *prev = d->dDesc[d->slot_of(d->current - 1)];
     if (prevCount) *prevCount = d->prevCount;
     if (capacity) *capacity = (int)d->kp.capFinal;
     return SIFT_HIP_OK;
@@ -595,16 +759,18 @@ int sift_hip_results_device(sift_hip_t d, const float** k3, const float** f4, co
 int sift_hip_copy_to_host(sift_hip_t d, float* k3, float* f4, uint16_t* desc, int cap) {
     CHECK_HANDLE(d);
     const int n = std::min(d->count, cap);
+    // On the copy stream, ordered after the current frame only: frames
+    // submitted after it keep running.
+    hipStream_t s;
+    if (int rc = copy_stream(d, &s)) return rc;
+    HIPCHK(hipStreamWaitEvent(s, d->evFrame[d->cur], 0));
     if (n > 0) {
-        if (k3)
-            HIPCHK(hipMemcpyAsync(k3, d->dKpts3[d->cur], sizeof(float) * 3 * n, hipMemcpyDeviceToHost, d->stream));
-        if (f4)
-            HIPCHK(hipMemcpyAsync(f4, d->dFeats4[d->cur], sizeof(float) * 4 * n, hipMemcpyDeviceToHost, d->stream));
+        if (k3) HIPCHK(hipMemcpyAsync(k3, d->dKpts3[d->cur], sizeof(float) * 3 * n, hipMemcpyDeviceToHost, s));
+        if (f4) HIPCHK(hipMemcpyAsync(f4, d->dFeats4[d->cur], sizeof(float) * 4 * n, hipMemcpyDeviceToHost, s));
         if (desc)
-            HIPCHK(hipMemcpyAsync(desc, d->dDesc[d->cur], sizeof(uint16_t) * 128 * n, hipMemcpyDeviceToHost,
-                                  d->stream));
+            HIPCHK(hipMemcpyAsync(desc, d->dDesc[d->cur], sizeof(uint16_t) * 128 * n, hipMemcpyDeviceToHost, s));
     }
-    HIPCHK(hipStreamSynchronize(d->stream));
+    HIPCHK(hipStreamSynchronize(s));
     return SIFT_HIP_OK;
 }
 
@@ -612,6 +778,7 @@ int sift_hip_copy_descriptors_device(sift_hip_t d, uint16_t* dst, int cap, void*
     CHECK_HANDLE(d);
     const int n = std::min(d->count, cap);
     hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+    if (s != d->stream) HIPCHK(hipStreamWaitEvent(s, d->evFrame[d->cur], 0));
     if (n > 0) HIPCHK(hipMemcpyAsync(dst, d->dDesc[d->cur], sizeof(uint16_t) * 128 * n, hipMemcpyDeviceToDevice, s));
     if (!stream) HIPCHK(hipStreamSynchronize(s));
     return SIFT_HIP_OK;
@@ -656,8 +823,9 @@ int sift_hip_debug_gaussian(sift_hip_t d, int o, int layer, float* out) {
 
 int sift_hip_debug_candidates(sift_hip_t d, int* quads, int cap, int* count) {
     CHECK_HANDLE(d);
-    const int n = (int)std::min<unsigned>(d->hCtr->cand, d->capCand);
-    if (count) *count = (int)d->hCtr->cand;
+    const Counters& c = d->hCtr[d->cur];
+    const int n = (int)std::min<unsigned>(c.cand, d->capCand);
+    if (count) *count = (int)c.cand;
     const int m = std::min(n, cap);
     if (m > 0 && quads) {
         std::vector<uint2> tmp(m);

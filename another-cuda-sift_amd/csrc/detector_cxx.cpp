@@ -93,6 +93,48 @@ void Detector::detectAndCompute(const Imagef& image) {
     refreshViews();
 }
 
+namespace {
+
+template <class T>
+void check_shape(const Image<T>& image, const CudaSiftConfig& c, const char* what) {
+    if (!image.m_data || image.cols() != c.col_width || image.rows() != c.row_width) {
+        std::fprintf(stderr, "%s: image is %dx%d, detector configured for %dx%d\n", what, image.cols(), image.rows(),
+                     c.col_width, c.row_width);
+        std::exit(EXIT_FAILURE);
+    }
+}
+
+}  // namespace
+
+void Detector::detectAndCompute(const Image8U& image) {
+    if (!m_initialized && !gpuWarmUpAndAllocate()) return;
+    check_shape(image, m_config, "detectAndCompute");
+    check(sift_hip_detect_u8(m_handle, image.m_data->data(), (size_t)image.cols()), "detectAndCompute");
+    refreshViews();
+}
+
+long long Detector::submit(const Imagef& image) {
+    if (!m_initialized && !gpuWarmUpAndAllocate()) return -1;
+    check_shape(image, m_config, "submit");
+    long long t = -1;
+    check(sift_hip_submit(m_handle, image.m_data->data(), sizeof(float) * (size_t)image.cols(), SIFT_HIP_F32, &t),
+          "submit");
+    return t;
+}
+
+long long Detector::submit(const Image8U& image) {
+    if (!m_initialized && !gpuWarmUpAndAllocate()) return -1;
+    check_shape(image, m_config, "submit");
+    long long t = -1;
+    check(sift_hip_submit(m_handle, image.m_data->data(), (size_t)image.cols(), SIFT_HIP_U8, &t), "submit");
+    return t;
+}
+
+void Detector::wait(long long ticket) {
+    check(sift_hip_wait(m_handle, ticket), "wait");
+    refreshViews();
+}
+
 void Detector::detectAndComputeDevice(const float* dev, size_t stride, void* stream) {
     if (!m_initialized && !gpuWarmUpAndAllocate()) return;
     check(sift_hip_detect_device(m_handle, dev, stride, stream), "detectAndComputeDevice");

@@ -27,7 +27,8 @@ __device__ __forceinline__ void up_coeff(int d, int slen, int& s, float& a0, flo
     a1 = f;
 }
 
-__global__ __launch_bounds__(256) void k_upsample2x(const float* __restrict__ src, int spitch, int W, int H,
+template <typename T>
+__global__ __launch_bounds__(256) void k_upsample2x(const T* __restrict__ src, int spitch, int W, int H,
                                                     float* __restrict__ dst, int dpitch) {
     const int x = blockIdx.x * 64 + (threadIdx.x & 63);
     const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
@@ -37,16 +38,21 @@ __global__ __launch_bounds__(256) void k_upsample2x(const float* __restrict__ sr
     up_coeff(x, W, sx, ax0, ax1);
     up_coeff(y, H, sy, ay0, ay1);
     const int sx1 = min(sx + 1, W - 1), sy1 = min(sy + 1, H - 1);
-    const float* r0 = src + (size_t)sy * spitch;
-    const float* r1 = src + (size_t)sy1 * spitch;
-    const float h0 = r0[sx] * ax0 + r0[sx1] * ax1;
-    const float h1 = r1[sx] * ax0 + r1[sx1] * ax1;
+    const T* r0 = src + (size_t)sy * spitch;
+    const T* r1 = src + (size_t)sy1 * spitch;
+    const float h0 = (float)r0[sx] * ax0 + (float)r0[sx1] * ax1;
+    const float h1 = (float)r1[sx] * ax0 + (float)r1[sx1] * ax1;
     dst[(size_t)y * dpitch + x] = h0 * ay0 + h1 * ay1;
 }
 
 void launch_upsample2x(const float* src, int spitch, int W, int H, float* dst, int dpitch, hipStream_t s) {
     dim3 grid((2 * W + 63) / 64, (2 * H + 3) / 4);
-    hipLaunchKernelGGL(k_upsample2x, grid, dim3(256), 0, s, src, spitch, W, H, dst, dpitch);
+    hipLaunchKernelGGL(k_upsample2x<float>, grid, dim3(256), 0, s, src, spitch, W, H, dst, dpitch);
+}
+
+void launch_upsample2x_u8(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, hipStream_t s) {
+    dim3 grid((2 * W + 63) / 64, (2 * H + 3) / 4);
+    hipLaunchKernelGGL(k_upsample2x<uint8_t>, grid, dim3(256), 0, s, src, spitch, W, H, dst, dpitch);
 }
 
 // ---------------------------------------------------------------------------
@@ -74,8 +80,11 @@ __device__ __forceinline__ f32x2 pk_mov_hi_lo(f32x2 a, f32x2 b) {
 constexpr int BLUR_TW = 64;
 constexpr int BLUR_TH = 32;
 
-template <int R>
-__global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, int spitch, int sstep, int W, int H,
+// T = float, or uint8_t for a caller's 8-bit frame read by the frame's first
+// blur (OpenCV converts CV_8U to float exactly, so the planes are those of the
+// float frame with the same values).
+template <int R, typename T = float>
+__global__ __launch_bounds__(256) void k_blur(const T* __restrict__ src, int spitch, int sstep, int W, int H,
                                               float* __restrict__ dst, int dpitch, float* __restrict__ copy_out,
                                               Taps taps, unsigned* __restrict__ range_keys,
                                               Counters* __restrict__ zero_ctr) {
@@ -116,16 +125,22 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, int
             return reflect101(p, len);
         };
         const int gx0 = refl(x0 - R + lane, W), gx1 = refl(x0 - R + 64 + min(lane, RW - 65), W);
+        constexpr int ES = (int)sizeof(T);
         const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<float*>(src), 0, (int)min((long)spitch * sstep * H * 4, 0x7fffffffL), 0x00020000);
-        const unsigned c0 = (unsigned)(gx0 * sstep) * 4u, c1 = (unsigned)(gx1 * sstep) * 4u;
+            const_cast<T*>(src), 0, (int)min((long)spitch * sstep * H * ES, 0x7fffffffL), 0x00020000);
+        const unsigned c0 = (unsigned)(gx0 * sstep) * ES, c1 = (unsigned)(gx1 * sstep) * ES;
         float v0[RPW], v1[RPW];
 #pragma unroll
         for (int i = 0; i < RPW; i++) {
             const int ly = min(wv + 4 * i, IH - 1);
-            const int roff = __builtin_amdgcn_readfirstlane(refl(y0 - R + ly, H) * spitch * sstep * 4);
-            v0[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, c0, roff, 0));
-            v1[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, c1, roff, 0));
+            const int roff = __builtin_amdgcn_readfirstlane(refl(y0 - R + ly, H) * spitch * sstep * ES);
+            if constexpr (ES == 1) {
+                v0[i] = (float)__builtin_amdgcn_raw_buffer_load_b8(rsrc, c0, roff, 0);
+                v1[i] = (float)__builtin_amdgcn_raw_buffer_load_b8(rsrc, c1, roff, 0);
+            } else {
+                v0[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, c0, roff, 0));
+                v1[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, c1, roff, 0));
+            }
         }
 #pragma unroll
         for (int i = 0; i < RPW; i++) {
@@ -135,7 +150,7 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, int
                 if (lane < RW - 64) in[ly * IW + 64 + lane] = v1[i];
             }
         }
-        if (copy_out) {  // decimated base plane of this octave = the tile's interior inputs
+        if (ES == 4 && copy_out) {  // decimated base plane of this octave = the tile's interior inputs
 #pragma unroll
             for (int i = 0; i < RPW; i++) {
                 const int ly = wv + 4 * i, gy = y0 - R + ly;
@@ -276,6 +291,37 @@ constexpr std::array<BlurLaunch, sizeof...(Rs)> blur_table(std::integer_sequence
     return {&blur_launch_r<Rs + 1>...};
 }
 static const std::array<BlurLaunch, kMaxTaps / 2> kBlurTable = blur_table(std::make_integer_sequence<int, kMaxTaps / 2>{});
+
+// 8-bit frames: the first blur reads the bytes itself for the default init
+// radii (sigma 1.6: 13 taps without upscale); any other radius converts the
+// frame to float first (k_u8_to_f32) and runs the float blur.
+bool launch_blur_u8(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, const Taps& taps,
+                    hipStream_t s, unsigned* range_keys, Counters* zero_ctr) {
+    const int r = taps.n >> 1;
+    dim3 grid((W + BLUR_TW - 1) / BLUR_TW, (H + BLUR_TH - 1) / BLUR_TH);
+    switch (r) {
+        case 5:
+            hipLaunchKernelGGL((k_blur<5, uint8_t>), grid, dim3(256), 0, s, src, spitch, 1, W, H, dst, dpitch, nullptr,
+                               taps, range_keys, zero_ctr);
+            return true;
+        case 6:
+            hipLaunchKernelGGL((k_blur<6, uint8_t>), grid, dim3(256), 0, s, src, spitch, 1, W, H, dst, dpitch, nullptr,
+                               taps, range_keys, zero_ctr);
+            return true;
+        default:
+            return false;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_u8_to_f32(const uint8_t* __restrict__ src, int spitch, int W, int H,
+                                                   float* __restrict__ dst, int dpitch) {
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x < W) dst[(size_t)y * dpitch + x] = (float)src[(size_t)y * spitch + x];
+}
+
+void launch_u8_to_f32(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, hipStream_t s) {
+    hipLaunchKernelGGL(k_u8_to_f32, dim3((W + 255) / 256, H), dim3(256), 0, s, src, spitch, W, H, dst, dpitch);
+}
 
 void launch_blur(const float* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, float* copy_out,
                  const Taps& taps, hipStream_t s, unsigned* range_keys, Counters* zero_ctr) {

@@ -70,6 +70,13 @@ constexpr int kRangeSlots = 256;
 // zero_ctr (nullable): counters to zero (the frame's first blur).
 void launch_blur(const float* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, float* copy_out,
                  const Taps& taps, hipStream_t s, unsigned* range_keys = nullptr, Counters* zero_ctr = nullptr);
+// 8-bit frames (pitches in bytes).  launch_blur_u8 returns false (nothing
+// launched) for an init radius without a fused 8-bit instantiation; the caller
+// then converts with launch_u8_to_f32 and uses launch_blur.
+bool launch_blur_u8(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, const Taps& taps,
+                    hipStream_t s, unsigned* range_keys, Counters* zero_ctr);
+void launch_u8_to_f32(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, hipStream_t s);
+void launch_upsample2x_u8(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, hipStream_t s);
 void launch_extrema(const PyrDesc& pyr, int o, float threshold, uint2* cand, Counters* ctr, unsigned cap,
                     hipStream_t s);
 

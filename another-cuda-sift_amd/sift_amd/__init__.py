@@ -28,6 +28,7 @@ LIB_DIR = os.path.normpath(os.path.join(_HERE, "..", "lib"))
 LIB_PATH = os.environ.get("SIFT_HIP_LIB") or os.path.join(LIB_DIR, "libsift_hip.so")
 
 SIFT_HIP_OK = 0
+SIFT_HIP_F32, SIFT_HIP_U8 = 0, 1  # pixel formats (include/sift_hip.h)
 _lib = None
 
 
@@ -70,6 +71,10 @@ def lib() -> ctypes.CDLL:
         "sift_hip_octave_dims": (i, [vp, i, ip, ip, ip]),
         "sift_hip_detect": (i, [vp, vp, sz]),
         "sift_hip_detect_device": (i, [vp, vp, sz, vp]),
+        "sift_hip_detect_u8": (i, [vp, vp, sz]),
+        "sift_hip_detect_device_fmt": (i, [vp, vp, sz, i, vp]),
+        "sift_hip_submit": (i, [vp, vp, sz, i, ctypes.POINTER(ctypes.c_longlong)]),
+        "sift_hip_wait": (i, [vp, ctypes.c_longlong]),
         "sift_hip_sync": (i, [vp]),
         "sift_hip_num_keypoints": (i, [vp, ip]),
         "sift_hip_overflow_flags": (i, [vp, ip]),
@@ -219,18 +224,44 @@ class Detector:
         lib().sift_hip_num_keypoints(self._h, ctypes.byref(n))
         self.total_size = n.value
 
-    def detectAndCompute(self, image: np.ndarray) -> None:
-        """Detector.cu:133-233.  `image`: float32 (rows, cols) 0..255."""
-        self.gpuWarmUpAndAllocate()
-        img = np.ascontiguousarray(image, dtype=np.float32)
+    def _host_frame(self, image: np.ndarray):
+        """(array, format): uint8 frames stay 8-bit (Image8U); anything else is float32 (Imagef)."""
+        if image.dtype == np.uint8:
+            img, fmt = np.ascontiguousarray(image), SIFT_HIP_U8
+        else:
+            img, fmt = np.ascontiguousarray(image, dtype=np.float32), SIFT_HIP_F32
         if img.shape != (self.config.row_width, self.config.col_width):
             raise SiftHipError(f"image shape {img.shape} != configured {(self.config.row_width, self.config.col_width)}")
-        _check(lib().sift_hip_detect(self._h, _ptr(img), img.strides[0]), "detectAndCompute")
+        return img, fmt
+
+    def detectAndCompute(self, image: np.ndarray) -> None:
+        """Detector.cu:133-233.  `image`: (rows, cols) float32 0..255 (Imagef) or uint8 (Image8U)."""
+        self.gpuWarmUpAndAllocate()
+        img, fmt = self._host_frame(image)
+        if fmt == SIFT_HIP_U8:
+            _check(lib().sift_hip_detect_u8(self._h, _ptr(img), img.strides[0]), "detectAndCompute")
+        else:
+            _check(lib().sift_hip_detect(self._h, _ptr(img), img.strides[0]), "detectAndCompute")
         self._refresh()
 
-    def detectAndComputeDevice(self, dev_ptr: int, row_stride_bytes: int, stream: Optional[int] = None, sync: bool = True) -> None:
+    def submit(self, image: np.ndarray) -> int:
+        """Pipelined input (sift_hip_submit): stage + upload + enqueue, no wait.  Returns the frame ticket."""
         self.gpuWarmUpAndAllocate()
-        _check(lib().sift_hip_detect_device(self._h, dev_ptr, row_stride_bytes, stream), "detectAndComputeDevice")
+        img, fmt = self._host_frame(image)
+        t = ctypes.c_longlong()
+        _check(lib().sift_hip_submit(self._h, _ptr(img), img.strides[0], fmt, ctypes.byref(t)), "submit")
+        return t.value
+
+    def wait(self, ticket: int) -> None:
+        """Block until frame `ticket` is complete and expose its results (prev = frame ticket-1)."""
+        _check(lib().sift_hip_wait(self._h, ticket), "wait")
+        self._refresh()
+
+    def detectAndComputeDevice(self, dev_ptr: int, row_stride_bytes: int, stream: Optional[int] = None, sync: bool = True,
+                               u8: bool = False) -> None:
+        self.gpuWarmUpAndAllocate()
+        fmt = SIFT_HIP_U8 if u8 else SIFT_HIP_F32
+        _check(lib().sift_hip_detect_device_fmt(self._h, dev_ptr, row_stride_bytes, fmt, stream), "detectAndComputeDevice")
         if sync:
             self.sync()
 

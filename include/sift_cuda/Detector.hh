@@ -27,6 +27,17 @@ public:
 
     // Detector.cu:133-233: synchronous; results valid until the next call.
     void detectAndCompute(const Imagef& image);
+    // Extra: 8-bit frame (Image8U, HostImage.hh:187); converted on the GPU,
+    // results identical to the Imagef holding the same values.
+    void detectAndCompute(const Image8U& image);
+    // Extra: pipelined input (sift_hip_submit / sift_hip_wait).  submit()
+    // stages and uploads the frame while earlier frames compute and returns a
+    // ticket; wait(ticket) makes that frame's results (and its predecessor's
+    // descriptors as prev_descriptor) current.  At most two frames in flight
+    // past the last waited one.
+    long long submit(const Imagef& image);
+    long long submit(const Image8U& image);
+    void wait(long long ticket);
     // Extra: image already in device memory (fp32, row stride in bytes).
     void detectAndComputeDevice(const float* device_image, size_t row_stride_bytes, void* hip_stream = nullptr);
 

@@ -77,10 +77,38 @@ int sift_hip_octave_dims(sift_hip_t h, int octave, int* w, int* hgt, int* pitch_
  * returns when results are ready.  Keypoint count via sift_hip_num_keypoints. */
 int sift_hip_detect(sift_hip_t h, const float* host_img, size_t row_stride_bytes);
 
+/* Pixel formats of a caller's frame.  OpenCV converts CV_8U input to float
+ * exactly (createInitialImage), so an 8-bit frame gives the results of the
+ * float frame holding the same values; it crosses PCIe in a quarter of the
+ * bytes and is converted inside the first GPU kernel. */
+#define SIFT_HIP_F32 0  /* float, 0..255 (Imagef, HostImage.hh:188)        */
+#define SIFT_HIP_U8  1  /* uint8 (Image8U, HostImage.hh:187; cv::Mat CV_8U) */
+
+/* Detector::detectAndCompute for an 8-bit host frame (the reference converts
+ * cv::Mat to Imagef first, cvUtils/ConversionImpl.hpp:8-31).  Synchronous. */
+int sift_hip_detect_u8(sift_hip_t h, const uint8_t* host_img, size_t row_stride_bytes);
+
 /* Same, for an image already in device memory (HBM-resident input); enqueued on
- * `stream` (NULL = internal) and NOT synchronised: call sift_hip_sync. */
+ * `stream` (NULL = internal) and NOT synchronised: call sift_hip_sync.  The
+ * result accessors address this frame at once (device-ordered use); counts
+ * are valid after sift_hip_sync. */
 int sift_hip_detect_device(sift_hip_t h, const float* dev_img, size_t row_stride_bytes, void* stream);
+int sift_hip_detect_device_fmt(sift_hip_t h, const void* dev_img, size_t row_stride_bytes, int format,
+                               void* stream);
 int sift_hip_sync(sift_hip_t h);
+
+/* Pipelined host input (replaces the synchronous upload of CudaImage.cu:97-105
+ * and the per-frame loop of extract_and_match_example.cc:69-101).
+ * sift_hip_submit copies the frame into a pinned staging ring (the caller's
+ * buffer is free again on return), uploads it on a copy stream while earlier
+ * frames compute, enqueues the pipeline and returns a ticket without waiting.
+ * sift_hip_wait(ticket) blocks until that frame is complete and makes it the
+ * frame the result accessors address (prev_desc = frame ticket-1).  At most two
+ * frames may be in flight past the last waited one (SIFT_HIP_ERR_STATE
+ * otherwise); sift_hip_detect / sift_hip_detect_u8 = submit + wait. */
+int sift_hip_submit(sift_hip_t h, const void* host_img, size_t row_stride_bytes, int format,
+                    long long* ticket);
+int sift_hip_wait(sift_hip_t h, long long ticket);
 
 /* Detector::total_size (Detector.hh:62, Detector.cu:584-604). */
 int sift_hip_num_keypoints(sift_hip_t h, int* n);

@@ -36,7 +36,8 @@ def exported(lib):
 def test_header_declares_expected_surface():
     fns = header_functions()
     for f in ["sift_hip_create", "sift_hip_destroy", "sift_hip_warmup", "sift_hip_detect", "sift_hip_copy_to_host",
-              "sift_hip_results_device", "sift_hip_match_device", "sift_hip_match_host", "sift_hip_last_error"]:
+              "sift_hip_results_device", "sift_hip_match_device", "sift_hip_match_host", "sift_hip_last_error",
+              "sift_hip_detect_u8", "sift_hip_submit", "sift_hip_wait", "sift_hip_detect_device_fmt"]:
         assert f in fns
     assert len(fns) >= 30
 

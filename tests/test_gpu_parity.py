@@ -233,3 +233,8 @@ def test_cpp_tools(sift):
     assert "keypoints" in r.stdout
     r = subprocess.run([os.path.join(lib, "extract_and_match_example"), "--frames", "3"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
+    # 8-bit frames through submit/wait: the same keypoints and matches.
+    p = subprocess.run([os.path.join(lib, "extract_and_match_example"), "--frames", "3", "--pipelined"],
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert p.stdout == r.stdout

@@ -2,6 +2,9 @@
 // consecutive frames and match each frame against the previous one through
 // Detector::prev_descriptor + matchBruteForce.  Frames: a synthetic frame and
 // copies shifted by (k*dx, k*dy) pixels, so good matches must agree with the shift.
+// --pipelined: 8-bit frames through Detector::submit / wait, frame f+1 staged
+// and uploaded while frame f computes; prints the same lines as the default
+// synchronous Imagef loop.
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -12,9 +15,11 @@
 
 int main(int argc, char** argv) {
     int W = 752, H = 480, frames = 4, dx = 3, dy = 2;
+    bool pipelined = false;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
-        if (a == "--width" && i + 1 < argc) W = std::atoi(argv[++i]);
+        if (a == "--pipelined") pipelined = true;
+        else if (a == "--width" && i + 1 < argc) W = std::atoi(argv[++i]);
         else if (a == "--height" && i + 1 < argc) H = std::atoi(argv[++i]);
         else if (a == "--frames" && i + 1 < argc) frames = std::atoi(argv[++i]);
     }
@@ -32,11 +37,26 @@ int main(int argc, char** argv) {
     int prev_size = 0;
     std::vector<sift_cuda::Float3> prev_kpts;
     int failures = 0;
-    for (int f = 0; f < frames; f++) {
-        Imagef img(H, W);
+    auto frame = [&](int f, auto& img) {
         for (int y = 0; y < H; y++)
             for (int x = 0; x < W; x++) img.at(y, x) = big[(size_t)(y + f * dy) * PW + x + f * dx];
-        detector.detectAndCompute(img);
+    };
+    std::vector<long long> ticket(frames, -1);
+    auto submit = [&](int f) {
+        Image8U img(H, W);
+        frame(f, img);
+        ticket[f] = detector.submit(img);
+    };
+    if (pipelined) submit(0);
+    for (int f = 0; f < frames; f++) {
+        if (pipelined) {
+            if (f + 1 < frames) submit(f + 1);
+            detector.wait(ticket[f]);
+        } else {
+            Imagef img(H, W);
+            frame(f, img);
+            detector.detectAndCompute(img);
+        }
         detector.copyToHost(false);
         const int curr_size = detector.total_size;
         if (f > 0) {
