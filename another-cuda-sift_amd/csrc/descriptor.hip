@@ -4,8 +4,8 @@
 // per keypoint, 8 shared-memory float atomics per sample, modff bins, serial
 // lane-0 normalisation, half(x512) output).
 //
-// Two wavefronts (a 128-thread workgroup) per keypoint, ~10 keypoints in
-// flight per CU, so memory latency of one keypoint hides behind the others'
+// Four wavefronts (a 256-thread workgroup) per keypoint, several keypoints
+// in flight per CU, so memory latency of one keypoint hides behind the others'
 // ALU work:
 //   * k_bucket_rank already computed the keypoint's window (DescJob), read
 //     here with scalar loads;
@@ -16,10 +16,12 @@
 //   * gradients are read straight from the Gaussian plane (L1/L2 resident:
 //     neighbouring keypoints share it) with bounds-checked buffer loads, four
 //     samples' loads in flight per lane;
-//   * each sample is computed exactly as the oracle (fastAtan2, magnitude,
-//     exp32f weight, cvFloor bins, trilinear split in OpenCV's operation
-//     order) and its 8 contributions go to the LDS histogram as 4 ds_add_u64,
-//     each carrying the orientation pair (o0, o0+1) as two u32 words.
+//   * each sample follows the oracle's operations (fastAtan2 polynomial,
+//     magnitude, Gaussian weight, cvFloor bins, trilinear split in OpenCV's
+//     order) with native v_rcp/v_sqrt/v_exp for the transcendentals (see
+//     desc_atan2), and its 8 contributions go to the LDS histogram as 4
+//     ds_add_u64, each carrying the orientation pair (o0, o0+1) as two u32
+//     words.
 // The histogram is fixed point (scale 2^S per keypoint, chosen from the
 // frame's pixel range so no bin can reach 2^31): on gfx950 an LDS f32 atomic
 // costs ~193 cycles per wave instruction against ~9 for u32 and ~17 for u64

@@ -473,72 +473,93 @@ __global__ __launch_bounds__(256) void k_extrema(OctGeom g, int Lrt, int o, floa
     }
 }
 
-// Register-streaming variant for L = 1..6 (the common case).  One wave per
-// 62-column x EX2_TH-row strip: lane = column (lanes 0 and 63 only feed their
-// neighbours), rows stream top to bottom.  Per row: the L+3 Gaussian values
-// (one buffer address, plane offset in SGPR), the L+2 DoG values, each DoG
-// plane's horizontal 3-max/3-min through DPP wave shifts + v_max3/v_min3, then
-// the vertical 3-max/min over a 3-row ring and the 3-plane max/min per layer.
-// "v >= all 26 neighbours" is exactly "v >= max of the 3x3x3 block" (the block
-// contains v), so the test is OpenCV's, with ~4x fewer instructions than 26
-// LDS compares and no LDS staging.
-constexpr int EX2_TH = 8;              // output rows per wave
-constexpr int EX2_COLS = 62;           // output columns per wave (64 lanes - 2 halo)
+// ---------------------------------------------------------------------------
+// Register-streaming extrema for L = 1..6 (the common case; k_extrema above
+// serves larger L).  Four columns per lane: one wave covers a 256-column x
+// EX4_TR-row strip, rows streaming top to bottom with EX4_AHEAD rows' loads in
+// flight, with
+// 16-byte loads (one buffer_load_dwordx4 per row and plane), plus one dword
+// per row and plane for the strip's outer neighbours (lane 0: column x0-1,
+// lane 63: column x0+256).  Per row the 5 DoG planes are formed in registers
+// and kept in a 3-row ring; a tested row takes the vertical max/min of its
+// three rows per column, then the horizontal 3-max in-lane, with the columns
+// across lane boundaries brought in by one DPP move each (lane 0 / 63 keep
+// their own outer column as the DPP's old value).  "v >= all 26 neighbours"
+// is exactly "v == max of the 3x3x3 block" (the block contains v), so the
+// decision per pixel is OpenCV's and the oracle's: |v| > threshold and
+// v >= (<=) all 26, with no LDS staging.
+// ---------------------------------------------------------------------------
+constexpr int EX4_LIST = 2048;  // per-workgroup candidate list (LDS): a 256 x 32 x L block can hold
+                                // ~7 % extrema on textured frames; overflow spills to HBM
+constexpr int EX4_COLS = 256;  // columns per wave
 
-__device__ __forceinline__ float dpp_from_left(float v) {  // lane i <- lane i-1
-    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x138, 0xf, 0xf, false));
+__device__ __forceinline__ float dpp_left_or(float own, float v) {  // lane i <- lane i-1, lane 0 <- own
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own), __float_as_int(v), 0x138, 0xf, 0xf, false));
 }
-__device__ __forceinline__ float dpp_from_right(float v) {  // lane i <- lane i+1
-    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x130, 0xf, 0xf, false));
+__device__ __forceinline__ float dpp_right_or(float own, float v) {  // lane i <- lane i+1, lane 63 <- own
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own), __float_as_int(v), 0x130, 0xf, 0xf, false));
 }
 
-template <int LT>
-__global__ __launch_bounds__(256) void k_extrema_rows(OctGeom g, int o, float thr, uint2* __restrict__ cand,
-                                                      Counters* __restrict__ ctr, unsigned cap) {
+template <int LT, int EX4_TR, int EX4_AHEAD>
+__global__ __launch_bounds__(256) void k_extrema_x4(OctGeom g, int o, float thr, uint2* __restrict__ cand,
+                                                    Counters* __restrict__ ctr, unsigned cap) {
     constexpr int NG = LT + 3, ND = LT + 2;
+    static_assert(4 * LT <= 31, "hit bits per row");
+    typedef float f4 __attribute__((ext_vector_type(4)));
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int tile = xcd_tile(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
-    const int x0 = (tile % gridDim.x) * EX2_COLS, y0 = ((tile / gridDim.x) * 4 + wave) * EX2_TH;
+    const int x0 = (tile % gridDim.x) * EX4_COLS, y0 = ((tile / gridDim.x) * 4 + wave) * EX4_TR;
     const int W = g.W, H = g.H, pitch = g.pitch;
-    const int x = x0 - 1 + lane;
-    const bool colOK = lane >= 1 && lane <= EX2_COLS && x >= 5 && x < W - 5;
-    const int xc = min(max(x, 0), W - 1);
+    const int xl = x0 + 4 * lane;
+    const int xe = min(max(lane == 0 ? x0 - 1 : x0 + EX4_COLS, 0), W - 1);
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         g.base, 0, (int)min((long)NG * g.planeStride * 4, 0x7fffffffL), 0x00020000);
     __shared__ unsigned s_cnt, s_base;
-    __shared__ uint2 s_list[EX_LIST];
+    __shared__ uint2 s_list[EX4_LIST];
     if (tid == 0) s_cnt = 0;
     __syncthreads();
 
-    auto load_row = [&](int y, float (&gv)[NG]) {
-        const unsigned off = (unsigned)(min(max(y, 0), H - 1) * pitch + xc) * 4u;
+    bool colOK[4];
 #pragma unroll
-        for (int d = 0; d < NG; d++)
-            gv[d] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                  rsrc, off, (int)((long)d * g.planeStride * 4), 0));
-    };
-    // Per ring slot: horizontal max/min of every DoG plane, centre DoG of layers.
-    float hmx[3][ND], hmn[3][ND], dc[3][LT];
-    auto push_row = [&](const float (&gv)[NG], float (&mx)[ND], float (&mn)[ND], float (&c)[LT]) {
+    for (int c = 0; c < 4; c++) colOK[c] = xl + c >= 5 && xl + c < W - 5;
+
+    // Ring slot: DoG of the lane's 4 columns and of its outer column, per plane.
+    f4 rd[3][ND];
+    float re[3][ND];
+    // Raw rows in flight: EX4_AHEAD + 1 register sets, loads issued EX4_AHEAD
+    // rows ahead of the row being formed.
+    f4 rv[EX4_AHEAD + 1][NG];
+    float rev[EX4_AHEAD + 1][NG];
+    auto issue_row = [&](int y, f4 (&v)[NG], float (&e)[NG]) {
+        const int yc = min(max(y, 0), H - 1);
+        const unsigned off4 = (unsigned)(yc * pitch + xl) * 4u, offe = (unsigned)(yc * pitch + xe) * 4u;
 #pragma unroll
-        for (int d = 0; d < ND; d++) {
-            const float v = gv[d + 1] - gv[d];
-            const float l = dpp_from_left(v), r = dpp_from_right(v);
-            mx[d] = fmaxf(fmaxf(v, l), r);
-            mn[d] = fminf(fminf(v, l), r);
-            if (d >= 1 && d <= LT) c[d - 1] = v;
+        for (int d = 0; d < NG; d++) {
+            const int so = (int)((long)d * g.planeStride * 4);
+            v[d] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off4, so, 0));
+            e[d] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, offe, so, 0));
         }
     };
-    auto emit = [&](bool hit, int layer, int r) {
-        const unsigned long long mask = __ballot(hit);
-        if (!mask) return;
-        unsigned basepos = 0;
-        if (lane == 0) basepos = atomicAdd(&s_cnt, (unsigned)__popcll(mask));
-        basepos = __shfl(basepos, 0);
-        if (hit) {
-            const unsigned pos = basepos + (unsigned)__popcll(mask & ((1ull << lane) - 1ull));
-            const uint2 q = make_uint2((unsigned)(o << 8 | layer), (unsigned)(r << 16 | x));
-            if (pos < EX_LIST) {
+    // Candidates of one tested row: one LDS reservation per row with hits;
+    // each lane's slot offset is the exclusive prefix of the per-lane hit
+    // counts, taken from ballots of the count's bits (count <= 4 * LT < 32).
+    auto emit_row = [&](int r, unsigned hits) {
+        if (!__ballot(hits != 0)) return;  // wave-uniform
+        const unsigned cnt = (unsigned)__popc(hits);
+        unsigned excl = 0, tot = 0;
+#pragma unroll
+        for (int b = 0; b < 5; b++) {
+            const unsigned long long bm = __ballot((cnt >> b) & 1u);
+            excl += __builtin_amdgcn_mbcnt_hi((unsigned)(bm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bm, 0u)) << b;
+            tot += (unsigned)__popcll(bm) << b;
+        }
+        unsigned base = 0;
+        if (lane == 0) base = atomicAdd(&s_cnt, tot);
+        unsigned pos = __builtin_amdgcn_readfirstlane(base) + excl;
+        for (unsigned m = hits; m; m &= m - 1u, pos++) {
+            const int f = __builtin_ctz(m), l = f / 4 + 1, c = f & 3;
+            const uint2 q = make_uint2((unsigned)(o << 8 | l), (unsigned)(r << 16 | (xl + c)));
+            if (pos < EX4_LIST) {
                 s_list[pos] = q;
             } else {  // plateau-heavy tile: spill straight to the global list
                 const unsigned gp = atomicAdd(&ctr->cand, 1u);
@@ -549,43 +570,73 @@ __global__ __launch_bounds__(256) void k_extrema_rows(OctGeom g, int o, float th
             }
         }
     };
-    // Test row r (ring slot B = centre, A above, C below).
-    auto test_row = [&](int r, int A, int B, int C) {
-        if (r < 5 || r >= H - 5) return;  // wave-uniform
-        float vmx[ND], vmn[ND];
+    auto test_row = [&](int r, int A, int B, int C) -> unsigned {
+        const bool rowOK = r >= 5 && r < H - 5;
+        f4 hx[ND], hn[ND];
 #pragma unroll
         for (int d = 0; d < ND; d++) {
-            vmx[d] = fmaxf(fmaxf(hmx[A][d], hmx[B][d]), hmx[C][d]);
-            vmn[d] = fminf(fminf(hmn[A][d], hmn[B][d]), hmn[C][d]);
-        }
+            f4 vx, vn;
 #pragma unroll
-        for (int l = 1; l <= LT; l++) {
-            const float v = dc[B][l - 1];
-            const float M = fmaxf(fmaxf(vmx[l - 1], vmx[l]), vmx[l + 1]);
-            const float m = fminf(fminf(vmn[l - 1], vmn[l]), vmn[l + 1]);
-            const bool hit = colOK && fabsf(v) > thr && ((v > 0 && v >= M) || (v < 0 && v <= m));
-            emit(hit, l, r);
+            for (int c = 0; c < 4; c++) {
+                vx[c] = fmaxf(fmaxf(rd[A][d][c], rd[B][d][c]), rd[C][d][c]);
+                vn[c] = fminf(fminf(rd[A][d][c], rd[B][d][c]), rd[C][d][c]);
+            }
+            const float ex = fmaxf(fmaxf(re[A][d], re[B][d]), re[C][d]);
+            const float en = fminf(fminf(re[A][d], re[B][d]), re[C][d]);
+            const float lx = dpp_left_or(ex, vx[3]), ln = dpp_left_or(en, vn[3]);
+            const float rx = dpp_right_or(ex, vx[0]), rn = dpp_right_or(en, vn[0]);
+            hx[d][0] = fmaxf(fmaxf(lx, vx[0]), vx[1]);
+            hx[d][1] = fmaxf(fmaxf(vx[0], vx[1]), vx[2]);
+            hx[d][2] = fmaxf(fmaxf(vx[1], vx[2]), vx[3]);
+            hx[d][3] = fmaxf(fmaxf(vx[2], vx[3]), rx);
+            hn[d][0] = fminf(fminf(ln, vn[0]), vn[1]);
+            hn[d][1] = fminf(fminf(vn[0], vn[1]), vn[2]);
+            hn[d][2] = fminf(fminf(vn[1], vn[2]), vn[3]);
+            hn[d][3] = fminf(fminf(vn[2], vn[3]), rn);
         }
+        unsigned hits = 0;  // bit (l - 1) * 4 + c
+#pragma unroll
+        for (int l = 1; l <= LT; l++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const float v = rd[B][l][c];
+                const float M = fmaxf(fmaxf(hx[l - 1][c], hx[l][c]), hx[l + 1][c]);
+                const float m = fminf(fminf(hn[l - 1][c], hn[l][c]), hn[l + 1][c]);
+                // M >= v >= m always (v is one of the 27), so "v >= all" is v == M;
+                // |v| > thr >= 0 excludes v == 0, and the sign picks the test.
+                const bool h = rowOK && colOK[c] && fabsf(v) > thr && v == (v > 0 ? M : m);
+                hits |= (unsigned)h << ((l - 1) * 4 + c);
+            }
+        return hits;
     };
 
     if (y0 < H) {
-        // All EX2_TH + 2 rows' loads in flight at once (one memory latency per
-        // strip), then the rows stream through the 3-row ring.
-        float gr[EX2_TH + 2][NG];
+        // Strip row m = 0 .. EX4_TR + 1 (image row y0 - 1 + m) is loaded into raw
+        // set m % NS; once formed, its set is reloaded with strip row m + NS.
+        constexpr int NS = EX4_AHEAD + 1, NR = EX4_TR + 2;
+        auto form = [&](int m, f4 (&d4)[ND], float (&de)[ND]) {
+            const int k = m % NS;
 #pragma unroll
-        for (int k = 0; k < EX2_TH + 2; k++) load_row(y0 - 1 + k, gr[k]);
-        push_row(gr[0], hmx[0], hmn[0], dc[0]);
-        push_row(gr[1], hmx[1], hmn[1], dc[1]);
-        // Row y0 + k + 1 enters slot (k + 2) % 3, row y0 + k is tested.
+            for (int d = 0; d < ND; d++) {
+                d4[d] = rv[k][d + 1] - rv[k][d];
+                de[d] = rev[k][d + 1] - rev[k][d];
+            }
+            if (m + NS < NR) issue_row(y0 - 1 + m + NS, rv[k], rev[k]);
+        };
 #pragma unroll
-        for (int k = 0; k < EX2_TH; k++) {
+        for (int m = 0; m < NS && m < NR; m++) issue_row(y0 - 1 + m, rv[m], rev[m]);
+        form(0, rd[0], re[0]);
+        form(1, rd[1], re[1]);
+        // Row y0 + k + 1 (strip row k + 2) enters ring slot (k + 2) % 3, row y0 + k is tested.
+#pragma unroll
+        for (int k = 0; k < EX4_TR; k++) {
             const int A = k % 3, B = (k + 1) % 3, C = (k + 2) % 3;
-            push_row(gr[k + 2], hmx[C], hmn[C], dc[C]);
-            if (y0 + k < H) test_row(y0 + k, A, B, C);
+            form(k + 2, rd[C], re[C]);
+            emit_row(y0 + k, test_row(y0 + k, A, B, C));
         }
     }
     __syncthreads();
-    const unsigned nl = min(s_cnt, (unsigned)EX_LIST);
+    const unsigned nl = min(s_cnt, (unsigned)EX4_LIST);
     if (tid == 0) s_base = nl ? atomicAdd(&ctr->cand, nl) : 0u;
     __syncthreads();
     for (unsigned k = tid; k < nl; k += 256) {
@@ -601,10 +652,22 @@ void launch_extrema(const PyrDesc& pyr, int o, float threshold, uint2* cand, Cou
                     hipStream_t s) {
     const OctGeom& g = pyr.oct[o];
     if (pyr.L >= 1 && pyr.L <= 6) {
-        dim3 grid((g.W + EX2_COLS - 1) / EX2_COLS, (g.H + 4 * EX2_TH - 1) / (4 * EX2_TH));
-        switch (pyr.L) {
-#define SIFT_EX_CASE(LV) \
-    case LV: hipLaunchKernelGGL(k_extrema_rows<LV>, grid, dim3(256), 0, s, g, o, threshold, cand, ctr, cap); break;
+        // Tall strips (6 rows per wave) where they still give >= 1024 waves,
+        // else 2 rows per wave: small octaves are latency-bound and want waves
+        // (tools/kernel_bench: 1920x1200 16.7 us at 6 rows vs 19.8 at 2; 960x600
+        // 9.2 us at 2 rows vs 10.8 at 6).
+        const int strips = (g.W + EX4_COLS - 1) / EX4_COLS;
+        const bool tall = strips * ((g.H + 5) / 6) >= 1024;
+        const int tr = tall ? 6 : 2;
+        dim3 grid(strips, (g.H + 4 * tr - 1) / (4 * tr));
+        switch (pyr.L * 2 + (tall ? 1 : 0)) {
+#define SIFT_EX_CASE(LV)                                                                                         \
+    case 2 * LV:                                                                                                 \
+        hipLaunchKernelGGL((k_extrema_x4<LV, 2, 2>), grid, dim3(256), 0, s, g, o, threshold, cand, ctr, cap); \
+        break;                                                                                                   \
+    case 2 * LV + 1:                                                                                             \
+        hipLaunchKernelGGL((k_extrema_x4<LV, 6, 2>), grid, dim3(256), 0, s, g, o, threshold, cand, ctr, cap); \
+        break;
             SIFT_EX_CASE(1)
             SIFT_EX_CASE(2)
             SIFT_EX_CASE(3)
