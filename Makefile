@@ -52,5 +52,5 @@ clean:
 
 # Isolated kernel timing (tools/kernel_bench.hip), not part of `all`.
 tools/kernel_bench: tools/kernel_bench.hip $(OUT)/obj/pyramid.o $(OUT)/obj/synth_frame.o
-	$(HIPCC) $(HIPFLAGS) -c $< -o $(OUT)/obj/kernel_bench.o
-	$(HIPCC) --offload-arch=$(ARCH) -o $@ $(OUT)/obj/kernel_bench.o $(OUT)/obj/pyramid.o $(OUT)/obj/synth_frame.o
+	$(HIPCC) $(HIPFLAGS) -c $< -o tools/kernel_bench.o
+	$(HIPCC) --offload-arch=$(ARCH) -o $@ tools/kernel_bench.o $(OUT)/obj/pyramid.o $(OUT)/obj/synth_frame.o

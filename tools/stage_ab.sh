@@ -12,6 +12,7 @@ V[no_desc]="descriptor"
 V[no_ori]="orientation"
 V[no_refine]="refine"
 V[pyr_only]="extrema,$KP"
+V[no_kp]="$KP"
 V[blur_o0_only]="blur_o1,blur_o2,extrema,$KP"
 V[init_only]="blur_o0,blur_o1,blur_o2,extrema,$KP"
 if [ "$1" = build ]; then
