@@ -451,11 +451,18 @@ void enqueue_body(sift_hip_detector* d, int slot) {
     }
     d->timed("refine", 0, [&] { launch_refine(d->pyr, d->dCand, d->capCand, d->dCtr, d->dBitmap, d->dRef, d->kp, s); });
     d->timed("orientation", 0, [&] { launch_orientation(d->pyr, d->dRef, d->dCtr, d->dOri, d->dBitmap, d->kp, s); });
-    d->timed("select", 0, [&] { launch_select(d->dOri, d->dCtr, range_keys(d, parity ^ 1), d->kp, s); });
-    d->timed("bucket_count", 0, [&] { launch_bucket_count(d->dOri, d->dCtr, d->dBcount, d->dSlot, d->kp, s); });
-    d->timed("bucket_scan", 0, [&] { launch_bucket_scan(d->dBcount, d->dBoff, d->dCtr, d->kp, s); });
-    d->timed("bucket_scatter", 0,
-             [&] { launch_bucket_scatter(d->dOri, d->dCtr, d->dBoff, d->dSlot, d->dOrder, d->kp, s); });
+    if (d->kp.numBuckets <= kOrderMaxBuckets) {
+        d->timed("order", 0, [&] {
+            launch_order(d->dOri, d->dCtr, range_keys(d, parity ^ 1), d->dBcount, d->dBoff, d->dSlot, d->dOrder, d->kp,
+                         s);
+        });
+    } else {
+        d->timed("select", 0, [&] { launch_select(d->dOri, d->dCtr, range_keys(d, parity ^ 1), d->kp, s); });
+        d->timed("bucket_count", 0, [&] { launch_bucket_count(d->dOri, d->dCtr, d->dBcount, d->dSlot, d->kp, s); });
+        d->timed("bucket_scan", 0, [&] { launch_bucket_scan(d->dBcount, d->dBoff, d->dCtr, d->kp, s); });
+        d->timed("bucket_scatter", 0,
+                 [&] { launch_bucket_scatter(d->dOri, d->dCtr, d->dBoff, d->dSlot, d->dOrder, d->kp, s); });
+    }
     d->timed("bucket_rank", 0, [&] {
         launch_bucket_rank(d->pyr, d->dOri, d->dBcount, d->dBoff, d->dOrder, d->dCtr, d->dJobs, d->dKpts3[slot],
                            d->dFeats4[slot], d->kp, s);

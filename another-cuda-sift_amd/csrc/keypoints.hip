@@ -489,6 +489,136 @@ void launch_bucket_scatter(const OriKpt* kpts, const Counters* ctr, const unsign
     hipLaunchKernelGGL(k_bucket_scatter, dim3(256), dim3(256), 0, s, kpts, ctr, boff, slot, order, kp);
 }
 
+// ---------------------------------------------------------------------------
+// k_select + k_bucket_count + k_bucket_scan + k_bucket_scatter in ONE
+// workgroup (one launch instead of four; ~10^4 keypoints per frame): the
+// retainBest threshold by the same radix select, row-bucket counts by LDS
+// atomics, their exclusive scan in place in LDS, and the scatter into bucket
+// order.  Written to global memory: thr_bits, final_n, and for every
+// non-empty bucket its count and offset (k_bucket_rank reads both and zeroes
+// the counts), and order[].  Used when the buckets fit in LDS
+// (kOrderMaxBuckets); the four kernels above remain for larger pyramids.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_order(const OriKpt* __restrict__ kpts, Counters* __restrict__ ctr,
+                                                unsigned* __restrict__ zero_range, unsigned* __restrict__ bcount,
+                                                unsigned* __restrict__ boff, int* __restrict__ slot,
+                                                int* __restrict__ order, KeypointParams kp) {
+    extern __shared__ unsigned s_bucket[];  // counts, then exclusive offsets
+    __shared__ unsigned hist[256], wsum[16];
+    __shared__ unsigned s_prefix, s_k;
+    const unsigned n = min(ctr->oriented, kp.capOriented);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int nb = kp.numBuckets;
+    for (int i = tid; i < 2 * kRangeSlots; i += 1024) zero_range[i] = 0u;  // next frame's range keys
+    for (int i = tid; i < nb; i += 1024) s_bucket[i] = 0u;
+    if (tid == 0) {
+        s_prefix = 0;
+        s_k = (unsigned)kp.numFeatures;
+    }
+    __syncthreads();
+    // retainBest threshold (k_select's radix select)
+    const bool sel = kp.numFeatures > 0 && n > (unsigned)kp.numFeatures;
+    if (sel) {
+        unsigned pmask = 0;
+        for (int shift = 24; shift >= 0; shift -= 8) {
+            for (int i = tid; i < 256; i += 1024) hist[i] = 0;
+            __syncthreads();
+            const unsigned prefix = s_prefix;
+            for (unsigned i = tid; i < n; i += 1024) {
+                const unsigned b = __float_as_uint(kpts[i].response);
+                if ((b & pmask) == prefix) atomicAdd(&hist[(b >> shift) & 255u], 1u);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                unsigned k = s_k, cum = 0;
+                int digit = 0;
+                for (int d = 255; d >= 0; d--) {
+                    if (cum + hist[d] >= k) {
+                        digit = d;
+                        k -= cum;
+                        break;
+                    }
+                    cum += hist[d];
+                }
+                s_k = k;
+                s_prefix = prefix | ((unsigned)digit << shift);
+            }
+            pmask |= 255u << shift;
+            __syncthreads();
+        }
+    }
+    const unsigned thr_bits = sel ? s_prefix : 0u;
+    if (tid == 0) ctr->thr_bits = thr_bits;
+    const float thr = __uint_as_float(thr_bits);
+    // counts (the slot order inside a bucket is re-ranked by k_bucket_rank);
+    // four keypoints' loads in flight per thread
+    for (unsigned i0 = tid; i0 < n; i0 += 4 * 1024) {
+        int bk[4];
+        float rs[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const unsigned i = min(i0 + 1024u * u, n - 1);
+            bk[u] = kpts[i].bucket;
+            rs[u] = kpts[i].response;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const unsigned i = i0 + 1024u * u;
+            if (i < n) slot[i] = rs[u] >= thr ? (int)atomicAdd(&s_bucket[bk[u]], 1u) : -1;
+        }
+    }
+    __syncthreads();
+    // Exclusive scan in place: each thread sums a contiguous run of buckets,
+    // one workgroup scan of the 1024 run sums, then each run is rewritten as
+    // offsets; non-empty buckets are published for k_bucket_rank.
+    {
+        const int per = (nb + 1023) / 1024;
+        const int b0 = min(tid * per, nb), b1 = min(b0 + per, nb);
+        unsigned sum = 0;
+        for (int b = b0; b < b1; b++) sum += s_bucket[b];
+        unsigned x = sum;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const unsigned y = __shfl_up(x, off);
+            if (lane >= off) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        unsigned run = x - sum, total = 0;
+        for (int k = 0; k < 16; k++) {
+            if (k < w) run += wsum[k];
+            total += wsum[k];
+        }
+        for (int b = b0; b < b1; b++) {
+            const unsigned v = s_bucket[b];
+            if (v) {
+                s_bucket[b] = run;
+                bcount[b] = v;
+                boff[b] = run;
+            }
+            run += v;
+        }
+        if (tid == 0) {
+            ctr->final_n = min(total, kp.capFinal);
+            if (total > kp.capFinal) atomicOr(&ctr->overflow, 8u);
+        }
+    }
+    __syncthreads();
+    // scatter (slot[i] was written by this same thread above)
+    for (unsigned i = tid; i < n; i += 1024) {
+        const int sl = slot[i];
+        if (sl >= 0) order[s_bucket[kpts[i].bucket] + (unsigned)sl] = (int)i;
+    }
+}
+
+bool launch_order(const OriKpt* kpts, Counters* ctr, unsigned* zero_range, unsigned* bcount, unsigned* boff, int* slot,
+                  int* order, const KeypointParams& kp, hipStream_t s) {
+    if (kp.numBuckets > kOrderMaxBuckets) return false;
+    hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), sizeof(unsigned) * (size_t)kp.numBuckets, s, kpts, ctr,
+                       zero_range, bcount, boff, slot, order, kp);
+    return true;
+}
+
 // Descriptor job of one final keypoint: calcDescriptorsComputer (unpackOctave,
 // octave scale, angle flip 360 - angle) and the head of calcSIFTDescriptor
 // (cos/sin / hist_width, radius clamped to the image diagonal), computed once

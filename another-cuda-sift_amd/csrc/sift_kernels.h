@@ -49,7 +49,7 @@ struct OriKpt {
     int bucket, sub;
 };
 
-// Per-frame counters, zeroed by one memset node at the head of the graph.
+// Per-frame counters, zeroed by the frame's first blur (no memset node).
 struct Counters {
     unsigned cand;       // 3x3x3 extrema candidates
     unsigned refined;    // after adjustLocalExtrema + dedupe
@@ -97,6 +97,11 @@ void launch_orientation(const PyrDesc& pyr, const RefKpt* in, Counters* ctr, Ori
 // zero_range: the other frame buffer's 2 * kRangeSlots range keys (zeroed here
 // for the next frame, so no memset node is needed).
 void launch_select(const OriKpt* kpts, Counters* ctr, unsigned* zero_range, const KeypointParams& kp, hipStream_t s);
+// select + bucket count + scan + scatter in one single-workgroup launch;
+// false (nothing launched) when the row buckets exceed kOrderMaxBuckets.
+constexpr int kOrderMaxBuckets = 16384;  // 64 KiB of LDS
+bool launch_order(const OriKpt* kpts, Counters* ctr, unsigned* zero_range, unsigned* bcount, unsigned* boff, int* slot,
+                  int* order, const KeypointParams& kp, hipStream_t s);
 void launch_bucket_count(const OriKpt* kpts, const Counters* ctr, unsigned* bcount, int* slot,
                          const KeypointParams& kp, hipStream_t s);
 void launch_bucket_scan(unsigned* bcount, unsigned* boff, Counters* ctr, const KeypointParams& kp, hipStream_t s);

@@ -88,6 +88,46 @@ __global__ __launch_bounds__(256) void k_read_probe(const float* base, long plan
     out[(blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x] = acc;
 }
 
+__global__ void k_empty(int* p) {
+    if (p && threadIdx.x == 1023) p[0] = 1;
+}
+
+// Dispatch floor: a captured chain of `n` dependent empty kernels (as many
+// launches as one frame's graph), replayed back to back on `ns` streams.
+static void graph_floor(int n, int ns, int iters) {
+    std::vector<hipStream_t> st(ns);
+    for (auto& x : st) CK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+    std::vector<hipGraphExec_t> ex(ns);
+    for (int k = 0; k < ns; k++) {
+        hipGraph_t g;
+        CK(hipStreamBeginCapture(st[k], hipStreamCaptureModeThreadLocal));
+        for (int i = 0; i < n; i++) hipLaunchKernelGGL(k_empty, dim3(256), dim3(256), 0, st[k], nullptr);
+        CK(hipStreamEndCapture(st[k], &g));
+        CK(hipGraphInstantiate(&ex[k], g, nullptr, nullptr, 0));
+        CK(hipGraphDestroy(g));
+    }
+    for (int i = 0; i < 10; i++) CK(hipGraphLaunch(ex[i % ns], st[i % ns]));
+    CK(hipDeviceSynchronize());
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    CK(hipEventRecord(a, st[0]));
+    for (int k = 1; k < ns; k++) CK(hipStreamWaitEvent(st[k], a, 0));
+    for (int i = 0; i < iters; i++) CK(hipGraphLaunch(ex[i % ns], st[i % ns]));
+    for (int k = 1; k < ns; k++) {
+        hipEvent_t ev;
+        CK(hipEventCreate(&ev));
+        CK(hipEventRecord(ev, st[k]));
+        CK(hipStreamWaitEvent(st[0], ev, 0));
+    }
+    CK(hipEventRecord(b, st[0]));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    std::printf("{\"kernel\": \"graph of %d empty kernels\", \"streams\": %d, \"us_per_graph\": %.3f}\n", n, ns,
+                ms * 1e3 / iters);
+}
+
 template <class F>
 static double time_us(int iters, hipStream_t s, F&& f);
 
@@ -222,6 +262,8 @@ int main(int argc, char** argv) {
     probe<6, 6, true>(pyr.oct[0], dOut, s, iters);
     probe<6, 4, true>(pyr.oct[0], dOut, s, iters);
     probe<6, 18, true>(pyr.oct[0], dOut, s, iters);
+    for (int ns : {1, 3})
+        for (int n : {1, 8, 27}) graph_floor(n, ns, 300);
     us = time_us(iters, s, [&] { CK(hipMemsetAsync(dCtr, 0, sizeof(Counters), s)); });
     std::printf("{\"kernel\": \"memset 32B\", \"us\": %.3f}\n", us);
     return 0;
