@@ -443,12 +443,12 @@ void enqueue_body(sift_hip_detector* d, int slot) {
             }
         }
     }
-    for (int o = 0; o < d->nOct; o++) {
-        const OctGeom& g = d->pyr.oct[o];
-        d->timed("extrema", (double)g.W * g.H * 4 * (L + 3), [&] {
-            launch_extrema(d->pyr, o, d->threshold, d->dCand, d->dCtr, d->capCand, s);
-        });
-    }
+    double exBytes = 0;
+    for (int o = 0; o < d->nOct; o++) exBytes += (double)d->pyr.oct[o].W * d->pyr.oct[o].H * 4 * (L + 3);
+    d->timed("extrema", exBytes, [&] {
+        if (!launch_extrema_all(d->pyr, d->threshold, d->dCand, d->dCtr, d->capCand, s))
+            for (int o = 0; o < d->nOct; o++) launch_extrema(d->pyr, o, d->threshold, d->dCand, d->dCtr, d->capCand, s);
+    });
     d->timed("refine", 0, [&] { launch_refine(d->pyr, d->dCand, d->capCand, d->dCtr, d->dBitmap, d->dRef, d->kp, s); });
     d->timed("orientation", 0, [&] { launch_orientation(d->pyr, d->dRef, d->dCtr, d->dOri, d->dBitmap, d->kp, s); });
     if (d->kp.numBuckets <= kOrderMaxBuckets) {

@@ -500,22 +500,23 @@ __device__ __forceinline__ float dpp_right_or(float own, float v) {  // lane i <
     return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own), __float_as_int(v), 0x130, 0xf, 0xf, false));
 }
 
+// One workgroup = 4 waves stacked vertically over a 256-column strip: block
+// `blk` of the octave's `nblk` (strips across, xcd_tile order).
 template <int LT, int EX4_TR, int EX4_AHEAD>
-__global__ __launch_bounds__(256) void k_extrema_x4(OctGeom g, int o, float thr, uint2* __restrict__ cand,
-                                                    Counters* __restrict__ ctr, unsigned cap) {
+__device__ __forceinline__ void extrema_block(const OctGeom& g, int o, float thr, uint2* __restrict__ cand,
+                                              Counters* __restrict__ ctr, unsigned cap, int blk, int strips,
+                                              int nblk, uint2* s_list, unsigned& s_cnt, unsigned& s_base) {
     constexpr int NG = LT + 3, ND = LT + 2;
     static_assert(4 * LT <= 31, "hit bits per row");
     typedef float f4 __attribute__((ext_vector_type(4)));
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int tile = xcd_tile(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
-    const int x0 = (tile % gridDim.x) * EX4_COLS, y0 = ((tile / gridDim.x) * 4 + wave) * EX4_TR;
+    const int tile = xcd_tile(blk, nblk);
+    const int x0 = (tile % strips) * EX4_COLS, y0 = ((tile / strips) * 4 + wave) * EX4_TR;
     const int W = g.W, H = g.H, pitch = g.pitch;
     const int xl = x0 + 4 * lane;
     const int xe = min(max(lane == 0 ? x0 - 1 : x0 + EX4_COLS, 0), W - 1);
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         g.base, 0, (int)min((long)NG * g.planeStride * 4, 0x7fffffffL), 0x00020000);
-    __shared__ unsigned s_cnt, s_base;
-    __shared__ uint2 s_list[EX4_LIST];
     if (tid == 0) s_cnt = 0;
     __syncthreads();
 
@@ -648,39 +649,69 @@ __global__ __launch_bounds__(256) void k_extrema_x4(OctGeom g, int o, float thr,
     }
 }
 
+// All octaves of the frame in one launch (L = 1..6): blocks [start[o],
+// start[o+1]) take octave o, with tall strips (6 rows per wave) where they
+// still give >= 1024 waves, else 2 rows per wave (small octaves are
+// latency-bound and want waves; tools/kernel_bench: 1920x1200 16.7 us at 6
+// rows vs 19.8 at 2; 960x600 9.2 us at 2 rows vs 10.8 at 6).
+struct ExtremaPlan {
+    int start[kMaxOctaves + 1];
+    int strips[kMaxOctaves];
+    int tall[kMaxOctaves];
+};
+
+template <int LT>
+__global__ __launch_bounds__(256) void k_extrema_all(PyrDesc pyr, ExtremaPlan plan, float thr,
+                                                     uint2* __restrict__ cand, Counters* __restrict__ ctr,
+                                                     unsigned cap) {
+    __shared__ unsigned s_cnt, s_base;
+    __shared__ uint2 s_list[EX4_LIST];
+    const int b = blockIdx.x;
+    int o = 0;
+    while (o + 1 < pyr.nOct && b >= plan.start[o + 1]) o++;
+    const int blk = b - plan.start[o], nblk = plan.start[o + 1] - plan.start[o];
+    if (plan.tall[o])
+        extrema_block<LT, 6, 2>(pyr.oct[o], o, thr, cand, ctr, cap, blk, plan.strips[o], nblk, s_list, s_cnt, s_base);
+    else
+        extrema_block<LT, 2, 2>(pyr.oct[o], o, thr, cand, ctr, cap, blk, plan.strips[o], nblk, s_list, s_cnt, s_base);
+}
+
+// Octave o alone, for L > 6 (LDS-staged k_extrema).
 void launch_extrema(const PyrDesc& pyr, int o, float threshold, uint2* cand, Counters* ctr, unsigned cap,
                     hipStream_t s) {
     const OctGeom& g = pyr.oct[o];
-    if (pyr.L >= 1 && pyr.L <= 6) {
-        // Tall strips (6 rows per wave) where they still give >= 1024 waves,
-        // else 2 rows per wave: small octaves are latency-bound and want waves
-        // (tools/kernel_bench: 1920x1200 16.7 us at 6 rows vs 19.8 at 2; 960x600
-        // 9.2 us at 2 rows vs 10.8 at 6).
-        const int strips = (g.W + EX4_COLS - 1) / EX4_COLS;
-        const bool tall = strips * ((g.H + 5) / 6) >= 1024;
-        const int tr = tall ? 6 : 2;
-        dim3 grid(strips, (g.H + 4 * tr - 1) / (4 * tr));
-        switch (pyr.L * 2 + (tall ? 1 : 0)) {
-#define SIFT_EX_CASE(LV)                                                                                         \
-    case 2 * LV:                                                                                                 \
-        hipLaunchKernelGGL((k_extrema_x4<LV, 2, 2>), grid, dim3(256), 0, s, g, o, threshold, cand, ctr, cap); \
-        break;                                                                                                   \
-    case 2 * LV + 1:                                                                                             \
-        hipLaunchKernelGGL((k_extrema_x4<LV, 6, 2>), grid, dim3(256), 0, s, g, o, threshold, cand, ctr, cap); \
-        break;
-            SIFT_EX_CASE(1)
-            SIFT_EX_CASE(2)
-            SIFT_EX_CASE(3)
-            SIFT_EX_CASE(4)
-            SIFT_EX_CASE(5)
-            SIFT_EX_CASE(6)
-#undef SIFT_EX_CASE
-        }
-        return;
-    }
     dim3 grid((g.W + EX_TW - 1) / EX_TW, (g.H + EX_TH - 1) / EX_TH);
     const size_t lds = sizeof(float) * (size_t)(pyr.L + 2) * EX_SH * EX_SW;
     hipLaunchKernelGGL(k_extrema<0>, grid, dim3(256), lds, s, g, pyr.L, o, threshold, cand, ctr, cap);
+}
+
+bool launch_extrema_all(const PyrDesc& pyr, float threshold, uint2* cand, Counters* ctr, unsigned cap, hipStream_t s) {
+    if (pyr.L < 1 || pyr.L > 6) return false;
+    ExtremaPlan plan{};
+    int total = 0;
+    for (int o = 0; o < pyr.nOct; o++) {
+        const OctGeom& g = pyr.oct[o];
+        const int strips = (g.W + EX4_COLS - 1) / EX4_COLS;
+        const bool tall = strips * ((g.H + 5) / 6) >= 1024;
+        const int tr = tall ? 6 : 2;
+        plan.start[o] = total;
+        plan.strips[o] = strips;
+        plan.tall[o] = tall;
+        total += strips * ((g.H + 4 * tr - 1) / (4 * tr));
+    }
+    plan.start[pyr.nOct] = total;
+    switch (pyr.L) {
+#define SIFT_EX_CASE(LV) \
+    case LV: hipLaunchKernelGGL(k_extrema_all<LV>, dim3(total), dim3(256), 0, s, pyr, plan, threshold, cand, ctr, cap); break;
+        SIFT_EX_CASE(1)
+        SIFT_EX_CASE(2)
+        SIFT_EX_CASE(3)
+        SIFT_EX_CASE(4)
+        SIFT_EX_CASE(5)
+        SIFT_EX_CASE(6)
+#undef SIFT_EX_CASE
+    }
+    return true;
 }
 
 }  // namespace sift_amd

@@ -77,6 +77,9 @@ bool launch_blur_u8(const uint8_t* src, int spitch, int W, int H, float* dst, in
                     hipStream_t s, unsigned* range_keys, Counters* zero_ctr);
 void launch_u8_to_f32(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, hipStream_t s);
 void launch_upsample2x_u8(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, hipStream_t s);
+// 3x3x3 extrema of every octave in one launch (L = 1..6; false = nothing
+// launched), else per octave with launch_extrema.
+bool launch_extrema_all(const PyrDesc& pyr, float threshold, uint2* cand, Counters* ctr, unsigned cap, hipStream_t s);
 void launch_extrema(const PyrDesc& pyr, int o, float threshold, uint2* cand, Counters* ctr, unsigned cap,
                     hipStream_t s);
 

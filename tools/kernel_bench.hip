@@ -245,23 +245,16 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&dCand, sizeof(uint2) << 20));
     CK(hipMalloc(&dCtr, sizeof(Counters)));
     const float thr = std::floor(0.5 * 0.04 / L * 255);
-    for (int o = 0; o < 3; o++) {
-        const OctGeom& g = pyr.oct[o];
-        const double bytes = 4.0 * (L + 3) * g.W * g.H;
+    {
+        double bytes = 0;
+        for (int o = 0; o < 3; o++) bytes += 4.0 * (L + 3) * pyr.oct[o].W * pyr.oct[o].H;
         us = time_us(iters, s, [&] {
             CK(hipMemsetAsync(dCtr, 0, sizeof(Counters), s));
-            launch_extrema(pyr, o, thr, dCand, dCtr, 1u << 20, s);
+            launch_extrema_all(pyr, thr, dCand, dCtr, 1u << 20, s);
         });
-        std::printf("{\"kernel\": \"k_extrema_rows+memset\", \"octave\": %d, \"us\": %.3f, \"GBps\": %.1f}\n", o, us,
+        std::printf("{\"kernel\": \"k_extrema_all (3 octaves)+memset\", \"us\": %.3f, \"GBps\": %.1f}\n", us,
                     bytes / us / 1e3);
     }
-    float* dOut;
-    CK(hipMalloc(&dOut, sizeof(float) << 24));
-    probe<6, 10, false>(pyr.oct[0], dOut, s, iters);
-    probe<6, 10, true>(pyr.oct[0], dOut, s, iters);
-    probe<6, 6, true>(pyr.oct[0], dOut, s, iters);
-    probe<6, 4, true>(pyr.oct[0], dOut, s, iters);
-    probe<6, 18, true>(pyr.oct[0], dOut, s, iters);
     for (int ns : {1, 3})
         for (int n : {1, 8, 27}) graph_floor(n, ns, 300);
     us = time_us(iters, s, [&] { CK(hipMemsetAsync(dCtr, 0, sizeof(Counters), s)); });
