@@ -299,8 +299,9 @@ class Detector:
         return q[: min(cnt.value, cap)]
 
     # --- stage timing (roofline) ---------------------------------------------
-    def set_timing(self, enable: bool) -> None:
-        _check(lib().sift_hip_set_timing(self._h, int(enable)), "set_timing")
+    def set_timing(self, enable, blur_reps: int = 1) -> None:
+        mode = (blur_reps if blur_reps > 1 else 1) if enable else 0
+        _check(lib().sift_hip_set_timing(self._h, mode), "set_timing")
 
     def timing(self) -> dict:
         n = ctypes.c_int()

@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--streams", type=int, default=3, help="detectors (HIP streams) frames rotate over")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-oracle sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--roofline-only", action="store_true",
+                    help="only the eager per-kernel timing pass (every launch event-bracketed): the command whose "
+                         "rocprofv3 --kernel-trace --stats summary is committed beside the roofline numbers")
     ap.add_argument("--traffic-summary", default=os.path.join(ROOT, "profiles", "round1", "pmc_summary.json"),
                     help="PMC summary (tools/pmc_summary.py) with FETCH_SIZE/WRITE_SIZE of this code")
     return ap.parse_args()
@@ -101,6 +104,56 @@ def pmc_traffic(summary_path, kernel_prefix, grids):
     return {"bytes_per_launch": round(tot / n), "launches": n, "source": os.path.relpath(summary_path, ROOT)} if n else None
 
 
+BLUR_REPS = 10
+
+
+def stage_table(timing, nt):
+    """Per-frame microseconds per stage (blur stages were repeated BLUR_REPS times)."""
+    per = {k: v["ms"] / nt * 1e3 / (BLUR_REPS if k.startswith("blur_") else 1) for k, v in timing.items()}
+    return {k: round(v, 2) for k, v in sorted(per.items(), key=lambda kv: -kv[1])}
+
+
+def measure_roofline(det, frames, stride, traffic_summary, nt=20, warm=3):
+    """k_blur, the kernel with the largest share of frame time (all its launches):
+    algorithmic bytes per launch / average launch duration, by HIP events on the
+    detector's own stream (eager timing mode).  Each blur launch of the frame is
+    repeated BLUR_REPS times back to back inside its event pair (blurs are
+    pure), so the average carries the stream's inter-kernel gap but not one
+    event pair per launch."""
+    det.set_timing(True, blur_reps=BLUR_REPS)
+    for s in range(warm):
+        det.detectAndComputeDevice(frames[s % len(frames)].data_ptr(), stride, sync=True)
+    det.timing_reset()
+    for s in range(nt):
+        det.detectAndComputeDevice(frames[s % len(frames)].data_ptr(), stride, sync=True)
+    timing = det.timing()
+    det.set_timing(False)
+    blurs = [v for k, v in timing.items() if k.startswith("blur_")]
+    blur_launches = sum(v["launches"] for v in blurs)
+    per_launch_bytes = sum(v["bytes"] for v in blurs) / blur_launches
+    per_launch_s = sum(v["ms"] for v in blurs) / blur_launches / 1e3
+    achieved = per_launch_bytes / per_launch_s / 1e9
+    grids = set()
+    for o in range(det.nOctaves):
+        ow, oh, _ = det.octave_dims(o)
+        grids.add(((ow + 63) // 64) * ((oh + 31) // 32) * 256)
+    traffic = pmc_traffic(traffic_summary, "k_blur", grids)
+    roof = {
+        "kernel": f"k_blur (all {blur_launches // nt // BLUR_REPS} launches/frame, each x{BLUR_REPS} back to back "
+                  f"between HIP events, eager)",
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": traffic["bytes_per_launch"] if traffic else None,
+        "traffic_source": traffic,
+        "algo_bytes_per_launch": per_launch_bytes,
+        "avg_launch_us": round(per_launch_s * 1e6, 3),
+    }
+    return {"roofline": roof, "timing": timing, "frames": nt}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -133,7 +186,7 @@ def main():
     # a.streams detectors (one HIP stream + graph pair each) take consecutive
     # frames round-robin, so independent frames overlap on the GPU; every step
     # is still one complete frame.
-    dets = [sift.Detector(cfg, device=local) for _ in range(a.streams)]
+    dets = [sift.Detector(cfg, device=local) for _ in range(1 if a.roofline_only else a.streams)]
     for d in dets:
         d.gpuWarmUpAndAllocate()
     det = dets[0]
@@ -141,6 +194,14 @@ def main():
     frames = [torch.from_numpy(sift.synth_frame(1000 * rank + i, W, H)).to(dev) for i in range(nframes)]
     stride = W * 4
     torch.cuda.synchronize()
+    if a.roofline_only:
+        rl = measure_roofline(det, frames, stride, a.traffic_summary, nt=a.steps)
+        if rank == 0:
+            nt = rl["frames"]
+            print(json.dumps({"roofline": rl["roofline"], "frames": nt,
+                              "stage_us_per_frame_eager": stage_table(rl["timing"], nt)}),
+                  flush=True)
+        return
     for s in range(a.warmup):
         dets[s % a.streams].detectAndComputeDevice(frames[s % nframes].data_ptr(), stride, sync=False)
     for d in dets:
@@ -235,27 +296,11 @@ def main():
     }
 
     # ---- per-kernel roofline: HIP events on the detector's own stream --------
-    det.set_timing(True)
-    det.timing_reset()
-    nt = 20
-    for s in range(nt):
-        det.detectAndComputeDevice(frames[s % nframes].data_ptr(), stride, sync=True)
-    timing = det.timing()
-    det.set_timing(False)
-    total_ms = sum(v["ms"] for v in timing.values())
-    dom = max(timing, key=lambda k: timing[k]["ms"])
-    stages = {k: round(v["ms"] / nt * 1e3, 2) for k, v in sorted(timing.items(), key=lambda kv: -kv[1]["ms"])}
-    # k_blur: the kernel with the largest share of frame time (all launches).
-    blurs = [v for k, v in timing.items() if k.startswith("blur_")]
-    blur_launches = sum(v["launches"] for v in blurs)
-    per_launch_bytes = sum(v["bytes"] for v in blurs) / blur_launches
-    per_launch_s = sum(v["ms"] for v in blurs) / blur_launches / 1e3
-    achieved = per_launch_bytes / per_launch_s / 1e9
-    grids = set()
-    for o in range(det.nOctaves):
-        ow, oh, _ = det.octave_dims(o)
-        grids.add(((ow + 63) // 64) * ((oh + 31) // 32) * 256)
-    traffic = pmc_traffic(a.traffic_summary, "k_blur", grids)
+    rl = measure_roofline(det, frames, stride, a.traffic_summary)
+    timing, nt = rl["timing"], rl["frames"]
+    stages = stage_table(timing, nt)
+    total_ms = sum(stages.values()) * nt / 1e3
+    dom = next(iter(stages))
 
     # ---- C3: 2000 x 2000 x 128 match -----------------------------------------
     det2 = sift.Detector(make_config(numOctaves=0), device=local)
@@ -409,18 +454,7 @@ def main():
                 "parallelism": f"frame-sharded x{world}, no data-path collective",
                 "keypoints_per_frame": kcount,
             },
-            "roofline": {
-                "kernel": f"k_blur (all {blur_launches // nt} launches/frame, eager HIP-event timing)",
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic["bytes_per_launch"] if traffic else None,
-                "traffic_source": traffic,
-                "algo_bytes_per_launch": per_launch_bytes,
-                "avg_launch_us": round(per_launch_s * 1e6, 3),
-            },
+            "roofline": rl["roofline"],
             "cpu_baseline": cpu,
             "pipeline_hbm_frac": round(88.0 * sum_px / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             "sync_ms_per_frame": round(sync_ms, 4),

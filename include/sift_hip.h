@@ -132,7 +132,10 @@ int sift_hip_copy_to_host(sift_hip_t h, float* kpts3, float* feats4, uint16_t* d
 int sift_hip_copy_descriptors_device(sift_hip_t h, uint16_t* dst, int cap, void* stream);
 
 /* Stage timing for roofline reporting: when enabled, the next detect calls run
- * un-graphed with HIP events around every kernel; names are stable strings. */
+ * un-graphed with HIP events around every kernel; names are stable strings.
+ * enable >= 2 also repeats each (pure) blur launch `enable` times back to back
+ * inside its event pair, so the per-launch figure carries one event pair per
+ * `enable` launches instead of one per launch. */
 int sift_hip_set_timing(sift_hip_t h, int enable);
 int sift_hip_timing_count(sift_hip_t h, int* n);
 int sift_hip_timing_entry(sift_hip_t h, int i, const char** name, double* total_ms,

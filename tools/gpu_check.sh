@@ -13,3 +13,6 @@ timeout -k 10 400 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/ben
 cat gpurun_out/bench_$TAG.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 50 --warmup 10 --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1
 echo "prof rc=$?"
+# Roofline pass alone under rocprofv3: its k_blur average must match bench.py's avg_launch_us.
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/roof_$TAG -o run --output-format csv -- python bench.py --roofline-only --steps 100 > gpurun_out/roof_$TAG.json 2> gpurun_out/roof_$TAG.err
+echo "roofline prof rc=$?"

@@ -1,0 +1,30 @@
+"""Compare bench.py --roofline-only's event-timed k_blur average with the
+rocprofv3 kernel-trace of the same command (kernel-only durations).
+
+    python tools/roofline_check.py gpurun_out/roof_TAG.json gpurun_out/roof_TAG/run_kernel_trace.csv
+"""
+import csv
+import json
+import sys
+
+
+def main(bench_json, trace_csv):
+    with open(bench_json) as f:
+        line = [l for l in f if l.strip().startswith("{")][-1]
+    roof = json.loads(line)["roofline"]
+    durs = []
+    for r in csv.DictReader(open(trace_csv)):
+        if "k_blur" in r["Kernel_Name"]:
+            durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    avg = sum(durs) / len(durs)
+    out = {"bench_avg_launch_us": roof["avg_launch_us"], "rocprof_avg_us": round(avg, 3), "rocprof_launches": len(durs),
+           "ratio_bench_over_rocprof": round(roof["avg_launch_us"] / avg, 3),
+           "rocprof_achieved_GBps": round(roof["algo_bytes_per_launch"] / avg / 1e3, 1),
+           "note": "bench brackets every launch with HIP events (includes dispatch latency); rocprof counts kernel "
+                   "execution only; includes the detector's warm-up frames"}
+    json.dump(out, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
