@@ -176,10 +176,12 @@ void launch_refine(const PyrDesc& pyr, const uint2* cand, unsigned capCand, Coun
 // refined layer.  OpenCV sums each of the 36 bins sequentially in float over
 // the window's samples in raster order, so that order is kept exactly:
 // samples are produced 64 at a time in raster order (lane = sample; gradients
-// by bounds-checked buffer loads straight from the plane); six ballots group
-// the chunk's lanes by bin, a scan over the 36 group sizes packs the chunk's
-// values bin by bin (lane order inside a bin) into a 64-entry LDS buffer, and
-// lane b (< 36) adds its bin's values to its running sum in that order --
+// by bounds-checked buffer loads straight from the plane); six ballots on the
+// bin bits give every sample its radix rank (samples of smaller bins + its
+// lane rank inside its bin), which packs the chunk's values bin by bin (lane
+// order inside a bin) into a 64-entry LDS buffer, and lane b (< 36) -- whose
+// range is the radix rank of key b -- adds its bin's values in that order to
+// its running sum --
 // OpenCV's sequential sum, carried in a register across chunks.  <1 KB of LDS
 // per keypoint.  Smoothing, max and peak interpolation use wave shuffles.
 // Reference: SiftOps.cu:237-376 (DoG plane, 32-lane LDS atomics, floor bins,
@@ -202,8 +204,6 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
                                                     Counters* __restrict__ ctr, OriKpt* __restrict__ out,
                                                     uint32_t* __restrict__ bitmap, KeypointParams kp) {
     __shared__ float chunk[64];
-    __shared__ __attribute__((aligned(16))) int ccnt[kOriBins + 4];
-    __shared__ int coff[kOriBins + 4];
     __shared__ float s_exptab[64];
     const int lane = threadIdx.x;
     s_exptab[lane] = c_exptab[lane];
@@ -266,32 +266,39 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
             int bin = cv_round((kOriBins / 360.f) * ori);
             if (bin >= kOriBins) bin -= kOriBins;
             if (bin < 0) bin += kOriBins;
-            // Lanes holding a sample of the same bin: six ballots on its bits.
-            unsigned long long eq = __ballot(valid);
+            // Radix ranks from six ballots on the bin bits (MSB first): for each
+            // key k, `less(k)` = valid samples with a smaller bin and `eq(k)` =
+            // those with bin k.  A sample's slot is less(bin) + its lane rank
+            // inside eq(bin) (raster order); lane b < 36 sums slots
+            // [less(b), less(b) + |eq(b)|) -- no LDS counts, no scan.
+            unsigned long long m[6];
 #pragma unroll
-            for (int bit = 0; bit < 6; bit++) {
-                const unsigned long long m = __ballot((bin >> bit) & 1);
-                eq &= ((bin >> bit) & 1) ? m : ~m;
-            }
-            const int rank = __popcll(eq & lt_mask);
-            if (lane < kOriBins) ccnt[lane] = 0;
-            lds_barrier();
-            if (valid && rank == 0) ccnt[bin] = __popcll(eq);  // one leader per bin present
-            lds_barrier();
-            const int cb = lane < kOriBins ? ccnt[lane] : 0;
-            int incl = cb;
+            for (int bit = 0; bit < 6; bit++) m[bit] = __ballot(valid && ((bin >> bit) & 1));
+            const unsigned long long vmask = __ballot(valid);
+            auto rank_of = [&](int key, int& less) {
+                unsigned long long eq = vmask;
+                less = 0;
 #pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const int t = __shfl_up(incl, d);
-                if (lane >= d) incl += t;
-            }
-            if (lane < kOriBins) coff[lane] = incl - cb;
-            lds_barrier();
-            if (valid) chunk[coff[bin] + rank] = w * mag;
+                for (int bit = 5; bit >= 0; bit--) {
+                    if ((key >> bit) & 1) {
+                        less += __popcll(eq & ~m[bit]);
+                        eq &= m[bit];
+                    } else {
+                        eq &= ~m[bit];
+                    }
+                }
+                return eq;
+            };
+            int less_s;
+            const unsigned long long eq_s = rank_of(bin, less_s);
+            if (valid) chunk[less_s + __popcll(eq_s & lt_mask)] = w * mag;
+            int start;  // lanes >= 36 query bins no sample has: cb = 0
+            const int cb = __popcll(rank_of(lane, start));
+            const int incl = start + cb;
             lds_barrier();
             // Lane b (< 36; others have cb = 0) adds its bin's values in order,
             // four LDS reads in flight at a time.
-            for (int t0 = incl - cb; t0 < incl; t0 += 4) {
+            for (int t0 = start; t0 < incl; t0 += 4) {
                 const float v0 = chunk[t0], v1 = chunk[min(t0 + 1, 63)], v2 = chunk[min(t0 + 2, 63)],
                             v3 = chunk[min(t0 + 3, 63)];
                 acc = acc + v0;
@@ -299,7 +306,7 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
                 if (t0 + 2 < incl) acc = acc + v2;
                 if (t0 + 3 < incl) acc = acc + v3;
             }
-            lds_barrier();  // chunk / ccnt are rewritten by the next 64 samples
+            lds_barrier();  // chunk is rewritten by the next 64 samples
         }
 
         // Circular [1 4 6 4 1]/16 smoothing (SIMD body, fma form).
