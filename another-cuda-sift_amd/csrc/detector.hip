@@ -431,23 +431,77 @@ void enqueue_body(sift_hip_detector* d, int slot) {
     static const char* blurNames[kMaxOctaves] = {"blur_o0", "blur_o1", "blur_o2", "blur_o3", "blur_o4", "blur_o5",
                                                  "blur_o6", "blur_o7", "blur_o8", "blur_o9", "blur_o10", "blur_o11",
                                                  "blur_o12", "blur_o13", "blur_o14", "blur_o15"};
+    // Blur jobs (o, i): plane i of octave o from plane i-1, or for i = 1 of
+    // octaves > 0 from plane L of octave o-1 (decimated, base plane copied
+    // out).  List-scheduled in (o, i) order: a job is ready once its input
+    // plane's job has been launched (stream order); the two oldest ready jobs
+    // share one launch when their radii have a pair kernel -- with L = 3,
+    // (o, 4) + (o+1, 1) and (o, 5) + (o+1, 2): 11 launches instead of 15 for
+    // three octaves.
+    struct Job {
+        int o, i;
+        BlurDesc b;
+        double bytes;
+    };
+    std::vector<Job> jobs;
     for (int o = 0; o < d->nOct; o++) {
         const OctGeom& g = d->pyr.oct[o];
         for (int i = 1; i < L + 3; i++) {
-            float* dst = g.base + (size_t)i * g.planeStride;
+            Job j{o, i, {}, 0};
+            j.b.dst = g.base + (size_t)i * g.planeStride;
+            j.b.dpitch = g.pitch;
+            j.b.W = g.W;
+            j.b.H = g.H;
+            j.b.taps = &d->layerTaps[i];
             if (i == 1 && o > 0) {
                 const OctGeom& p = d->pyr.oct[o - 1];
-                d->timed(blurNames[o], (double)g.W * g.H * 12, [&] {
-                    launch_blur(p.base + (size_t)L * p.planeStride, p.pitch, 2, g.W, g.H, dst, g.pitch, g.base,
-                                d->layerTaps[i], s);
-                });
+                j.b.src = p.base + (size_t)L * p.planeStride;
+                j.b.spitch = p.pitch;
+                j.b.sstep = 2;
+                j.b.copy_out = g.base;
+                j.bytes = (double)g.W * g.H * 12;
             } else {
-                d->timed(blurNames[o], (double)g.W * g.H * 8, [&] {
-                    launch_blur(g.base + (size_t)(i - 1) * g.planeStride, g.pitch, 1, g.W, g.H, dst, g.pitch,
-                                nullptr, d->layerTaps[i], s);
-                });
+                j.b.src = g.base + (size_t)(i - 1) * g.planeStride;
+                j.b.spitch = g.pitch;
+                j.b.sstep = 1;
+                j.b.copy_out = nullptr;
+                j.bytes = (double)g.W * g.H * 8;
+            }
+            jobs.push_back(j);
+        }
+    }
+    std::vector<bool> done(jobs.size(), false);
+    auto idx = [&](int o, int i) { return o * (L + 2) + (i - 1); };
+    auto ready = [&](size_t k) {
+        const Job& j = jobs[k];
+        if (done[k]) return false;
+        if (j.i >= 2) return (bool)done[idx(j.o, j.i - 1)];
+        return j.o == 0 || (bool)done[idx(j.o - 1, L)];
+    };
+    auto single = [&](const Job& j) {
+        d->timed(blurNames[j.o], j.bytes, [&] {
+            launch_blur(j.b.src, j.b.spitch, j.b.sstep, j.b.W, j.b.H, j.b.dst, j.b.dpitch, j.b.copy_out, *j.b.taps, s);
+        });
+    };
+    for (size_t left = jobs.size(); left > 0;) {
+        int a = -1, b = -1;
+        for (size_t k = 0; k < jobs.size() && b < 0; k++)
+            if (ready(k)) (a < 0 ? a : b) = (int)k;
+        const Job& ja = jobs[a];
+        bool paired = false;
+        if (b >= 0) {
+            const Job& jb = jobs[b];
+            char name[16];
+            snprintf(name, sizeof name, "blur_o%d+o%d", ja.o, jb.o);
+            d->timed(name, ja.bytes + jb.bytes, [&] { paired = launch_blur_pair(ja.b, jb.b, s); });
+            if (paired) {
+                done[b] = true;
+                left--;
             }
         }
+        if (!paired) single(ja);
+        done[a] = true;
+        left--;
     }
     double exBytes = 0;
     for (int o = 0; o < d->nOct; o++) exBytes += (double)d->pyr.oct[o].W * d->pyr.oct[o].H * 4 * (L + 3);

@@ -80,25 +80,46 @@ __device__ __forceinline__ f32x2 pk_mov_hi_lo(f32x2 a, f32x2 b) {
 constexpr int BLUR_TW = 64;
 constexpr int BLUR_TH = 32;
 
-// T = float, or uint8_t for a caller's 8-bit frame read by the frame's first
-// blur (OpenCV converts CV_8U to float exactly, so the planes are those of the
-// float frame with the same values).
-template <int R, typename T = float>
-__global__ __launch_bounds__(256) void k_blur(const T* __restrict__ src, int spitch, int sstep, int W, int H,
-                                              float* __restrict__ dst, int dpitch, float* __restrict__ copy_out,
-                                              Taps taps, unsigned* __restrict__ range_keys,
-                                              Counters* __restrict__ zero_ctr) {
+// One blur launch's job: plane src (stride-sstep read = fused INTER_NEAREST
+// decimation) -> dst, optional decimated base copy, pixel range, counters.
+struct BlurJob {
+    const void* src;  // float, or uint8_t for the frame's first blur of an 8-bit frame
+    float* dst;
+    float* copy_out;
+    unsigned* range_keys;
+    Counters* zero_ctr;
+    int spitch, sstep, W, H, dpitch, tilesX, ntiles;
+    Taps taps;
+};
+
+template <int R>
+constexpr int blur_lds_floats() {
+    return (BLUR_TW + 2 * R + 3 & ~3) * (BLUR_TH + 2 * R) + 4;
+}
+
+// Tile `blk` of job J (64 x 32 outputs) with LDS `in`.  T = float, or uint8_t
+// for a caller's 8-bit frame read by the frame's first blur (OpenCV converts
+// CV_8U to float exactly, so the planes are those of the float frame with the
+// same values).
+template <int R, typename T>
+__device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __restrict__ in) {
     constexpr int IW = (BLUR_TW + 2 * R + 3) & ~3;  // row stride, multiple of 4 floats
     constexpr int IH = BLUR_TH + 2 * R;
     constexpr int NW = (2 * R + 4 + 3) / 4;          // float4 reads per row window
+    const T* __restrict__ src = static_cast<const T*>(J.src);
+    float* __restrict__ dst = J.dst;
+    float* __restrict__ copy_out = J.copy_out;
+    unsigned* __restrict__ range_keys = J.range_keys;
+    Counters* __restrict__ zero_ctr = J.zero_ctr;
+    const int spitch = J.spitch, sstep = J.sstep, W = J.W, H = J.H, dpitch = J.dpitch;
+    const Taps& taps = J.taps;
     // Row-pass results (`mid`, pitch IW) overwrite their own input row of
     // `in` in place: a row is read and written only by the same 16 lanes of
     // one wave, whose LDS reads complete before its writes (in-order LDS per
     // wave), so one tile of LDS serves both passes (more workgroups per CU).
-    __shared__ __attribute__((aligned(16))) float in[IH * IW + 4];
     float* const mid = in;
-    const int tile = xcd_tile(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
-    const int x0 = (tile % gridDim.x) * BLUR_TW, y0 = (tile / gridDim.x) * BLUR_TH;
+    const int tile = xcd_tile(blk, J.ntiles);
+    const int x0 = (tile % J.tilesX) * BLUR_TW, y0 = (tile / J.tilesX) * BLUR_TH;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // The frame's first blur also zeroes the frame counters (no memset node).
     if (zero_ctr && tile == 0 && tid < (int)(sizeof(Counters) / 4)) reinterpret_cast<unsigned*>(zero_ctr)[tid] = 0u;
@@ -268,7 +289,7 @@ __global__ __launch_bounds__(256) void k_blur(const T* __restrict__ src, int spi
             }
             __syncthreads();
             if (tid == 0) {  // spread over kRangeSlots address pairs: no single hot atomic
-                unsigned* slot = range_keys + 2 * ((blockIdx.y * gridDim.x + blockIdx.x) % kRangeSlots);
+                unsigned* slot = range_keys + 2 * (blk % kRangeSlots);
                 atomicMax(slot, range_key(fmaxf(fmaxf(mid[0], mid[1]), fmaxf(mid[2], mid[3]))));
                 atomicMax(slot + 1, range_key(fmaxf(fmaxf(mid[4], mid[5]), fmaxf(mid[6], mid[7]))));
             }
@@ -276,14 +297,51 @@ __global__ __launch_bounds__(256) void k_blur(const T* __restrict__ src, int spi
     }
 }
 
-using BlurLaunch = void (*)(dim3, hipStream_t, const float*, int, int, int, int, float*, int, float*, const Taps&,
-                            unsigned*, Counters*);
+template <int R, typename T = float>
+__global__ __launch_bounds__(256) void k_blur(BlurJob J) {
+    __shared__ __attribute__((aligned(16))) float in[blur_lds_floats<R>()];
+    blur_tile<R, T>(J, blockIdx.x, in);
+}
+
+// Two independent blur jobs in one launch (blocks [0, A.ntiles) take A): the
+// first blurs of octave o+1 run beside the last blurs of octave o, which they
+// do not depend on, so a frame needs fewer launches (each costs ~0.7-1.5 us of
+// dispatch) and small-octave tiles fill CUs the larger
+// job leaves idle.
+template <int RA, int RB>
+__global__ __launch_bounds__(256) void k_blur2(BlurJob A, BlurJob B) {
+    constexpr int NA = blur_lds_floats<RA>(), NB = blur_lds_floats<RB>();
+    __shared__ __attribute__((aligned(16))) float in[NA > NB ? NA : NB];
+    if ((int)blockIdx.x < A.ntiles)
+        blur_tile<RA, float>(A, blockIdx.x, in);
+    else
+        blur_tile<RB, float>(B, blockIdx.x - A.ntiles, in);
+}
+
+static BlurJob make_job(const void* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, float* copy_out,
+                        const Taps& taps, unsigned* range_keys, Counters* zero_ctr) {
+    BlurJob j;
+    j.src = src;
+    j.dst = dst;
+    j.copy_out = copy_out;
+    j.range_keys = range_keys;
+    j.zero_ctr = zero_ctr;
+    j.spitch = spitch;
+    j.sstep = sstep;
+    j.W = W;
+    j.H = H;
+    j.dpitch = dpitch;
+    j.tilesX = (W + BLUR_TW - 1) / BLUR_TW;
+    j.ntiles = j.tilesX * ((H + BLUR_TH - 1) / BLUR_TH);
+    j.taps = taps;
+    return j;
+}
+
+using BlurLaunch = void (*)(const BlurJob&, hipStream_t);
 
 template <int R>
-void blur_launch_r(dim3 grid, hipStream_t s, const float* src, int spitch, int sstep, int W, int H, float* dst,
-                   int dpitch, float* copy_out, const Taps& taps, unsigned* range_keys, Counters* zero_ctr) {
-    hipLaunchKernelGGL(k_blur<R>, grid, dim3(256), 0, s, src, spitch, sstep, W, H, dst, dpitch, copy_out, taps,
-                       range_keys, zero_ctr);
+void blur_launch_r(const BlurJob& j, hipStream_t s) {
+    hipLaunchKernelGGL(k_blur<R>, dim3(j.ntiles), dim3(256), 0, s, j);
 }
 
 template <int... Rs>
@@ -292,24 +350,55 @@ constexpr std::array<BlurLaunch, sizeof...(Rs)> blur_table(std::integer_sequence
 }
 static const std::array<BlurLaunch, kMaxTaps / 2> kBlurTable = blur_table(std::make_integer_sequence<int, kMaxTaps / 2>{});
 
+// Pair instantiations: the radii of the default pyramid (sigma 1.6, 3 layers:
+// 5, 6, 8, 10, 13), larger radius first.  Other pairs launch separately.
+template <int RA, int RB>
+void blur2_launch(const BlurJob& a, const BlurJob& b, hipStream_t s) {
+    hipLaunchKernelGGL((k_blur2<RA, RB>), dim3(a.ntiles + b.ntiles), dim3(256), 0, s, a, b);
+}
+bool launch_blur_pair_jobs(const BlurJob& a, const BlurJob& b, hipStream_t s) {
+    const int ra = a.taps.n >> 1, rb = b.taps.n >> 1;
+#define SIFT_PAIR(X, Y)                      \
+    if (ra == X && rb == Y) {                \
+        blur2_launch<X, Y>(a, b, s);         \
+        return true;                         \
+    }                                        \
+    if (ra == Y && rb == X) {                \
+        blur2_launch<X, Y>(b, a, s);         \
+        return true;                         \
+    }
+    SIFT_PAIR(6, 5)
+    SIFT_PAIR(8, 5)
+    SIFT_PAIR(8, 6)
+    SIFT_PAIR(10, 5)
+    SIFT_PAIR(10, 6)
+    SIFT_PAIR(10, 8)
+    SIFT_PAIR(13, 5)
+    SIFT_PAIR(13, 6)
+    SIFT_PAIR(13, 8)
+    SIFT_PAIR(13, 10)
+#undef SIFT_PAIR
+    return false;
+}
+
+bool launch_blur_pair(const BlurDesc& a, const BlurDesc& b, hipStream_t s) {
+    return launch_blur_pair_jobs(make_job(a.src, a.spitch, a.sstep, a.W, a.H, a.dst, a.dpitch, a.copy_out, *a.taps,
+                                          nullptr, nullptr),
+                                 make_job(b.src, b.spitch, b.sstep, b.W, b.H, b.dst, b.dpitch, b.copy_out, *b.taps,
+                                          nullptr, nullptr),
+                                 s);
+}
+
 // 8-bit frames: the first blur reads the bytes itself for the default init
 // radii (sigma 1.6: 13 taps without upscale); any other radius converts the
 // frame to float first (k_u8_to_f32) and runs the float blur.
 bool launch_blur_u8(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, const Taps& taps,
                     hipStream_t s, unsigned* range_keys, Counters* zero_ctr) {
-    const int r = taps.n >> 1;
-    dim3 grid((W + BLUR_TW - 1) / BLUR_TW, (H + BLUR_TH - 1) / BLUR_TH);
-    switch (r) {
-        case 5:
-            hipLaunchKernelGGL((k_blur<5, uint8_t>), grid, dim3(256), 0, s, src, spitch, 1, W, H, dst, dpitch, nullptr,
-                               taps, range_keys, zero_ctr);
-            return true;
-        case 6:
-            hipLaunchKernelGGL((k_blur<6, uint8_t>), grid, dim3(256), 0, s, src, spitch, 1, W, H, dst, dpitch, nullptr,
-                               taps, range_keys, zero_ctr);
-            return true;
-        default:
-            return false;
+    const BlurJob j = make_job(src, spitch, 1, W, H, dst, dpitch, nullptr, taps, range_keys, zero_ctr);
+    switch (taps.n >> 1) {
+        case 5: hipLaunchKernelGGL((k_blur<5, uint8_t>), dim3(j.ntiles), dim3(256), 0, s, j); return true;
+        case 6: hipLaunchKernelGGL((k_blur<6, uint8_t>), dim3(j.ntiles), dim3(256), 0, s, j); return true;
+        default: return false;
     }
 }
 
@@ -326,8 +415,7 @@ void launch_u8_to_f32(const uint8_t* src, int spitch, int W, int H, float* dst, 
 void launch_blur(const float* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, float* copy_out,
                  const Taps& taps, hipStream_t s, unsigned* range_keys, Counters* zero_ctr) {
     const int r = taps.n >> 1;  // 1 .. kMaxTaps/2 (taps.n >= 3 by construction)
-    dim3 grid((W + BLUR_TW - 1) / BLUR_TW, (H + BLUR_TH - 1) / BLUR_TH);
-    kBlurTable[r - 1](grid, s, src, spitch, sstep, W, H, dst, dpitch, copy_out, taps, range_keys, zero_ctr);
+    kBlurTable[r - 1](make_job(src, spitch, sstep, W, H, dst, dpitch, copy_out, taps, range_keys, zero_ctr), s);
 }
 
 // ---------------------------------------------------------------------------

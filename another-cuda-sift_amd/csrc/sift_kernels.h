@@ -70,6 +70,17 @@ constexpr int kRangeSlots = 256;
 // zero_ctr (nullable): counters to zero (the frame's first blur).
 void launch_blur(const float* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, float* copy_out,
                  const Taps& taps, hipStream_t s, unsigned* range_keys = nullptr, Counters* zero_ctr = nullptr);
+// Two independent float blurs in one launch (no range keys / counters);
+// false (nothing launched) when the radius pair has no instantiation.
+struct BlurDesc {
+    const float* src;
+    int spitch, sstep, W, H;
+    float* dst;
+    int dpitch;
+    float* copy_out;
+    const Taps* taps;
+};
+bool launch_blur_pair(const BlurDesc& a, const BlurDesc& b, hipStream_t s);
 // 8-bit frames (pitches in bytes).  launch_blur_u8 returns false (nothing
 // launched) for an init radius without a fused 8-bit instantiation; the caller
 // then converts with launch_u8_to_f32 and uses launch_blur.

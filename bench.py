@@ -79,14 +79,16 @@ def make_config(**kw):
     return sift.CudaSiftConfig(**cfg)
 
 
-def pmc_traffic(summary_path, kernel_prefix, grids):
+def pmc_traffic(summary_path, kernel_names):
     """HBM bytes per launch of a kernel family from a committed PMC summary
-    (tools/pmc.sh + tools/pmc_summary.py on the same code).
+    (tools/pmc.sh + tools/pmc_summary.py over tools/profile_frames.py, i.e.
+    the bench's C2 frame, on the same code): total over every dispatch of the
+    named kernels / their dispatch count, so it averages over the frame's
+    launches exactly like `achieved`.
 
     MI355X_MICROARCH.md HBM section + our calibration (tools/hbm_calib.hip, in
     the summary): FETCH_SIZE counts 1/2 of the bytes read, WRITE_SIZE is exact;
-    both in KiB.  `grids` selects the launches of the bench workload (grid size
-    in threads, one per pyramid octave)."""
+    both in KiB."""
     try:
         with open(summary_path) as f:
             summ = json.load(f)
@@ -97,14 +99,11 @@ def pmc_traffic(summary_path, kernel_prefix, grids):
     write_scale = 1.0 / cal.get("copy4:WRITE_SIZE", 1.0)
     tot, n = 0.0, 0
     for k in summ.get("kernels", []):
-        if k["kernel"].split("<")[0].endswith(kernel_prefix) and k["grid_size"] in grids \
-                and "FETCH_SIZE" in k and "WRITE_SIZE" in k:
+        base = k["kernel"].split("<")[0].split("::")[-1]
+        if base in kernel_names and "FETCH_SIZE" in k and "WRITE_SIZE" in k:
             tot += (k["FETCH_SIZE"] * fetch_scale + k["WRITE_SIZE"] * write_scale) * 1024 * k["dispatches"]
             n += k["dispatches"]
     return {"bytes_per_launch": round(tot / n), "launches": n, "source": os.path.relpath(summary_path, ROOT)} if n else None
-
-
-BLUR_REPS = 10
 
 
 def stage_table(timing, nt):
@@ -133,14 +132,10 @@ def measure_roofline(det, frames, stride, traffic_summary, nt=20, warm=3):
     per_launch_bytes = sum(v["bytes"] for v in blurs) / blur_launches
     per_launch_s = sum(v["ms"] for v in blurs) / blur_launches / 1e3
     achieved = per_launch_bytes / per_launch_s / 1e9
-    grids = set()
-    for o in range(det.nOctaves):
-        ow, oh, _ = det.octave_dims(o)
-        grids.add(((ow + 63) // 64) * ((oh + 31) // 32) * 256)
-    traffic = pmc_traffic(traffic_summary, "k_blur", grids)
+    traffic = pmc_traffic(traffic_summary, ("k_blur", "k_blur2"))
     roof = {
-        "kernel": f"k_blur (all {blur_launches // nt // BLUR_REPS} launches/frame, each x{BLUR_REPS} back to back "
-                  f"between HIP events, eager)",
+        "kernel": f"k_blur / k_blur2 (all {blur_launches // nt // BLUR_REPS} blur launches/frame, each x{BLUR_REPS} "
+                  f"back to back between HIP events, eager)",
         "bound": "hbm",
         "achieved": round(achieved, 1),
         "peak": HBM_PEAK_GBS,
