@@ -106,6 +106,9 @@ def pmc_traffic(summary_path, kernel_names):
     return {"bytes_per_launch": round(tot / n), "launches": n, "source": os.path.relpath(summary_path, ROOT)} if n else None
 
 
+BLUR_REPS = 10
+
+
 def stage_table(timing, nt):
     """Per-frame microseconds per stage (blur stages were repeated BLUR_REPS times)."""
     per = {k: v["ms"] / nt * 1e3 / (BLUR_REPS if k.startswith("blur_") else 1) for k, v in timing.items()}
