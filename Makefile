@@ -23,7 +23,7 @@ HIP_OBJS := $(patsubst $(SRC)/%.hip,$(OUT)/obj/%.o,$(HIP_SRCS)) $(OUT)/obj/synth
 
 all: $(OUT)/libsift_hip.so $(OUT)/libsift_cuda.so tools
 
-$(OUT)/obj/%.o: $(SRC)/%.hip $(SRC)/sift_kernels.h $(SRC)/sift_math.h $(SRC)/sift_match.h include/sift_hip.h
+$(OUT)/obj/%.o: $(SRC)/%.hip $(SRC)/sift_kernels.h $(SRC)/sift_math.h $(SRC)/sift_match.h $(SRC)/sift_refine.h include/sift_hip.h
 	@mkdir -p $(OUT)/obj
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -1,0 +1,145 @@
+// adjustLocalExtrema (OpenCV 4.x sift.simd.hpp) for one 3x3x3 candidate, shared
+// by k_refine (keypoints.hip) and the extrema kernel's epilogue (pyramid.hip).
+// DoG values are re-formed from the Gaussian planes (G_{l+1} - G_l: the same
+// single rounding as a stored DoG).  Accepted keypoints are de-duplicated by
+// final grid position with a bitmap (OpenCV removes the same duplicates later
+// in removeDuplicatedSorted) and compacted with an atomic.
+// Reference: SiftOps.cu:63-208 + collectKpts SiftOps.cu:210-235.
+#pragma once
+#include <climits>
+
+#include "sift_kernels.h"
+#include "sift_math.h"
+
+namespace sift_amd {
+
+constexpr int kBorder = 5;
+constexpr int kMaxInterpSteps = 5;
+
+__device__ __forceinline__ const OctGeom& octave_geom(const PyrDesc& pyr, int o) { return pyr.oct[o]; }
+
+__device__ __forceinline__ float dog_at(const float* g, long ps, int pitch, int layer, int r, int c) {
+    const float* p = g + (size_t)r * pitch + c;
+    return p[(size_t)(layer + 1) * ps] - p[(size_t)layer * ps];
+}
+
+// q = {octave << 8 | layer, r << 16 | c} as the extrema kernels emit it.
+__device__ __forceinline__ void refine_candidate(const PyrDesc& pyr, uint2 q, Counters* __restrict__ ctr,
+                                                 uint32_t* __restrict__ bitmap, RefKpt* __restrict__ out,
+                                                 const KeypointParams& kp) {
+    const int L = pyr.L;
+    const float img_scale = 1.f / 255.f;
+    const float deriv_scale = img_scale * 0.5f;
+    const float second_deriv_scale = img_scale;
+    const float cross_deriv_scale = img_scale * 0.25f;
+    const int o = (int)(q.x >> 8);
+    int layer = (int)(q.x & 255);
+    int r = (int)(q.y >> 16), c = (int)(q.y & 0xffff);
+    const OctGeom& g = octave_geom(pyr, o);
+    const float* G = g.base;
+    const long ps = g.planeStride;
+    const int pitch = g.pitch;
+
+    float xi = 0, xr = 0, xc = 0;
+    int it = 0;
+    bool ok = true;
+    for (; it < kMaxInterpSteps; it++) {
+        const float c0 = dog_at(G, ps, pitch, layer, r, c);
+        const float cl = dog_at(G, ps, pitch, layer, r, c - 1), cr = dog_at(G, ps, pitch, layer, r, c + 1);
+        const float cu = dog_at(G, ps, pitch, layer, r - 1, c), cd = dog_at(G, ps, pitch, layer, r + 1, c);
+        const float pc = dog_at(G, ps, pitch, layer - 1, r, c), nc = dog_at(G, ps, pitch, layer + 1, r, c);
+        const float dD0 = (cr - cl) * deriv_scale;
+        const float dD1 = (cd - cu) * deriv_scale;
+        const float dD2 = (nc - pc) * deriv_scale;
+        const float v2 = c0 * 2;
+        const float dxx = (cr + cl - v2) * second_deriv_scale;
+        const float dyy = (cd + cu - v2) * second_deriv_scale;
+        const float dss = (nc + pc - v2) * second_deriv_scale;
+        const float dxy = (dog_at(G, ps, pitch, layer, r + 1, c + 1) - dog_at(G, ps, pitch, layer, r + 1, c - 1) -
+                           dog_at(G, ps, pitch, layer, r - 1, c + 1) + dog_at(G, ps, pitch, layer, r - 1, c - 1)) *
+                          cross_deriv_scale;
+        const float dxs = (dog_at(G, ps, pitch, layer + 1, r, c + 1) - dog_at(G, ps, pitch, layer + 1, r, c - 1) -
+                           dog_at(G, ps, pitch, layer - 1, r, c + 1) + dog_at(G, ps, pitch, layer - 1, r, c - 1)) *
+                          cross_deriv_scale;
+        const float dys = (dog_at(G, ps, pitch, layer + 1, r + 1, c) - dog_at(G, ps, pitch, layer + 1, r - 1, c) -
+                           dog_at(G, ps, pitch, layer - 1, r + 1, c) + dog_at(G, ps, pitch, layer - 1, r - 1, c)) *
+                          cross_deriv_scale;
+        // Matx_FastSolveOp<float,3,1>: Cramer's rule, det from Matx_DetOp.
+        const float a00 = dxx, a01 = dxy, a02 = dxs, a10 = dxy, a11 = dyy, a12 = dys, a20 = dxs, a21 = dys,
+                    a22 = dss;
+        const float b0 = dD0, b1 = dD1, b2 = dD2;
+        float X0 = 0, X1 = 0, X2 = 0;
+        float d = a00 * (a11 * a22 - a21 * a12) - a01 * (a10 * a22 - a20 * a12) + a02 * (a10 * a21 - a20 * a11);
+        if (d != 0) {
+            d = 1 / d;
+            X0 = d * (b0 * (a11 * a22 - a12 * a21) - a01 * (b1 * a22 - a12 * b2) + a02 * (b1 * a21 - a11 * b2));
+            X1 = d * (a00 * (b1 * a22 - a12 * b2) - b0 * (a10 * a22 - a12 * a20) + a02 * (a10 * b2 - b1 * a20));
+            X2 = d * (a00 * (a11 * b2 - b1 * a21) - a01 * (a10 * b2 - b1 * a20) + b0 * (a10 * a21 - a11 * a20));
+        }
+        xi = -X2;
+        xr = -X1;
+        xc = -X0;
+        if (fabsf(xi) < 0.5f && fabsf(xr) < 0.5f && fabsf(xc) < 0.5f) break;
+        const float big = (float)(INT_MAX / 3);
+        if (fabsf(xi) > big || fabsf(xr) > big || fabsf(xc) > big) {
+            ok = false;
+            break;
+        }
+        c += cv_round(xc);
+        r += cv_round(xr);
+        layer += cv_round(xi);
+        if (layer < 1 || layer > L || c < kBorder || c >= g.W - kBorder || r < kBorder || r >= g.H - kBorder) {
+            ok = false;
+            break;
+        }
+    }
+    if (!ok || it >= kMaxInterpSteps) return;
+
+    const float c0 = dog_at(G, ps, pitch, layer, r, c);
+    const float cl = dog_at(G, ps, pitch, layer, r, c - 1), cr = dog_at(G, ps, pitch, layer, r, c + 1);
+    const float cu = dog_at(G, ps, pitch, layer, r - 1, c), cd = dog_at(G, ps, pitch, layer, r + 1, c);
+    const float pc = dog_at(G, ps, pitch, layer - 1, r, c), nc = dog_at(G, ps, pitch, layer + 1, r, c);
+    const float dD0 = (cr - cl) * deriv_scale;
+    const float dD1 = (cd - cu) * deriv_scale;
+    const float dD2 = (nc - pc) * deriv_scale;
+    float t = 0.f;
+    t += dD0 * xc;
+    t += dD1 * xr;
+    t += dD2 * xi;
+    const float contr = c0 * img_scale + t * 0.5f;
+    if (fabsf(contr) * L < kp.contrastThreshold) return;
+    const float v2 = c0 * 2.f;
+    const float dxx = (cr + cl - v2) * second_deriv_scale;
+    const float dyy = (cd + cu - v2) * second_deriv_scale;
+    const float dxy = (dog_at(G, ps, pitch, layer, r + 1, c + 1) - dog_at(G, ps, pitch, layer, r + 1, c - 1) -
+                       dog_at(G, ps, pitch, layer, r - 1, c + 1) + dog_at(G, ps, pitch, layer, r - 1, c - 1)) *
+                      cross_deriv_scale;
+    const float tr = dxx + dyy;
+    const float det = dxx * dyy - dxy * dxy;
+    const float et = kp.edgeThreshold;
+    if (det <= 0 || tr * tr * et >= (et + 1) * (et + 1) * det) return;
+
+    // Duplicate (same final octave/layer/r/c) -> identical keypoint: keep one.
+    const long bit = g.bitBase + ((long)(layer - 1) * g.H + r) * g.W + c;
+    const uint32_t m = 1u << (bit & 31);
+    if (atomicOr(&bitmap[bit >> 5], m) & m) return;
+
+    RefKpt k;
+    k.x = ((float)c + xc) * (float)(1 << o);
+    k.y = ((float)r + xr) * (float)(1 << o);
+    k.octave = o + (layer << 8) + ((int)rint(((double)xi + 0.5) * 255) << 16);
+    k.size = kp.sigma * pow2_via_double((layer + xi) / (float)L) * (float)(1 << o) * 2;
+    k.response = fabsf(contr);
+    k.o = o;
+    k.layer = layer;
+    k.rc = r << 16 | c;
+    const unsigned slot = atomicAdd(&ctr->refined, 1u);
+    if (slot < kp.capRefined) {
+        out[slot] = k;
+    } else {
+        atomicOr(&ctr->overflow, 2u);
+        atomicAnd(&bitmap[bit >> 5], ~m);  // every set bit belongs to a stored keypoint
+    }
+}
+
+}  // namespace sift_amd

@@ -1,0 +1,63 @@
+"""GPU parity on the code paths the default configuration does not take.
+
+* numOctaveLayers > 6: the LDS-staged per-octave extrema kernel (k_extrema)
+  instead of the register-streaming all-octave one.
+* More than 16384 row buckets (tall, doubled images): retainBest select,
+  bucket count, scan and scatter as four kernels instead of k_order.
+* maxKeypoints below the keypoint count: results are the first maxKeypoints
+  of the full, deterministic output order, and overflow bit 3 is raised.
+Same bar as test_gpu_parity.py: keypoints bit-exact, descriptors |diff| <= 1
+with >= 99.5 % exact.
+"""
+import numpy as np
+import pytest
+
+from test_gpu_parity import assert_same_keypoints, gpu_keypoints, make_detector, sort_keys
+
+pytestmark = pytest.mark.gpu
+
+
+def check_vs_oracle(sift, oracle, cfg, det, img):
+    gk, gd, _ = gpu_keypoints(det)
+    ok, od = oracle.detect_and_compute(img, oracle.from_config(cfg))
+    assert len(ok) > 20
+    assert_same_keypoints(gk, ok)
+    diff = np.abs(gd[sort_keys(gk)] - od[sort_keys(ok)])
+    assert diff.max() <= 1.0 and (diff == 0).mean() >= 0.995, ((diff == 0).mean(), diff.max())
+
+
+@pytest.mark.parametrize("layers", [7, 9])
+def test_many_layers_lds_extrema(sift, oracle, layers):
+    w, h = 320, 240
+    img = sift.synth_frame(12, w, h)
+    cfg, det = make_detector(sift, w, h, upscale=True, numOctaveLayers=layers, numFeatures=0)
+    det.detectAndCompute(img)
+    cand = det.debug_candidates()
+    ref = oracle.extrema(img, oracle.from_config(cfg))
+    assert np.array_equal(cand[np.lexsort(cand.T[::-1])], ref[np.lexsort(ref.T[::-1])])
+    check_vs_oracle(sift, oracle, cfg, det, img)
+
+
+def test_many_buckets_four_kernel_order(sift, oracle):
+    # doubled 300 x 1400 -> 600 x 2800 base, 6 layers: ~33k row buckets > 16384
+    w, h = 300, 1400
+    img = sift.synth_frame(13, w, h)
+    cfg, det = make_detector(sift, w, h, upscale=True, numOctaveLayers=6, numFeatures=700)
+    det.detectAndCompute(img)
+    check_vs_oracle(sift, oracle, cfg, det, img)
+
+
+def test_max_keypoints_truncates_in_order(sift):
+    w, h = 752, 480
+    img = sift.synth_frame(14, w, h)
+    _, full = make_detector(sift, w, h, numFeatures=0)
+    full.detectAndCompute(img)
+    fk, fd, _ = gpu_keypoints(full)
+    assert full.overflow_flags() == 0 and len(fk) > 300
+    cap = 257
+    _, det = make_detector(sift, w, h, numFeatures=0, maxKeypoints=cap)
+    det.detectAndCompute(img)
+    assert det.total_size == cap
+    assert det.overflow_flags() & 8
+    k, d, _ = gpu_keypoints(det)
+    assert np.array_equal(k, fk[:cap]) and np.array_equal(d, fd[:cap])
