@@ -35,6 +35,8 @@
 // oracle's float operations.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "sift_kernels.h"
 #include "sift_math.h"
 
@@ -143,7 +145,8 @@ __device__ __forceinline__ DescJob load_job(const DescJob* jobs, unsigned p) {
 
 __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ jobs, const Counters* __restrict__ ctr,
                                                    const unsigned* __restrict__ range_keys,
-                                                   uint16_t* __restrict__ desc, Counters* __restrict__ host_ctr) {
+                                                   uint16_t* __restrict__ desc, Counters* __restrict__ host_ctr,
+                                                   long fs) {
     // Two u32 fixed-point histograms so that each sample's orientation pair
     // (o0, o0+1) is one naturally aligned ds_add_u64 (low word o0, high word
     // o0+1): even o0 -> histE[cell*8 + o], odd o0 -> histO[cell*10 + 1 + o]
@@ -156,6 +159,12 @@ __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ 
     __shared__ float s_norm[12];
 
     const int tid = threadIdx.x, lane = tid & 63;
+    const long foff = blockIdx.y * fs;  // frame blockIdx.y
+    jobs = fptr(jobs, foff);
+    ctr = fptr(ctr, foff);
+    range_keys = fptr(range_keys, foff);
+    desc = fptr(desc, foff);
+    host_ctr += blockIdx.y;
     const unsigned n = ctr->final_n;
     // The frame's counters are final before this (last) kernel starts: hand
     // them to the host's pinned copy directly (no D2H copy node in the graph).
@@ -382,9 +391,11 @@ __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ 
 }
 
 void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned* range_keys, uint16_t* desc,
-                       Counters* host_ctr, const KeypointParams& kp, hipStream_t s) {
+                       Counters* host_ctr, const KeypointParams& kp, const Frames& fr, hipStream_t s) {
     (void)kp;
-    hipLaunchKernelGGL(k_descriptor, dim3(8192), dim3(kDT), 0, s, jobs, ctr, range_keys, desc, host_ctr);
+    const int per = fr.nf <= 1 ? 8192 : std::max(2048, 16384 / fr.nf);  // workgroups per frame
+    hipLaunchKernelGGL(k_descriptor, dim3(per, fr.nf), dim3(kDT), 0, s, jobs, ctr, range_keys, desc, host_ctr,
+                       fr.stride);
 }
 
 }  // namespace sift_amd

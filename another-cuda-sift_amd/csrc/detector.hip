@@ -106,6 +106,15 @@ struct sift_hip_detector {
     void* hStage[kInSlots] = {};                         // pinned staging
     hipEvent_t evUp[kInSlots] = {}, evRead[kInSlots] = {};  // upload done / first kernel done
 
+    // Frame batches: up to B frames per launch (sift_hip_set_batch).  Every
+    // per-frame buffer below lives in frame 0's arena; frame f's copy is at
+    // + f * afs bytes (Frames, sift_kernels.h).  nfOf[slot] = frames of the
+    // launch group that wrote results slot `slot`.
+    int B = 1;
+    long afs = 0;
+    char* dArena = nullptr;
+    int nfOf[kSlots] = {};
+
     PyrDesc pyr{};
     Taps initTaps{};
     std::vector<Taps> layerTaps;
@@ -129,14 +138,15 @@ struct sift_hip_detector {
     uint32_t* dBitmap = nullptr;
     size_t bitmapWords = 0;
     Counters* dCtr = nullptr;
-    Counters* hCtr = nullptr;     // kSlots pinned host copies of the counters (written by k_descriptor)
+    Counters* hCtr = nullptr;     // kSlots x B pinned host copies of the counters (written by k_descriptor)
     Counters* hCtrDev = nullptr;  // their device-side address
     float* dKpts3[kSlots] = {};
     float* dFeats4[kSlots] = {};
     uint16_t* dDesc[kSlots] = {};
     int cur = 0, count = 0, prevCount = 0;  // slot_of(current) and the counts of current, current - 1
 
-    hipGraphExec_t exec[kSlots] = {};
+    hipGraphExec_t exec[kSlots] = {};   // B frames per launch
+    hipGraphExec_t exec1[kSlots] = {};  // one frame (B > 1 only; exec when B = 1)
     bool useGraph = true;
 
     bool timing = false;
@@ -196,15 +206,11 @@ struct sift_hip_detector {
             (void)hipSetDevice(device);
             for (auto& e : exec)
                 if (e) (void)hipGraphExecDestroy(e);
-            void* bufs[] = {dInput, dUp, dPyr, dCand, dRef, dOri, dSlot, dOrder, dJobs, dRange, dBcount, dBoff,
-                            dBitmap, dCtr};
-            for (void* b : bufs)
-                if (b) (void)hipFree(b);
-            for (int k = 0; k < kSlots; k++) {
-                for (void* b : {(void*)dKpts3[k], (void*)dFeats4[k], (void*)dDesc[k]})
-                    if (b) (void)hipFree(b);
+            for (auto& e : exec1)
+                if (e) (void)hipGraphExecDestroy(e);
+            if (dArena) (void)hipFree(dArena);
+            for (int k = 0; k < kSlots; k++)
                 if (evFrame[k]) (void)hipEventDestroy(evFrame[k]);
-            }
             for (int k = 0; k < kInSlots; k++) {
                 if (dIn[k]) (void)hipFree(dIn[k]);
                 if (hStage[k]) (void)hipHostFree(hStage[k]);
@@ -321,10 +327,9 @@ int allocate(sift_hip_detector* d) {
     HIPCHK(hipEventCreateWithFlags(&d->evOut, hipEventDisableTiming));
     const int W = d->cfg.col_width, H = d->cfg.row_width;
     d->inPitch = (W + 63) / 64 * 64;
-    int rc;
-    if ((rc = dalloc(&d->dInput, (size_t)d->inPitch * H))) return rc;
-    // Upload ring: sized for f32 rows of pitch inPitch (an 8-bit frame uses
-    // the first quarter with a byte pitch of inPitch).
+    // Upload ring (host input path, one frame at a time): sized for f32 rows
+    // of pitch inPitch (an 8-bit frame uses the first quarter with a byte
+    // pitch of inPitch).
     const size_t inBytes = sizeof(float) * (size_t)d->inPitch * H;
     for (int k = 0; k < d->kInSlots; k++) {
         if (hipMalloc(&d->dIn[k], inBytes) != hipSuccess) return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc failed");
@@ -338,45 +343,72 @@ int allocate(sift_hip_detector* d) {
         HIPCHK(hipEventCreateWithFlags(&d->evFrame[k], hipEventDisableTiming));
         HIPCHK(hipEventRecord(d->evFrame[k], d->stream));
     }
-    if (d->firstOctave < 0) {
-        d->upPitch = (2 * W + 63) / 64 * 64;
-        if ((rc = dalloc(&d->dUp, (size_t)d->upPitch * 2 * H))) return rc;
-    }
+    if (d->firstOctave < 0) d->upPitch = (2 * W + 63) / 64 * 64;
     size_t pyrFloats = 0;
     for (int o = 0; o < d->nOct; o++) pyrFloats += (size_t)d->pyr.oct[o].planeStride * (d->L + 3);
-    if ((rc = dalloc(&d->dPyr, pyrFloats))) return rc;
-    HIPCHK(hipMemset(d->dPyr, 0, sizeof(float) * pyrFloats));
+    const unsigned capO = d->kp.capOriented, capF = d->kp.capFinal;
+
+    // Frame arena: every per-frame buffer at a 256-B aligned offset; B arenas
+    // back to back.  Zeroed once here; afterwards the kernels keep the
+    // scratch zero for the next frame (first blur: counters, k_order /
+    // k_select: range keys, k_bucket_rank: bucket counts, k_orientation:
+    // dedupe bits), so the frame graph has no memset node.
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off += (std::max<size_t>(bytes, 1) + 255) & ~(size_t)255;
+        return o;
+    };
+    const size_t oInput = take(sizeof(float) * (size_t)d->inPitch * H);  // blank warm-up frame / u8 -> f32 scratch
+    const size_t oUp = d->firstOctave < 0 ? take(sizeof(float) * (size_t)d->upPitch * 2 * H) : 0;
+    const size_t oPyr = take(sizeof(float) * pyrFloats);
+    const size_t oCand = take(sizeof(uint2) * d->capCand);
+    const size_t oRef = take(sizeof(RefKpt) * d->kp.capRefined);
+    const size_t oOri = take(sizeof(OriKpt) * capO);
+    const size_t oSlot = take(sizeof(int) * capO);
+    const size_t oOrder = take(sizeof(int) * capO);
+    const size_t oJobs = take(sizeof(DescJob) * capF);
+    const size_t oRange = take(sizeof(unsigned) * 2 * 2 * kRangeSlots);  // one set per frame parity
+    const size_t oBcount = take(sizeof(unsigned) * (size_t)d->kp.numBuckets);
+    const size_t oBoff = take(sizeof(unsigned) * (size_t)d->kp.numBuckets);
+    const size_t oBitmap = take(sizeof(uint32_t) * d->bitmapWords);
+    const size_t oCtr = take(sizeof(Counters));
+    size_t oK3[sift_hip_detector::kSlots], oF4[sift_hip_detector::kSlots], oDesc[sift_hip_detector::kSlots];
+    for (int b = 0; b < d->kSlots; b++) {
+        oK3[b] = take(sizeof(float) * 3 * (size_t)capF);
+        oF4[b] = take(sizeof(float) * 4 * (size_t)capF);
+        oDesc[b] = take(sizeof(uint16_t) * 128 * (size_t)capF);
+    }
+    d->afs = (long)off;
+    if (hipMalloc((void**)&d->dArena, off * d->B) != hipSuccess)
+        return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc of the frame arenas failed");
+    HIPCHK(hipMemset(d->dArena, 0, off * d->B));
+    char* A = d->dArena;
+    d->dInput = reinterpret_cast<float*>(A + oInput);
+    d->dUp = d->firstOctave < 0 ? reinterpret_cast<float*>(A + oUp) : nullptr;
+    d->dPyr = reinterpret_cast<float*>(A + oPyr);
     for (int o = 0; o < d->nOct; o++)
         d->pyr.oct[o].base = d->dPyr + reinterpret_cast<size_t>(d->pyr.oct[o].base);
-    const unsigned capO = d->kp.capOriented, capF = d->kp.capFinal;
-    if ((rc = dalloc(&d->dCand, d->capCand))) return rc;
-    if ((rc = dalloc(&d->dRef, d->kp.capRefined))) return rc;
-    if ((rc = dalloc(&d->dOri, capO))) return rc;
-    if ((rc = dalloc(&d->dSlot, capO))) return rc;
-    if ((rc = dalloc(&d->dOrder, capO))) return rc;
-    if ((rc = dalloc(&d->dJobs, capF))) return rc;
-    if ((rc = dalloc(&d->dRange, 2 * 2 * kRangeSlots))) return rc;  // one set per frame buffer
-    if ((rc = dalloc(&d->dBcount, (size_t)d->kp.numBuckets))) return rc;
-    if ((rc = dalloc(&d->dBoff, (size_t)d->kp.numBuckets))) return rc;
-    if ((rc = dalloc(&d->dBitmap, d->bitmapWords))) return rc;
-    if ((rc = dalloc(&d->dCtr, 1))) return rc;
-    // Zeroed once here; afterwards the kernels keep them zero for the next
-    // frame (first blur: counters, k_select: range keys, k_bucket_rank: bucket
-    // counts, k_orientation: dedupe bits), so the frame graph has no memset node.
-    HIPCHK(hipMemset(d->dCtr, 0, sizeof(Counters)));
-    HIPCHK(hipMemset(d->dRange, 0, sizeof(unsigned) * 2 * 2 * kRangeSlots));
-    HIPCHK(hipMemset(d->dBcount, 0, sizeof(unsigned) * (size_t)d->kp.numBuckets));
-    HIPCHK(hipMemset(d->dBitmap, 0, sizeof(uint32_t) * d->bitmapWords));
-    HIPCHK(hipHostMalloc((void**)&d->hCtr, sizeof(Counters) * d->kSlots, hipHostMallocMapped | hipHostMallocCoherent));
-    memset(d->hCtr, 0, sizeof(Counters) * d->kSlots);
-    HIPCHK(hipHostGetDevicePointer((void**)&d->hCtrDev, d->hCtr, 0));
+    d->dCand = reinterpret_cast<uint2*>(A + oCand);
+    d->dRef = reinterpret_cast<RefKpt*>(A + oRef);
+    d->dOri = reinterpret_cast<OriKpt*>(A + oOri);
+    d->dSlot = reinterpret_cast<int*>(A + oSlot);
+    d->dOrder = reinterpret_cast<int*>(A + oOrder);
+    d->dJobs = reinterpret_cast<DescJob*>(A + oJobs);
+    d->dRange = reinterpret_cast<unsigned*>(A + oRange);
+    d->dBcount = reinterpret_cast<unsigned*>(A + oBcount);
+    d->dBoff = reinterpret_cast<unsigned*>(A + oBoff);
+    d->dBitmap = reinterpret_cast<uint32_t*>(A + oBitmap);
+    d->dCtr = reinterpret_cast<Counters*>(A + oCtr);
     for (int b = 0; b < d->kSlots; b++) {
-        if ((rc = dalloc(&d->dKpts3[b], (size_t)capF * 3))) return rc;
-        if ((rc = dalloc(&d->dFeats4[b], (size_t)capF * 4))) return rc;
-        if ((rc = dalloc(&d->dDesc[b], (size_t)capF * 128))) return rc;
-        HIPCHK(hipMemset(d->dDesc[b], 0, sizeof(uint16_t) * (size_t)capF * 128));
+        d->dKpts3[b] = reinterpret_cast<float*>(A + oK3[b]);
+        d->dFeats4[b] = reinterpret_cast<float*>(A + oF4[b]);
+        d->dDesc[b] = reinterpret_cast<uint16_t*>(A + oDesc[b]);
     }
-    HIPCHK(hipMemset(d->dInput, 0, sizeof(float) * (size_t)d->inPitch * H));
+    const size_t nh = (size_t)d->kSlots * d->B;
+    HIPCHK(hipHostMalloc((void**)&d->hCtr, sizeof(Counters) * nh, hipHostMallocMapped | hipHostMallocCoherent));
+    memset(d->hCtr, 0, sizeof(Counters) * nh);
+    HIPCHK(hipHostGetDevicePointer((void**)&d->hCtrDev, d->hCtr, 0));
     upload_exp_tab();
     return SIFT_HIP_OK;
 }
@@ -387,44 +419,49 @@ int allocate(sift_hip_detector* d) {
 // the other set for the next frame).
 unsigned* range_keys(sift_hip_detector* d, int p) { return d->dRange + (size_t)p * 2 * kRangeSlots; }
 
-// pitch in elements of the frame's format (bytes for SIFT_HIP_U8).
-void enqueue_head(sift_hip_detector* d, const void* img, int pitch, int fmt, int parity) {
+// pitch in elements of the frame's format (bytes for SIFT_HIP_U8); nf frames
+// at byte stride sfs.
+void enqueue_head(sift_hip_detector* d, const void* img, int pitch, int fmt, int parity, int nf, long sfs) {
     const int W = d->cfg.col_width, H = d->cfg.row_width;
     const bool u8 = fmt == SIFT_HIP_U8;
-    const double inB = (double)W * H * (u8 ? 1 : 4);
+    const Frames fr{nf, d->afs};
+    const double inB = (double)W * H * (u8 ? 1 : 4) * nf;
     // Counters first: the initial blur accumulates the frame's pixel range.
     if (d->firstOctave < 0) {
-        d->timed("upsample", inB + (double)W * H * 16, [&] {
+        d->timed("upsample", inB + (double)W * H * 16 * nf, [&] {
             if (u8)
-                launch_upsample2x_u8((const uint8_t*)img, pitch, W, H, d->dUp, d->upPitch, d->stream);
+                launch_upsample2x_u8((const uint8_t*)img, pitch, W, H, d->dUp, d->upPitch, fr, sfs, d->stream);
             else
-                launch_upsample2x((const float*)img, pitch, W, H, d->dUp, d->upPitch, d->stream);
+                launch_upsample2x((const float*)img, pitch, W, H, d->dUp, d->upPitch, fr, sfs, d->stream);
         });
     } else {
         const OctGeom& g = d->pyr.oct[0];
-        d->timed("blur_init", inB + (double)W * H * 4, [&] {
+        d->timed("blur_init", inB + (double)W * H * 4 * nf, [&] {
+            long s = sfs;
             if (u8) {
-                if (launch_blur_u8((const uint8_t*)img, pitch, W, H, g.base, g.pitch, d->initTaps, d->stream,
+                if (launch_blur_u8((const uint8_t*)img, pitch, W, H, g.base, g.pitch, d->initTaps, fr, sfs, d->stream,
                                    range_keys(d, parity), d->dCtr))
                     return;
-                launch_u8_to_f32((const uint8_t*)img, pitch, W, H, d->dInput, d->inPitch, d->stream);
+                launch_u8_to_f32((const uint8_t*)img, pitch, W, H, d->dInput, d->inPitch, fr, sfs, d->stream);
                 img = d->dInput;
                 pitch = d->inPitch;
+                s = d->afs;
             }
-            launch_blur((const float*)img, pitch, 1, W, H, g.base, g.pitch, nullptr, d->initTaps, d->stream,
+            launch_blur((const float*)img, pitch, 1, W, H, g.base, g.pitch, nullptr, d->initTaps, fr, s, d->stream,
                         range_keys(d, parity), d->dCtr);
         });
     }
 }
 
-void enqueue_body(sift_hip_detector* d, int slot) {
+void enqueue_body(sift_hip_detector* d, int slot, int nf) {
     hipStream_t s = d->stream;
     const int L = d->L;
     const int parity = slot & 1;  // kSlots is even, so slot parity = frame parity
+    const Frames fr{nf, d->afs};
     if (d->firstOctave < 0) {
         const OctGeom& g = d->pyr.oct[0];
-        d->timed("blur_init", (double)g.W * g.H * 8, [&] {
-            launch_blur(d->dUp, d->upPitch, 1, g.W, g.H, g.base, g.pitch, nullptr, d->initTaps, s,
+        d->timed("blur_init", (double)g.W * g.H * 8 * nf, [&] {
+            launch_blur(d->dUp, d->upPitch, 1, g.W, g.H, g.base, g.pitch, nullptr, d->initTaps, fr, d->afs, s,
                         range_keys(d, parity), d->dCtr);
         });
     }
@@ -459,13 +496,13 @@ void enqueue_body(sift_hip_detector* d, int slot) {
                 j.b.spitch = p.pitch;
                 j.b.sstep = 2;
                 j.b.copy_out = g.base;
-                j.bytes = (double)g.W * g.H * 12;
+                j.bytes = (double)g.W * g.H * 12 * nf;
             } else {
                 j.b.src = g.base + (size_t)(i - 1) * g.planeStride;
                 j.b.spitch = g.pitch;
                 j.b.sstep = 1;
                 j.b.copy_out = nullptr;
-                j.bytes = (double)g.W * g.H * 8;
+                j.bytes = (double)g.W * g.H * 8 * nf;
             }
             jobs.push_back(j);
         }
@@ -480,7 +517,8 @@ void enqueue_body(sift_hip_detector* d, int slot) {
     };
     auto single = [&](const Job& j) {
         d->timed(blurNames[j.o], j.bytes, [&] {
-            launch_blur(j.b.src, j.b.spitch, j.b.sstep, j.b.W, j.b.H, j.b.dst, j.b.dpitch, j.b.copy_out, *j.b.taps, s);
+            launch_blur(j.b.src, j.b.spitch, j.b.sstep, j.b.W, j.b.H, j.b.dst, j.b.dpitch, j.b.copy_out, *j.b.taps, fr,
+                        d->afs, s);
         });
     };
     for (size_t left = jobs.size(); left > 0;) {
@@ -493,7 +531,7 @@ void enqueue_body(sift_hip_detector* d, int slot) {
             const Job& jb = jobs[b];
             char name[16];
             snprintf(name, sizeof name, "blur_o%d+o%d", ja.o, jb.o);
-            d->timed(name, ja.bytes + jb.bytes, [&] { paired = launch_blur_pair(ja.b, jb.b, s); });
+            d->timed(name, ja.bytes + jb.bytes, [&] { paired = launch_blur_pair(ja.b, jb.b, fr, s); });
             if (paired) {
                 done[b] = true;
                 left--;
@@ -504,59 +542,74 @@ void enqueue_body(sift_hip_detector* d, int slot) {
         left--;
     }
     double exBytes = 0;
-    for (int o = 0; o < d->nOct; o++) exBytes += (double)d->pyr.oct[o].W * d->pyr.oct[o].H * 4 * (L + 3);
+    for (int o = 0; o < d->nOct; o++) exBytes += (double)d->pyr.oct[o].W * d->pyr.oct[o].H * 4 * (L + 3) * nf;
     d->timed("extrema", exBytes, [&] {
-        if (!launch_extrema_all(d->pyr, d->threshold, d->dCand, d->dCtr, d->capCand, s))
-            for (int o = 0; o < d->nOct; o++) launch_extrema(d->pyr, o, d->threshold, d->dCand, d->dCtr, d->capCand, s);
+        if (!launch_extrema_all(d->pyr, d->threshold, d->dCand, d->dCtr, d->capCand, fr, s))
+            for (int o = 0; o < d->nOct; o++)
+                launch_extrema(d->pyr, o, d->threshold, d->dCand, d->dCtr, d->capCand, fr, s);
     });
-    d->timed("refine", 0, [&] { launch_refine(d->pyr, d->dCand, d->capCand, d->dCtr, d->dBitmap, d->dRef, d->kp, s); });
-    d->timed("orientation", 0, [&] { launch_orientation(d->pyr, d->dRef, d->dCtr, d->dOri, d->dBitmap, d->kp, s); });
+    d->timed("refine", 0,
+             [&] { launch_refine(d->pyr, d->dCand, d->capCand, d->dCtr, d->dBitmap, d->dRef, d->kp, fr, s); });
+    d->timed("orientation", 0,
+             [&] { launch_orientation(d->pyr, d->dRef, d->dCtr, d->dOri, d->dBitmap, d->kp, fr, s); });
     if (d->kp.numBuckets <= kOrderMaxBuckets) {
         d->timed("order", 0, [&] {
             launch_order(d->dOri, d->dCtr, range_keys(d, parity ^ 1), d->dBcount, d->dBoff, d->dSlot, d->dOrder, d->kp,
-                         s);
+                         fr, s);
         });
     } else {
-        d->timed("select", 0, [&] { launch_select(d->dOri, d->dCtr, range_keys(d, parity ^ 1), d->kp, s); });
-        d->timed("bucket_count", 0, [&] { launch_bucket_count(d->dOri, d->dCtr, d->dBcount, d->dSlot, d->kp, s); });
-        d->timed("bucket_scan", 0, [&] { launch_bucket_scan(d->dBcount, d->dBoff, d->dCtr, d->kp, s); });
+        d->timed("select", 0, [&] { launch_select(d->dOri, d->dCtr, range_keys(d, parity ^ 1), d->kp, fr, s); });
+        d->timed("bucket_count", 0,
+                 [&] { launch_bucket_count(d->dOri, d->dCtr, d->dBcount, d->dSlot, d->kp, fr, s); });
+        d->timed("bucket_scan", 0, [&] { launch_bucket_scan(d->dBcount, d->dBoff, d->dCtr, d->kp, fr, s); });
         d->timed("bucket_scatter", 0,
-                 [&] { launch_bucket_scatter(d->dOri, d->dCtr, d->dBoff, d->dSlot, d->dOrder, d->kp, s); });
+                 [&] { launch_bucket_scatter(d->dOri, d->dCtr, d->dBoff, d->dSlot, d->dOrder, d->kp, fr, s); });
     }
     d->timed("bucket_rank", 0, [&] {
         launch_bucket_rank(d->pyr, d->dOri, d->dBcount, d->dBoff, d->dOrder, d->dCtr, d->dJobs, d->dKpts3[slot],
-                           d->dFeats4[slot], d->kp, s);
+                           d->dFeats4[slot], d->kp, fr, s);
     });
     d->timed("descriptor", 0, [&] {
-        launch_descriptor(d->dJobs, d->dCtr, range_keys(d, parity), d->dDesc[slot], d->hCtrDev + slot, d->kp, s);
+        launch_descriptor(d->dJobs, d->dCtr, range_keys(d, parity), d->dDesc[slot], d->hCtrDev + (size_t)slot * d->B,
+                          d->kp, fr, s);
     });
+}
+
+int capture(sift_hip_detector* d, int slot, int nf, hipGraphExec_t* out) {
+    hipGraph_t g = nullptr;
+    HIPCHK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
+    enqueue_body(d, slot, nf);
+    HIPCHK(hipStreamEndCapture(d->stream, &g));
+    HIPCHK(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
+    HIPCHK(hipGraphDestroy(g));
+    return SIFT_HIP_OK;
 }
 
 int build_graphs(sift_hip_detector* d) {
     for (int b = 0; b < d->kSlots; b++) {
-        hipGraph_t g = nullptr;
-        HIPCHK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
-        enqueue_body(d, b);
-        HIPCHK(hipStreamEndCapture(d->stream, &g));
-        HIPCHK(hipGraphInstantiate(&d->exec[b], g, nullptr, nullptr, 0));
-        HIPCHK(hipGraphDestroy(g));
+        if (int rc = capture(d, b, d->B, &d->exec[b])) return rc;
+        if (d->B > 1)
+            if (int rc = capture(d, b, 1, &d->exec1[b])) return rc;
     }
     return SIFT_HIP_OK;
 }
 
-// Enqueues frame d->submitted on d->stream; `consumed` (nullable) is recorded
-// once the frame's input has been read.
-int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEvent_t consumed) {
+// Enqueues launch group d->submitted (nf frames at byte stride sfs) on
+// d->stream; `consumed` (nullable) is recorded once the input has been read.
+int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEvent_t consumed, int nf = 1,
+              long sfs = 0) {
     const long long f = d->submitted;
     const int slot = d->slot_of(f);
-    enqueue_head(d, img, pitch, fmt, slot & 1);
+    enqueue_head(d, img, pitch, fmt, slot & 1, nf, sfs);
     if (consumed) HIPCHK(hipEventRecord(consumed, d->stream));
-    if (d->useGraph && !d->timing) {
-        HIPCHK(hipGraphLaunch(d->exec[slot], d->stream));
-    } else {
-        enqueue_body(d, slot);
+    hipGraphExec_t g = nf == d->B ? d->exec[slot] : (nf == 1 ? d->exec1[slot] : nullptr);
+    if (d->useGraph && !d->timing && g) {
+        HIPCHK(hipGraphLaunch(g, d->stream));
+    } else {  // timing mode, or a partial batch: the same launches, eagerly
+        enqueue_body(d, slot, nf);
     }
     HIPCHK(hipEventRecord(d->evFrame[slot], d->stream));
+    d->nfOf[slot] = nf;
     d->submitted = f + 1;
     return SIFT_HIP_OK;
 }
@@ -571,7 +624,8 @@ void make_current(sift_hip_detector* d, long long f) {
 void complete_counts(sift_hip_detector* d) {
     const long long f = d->current;
     auto n = [&](long long g) {
-        return g < d->firstFrame ? 0 : (int)std::min<unsigned>(d->hCtr[d->slot_of(g)].final_n, d->kp.capFinal);
+        return g < d->firstFrame ? 0
+                                 : (int)std::min<unsigned>(d->hCtr[(size_t)d->slot_of(g) * d->B].final_n, d->kp.capFinal);
     };
     d->count = n(f);
     d->prevCount = n(f - 1);
@@ -713,9 +767,10 @@ int sift_hip_warmup(sift_hip_t d) {
     if (rc) return rc;
     rc = build_graphs(d);
     if (rc) return rc;
-    // One blank frame through each graph: first-touch, code-object load.
-    for (int i = 0; i < d->kSlots; i++) {
-        if ((rc = run_frame(d, d->dInput, d->inPitch, SIFT_HIP_F32, nullptr))) return rc;
+    // One blank frame (batch) through each graph: first-touch, code-object load.
+    for (int i = 0; i < d->kSlots * (d->B > 1 ? 2 : 1); i++) {
+        const int nf = i < d->kSlots ? d->B : 1;
+        if ((rc = run_frame(d, d->dInput, d->inPitch, SIFT_HIP_F32, nullptr, nf, d->afs))) return rc;
         if ((rc = finish_frame(d))) return rc;
     }
     d->firstFrame = d->submitted;
@@ -794,6 +849,93 @@ int sift_hip_detect_device(sift_hip_t d, const float* img, size_t stride, void* 
     return sift_hip_detect_device_fmt(d, img, stride, SIFT_HIP_F32, stream);
 }
 
+int sift_hip_set_batch(sift_hip_t d, int frames) {
+    if (!d) return fail(SIFT_HIP_ERR_INVALID, "null handle");
+    if (frames < 1 || frames > kMaxBatch) return fail(SIFT_HIP_ERR_INVALID, "batch size out of range (1..64)");
+    if (d->allocated) return fail(SIFT_HIP_ERR_STATE, "sift_hip_set_batch after sift_hip_warmup");
+    d->B = frames;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_batch_capacity(sift_hip_t d, int* frames) {
+    if (!d || !frames) return fail(SIFT_HIP_ERR_INVALID, "null argument");
+    *frames = d->B;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_detect_batch_device(sift_hip_t d, const void* frames, int n, size_t stride, size_t frame_stride,
+                                 int format, void* stream) {
+    CHECK_HANDLE(d);
+    if (!frames) return fail(SIFT_HIP_ERR_INVALID, "null frames");
+    if (n < 1 || n > d->B) return fail(SIFT_HIP_ERR_INVALID, "frame count outside 1..batch capacity");
+    const int es = format_size(format);
+    if (!es) return fail(SIFT_HIP_ERR_INVALID, "unknown pixel format");
+    const int W = d->cfg.col_width, H = d->cfg.row_width;
+    if (stride == 0) stride = (size_t)es * W;
+    if (stride % es || stride < (size_t)es * W)
+        return fail(SIFT_HIP_ERR_INVALID, "row stride must be a multiple of the pixel size and >= width");
+    if (frame_stride == 0) frame_stride = stride * H;
+    if (n > 1 && frame_stride < stride * (H - 1) + (size_t)es * W)
+        return fail(SIFT_HIP_ERR_INVALID, "frame stride smaller than one frame");
+    if (d->submitted > d->current + 2)
+        return fail(SIFT_HIP_ERR_STATE, "two launch groups already in flight past the current one: sync first");
+    hipStream_t ext = (hipStream_t)stream;
+    if (ext) {
+        HIPCHK(hipEventRecord(d->evIn, ext));
+        HIPCHK(hipStreamWaitEvent(d->stream, d->evIn, 0));
+    }
+    const long long f = d->submitted;
+    int rc = run_frame(d, frames, (int)(stride / es), format, nullptr, n, (long)frame_stride);
+    if (rc) return rc;
+    make_current(d, f);
+    if (ext) {
+        HIPCHK(hipEventRecord(d->evOut, d->stream));
+        HIPCHK(hipStreamWaitEvent(ext, d->evOut, 0));
+    }
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_batch_frames(sift_hip_t d, int* n) {
+    CHECK_HANDLE(d);
+    if (!n) return fail(SIFT_HIP_ERR_INVALID, "null argument");
+    *n = d->current < d->firstFrame ? 0 : d->nfOf[d->cur];
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_batch_results_device(sift_hip_t d, int i, int* count, int* overflow, const float** k3,
+                                  const float** f4, const uint16_t** desc) {
+    CHECK_HANDLE(d);
+    if (d->current < d->firstFrame || i < 0 || i >= d->nfOf[d->cur])
+        return fail(SIFT_HIP_ERR_INVALID, "no such frame in the current batch");
+    const Counters& c = d->hCtr[(size_t)d->cur * d->B + i];
+    const long o = (long)i * d->afs;
+    if (count) *count = (int)std::min<unsigned>(c.final_n, d->kp.capFinal);
+    if (overflow) *overflow = (int)c.overflow;
+    if (k3) *k3 = fptr(d->dKpts3[d->cur], o);
+    if (f4) *f4 = fptr(d->dFeats4[d->cur], o);
+    if (desc) *desc = fptr(d->dDesc[d->cur], o);
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_batch_copy_to_host(sift_hip_t d, int i, float* k3, float* f4, uint16_t* desc, int cap, int* count) {
+    int n = 0;
+    const float *dk = nullptr, *df = nullptr;
+    const uint16_t* dd = nullptr;
+    if (int rc = sift_hip_batch_results_device(d, i, &n, nullptr, &dk, &df, &dd)) return rc;
+    n = std::min(n, cap);
+    if (count) *count = n;
+    hipStream_t s;
+    if (int rc = copy_stream(d, &s)) return rc;
+    HIPCHK(hipStreamWaitEvent(s, d->evFrame[d->cur], 0));
+    if (n > 0) {
+        if (k3) HIPCHK(hipMemcpyAsync(k3, dk, sizeof(float) * 3 * n, hipMemcpyDeviceToHost, s));
+        if (f4) HIPCHK(hipMemcpyAsync(f4, df, sizeof(float) * 4 * n, hipMemcpyDeviceToHost, s));
+        if (desc) HIPCHK(hipMemcpyAsync(desc, dd, sizeof(uint16_t) * 128 * n, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    return SIFT_HIP_OK;
+}
+
 int sift_hip_sync(sift_hip_t d) {
     CHECK_HANDLE(d);
     return finish_frame(d);
@@ -807,7 +949,7 @@ int sift_hip_num_keypoints(sift_hip_t d, int* n) {
 
 int sift_hip_overflow_flags(sift_hip_t d, int* flags) {
     if (!d || !flags) return fail(SIFT_HIP_ERR_INVALID, "null argument");
-    *flags = d->hCtr ? (int)d->hCtr[d->cur].overflow : 0;
+    *flags = d->hCtr ? (int)d->hCtr[(size_t)d->cur * d->B].overflow : 0;
     return SIFT_HIP_OK;
 }
 
@@ -891,7 +1033,7 @@ int sift_hip_debug_gaussian(sift_hip_t d, int o, int layer, float* out) {
 
 int sift_hip_debug_candidates(sift_hip_t d, int* quads, int cap, int* count) {
     CHECK_HANDLE(d);
-    const Counters& c = d->hCtr[d->cur];
+    const Counters& c = d->hCtr[(size_t)d->cur * d->B];
     const int n = (int)std::min<unsigned>(c.cand, d->capCand);
     if (count) *count = (int)c.cand;
     const int m = std::min(n, cap);

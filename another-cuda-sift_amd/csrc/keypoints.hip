@@ -10,6 +10,8 @@
 // descriptor bytes may differ from the oracle by +-1 (tests/test_gpu_parity.py).
 #include <hip/hip_fp16.h>
 
+#include <algorithm>
+
 #include "sift_kernels.h"
 #include "sift_math.h"
 #include "sift_refine.h"
@@ -34,15 +36,26 @@ constexpr float kOriPeakRatio = 0.8f;
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_refine(PyrDesc pyr, const uint2* __restrict__ cand, unsigned capCand,
                                                 Counters* __restrict__ ctr, uint32_t* __restrict__ bitmap,
-                                                RefKpt* __restrict__ out, KeypointParams kp) {
+                                                RefKpt* __restrict__ out, KeypointParams kp, long fs) {
+    const long foff = blockIdx.y * fs;  // frame blockIdx.y
+    cand = fptr(cand, foff);
+    ctr = fptr(ctr, foff);
+    bitmap = fptr(bitmap, foff);
+    out = fptr(out, foff);
     const unsigned n = min(ctr->cand, capCand);
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        refine_candidate(pyr, cand[i], ctr, bitmap, out, kp);
+        refine_candidate(pyr, cand[i], ctr, bitmap, out, kp, foff);
 }
 
+// Workgroups per frame of the keypoint kernels: a single frame gets `one`
+// (>= its usual item count, one item per workgroup); a batch shares about
+// `one` * 2 among its frames, each workgroup looping over several items.
+static int per_frame_blocks(int one, int nf) { return nf <= 1 ? one : std::max(one / 4, 2 * one / nf); }
+
 void launch_refine(const PyrDesc& pyr, const uint2* cand, unsigned capCand, Counters* ctr, uint32_t* bitmap,
-                   RefKpt* out, const KeypointParams& kp, hipStream_t s) {
-    hipLaunchKernelGGL(k_refine, dim3(512), dim3(256), 0, s, pyr, cand, capCand, ctr, bitmap, out, kp);
+                   RefKpt* out, const KeypointParams& kp, const Frames& fr, hipStream_t s) {
+    hipLaunchKernelGGL(k_refine, dim3(per_frame_blocks(512, fr.nf), fr.nf), dim3(256), 0, s, pyr, cand, capCand, ctr,
+                       bitmap, out, kp, fr.stride);
 }
 
 // ---------------------------------------------------------------------------
@@ -77,8 +90,13 @@ __device__ __forceinline__ RefKpt load_ref(const RefKpt* in, unsigned k) {  // s
 
 __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* __restrict__ in,
                                                     Counters* __restrict__ ctr, OriKpt* __restrict__ out,
-                                                    uint32_t* __restrict__ bitmap, KeypointParams kp) {
+                                                    uint32_t* __restrict__ bitmap, KeypointParams kp, long fs) {
     __shared__ float chunk[64];
+    const long foff = blockIdx.y * fs;  // frame blockIdx.y
+    in = fptr(in, foff);
+    ctr = fptr(ctr, foff);
+    out = fptr(out, foff);
+    bitmap = fptr(bitmap, foff);
     __shared__ float s_exptab[64];
     const int lane = threadIdx.x;
     s_exptab[lane] = c_exptab[lane];
@@ -93,7 +111,7 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
             const long bit = g.bitBase + ((long)(layer - 1) * g.H + r) * g.W + c;
             atomicAnd(&bitmap[bit >> 5], ~(1u << (bit & 31)));
         }
-        const float* img = g.base + (size_t)layer * g.planeStride;
+        const float* img = fptr(g.base, foff) + (size_t)layer * g.planeStride;
         const int pitch = g.pitch, W = g.W, H = g.H;
         const float scl_octv = kpt.size * 0.5f / (float)(1 << o);
         const int radius = cv_round(kOriRadius * scl_octv);
@@ -234,8 +252,9 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
 }
 
 void launch_orientation(const PyrDesc& pyr, const RefKpt* in, Counters* ctr, OriKpt* out, uint32_t* bitmap,
-                        const KeypointParams& kp, hipStream_t s) {
-    hipLaunchKernelGGL(k_orientation, dim3(8192), dim3(64), 0, s, pyr, in, ctr, out, bitmap, kp);
+                        const KeypointParams& kp, const Frames& fr, hipStream_t s) {
+    hipLaunchKernelGGL(k_orientation, dim3(per_frame_blocks(8192, fr.nf), fr.nf), dim3(64), 0, s, pyr, in, ctr, out,
+                       bitmap, kp, fr.stride);
 }
 
 // ---------------------------------------------------------------------------
@@ -246,9 +265,13 @@ void launch_orientation(const PyrDesc& pyr, const RefKpt* in, Counters* ctr, Ori
 // Reference: keeps the first numFeatures in octave order (CudaMemcpyUtils.cu:38-49).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(1024) void k_select(const OriKpt* __restrict__ kpts, Counters* __restrict__ ctr,
-                                                 unsigned* __restrict__ zero_range, KeypointParams kp) {
+                                                 unsigned* __restrict__ zero_range, KeypointParams kp, long fs) {
     __shared__ unsigned hist[256];
     __shared__ unsigned s_prefix, s_k;
+    const long foff = blockIdx.y * fs;  // frame blockIdx.y
+    kpts = fptr(kpts, foff);
+    ctr = fptr(ctr, foff);
+    zero_range = fptr(zero_range, foff);
     const unsigned n = min(ctr->oriented, kp.capOriented);
     const int tid = threadIdx.x;
     for (int i = tid; i < 2 * kRangeSlots; i += 1024) zero_range[i] = 0u;  // next frame's range keys
@@ -290,8 +313,9 @@ __global__ __launch_bounds__(1024) void k_select(const OriKpt* __restrict__ kpts
     if (tid == 0) ctr->thr_bits = s_prefix;
 }
 
-void launch_select(const OriKpt* kpts, Counters* ctr, unsigned* zero_range, const KeypointParams& kp, hipStream_t s) {
-    hipLaunchKernelGGL(k_select, dim3(1), dim3(1024), 0, s, kpts, ctr, zero_range, kp);
+void launch_select(const OriKpt* kpts, Counters* ctr, unsigned* zero_range, const KeypointParams& kp, const Frames& fr,
+                   hipStream_t s) {
+    hipLaunchKernelGGL(k_select, dim3(1, fr.nf), dim3(1024), 0, s, kpts, ctr, zero_range, kp, fr.stride);
 }
 
 // ---------------------------------------------------------------------------
@@ -302,7 +326,12 @@ void launch_select(const OriKpt* kpts, Counters* ctr, unsigned* zero_range, cons
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_bucket_count(const OriKpt* __restrict__ kpts, const Counters* __restrict__ ctr,
                                                       unsigned* __restrict__ bcount, int* __restrict__ slot,
-                                                      KeypointParams kp) {
+                                                      KeypointParams kp, long fs) {
+    const long foff = blockIdx.y * fs;  // frame blockIdx.y
+    kpts = fptr(kpts, foff);
+    ctr = fptr(ctr, foff);
+    bcount = fptr(bcount, foff);
+    slot = fptr(slot, foff);
     const unsigned n = min(ctr->oriented, kp.capOriented);
     const float thr = __uint_as_float(ctr->thr_bits);
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -312,13 +341,17 @@ __global__ __launch_bounds__(256) void k_bucket_count(const OriKpt* __restrict__
 }
 
 void launch_bucket_count(const OriKpt* kpts, const Counters* ctr, unsigned* bcount, int* slot,
-                         const KeypointParams& kp, hipStream_t s) {
-    hipLaunchKernelGGL(k_bucket_count, dim3(256), dim3(256), 0, s, kpts, ctr, bcount, slot, kp);
+                         const KeypointParams& kp, const Frames& fr, hipStream_t s) {
+    hipLaunchKernelGGL(k_bucket_count, dim3(256, fr.nf), dim3(256), 0, s, kpts, ctr, bcount, slot, kp, fr.stride);
 }
 
 __global__ __launch_bounds__(1024) void k_bucket_scan(const unsigned* __restrict__ bcount, unsigned* __restrict__ boff,
-                                                      Counters* __restrict__ ctr, KeypointParams kp) {
+                                                      Counters* __restrict__ ctr, KeypointParams kp, long fs) {
     __shared__ unsigned wsum[16];
+    const long foff = blockIdx.y * fs;  // frame blockIdx.y
+    bcount = fptr(bcount, foff);
+    boff = fptr(boff, foff);
+    ctr = fptr(ctr, foff);
     __shared__ unsigned carry_s;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (tid == 0) carry_s = 0;
@@ -352,13 +385,20 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const unsigned* __restrict
     }
 }
 
-void launch_bucket_scan(unsigned* bcount, unsigned* boff, Counters* ctr, const KeypointParams& kp, hipStream_t s) {
-    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(1024), 0, s, bcount, boff, ctr, kp);
+void launch_bucket_scan(unsigned* bcount, unsigned* boff, Counters* ctr, const KeypointParams& kp, const Frames& fr,
+                        hipStream_t s) {
+    hipLaunchKernelGGL(k_bucket_scan, dim3(1, fr.nf), dim3(1024), 0, s, bcount, boff, ctr, kp, fr.stride);
 }
 
 __global__ __launch_bounds__(256) void k_bucket_scatter(const OriKpt* __restrict__ kpts, const Counters* __restrict__ ctr,
                                                         const unsigned* __restrict__ boff, const int* __restrict__ slot,
-                                                        int* __restrict__ order, KeypointParams kp) {
+                                                        int* __restrict__ order, KeypointParams kp, long fs) {
+    const long foff = blockIdx.y * fs;  // frame blockIdx.y
+    kpts = fptr(kpts, foff);
+    ctr = fptr(ctr, foff);
+    boff = fptr(boff, foff);
+    slot = fptr(slot, foff);
+    order = fptr(order, foff);
     const unsigned n = min(ctr->oriented, kp.capOriented);
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int s = slot[i];
@@ -367,8 +407,9 @@ __global__ __launch_bounds__(256) void k_bucket_scatter(const OriKpt* __restrict
 }
 
 void launch_bucket_scatter(const OriKpt* kpts, const Counters* ctr, const unsigned* boff, const int* slot, int* order,
-                           const KeypointParams& kp, hipStream_t s) {
-    hipLaunchKernelGGL(k_bucket_scatter, dim3(256), dim3(256), 0, s, kpts, ctr, boff, slot, order, kp);
+                           const KeypointParams& kp, const Frames& fr, hipStream_t s) {
+    hipLaunchKernelGGL(k_bucket_scatter, dim3(256, fr.nf), dim3(256), 0, s, kpts, ctr, boff, slot, order, kp,
+                       fr.stride);
 }
 
 // ---------------------------------------------------------------------------
@@ -384,10 +425,18 @@ void launch_bucket_scatter(const OriKpt* kpts, const Counters* ctr, const unsign
 __global__ __launch_bounds__(1024) void k_order(const OriKpt* __restrict__ kpts, Counters* __restrict__ ctr,
                                                 unsigned* __restrict__ zero_range, unsigned* __restrict__ bcount,
                                                 unsigned* __restrict__ boff, int* __restrict__ slot,
-                                                int* __restrict__ order, KeypointParams kp) {
+                                                int* __restrict__ order, KeypointParams kp, long fs) {
     extern __shared__ unsigned s_bucket[];  // counts, then exclusive offsets
     __shared__ unsigned hist[256], wsum[16];
     __shared__ unsigned s_prefix, s_k;
+    const long foff = blockIdx.y * fs;  // frame blockIdx.y
+    kpts = fptr(kpts, foff);
+    ctr = fptr(ctr, foff);
+    zero_range = fptr(zero_range, foff);
+    bcount = fptr(bcount, foff);
+    boff = fptr(boff, foff);
+    slot = fptr(slot, foff);
+    order = fptr(order, foff);
     const unsigned n = min(ctr->oriented, kp.capOriented);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nb = kp.numBuckets;
@@ -494,10 +543,10 @@ __global__ __launch_bounds__(1024) void k_order(const OriKpt* __restrict__ kpts,
 }
 
 bool launch_order(const OriKpt* kpts, Counters* ctr, unsigned* zero_range, unsigned* bcount, unsigned* boff, int* slot,
-                  int* order, const KeypointParams& kp, hipStream_t s) {
+                  int* order, const KeypointParams& kp, const Frames& fr, hipStream_t s) {
     if (kp.numBuckets > kOrderMaxBuckets) return false;
-    hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), sizeof(unsigned) * (size_t)kp.numBuckets, s, kpts, ctr,
-                       zero_range, bcount, boff, slot, order, kp);
+    hipLaunchKernelGGL(k_order, dim3(1, fr.nf), dim3(1024), sizeof(unsigned) * (size_t)kp.numBuckets, s, kpts, ctr,
+                       zero_range, bcount, boff, slot, order, kp, fr.stride);
     return true;
 }
 
@@ -505,7 +554,7 @@ bool launch_order(const OriKpt* kpts, Counters* ctr, unsigned* zero_range, unsig
 // octave scale, angle flip 360 - angle) and the head of calcSIFTDescriptor
 // (cos/sin / hist_width, radius clamped to the image diagonal), computed once
 // per keypoint here so the descriptor workgroup starts from scalar loads.
-__device__ DescJob make_desc_job(const PyrDesc& pyr, const OriKpt& kpt) {
+__device__ DescJob make_desc_job(const PyrDesc& pyr, const OriKpt& kpt, long foff) {
     DescJob j;
     int octave = kpt.octave & 255;
     const int layer = (kpt.octave >> 8) & 255;
@@ -514,7 +563,7 @@ __device__ DescJob make_desc_job(const PyrDesc& pyr, const OriKpt& kpt) {
     const float size = kpt.size * scale;
     const float ptfx = kpt.x * scale, ptfy = kpt.y * scale;
     const OctGeom& g = pyr.oct[octave - pyr.firstOctave];
-    j.img = g.base + (size_t)layer * g.planeStride;
+    j.img = fptr(g.base, foff) + (size_t)layer * g.planeStride;
     j.pitch = g.pitch;
     j.rows = g.H;
     j.cols = g.W;
@@ -543,7 +592,16 @@ __global__ __launch_bounds__(256) void k_bucket_rank(PyrDesc pyr, const OriKpt* 
                                                      const unsigned* __restrict__ boff, const int* __restrict__ order,
                                                      const Counters* __restrict__ ctr, DescJob* __restrict__ jobs,
                                                      float* __restrict__ kpts3, float* __restrict__ feats4,
-                                                     KeypointParams kp) {
+                                                     KeypointParams kp, long fs) {
+    const long foff = blockIdx.y * fs;  // frame blockIdx.y
+    kpts = fptr(kpts, foff);
+    bcount = fptr(bcount, foff);
+    boff = fptr(boff, foff);
+    order = fptr(order, foff);
+    ctr = fptr(ctr, foff);
+    jobs = fptr(jobs, foff);
+    kpts3 = fptr(kpts3, foff);
+    feats4 = fptr(feats4, foff);
     const int lane = threadIdx.x & 63;
     const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int nwaves = gridDim.x * 4;
@@ -569,7 +627,7 @@ __global__ __launch_bounds__(256) void k_bucket_rank(PyrDesc pyr, const OriKpt* 
             const unsigned pos = base + rank;
             if (e < cnt && pos < cap) {
                 const OriKpt k = kpts[idx];
-                jobs[pos] = make_desc_job(pyr, k);
+                jobs[pos] = make_desc_job(pyr, k, foff);
                 kpts3[3 * (size_t)pos + 0] = k.x;
                 kpts3[3 * (size_t)pos + 1] = k.y;
                 kpts3[3 * (size_t)pos + 2] = (float)((k.octave >> 8) & 255);
@@ -582,9 +640,9 @@ __global__ __launch_bounds__(256) void k_bucket_rank(PyrDesc pyr, const OriKpt* 
 
 void launch_bucket_rank(const PyrDesc& pyr, const OriKpt* kpts, unsigned* bcount, const unsigned* boff,
                         const int* order, const Counters* ctr, DescJob* jobs, float* kpts3, float* feats4,
-                        const KeypointParams& kp, hipStream_t s) {
-    hipLaunchKernelGGL(k_bucket_rank, dim3(256), dim3(256), 0, s, pyr, kpts, bcount, boff, order, ctr, jobs, kpts3,
-                       feats4, kp);
+                        const KeypointParams& kp, const Frames& fr, hipStream_t s) {
+    hipLaunchKernelGGL(k_bucket_rank, dim3(per_frame_blocks(256, fr.nf), fr.nf), dim3(256), 0, s, pyr, kpts, bcount,
+                       boff, order, ctr, jobs, kpts3, feats4, kp, fr.stride);
 }
 
 }  // namespace sift_amd

@@ -29,7 +29,9 @@ __device__ __forceinline__ void up_coeff(int d, int slen, int& s, float& a0, flo
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_upsample2x(const T* __restrict__ src, int spitch, int W, int H,
-                                                    float* __restrict__ dst, int dpitch) {
+                                                    float* __restrict__ dst, int dpitch, long sfs, long dfs) {
+    src = fptr(src, blockIdx.z * sfs);  // frame blockIdx.z
+    dst = fptr(dst, blockIdx.z * dfs);
     const int x = blockIdx.x * 64 + (threadIdx.x & 63);
     const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
     if (x >= 2 * W || y >= 2 * H) return;
@@ -45,14 +47,16 @@ __global__ __launch_bounds__(256) void k_upsample2x(const T* __restrict__ src, i
     dst[(size_t)y * dpitch + x] = h0 * ay0 + h1 * ay1;
 }
 
-void launch_upsample2x(const float* src, int spitch, int W, int H, float* dst, int dpitch, hipStream_t s) {
-    dim3 grid((2 * W + 63) / 64, (2 * H + 3) / 4);
-    hipLaunchKernelGGL(k_upsample2x<float>, grid, dim3(256), 0, s, src, spitch, W, H, dst, dpitch);
+void launch_upsample2x(const float* src, int spitch, int W, int H, float* dst, int dpitch, const Frames& fr, long sfs,
+                       hipStream_t s) {
+    dim3 grid((2 * W + 63) / 64, (2 * H + 3) / 4, fr.nf);
+    hipLaunchKernelGGL(k_upsample2x<float>, grid, dim3(256), 0, s, src, spitch, W, H, dst, dpitch, sfs, fr.stride);
 }
 
-void launch_upsample2x_u8(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, hipStream_t s) {
-    dim3 grid((2 * W + 63) / 64, (2 * H + 3) / 4);
-    hipLaunchKernelGGL(k_upsample2x<uint8_t>, grid, dim3(256), 0, s, src, spitch, W, H, dst, dpitch);
+void launch_upsample2x_u8(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, const Frames& fr,
+                          long sfs, hipStream_t s) {
+    dim3 grid((2 * W + 63) / 64, (2 * H + 3) / 4, fr.nf);
+    hipLaunchKernelGGL(k_upsample2x<uint8_t>, grid, dim3(256), 0, s, src, spitch, W, H, dst, dpitch, sfs, fr.stride);
 }
 
 // ---------------------------------------------------------------------------
@@ -89,6 +93,8 @@ struct BlurJob {
     unsigned* range_keys;
     Counters* zero_ctr;
     int spitch, sstep, W, H, dpitch, tilesX, ntiles;
+    int nf;         // frames; the launch has nf * ntiles tiles of this job
+    long sfs, dfs;  // byte strides between frames: source; dst / copy_out / range_keys / zero_ctr
     Taps taps;
 };
 
@@ -97,7 +103,8 @@ constexpr int blur_lds_floats() {
     return (BLUR_TW + 2 * R + 3 & ~3) * (BLUR_TH + 2 * R) + 4;
 }
 
-// Tile `blk` of job J (64 x 32 outputs) with LDS `in`.  T = float, or uint8_t
+// Tile `blk` of job J's nf * ntiles (64 x 32 outputs; frame-major, XCD order)
+// with LDS `in`.  T = float, or uint8_t
 // for a caller's 8-bit frame read by the frame's first blur (OpenCV converts
 // CV_8U to float exactly, so the planes are those of the float frame with the
 // same values).
@@ -106,11 +113,13 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
     constexpr int IW = (BLUR_TW + 2 * R + 3) & ~3;  // row stride, multiple of 4 floats
     constexpr int IH = BLUR_TH + 2 * R;
     constexpr int NW = (2 * R + 4 + 3) / 4;          // float4 reads per row window
-    const T* __restrict__ src = static_cast<const T*>(J.src);
-    float* __restrict__ dst = J.dst;
-    float* __restrict__ copy_out = J.copy_out;
-    unsigned* __restrict__ range_keys = J.range_keys;
-    Counters* __restrict__ zero_ctr = J.zero_ctr;
+    const int t = xcd_tile(blk, J.ntiles * J.nf);
+    const int f = t / J.ntiles, tile = t - f * J.ntiles;
+    const T* __restrict__ src = fptr(static_cast<const T*>(J.src), f * J.sfs);
+    float* __restrict__ dst = fptr(J.dst, f * J.dfs);
+    float* __restrict__ copy_out = J.copy_out ? fptr(J.copy_out, f * J.dfs) : nullptr;
+    unsigned* __restrict__ range_keys = J.range_keys ? fptr(J.range_keys, f * J.dfs) : nullptr;
+    Counters* __restrict__ zero_ctr = J.zero_ctr ? fptr(J.zero_ctr, f * J.dfs) : nullptr;
     const int spitch = J.spitch, sstep = J.sstep, W = J.W, H = J.H, dpitch = J.dpitch;
     const Taps& taps = J.taps;
     // Row-pass results (`mid`, pitch IW) overwrite their own input row of
@@ -118,7 +127,6 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
     // one wave, whose LDS reads complete before its writes (in-order LDS per
     // wave), so one tile of LDS serves both passes (more workgroups per CU).
     float* const mid = in;
-    const int tile = xcd_tile(blk, J.ntiles);
     const int x0 = (tile % J.tilesX) * BLUR_TW, y0 = (tile / J.tilesX) * BLUR_TH;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // The frame's first blur also zeroes the frame counters (no memset node).
@@ -289,7 +297,7 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
             }
             __syncthreads();
             if (tid == 0) {  // spread over kRangeSlots address pairs: no single hot atomic
-                unsigned* slot = range_keys + 2 * (blk % kRangeSlots);
+                unsigned* slot = range_keys + 2 * (tile % kRangeSlots);
                 atomicMax(slot, range_key(fmaxf(fmaxf(mid[0], mid[1]), fmaxf(mid[2], mid[3]))));
                 atomicMax(slot + 1, range_key(fmaxf(fmaxf(mid[4], mid[5]), fmaxf(mid[6], mid[7]))));
             }
@@ -312,15 +320,19 @@ template <int RA, int RB>
 __global__ __launch_bounds__(256) void k_blur2(BlurJob A, BlurJob B) {
     constexpr int NA = blur_lds_floats<RA>(), NB = blur_lds_floats<RB>();
     __shared__ __attribute__((aligned(16))) float in[NA > NB ? NA : NB];
-    if ((int)blockIdx.x < A.ntiles)
+    const int na = A.ntiles * A.nf;
+    if ((int)blockIdx.x < na)
         blur_tile<RA, float>(A, blockIdx.x, in);
     else
-        blur_tile<RB, float>(B, blockIdx.x - A.ntiles, in);
+        blur_tile<RB, float>(B, blockIdx.x - na, in);
 }
 
 static BlurJob make_job(const void* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, float* copy_out,
-                        const Taps& taps, unsigned* range_keys, Counters* zero_ctr) {
+                        const Taps& taps, unsigned* range_keys, Counters* zero_ctr, const Frames& fr, long sfs) {
     BlurJob j;
+    j.nf = fr.nf;
+    j.sfs = sfs;
+    j.dfs = fr.stride;
     j.src = src;
     j.dst = dst;
     j.copy_out = copy_out;
@@ -341,7 +353,7 @@ using BlurLaunch = void (*)(const BlurJob&, hipStream_t);
 
 template <int R>
 void blur_launch_r(const BlurJob& j, hipStream_t s) {
-    hipLaunchKernelGGL(k_blur<R>, dim3(j.ntiles), dim3(256), 0, s, j);
+    hipLaunchKernelGGL(k_blur<R>, dim3(j.ntiles * j.nf), dim3(256), 0, s, j);
 }
 
 template <int... Rs>
@@ -354,7 +366,7 @@ static const std::array<BlurLaunch, kMaxTaps / 2> kBlurTable = blur_table(std::m
 // 5, 6, 8, 10, 13), larger radius first.  Other pairs launch separately.
 template <int RA, int RB>
 void blur2_launch(const BlurJob& a, const BlurJob& b, hipStream_t s) {
-    hipLaunchKernelGGL((k_blur2<RA, RB>), dim3(a.ntiles + b.ntiles), dim3(256), 0, s, a, b);
+    hipLaunchKernelGGL((k_blur2<RA, RB>), dim3(a.ntiles * a.nf + b.ntiles * b.nf), dim3(256), 0, s, a, b);
 }
 bool launch_blur_pair_jobs(const BlurJob& a, const BlurJob& b, hipStream_t s) {
     const int ra = a.taps.n >> 1, rb = b.taps.n >> 1;
@@ -381,11 +393,11 @@ bool launch_blur_pair_jobs(const BlurJob& a, const BlurJob& b, hipStream_t s) {
     return false;
 }
 
-bool launch_blur_pair(const BlurDesc& a, const BlurDesc& b, hipStream_t s) {
+bool launch_blur_pair(const BlurDesc& a, const BlurDesc& b, const Frames& fr, hipStream_t s) {
     return launch_blur_pair_jobs(make_job(a.src, a.spitch, a.sstep, a.W, a.H, a.dst, a.dpitch, a.copy_out, *a.taps,
-                                          nullptr, nullptr),
+                                          nullptr, nullptr, fr, fr.stride),
                                  make_job(b.src, b.spitch, b.sstep, b.W, b.H, b.dst, b.dpitch, b.copy_out, *b.taps,
-                                          nullptr, nullptr),
+                                          nullptr, nullptr, fr, fr.stride),
                                  s);
 }
 
@@ -393,29 +405,34 @@ bool launch_blur_pair(const BlurDesc& a, const BlurDesc& b, hipStream_t s) {
 // radii (sigma 1.6: 13 taps without upscale); any other radius converts the
 // frame to float first (k_u8_to_f32) and runs the float blur.
 bool launch_blur_u8(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, const Taps& taps,
-                    hipStream_t s, unsigned* range_keys, Counters* zero_ctr) {
-    const BlurJob j = make_job(src, spitch, 1, W, H, dst, dpitch, nullptr, taps, range_keys, zero_ctr);
+                    const Frames& fr, long sfs, hipStream_t s, unsigned* range_keys, Counters* zero_ctr) {
+    const BlurJob j = make_job(src, spitch, 1, W, H, dst, dpitch, nullptr, taps, range_keys, zero_ctr, fr, sfs);
     switch (taps.n >> 1) {
-        case 5: hipLaunchKernelGGL((k_blur<5, uint8_t>), dim3(j.ntiles), dim3(256), 0, s, j); return true;
-        case 6: hipLaunchKernelGGL((k_blur<6, uint8_t>), dim3(j.ntiles), dim3(256), 0, s, j); return true;
+        case 5: hipLaunchKernelGGL((k_blur<5, uint8_t>), dim3(j.ntiles * j.nf), dim3(256), 0, s, j); return true;
+        case 6: hipLaunchKernelGGL((k_blur<6, uint8_t>), dim3(j.ntiles * j.nf), dim3(256), 0, s, j); return true;
         default: return false;
     }
 }
 
 __global__ __launch_bounds__(256) void k_u8_to_f32(const uint8_t* __restrict__ src, int spitch, int W, int H,
-                                                   float* __restrict__ dst, int dpitch) {
+                                                   float* __restrict__ dst, int dpitch, long sfs, long dfs) {
+    src = fptr(src, blockIdx.z * sfs);
+    dst = fptr(dst, blockIdx.z * dfs);
     const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
     if (x < W) dst[(size_t)y * dpitch + x] = (float)src[(size_t)y * spitch + x];
 }
 
-void launch_u8_to_f32(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, hipStream_t s) {
-    hipLaunchKernelGGL(k_u8_to_f32, dim3((W + 255) / 256, H), dim3(256), 0, s, src, spitch, W, H, dst, dpitch);
+void launch_u8_to_f32(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, const Frames& fr,
+                      long sfs, hipStream_t s) {
+    hipLaunchKernelGGL(k_u8_to_f32, dim3((W + 255) / 256, H, fr.nf), dim3(256), 0, s, src, spitch, W, H, dst, dpitch,
+                       sfs, fr.stride);
 }
 
 void launch_blur(const float* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, float* copy_out,
-                 const Taps& taps, hipStream_t s, unsigned* range_keys, Counters* zero_ctr) {
+                 const Taps& taps, const Frames& fr, long sfs, hipStream_t s, unsigned* range_keys,
+                 Counters* zero_ctr) {
     const int r = taps.n >> 1;  // 1 .. kMaxTaps/2 (taps.n >= 3 by construction)
-    kBlurTable[r - 1](make_job(src, spitch, sstep, W, H, dst, dpitch, copy_out, taps, range_keys, zero_ctr), s);
+    kBlurTable[r - 1](make_job(src, spitch, sstep, W, H, dst, dpitch, copy_out, taps, range_keys, zero_ctr, fr, sfs), s);
 }
 
 // ---------------------------------------------------------------------------
@@ -435,8 +452,11 @@ constexpr int EX_LIST = 512;  // per-workgroup candidate list (LDS)
 // LT = compile-time layer count (1..6), or 0 for the generic runtime-L path.
 template <int LT>
 __global__ __launch_bounds__(256) void k_extrema(OctGeom g, int Lrt, int o, float thr, uint2* __restrict__ cand,
-                                                 Counters* __restrict__ ctr, unsigned cap) {
+                                                 Counters* __restrict__ ctr, unsigned cap, long fs) {
     extern __shared__ float dog[];  // (L+2) planes of EX_SH x EX_SW
+    g.base = fptr(g.base, blockIdx.z * fs);  // frame blockIdx.z
+    cand = fptr(cand, blockIdx.z * fs);
+    ctr = fptr(ctr, blockIdx.z * fs);
     const int L = LT > 0 ? LT : Lrt;
     const int tid = threadIdx.x;
     const int tile = xcd_tile(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
@@ -589,16 +609,15 @@ __device__ __forceinline__ float dpp_right_or(float own, float v) {  // lane i <
 }
 
 // One workgroup = 4 waves stacked vertically over a 256-column strip: block
-// `blk` of the octave's `nblk` (strips across, xcd_tile order).
+// `tile` of the octave (strips across; the caller picks the XCD order).
 template <int LT, int EX4_TR, int EX4_AHEAD>
 __device__ __forceinline__ void extrema_block(const OctGeom& g, int o, float thr, uint2* __restrict__ cand,
-                                              Counters* __restrict__ ctr, unsigned cap, int blk, int strips,
-                                              int nblk, uint2* s_list, unsigned& s_cnt, unsigned& s_base) {
+                                              Counters* __restrict__ ctr, unsigned cap, int tile, int strips,
+                                              uint2* s_list, unsigned& s_cnt, unsigned& s_base) {
     constexpr int NG = LT + 3, ND = LT + 2;
     static_assert(4 * LT <= 31, "hit bits per row");
     typedef float f4 __attribute__((ext_vector_type(4)));
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int tile = xcd_tile(blk, nblk);
     const int x0 = (tile % strips) * EX4_COLS, y0 = ((tile / strips) * 4 + wave) * EX4_TR;
     const int W = g.W, H = g.H, pitch = g.pitch;
     const int xl = x0 + 4 * lane;
@@ -743,7 +762,7 @@ __device__ __forceinline__ void extrema_block(const OctGeom& g, int o, float thr
 // latency-bound and want waves; tools/kernel_bench: 1920x1200 16.7 us at 6
 // rows vs 19.8 at 2; 960x600 9.2 us at 2 rows vs 10.8 at 6).
 struct ExtremaPlan {
-    int start[kMaxOctaves + 1];
+    int start[kMaxOctaves + 1];  // start[nOct] = blocks per frame
     int strips[kMaxOctaves];
     int tall[kMaxOctaves];
 };
@@ -751,29 +770,39 @@ struct ExtremaPlan {
 template <int LT>
 __global__ __launch_bounds__(256) void k_extrema_all(PyrDesc pyr, ExtremaPlan plan, float thr,
                                                      uint2* __restrict__ cand, Counters* __restrict__ ctr,
-                                                     unsigned cap) {
+                                                     unsigned cap, long fs) {
     __shared__ unsigned s_cnt, s_base;
     __shared__ uint2 s_list[EX4_LIST];
-    const int b = blockIdx.x;
+    // Frame-major block order over all frames, XCD-aware: each XCD takes a
+    // contiguous run of (frame, octave, strip block), so vertically adjacent
+    // blocks (shared halo rows) meet in the same L2.
+    const int per = plan.start[pyr.nOct];
+    const int t = xcd_tile(blockIdx.x, gridDim.x);
+    const int f = t / per, b = t - f * per;
     int o = 0;
     while (o + 1 < pyr.nOct && b >= plan.start[o + 1]) o++;
-    const int blk = b - plan.start[o], nblk = plan.start[o + 1] - plan.start[o];
+    OctGeom g = pyr.oct[o];
+    g.base = fptr(g.base, f * fs);
+    cand = fptr(cand, f * fs);
+    ctr = fptr(ctr, f * fs);
+    const int blk = b - plan.start[o];
     if (plan.tall[o])
-        extrema_block<LT, 6, 2>(pyr.oct[o], o, thr, cand, ctr, cap, blk, plan.strips[o], nblk, s_list, s_cnt, s_base);
+        extrema_block<LT, 6, 2>(g, o, thr, cand, ctr, cap, blk, plan.strips[o], s_list, s_cnt, s_base);
     else
-        extrema_block<LT, 2, 2>(pyr.oct[o], o, thr, cand, ctr, cap, blk, plan.strips[o], nblk, s_list, s_cnt, s_base);
+        extrema_block<LT, 2, 2>(g, o, thr, cand, ctr, cap, blk, plan.strips[o], s_list, s_cnt, s_base);
 }
 
 // Octave o alone, for L > 6 (LDS-staged k_extrema).
 void launch_extrema(const PyrDesc& pyr, int o, float threshold, uint2* cand, Counters* ctr, unsigned cap,
-                    hipStream_t s) {
+                    const Frames& fr, hipStream_t s) {
     const OctGeom& g = pyr.oct[o];
-    dim3 grid((g.W + EX_TW - 1) / EX_TW, (g.H + EX_TH - 1) / EX_TH);
+    dim3 grid((g.W + EX_TW - 1) / EX_TW, (g.H + EX_TH - 1) / EX_TH, fr.nf);
     const size_t lds = sizeof(float) * (size_t)(pyr.L + 2) * EX_SH * EX_SW;
-    hipLaunchKernelGGL(k_extrema<0>, grid, dim3(256), lds, s, g, pyr.L, o, threshold, cand, ctr, cap);
+    hipLaunchKernelGGL(k_extrema<0>, grid, dim3(256), lds, s, g, pyr.L, o, threshold, cand, ctr, cap, fr.stride);
 }
 
-bool launch_extrema_all(const PyrDesc& pyr, float threshold, uint2* cand, Counters* ctr, unsigned cap, hipStream_t s) {
+bool launch_extrema_all(const PyrDesc& pyr, float threshold, uint2* cand, Counters* ctr, unsigned cap,
+                        const Frames& fr, hipStream_t s) {
     if (pyr.L < 1 || pyr.L > 6) return false;
     ExtremaPlan plan{};
     int total = 0;
@@ -790,7 +819,10 @@ bool launch_extrema_all(const PyrDesc& pyr, float threshold, uint2* cand, Counte
     plan.start[pyr.nOct] = total;
     switch (pyr.L) {
 #define SIFT_EX_CASE(LV) \
-    case LV: hipLaunchKernelGGL(k_extrema_all<LV>, dim3(total), dim3(256), 0, s, pyr, plan, threshold, cand, ctr, cap); break;
+    case LV:                                                                                                    \
+        hipLaunchKernelGGL(k_extrema_all<LV>, dim3(total * fr.nf), dim3(256), 0, s, pyr, plan, threshold, cand, ctr, \
+                           cap, fr.stride);                                                                         \
+        break;
         SIFT_EX_CASE(1)
         SIFT_EX_CASE(2)
         SIFT_EX_CASE(3)

@@ -8,6 +8,22 @@ namespace sift_amd {
 
 constexpr int kMaxOctaves = 16;
 constexpr int kMaxTaps = 63;  // r <= 31
+constexpr int kMaxBatch = 64;  // frames per launch
+
+// Frame batches: every launch processes `nf` frames.  Each frame owns one
+// "frame arena" (pyramid, candidate / keypoint lists, counters, result slots)
+// and the arenas sit at a fixed byte stride, so frame f's copy of any buffer
+// is the frame-0 pointer + f * stride.  Kernels take the frame from the grid
+// (blockIdx.y, or the XCD-ordered block index for the tiled pyramid kernels).
+// nf = 1 is the single-frame pipeline.
+struct Frames {
+    int nf;
+    long stride;  // bytes between consecutive frames' arenas
+};
+template <class T>
+__host__ __device__ __forceinline__ T* fptr(T* p, long off) {
+    return reinterpret_cast<T*>(reinterpret_cast<uintptr_t>(p) + off);
+}
 
 // Separable Gaussian taps (host-computed, OpenCV getGaussianKernel bit-exact
 // recipe) passed by value so they live in the kernarg segment (scalar loads).
@@ -61,7 +77,9 @@ struct Counters {
 };
 
 // --- launch wrappers (implemented in pyramid.hip / keypoints.hip / match.hip) --
-void launch_upsample2x(const float* src, int spitch, int W, int H, float* dst, int dpitch, hipStream_t s);
+// sfs: byte stride between the nf source frames (the caller's frames or arenas).
+void launch_upsample2x(const float* src, int spitch, int W, int H, float* dst, int dpitch, const Frames& fr, long sfs,
+                       hipStream_t s);
 // Pixel range of octave 0 / plane 0 (every later plane is a convex combination
 // of it), accumulated by the initial blur as kRangeSlots pairs of
 // order-preserving keys {max(v), max(-v)} (atomicMax spread over slots).
@@ -69,7 +87,8 @@ constexpr int kRangeSlots = 256;
 // range_keys (nullable): 2 * kRangeSlots keys, zeroed before the launch.
 // zero_ctr (nullable): counters to zero (the frame's first blur).
 void launch_blur(const float* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, float* copy_out,
-                 const Taps& taps, hipStream_t s, unsigned* range_keys = nullptr, Counters* zero_ctr = nullptr);
+                 const Taps& taps, const Frames& fr, long sfs, hipStream_t s, unsigned* range_keys = nullptr,
+                 Counters* zero_ctr = nullptr);
 // Two independent float blurs in one launch (no range keys / counters);
 // false (nothing launched) when the radius pair has no instantiation.
 struct BlurDesc {
@@ -80,19 +99,22 @@ struct BlurDesc {
     float* copy_out;
     const Taps* taps;
 };
-bool launch_blur_pair(const BlurDesc& a, const BlurDesc& b, hipStream_t s);
+bool launch_blur_pair(const BlurDesc& a, const BlurDesc& b, const Frames& fr, hipStream_t s);
 // 8-bit frames (pitches in bytes).  launch_blur_u8 returns false (nothing
 // launched) for an init radius without a fused 8-bit instantiation; the caller
 // then converts with launch_u8_to_f32 and uses launch_blur.
 bool launch_blur_u8(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, const Taps& taps,
-                    hipStream_t s, unsigned* range_keys, Counters* zero_ctr);
-void launch_u8_to_f32(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, hipStream_t s);
-void launch_upsample2x_u8(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, hipStream_t s);
+                    const Frames& fr, long sfs, hipStream_t s, unsigned* range_keys, Counters* zero_ctr);
+void launch_u8_to_f32(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, const Frames& fr,
+                      long sfs, hipStream_t s);
+void launch_upsample2x_u8(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, const Frames& fr,
+                          long sfs, hipStream_t s);
 // 3x3x3 extrema of every octave in one launch (L = 1..6; false = nothing
 // launched), else per octave with launch_extrema.
-bool launch_extrema_all(const PyrDesc& pyr, float threshold, uint2* cand, Counters* ctr, unsigned cap, hipStream_t s);
+bool launch_extrema_all(const PyrDesc& pyr, float threshold, uint2* cand, Counters* ctr, unsigned cap,
+                        const Frames& fr, hipStream_t s);
 void launch_extrema(const PyrDesc& pyr, int o, float threshold, uint2* cand, Counters* ctr, unsigned cap,
-                    hipStream_t s);
+                    const Frames& fr, hipStream_t s);
 
 struct KeypointParams {
     float contrastThreshold, edgeThreshold, sigma;
@@ -103,24 +125,26 @@ struct KeypointParams {
     int descNrec;           // LDS record bound of the descriptor's counting sort
 };
 void launch_refine(const PyrDesc& pyr, const uint2* cand, unsigned capCand, Counters* ctr, uint32_t* bitmap,
-                   RefKpt* out, const KeypointParams& kp, hipStream_t s);
+                   RefKpt* out, const KeypointParams& kp, const Frames& fr, hipStream_t s);
 // Also clears each refined keypoint's dedupe bit (k_refine set it), so the
 // bitmap is zero again for the next frame without a memset.
 void launch_orientation(const PyrDesc& pyr, const RefKpt* in, Counters* ctr, OriKpt* out, uint32_t* bitmap,
-                        const KeypointParams& kp, hipStream_t s);
+                        const KeypointParams& kp, const Frames& fr, hipStream_t s);
 // zero_range: the other frame buffer's 2 * kRangeSlots range keys (zeroed here
 // for the next frame, so no memset node is needed).
-void launch_select(const OriKpt* kpts, Counters* ctr, unsigned* zero_range, const KeypointParams& kp, hipStream_t s);
+void launch_select(const OriKpt* kpts, Counters* ctr, unsigned* zero_range, const KeypointParams& kp, const Frames& fr,
+                   hipStream_t s);
 // select + bucket count + scan + scatter in one single-workgroup launch;
 // false (nothing launched) when the row buckets exceed kOrderMaxBuckets.
 constexpr int kOrderMaxBuckets = 16384;  // 64 KiB of LDS
 bool launch_order(const OriKpt* kpts, Counters* ctr, unsigned* zero_range, unsigned* bcount, unsigned* boff, int* slot,
-                  int* order, const KeypointParams& kp, hipStream_t s);
+                  int* order, const KeypointParams& kp, const Frames& fr, hipStream_t s);
 void launch_bucket_count(const OriKpt* kpts, const Counters* ctr, unsigned* bcount, int* slot,
-                         const KeypointParams& kp, hipStream_t s);
-void launch_bucket_scan(unsigned* bcount, unsigned* boff, Counters* ctr, const KeypointParams& kp, hipStream_t s);
+                         const KeypointParams& kp, const Frames& fr, hipStream_t s);
+void launch_bucket_scan(unsigned* bcount, unsigned* boff, Counters* ctr, const KeypointParams& kp, const Frames& fr,
+                        hipStream_t s);
 void launch_bucket_scatter(const OriKpt* kpts, const Counters* ctr, const unsigned* boff, const int* slot,
-                           int* order, const KeypointParams& kp, hipStream_t s);
+                           int* order, const KeypointParams& kp, const Frames& fr, hipStream_t s);
 // One final keypoint's descriptor window (written by k_bucket_rank, read with
 // scalar loads by k_descriptor).  64 bytes.
 constexpr int kDescMaxRows = 128;  // enumerated windows: 2 * radius + 1 <= kDescMaxRows
@@ -138,10 +162,11 @@ static_assert(sizeof(DescJob) == 64, "DescJob is one 64-byte scalar load");
 
 void launch_bucket_rank(const PyrDesc& pyr, const OriKpt* kpts, unsigned* bcount, const unsigned* boff,
                         const int* order, const Counters* ctr, DescJob* jobs, float* kpts3, float* feats4,
-                        const KeypointParams& kp, hipStream_t s);
-// host_ctr: device-mapped pinned host memory receiving the frame's counters.
+                        const KeypointParams& kp, const Frames& fr, hipStream_t s);
+// host_ctr: device-mapped pinned host memory receiving the frames' counters
+// (frame f at host_ctr[f]).
 void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned* range_keys, uint16_t* desc,
-                       Counters* host_ctr, const KeypointParams& kp, hipStream_t s);
+                       Counters* host_ctr, const KeypointParams& kp, const Frames& fr, hipStream_t s);
 
 // Order-preserving unsigned key of a float (0 is below every key), so that
 // atomicMax over keys is a float max with a zeroed counter as the identity.

@@ -18,15 +18,12 @@ constexpr int kMaxInterpSteps = 5;
 
 __device__ __forceinline__ const OctGeom& octave_geom(const PyrDesc& pyr, int o) { return pyr.oct[o]; }
 
-__device__ __forceinline__ float dog_at(const float* g, long ps, int pitch, int layer, int r, int c) {
-    const float* p = g + (size_t)r * pitch + c;
-    return p[(size_t)(layer + 1) * ps] - p[(size_t)layer * ps];
-}
-
 // q = {octave << 8 | layer, r << 16 | c} as the extrema kernels emit it.
+// foff: byte offset of the candidate's frame arena (ctr / bitmap / out are
+// already that frame's).
 __device__ __forceinline__ void refine_candidate(const PyrDesc& pyr, uint2 q, Counters* __restrict__ ctr,
                                                  uint32_t* __restrict__ bitmap, RefKpt* __restrict__ out,
-                                                 const KeypointParams& kp) {
+                                                 const KeypointParams& kp, long foff) {
     const int L = pyr.L;
     const float img_scale = 1.f / 255.f;
     const float deriv_scale = img_scale * 0.5f;
@@ -36,18 +33,48 @@ __device__ __forceinline__ void refine_candidate(const PyrDesc& pyr, uint2 q, Co
     int layer = (int)(q.x & 255);
     int r = (int)(q.y >> 16), c = (int)(q.y & 0xffff);
     const OctGeom& g = octave_geom(pyr, o);
-    const float* G = g.base;
+    const float* G = fptr(g.base, foff);
     const long ps = g.planeStride;
     const int pitch = g.pitch;
+    // The 3x3 neighbourhood of Gaussian planes layer-1 .. layer+2 around
+    // (r, c): 12 row segments of 3 floats, one 12-byte buffer load each (all
+    // in flight together), instead of ~30 scattered dword loads per Newton
+    // step.  DoG values are formed from it exactly as a stored DoG
+    // (G_{l+1} - G_l, one rounding).  The block of the converged position
+    // stays in registers for the contrast and edge tests.
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(G), 0, (int)min((long)(L + 3) * ps * 4, 0x7fffffffL), 0x00020000);
+    float D[3][3][3];  // D[s][dy][dx] = DoG at (layer - 1 + s, r - 1 + dy, c - 1 + dx)
+    auto load_block = [&]() {
+        typedef unsigned u32x3 __attribute__((ext_vector_type(3)));
+        float v[4][3][3];
+#pragma unroll
+        for (int p = 0; p < 4; p++)
+#pragma unroll
+            for (int dy = 0; dy < 3; dy++) {
+                const unsigned off = (unsigned)((long)(layer - 1 + p) * ps + (long)(r - 1 + dy) * pitch + c - 1) * 4u;
+                const u32x3 w = __builtin_amdgcn_raw_buffer_load_b96(rsrc, off, 0, 0);
+                v[p][dy][0] = __uint_as_float(w.x);
+                v[p][dy][1] = __uint_as_float(w.y);
+                v[p][dy][2] = __uint_as_float(w.z);
+            }
+#pragma unroll
+        for (int p = 0; p < 3; p++)
+#pragma unroll
+            for (int dy = 0; dy < 3; dy++)
+#pragma unroll
+                for (int dx = 0; dx < 3; dx++) D[p][dy][dx] = v[p + 1][dy][dx] - v[p][dy][dx];
+    };
 
     float xi = 0, xr = 0, xc = 0;
     int it = 0;
     bool ok = true;
     for (; it < kMaxInterpSteps; it++) {
-        const float c0 = dog_at(G, ps, pitch, layer, r, c);
-        const float cl = dog_at(G, ps, pitch, layer, r, c - 1), cr = dog_at(G, ps, pitch, layer, r, c + 1);
-        const float cu = dog_at(G, ps, pitch, layer, r - 1, c), cd = dog_at(G, ps, pitch, layer, r + 1, c);
-        const float pc = dog_at(G, ps, pitch, layer - 1, r, c), nc = dog_at(G, ps, pitch, layer + 1, r, c);
+        load_block();
+        const float c0 = D[1][1][1];
+        const float cl = D[1][1][0], cr = D[1][1][2];
+        const float cu = D[1][0][1], cd = D[1][2][1];
+        const float pc = D[0][1][1], nc = D[2][1][1];
         const float dD0 = (cr - cl) * deriv_scale;
         const float dD1 = (cd - cu) * deriv_scale;
         const float dD2 = (nc - pc) * deriv_scale;
@@ -55,15 +82,9 @@ __device__ __forceinline__ void refine_candidate(const PyrDesc& pyr, uint2 q, Co
         const float dxx = (cr + cl - v2) * second_deriv_scale;
         const float dyy = (cd + cu - v2) * second_deriv_scale;
         const float dss = (nc + pc - v2) * second_deriv_scale;
-        const float dxy = (dog_at(G, ps, pitch, layer, r + 1, c + 1) - dog_at(G, ps, pitch, layer, r + 1, c - 1) -
-                           dog_at(G, ps, pitch, layer, r - 1, c + 1) + dog_at(G, ps, pitch, layer, r - 1, c - 1)) *
-                          cross_deriv_scale;
-        const float dxs = (dog_at(G, ps, pitch, layer + 1, r, c + 1) - dog_at(G, ps, pitch, layer + 1, r, c - 1) -
-                           dog_at(G, ps, pitch, layer - 1, r, c + 1) + dog_at(G, ps, pitch, layer - 1, r, c - 1)) *
-                          cross_deriv_scale;
-        const float dys = (dog_at(G, ps, pitch, layer + 1, r + 1, c) - dog_at(G, ps, pitch, layer + 1, r - 1, c) -
-                           dog_at(G, ps, pitch, layer - 1, r + 1, c) + dog_at(G, ps, pitch, layer - 1, r - 1, c)) *
-                          cross_deriv_scale;
+        const float dxy = (D[1][2][2] - D[1][2][0] - D[1][0][2] + D[1][0][0]) * cross_deriv_scale;
+        const float dxs = (D[2][1][2] - D[2][1][0] - D[0][1][2] + D[0][1][0]) * cross_deriv_scale;
+        const float dys = (D[2][2][1] - D[2][0][1] - D[0][2][1] + D[0][0][1]) * cross_deriv_scale;
         // Matx_FastSolveOp<float,3,1>: Cramer's rule, det from Matx_DetOp.
         const float a00 = dxx, a01 = dxy, a02 = dxs, a10 = dxy, a11 = dyy, a12 = dys, a20 = dxs, a21 = dys,
                     a22 = dss;
@@ -95,10 +116,11 @@ __device__ __forceinline__ void refine_candidate(const PyrDesc& pyr, uint2 q, Co
     }
     if (!ok || it >= kMaxInterpSteps) return;
 
-    const float c0 = dog_at(G, ps, pitch, layer, r, c);
-    const float cl = dog_at(G, ps, pitch, layer, r, c - 1), cr = dog_at(G, ps, pitch, layer, r, c + 1);
-    const float cu = dog_at(G, ps, pitch, layer, r - 1, c), cd = dog_at(G, ps, pitch, layer, r + 1, c);
-    const float pc = dog_at(G, ps, pitch, layer - 1, r, c), nc = dog_at(G, ps, pitch, layer + 1, r, c);
+    // D still holds the block of the converged (layer, r, c).
+    const float c0 = D[1][1][1];
+    const float cl = D[1][1][0], cr = D[1][1][2];
+    const float cu = D[1][0][1], cd = D[1][2][1];
+    const float pc = D[0][1][1], nc = D[2][1][1];
     const float dD0 = (cr - cl) * deriv_scale;
     const float dD1 = (cd - cu) * deriv_scale;
     const float dD2 = (nc - pc) * deriv_scale;
@@ -111,9 +133,7 @@ __device__ __forceinline__ void refine_candidate(const PyrDesc& pyr, uint2 q, Co
     const float v2 = c0 * 2.f;
     const float dxx = (cr + cl - v2) * second_deriv_scale;
     const float dyy = (cd + cu - v2) * second_deriv_scale;
-    const float dxy = (dog_at(G, ps, pitch, layer, r + 1, c + 1) - dog_at(G, ps, pitch, layer, r + 1, c - 1) -
-                       dog_at(G, ps, pitch, layer, r - 1, c + 1) + dog_at(G, ps, pitch, layer, r - 1, c - 1)) *
-                      cross_deriv_scale;
+    const float dxy = (D[1][2][2] - D[1][2][0] - D[1][0][2] + D[1][0][0]) * cross_deriv_scale;
     const float tr = dxx + dyy;
     const float det = dxx * dyy - dxy * dxy;
     const float et = kp.edgeThreshold;

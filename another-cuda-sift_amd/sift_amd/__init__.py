@@ -76,6 +76,12 @@ def lib() -> ctypes.CDLL:
         "sift_hip_submit": (i, [vp, vp, sz, i, ctypes.POINTER(ctypes.c_longlong)]),
         "sift_hip_wait": (i, [vp, ctypes.c_longlong]),
         "sift_hip_sync": (i, [vp]),
+        "sift_hip_set_batch": (i, [vp, i]),
+        "sift_hip_batch_capacity": (i, [vp, ip]),
+        "sift_hip_detect_batch_device": (i, [vp, vp, i, sz, sz, i, vp]),
+        "sift_hip_batch_frames": (i, [vp, ip]),
+        "sift_hip_batch_results_device": (i, [vp, i, ip, ip, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp)]),
+        "sift_hip_batch_copy_to_host": (i, [vp, i, vp, vp, vp, i, ip]),
         "sift_hip_num_keypoints": (i, [vp, ip]),
         "sift_hip_overflow_flags": (i, [vp, ip]),
         "sift_hip_results_device": (i, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), ip, ip]),
@@ -173,10 +179,15 @@ class DeviceBuffer:
 class Detector:
     """sift_cuda::Detector (Detector.hh:24-96) over the C ABI."""
 
-    def __init__(self, config: CudaSiftConfig, device: int = -1):
+    def __init__(self, config: CudaSiftConfig, device: int = -1, batch: int = 1):
+        """batch > 1: frame-batch handle (sift_hip_set_batch): detectBatchDevice runs up to `batch`
+        frames per launch; the single-frame methods keep working (frame 0's arena)."""
         self.config = config
+        self.batch = int(batch)
         self._h = ctypes.c_void_p()
         _check(lib().sift_hip_create(ctypes.byref(config._abi()), device, ctypes.byref(self._h)), "sift_hip_create")
+        if self.batch != 1:
+            _check(lib().sift_hip_set_batch(self._h, self.batch), "set_batch")
         n = ctypes.c_int()
         lib().sift_hip_num_octaves(self._h, ctypes.byref(n))
         self.nOctaves = n.value
@@ -268,6 +279,41 @@ class Detector:
     def sync(self) -> None:
         _check(lib().sift_hip_sync(self._h), "sync")
         self._refresh()
+
+    # --- frame batches ----------------------------------------------------------
+    def detectBatchDevice(self, dev_ptr: int, n: int, row_stride_bytes: int = 0, frame_stride_bytes: int = 0,
+                          stream: Optional[int] = None, sync: bool = True, u8: bool = False) -> None:
+        """n (<= batch) device frames at dev_ptr + i * frame_stride_bytes, one launch per stage for all."""
+        self.gpuWarmUpAndAllocate()
+        fmt = SIFT_HIP_U8 if u8 else SIFT_HIP_F32
+        _check(lib().sift_hip_detect_batch_device(self._h, dev_ptr, n, row_stride_bytes, frame_stride_bytes, fmt, stream),
+               "detectBatchDevice")
+        if sync:
+            self.sync()
+
+    def batch_frames(self) -> int:
+        n = ctypes.c_int()
+        _check(lib().sift_hip_batch_frames(self._h, ctypes.byref(n)), "batch_frames")
+        return n.value
+
+    def batch_results(self, i: int):
+        """(count, overflow flags, device kpts3 / feats4 / descriptor pointers) of frame i of the current batch."""
+        c, o = ctypes.c_int(), ctypes.c_int()
+        k3, f4, d = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        _check(lib().sift_hip_batch_results_device(self._h, i, ctypes.byref(c), ctypes.byref(o), ctypes.byref(k3),
+                                                   ctypes.byref(f4), ctypes.byref(d)), "batch_results")
+        return c.value, o.value, k3.value, f4.value, d.value
+
+    def batch_copy_to_host(self, i: int, descriptor: bool = True):
+        """Host copies (kpts3 (n,3), feats4 (n,4), descriptors (n,128) fp16 or None) of frame i of the current batch."""
+        n = self.batch_results(i)[0]
+        k3 = np.zeros((n, 3), np.float32)
+        f4 = np.zeros((n, 4), np.float32)
+        d = np.zeros((n, 128), np.uint16) if descriptor else None
+        got = ctypes.c_int()
+        _check(lib().sift_hip_batch_copy_to_host(self._h, i, _ptr(k3), _ptr(f4), _ptr(d) if d is not None else None, n,
+                                                 ctypes.byref(got)), "batch_copy_to_host")
+        return k3, f4, (d.view(np.float16) if d is not None else None)
 
     def copyToHost(self, descriptor: bool = True) -> None:
         """Detector.cu:606-634."""

@@ -5,16 +5,19 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (BASELINE.json configs[1], "C2"): one synthetic 1920x1200 frame per
-step per GPU, detectAndCompute with numOctaveLayers=3 (5 DoG scales per octave),
-3 octaves, upscale=false, numFeatures=5000; the frame is resident in HBM when
-the timed region starts (H2D excluded, like the reference's readme.md:11).
+Workload (BASELINE.json configs[1], "C2"): synthetic 1920x1200 frames,
+detectAndCompute with numOctaveLayers=3 (5 DoG scales per octave), 3 octaves,
+upscale=false, numFeatures=5000; frames are resident in HBM when the timed
+region starts (H2D excluded, like the reference's readme.md:11).  A step is one
+batch of --batch frames (default 8) through a frame-batch detector: every
+pipeline launch processes the whole batch (sift_hip_set_batch), and steps
+rotate over --streams detectors (default 2, each its own HIP stream + graphs)
+so consecutive batches overlap.  Every frame is fully processed (results are
+those of the single-frame pipeline, bit for bit: tests/test_gpu_batch.py).
 Frames shard per image across ranks with no data-path collective ("weak").
-Within a GPU, consecutive frames rotate over --streams detectors (default 3,
-each its own HIP stream + graphs), so independent frames overlap; each step is
-one complete frame.  value = all frames' pixels / max-over-ranks wall time, in
-Mpix/s; the strictly serial single-detector rate and the synchronous
-per-frame latency are reported beside it.
+value = all frames' pixels / max-over-ranks wall time, in Mpix/s; the strictly
+serial one-frame-at-a-time rate and the synchronous per-frame latency are
+reported beside it.
 
 Side measurements in the same JSON line: 2000x2000x128 brute-force match (C3),
 the 8-way all-gather + pairwise match (C5) when N > 1, the per-kernel roofline of
@@ -62,7 +65,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) on the 8-GPU node; gloo to rehearse N > 1 on one GPU")
-    ap.add_argument("--streams", type=int, default=3, help="detectors (HIP streams) frames rotate over")
+    ap.add_argument("--streams", type=int, default=2, help="detectors (HIP streams) steps rotate over")
+    ap.add_argument("--batch", type=int, default=8,
+                    help="frames per step: one launch per pipeline stage processes the whole batch "
+                         "(sift_hip_set_batch); 1 = single-frame graphs")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-oracle sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--roofline-only", action="store_true",
@@ -115,7 +121,7 @@ def stage_table(timing, nt):
     return {k: round(v, 2) for k, v in sorted(per.items(), key=lambda kv: -kv[1])}
 
 
-def measure_roofline(det, frames, stride, traffic_summary, nt=20, warm=3):
+def measure_roofline(det, frames, stride, traffic_summary, nt=20, warm=3, batch=None):
     """k_blur, the kernel with the largest share of frame time (all its launches):
     algorithmic bytes per launch / average launch duration, by HIP events on the
     detector's own stream (eager timing mode).  Each blur launch of the frame is
@@ -123,11 +129,18 @@ def measure_roofline(det, frames, stride, traffic_summary, nt=20, warm=3):
     pure), so the average carries the stream's inter-kernel gap but not one
     event pair per launch."""
     det.set_timing(True, blur_reps=BLUR_REPS)
+
+    def run(s):
+        if batch is not None:  # (tensor of B frames): every launch carries the B frames
+            det.detectBatchDevice(batch.data_ptr(), batch.shape[0], stride, batch[0].numel() * batch.element_size())
+        else:
+            det.detectAndComputeDevice(frames[s % len(frames)].data_ptr(), stride, sync=True)
+
     for s in range(warm):
-        det.detectAndComputeDevice(frames[s % len(frames)].data_ptr(), stride, sync=True)
+        run(s)
     det.timing_reset()
     for s in range(nt):
-        det.detectAndComputeDevice(frames[s % len(frames)].data_ptr(), stride, sync=True)
+        run(s)
     timing = det.timing()
     det.set_timing(False)
     blurs = [v for k, v in timing.items() if k.startswith("blur_")]
@@ -136,9 +149,11 @@ def measure_roofline(det, frames, stride, traffic_summary, nt=20, warm=3):
     per_launch_s = sum(v["ms"] for v in blurs) / blur_launches / 1e3
     achieved = per_launch_bytes / per_launch_s / 1e9
     traffic = pmc_traffic(traffic_summary, ("k_blur", "k_blur2"))
+    per = "step" if batch is not None else "frame"
+    fr = f", {batch.shape[0]} frames per launch" if batch is not None else ""
     roof = {
-        "kernel": f"k_blur / k_blur2 (all {blur_launches // nt // BLUR_REPS} blur launches/frame, each x{BLUR_REPS} "
-                  f"back to back between HIP events, eager)",
+        "kernel": f"k_blur / k_blur2 (all {blur_launches // nt // BLUR_REPS} blur launches/{per}{fr}, each "
+                  f"x{BLUR_REPS} back to back between HIP events, eager)",
         "bound": "hbm",
         "achieved": round(achieved, 1),
         "peak": HBM_PEAK_GBS,
@@ -184,24 +199,36 @@ def main():
     # a.streams detectors (one HIP stream + graph pair each) take consecutive
     # frames round-robin, so independent frames overlap on the GPU; every step
     # is still one complete frame.
-    dets = [sift.Detector(cfg, device=local) for _ in range(1 if a.roofline_only else a.streams)]
+    B = max(a.batch, 1)
+    nstreams = 1 if a.roofline_only else a.streams
+    dets = [sift.Detector(cfg, device=local, batch=B) for _ in range(nstreams)]
     for d in dets:
         d.gpuWarmUpAndAllocate()
     det = dets[0]
     nframes = 4
     frames = [torch.from_numpy(sift.synth_frame(1000 * rank + i, W, H)).to(dev) for i in range(nframes)]
     stride = W * 4
+    # A step's batch: B distinct frames, contiguous (frame stride W*H*4 bytes).
+    fb = torch.from_numpy(np.stack([sift.synth_frame(1000 * rank + i, W, H) for i in range(B)])).to(dev)
     torch.cuda.synchronize()
+
+    def step(s):
+        d = dets[s % len(dets)]
+        if B == 1:
+            d.detectAndComputeDevice(frames[s % nframes].data_ptr(), stride, sync=False)
+        else:
+            d.detectBatchDevice(fb.data_ptr(), B, stride, W * H * 4, sync=False)
+
     if a.roofline_only:
-        rl = measure_roofline(det, frames, stride, a.traffic_summary, nt=a.steps)
+        rl = measure_roofline(det, frames, stride, a.traffic_summary, nt=a.steps, batch=fb if B > 1 else None)
         if rank == 0:
-            nt = rl["frames"]
-            print(json.dumps({"roofline": rl["roofline"], "frames": nt,
+            nt = rl["frames"] * B
+            print(json.dumps({"roofline": rl["roofline"], "frames": nt, "frames_per_launch": B,
                               "stage_us_per_frame_eager": stage_table(rl["timing"], nt)}),
                   flush=True)
         return
     for s in range(a.warmup):
-        dets[s % a.streams].detectAndComputeDevice(frames[s % nframes].data_ptr(), stride, sync=False)
+        step(s)
     for d in dets:
         d.sync()
     kcount = det.total_size
@@ -209,16 +236,22 @@ def main():
     barrier()
     t0 = time.perf_counter()
     for s in range(a.steps):
-        dets[s % a.streams].detectAndComputeDevice(frames[s % nframes].data_ptr(), stride, sync=False)
+        step(s)
     for d in dets:
         d.sync()
     t1 = time.perf_counter()
     barrier()
     elapsed = max_over_ranks(t1 - t0)
     ms_per_step = elapsed / a.steps * 1e3
-    value = world * a.steps * W * H / 1e6 / elapsed
+    value = world * a.steps * B * W * H / 1e6 / elapsed
+    ms_per_frame = elapsed / (a.steps * B) * 1e3
+    detb = dets[0]  # kept for the roofline pass (same frames per launch as the timed steps)
+    del dets
 
-    # Same frames through ONE detector (frames strictly serialised), for reference.
+    # The same frames one at a time through ONE single-frame detector (frames
+    # strictly serialised): latency-side reference numbers.
+    det = sift.Detector(cfg, device=local)
+    det.gpuWarmUpAndAllocate()
     n1 = max(a.steps // 2, 1)
     barrier()
     t = time.perf_counter()
@@ -231,26 +264,37 @@ def main():
     # ---- C4: 256 synthetic 1600x900 frames sharded per image over the ranks -------
     W4, H4, N4 = 1600, 900, 256
     mine4 = multi.frame_shard(N4, rank, world)
-    dets4 = [sift.Detector(make_config(col_width=W4, row_width=H4, numOctaves=0), device=local)
+    dets4 = [sift.Detector(make_config(col_width=W4, row_width=H4, numOctaves=0), device=local, batch=B)
              for _ in range(a.streams)]
     for d in dets4:
         d.gpuWarmUpAndAllocate()
-    frames4 = [torch.from_numpy(sift.synth_frame(i, W4, H4)).to(dev) for i in mine4[:4]]
-    for s, _ in enumerate(mine4[:6]):
-        dets4[s % a.streams].detectAndComputeDevice(frames4[s % len(frames4)].data_ptr(), W4 * 4, sync=False)
+    nd4 = max(min(len(mine4), 4 if B == 1 else B), 1)  # distinct frames resident per rank
+    fb4 = torch.from_numpy(np.stack([sift.synth_frame(i, W4, H4) for i in (mine4 or [0])[:nd4]])).to(dev)
+    groups = [mine4[k:k + B] for k in range(0, len(mine4), B)]  # the last one may be a partial batch
+
+    def step4(s, n):
+        d = dets4[s % a.streams]
+        if B == 1:
+            d.detectAndComputeDevice(fb4[s % nd4].data_ptr(), W4 * 4, sync=False)
+        else:
+            d.detectBatchDevice(fb4.data_ptr(), n, W4 * 4, W4 * H4 * 4, sync=False)
+
+    for s in range(2 * a.streams):
+        step4(s, min(B, nd4))
     for d in dets4:
         d.sync()
     barrier()
     t = time.perf_counter()
-    for s, _ in enumerate(mine4):
-        dets4[s % a.streams].detectAndComputeDevice(frames4[s % len(frames4)].data_ptr(), W4 * 4, sync=False)
+    for s, g in enumerate(groups):
+        step4(s, len(g))
     for d in dets4:
         d.sync()
     t4 = max_over_ranks(time.perf_counter() - t)
     c4 = {"frames": N4, "frame": f"{W4}x{H4}", "octaves": "auto", "value": round(N4 * W4 * H4 / 1e6 / t4, 2),
-          "unit": "Mpix/s", "ms_total": round(t4 * 1e3, 3), "frames_per_rank": len(mine4),
-          "note": "frame i on rank i mod N (no collective); 4 distinct synthetic frames per rank cycled"}
-    del dets4, frames4
+          "unit": "Mpix/s", "ms_total": round(t4 * 1e3, 3), "frames_per_rank": len(mine4), "frames_per_launch": B,
+          "note": f"frame i on rank i mod N (no collective); {nd4} distinct synthetic frames per rank, "
+                  f"{B} frames per launch, batches rotating over {a.streams} streams"}
+    del dets4, fb4
 
     # Synchronous per-frame latency (reference semantics: detectAndCompute blocks).
     lat = []
@@ -294,8 +338,9 @@ def main():
     }
 
     # ---- per-kernel roofline: HIP events on the detector's own stream --------
-    rl = measure_roofline(det, frames, stride, a.traffic_summary)
-    timing, nt = rl["timing"], rl["frames"]
+    rl = measure_roofline(detb, frames, stride, a.traffic_summary, batch=fb if B > 1 else None)
+    timing, nt = rl["timing"], rl["frames"] * B
+    del detb
     stages = stage_table(timing, nt)
     total_ms = sum(stages.values()) * nt / 1e3
     dom = next(iter(stages))
@@ -445,16 +490,19 @@ def main():
             "dtype": "f32",
             "data": "synthetic",
             "config": {
-                "workload": "C2: detectAndCompute on one 1920x1200 frame per step per GPU, numOctaveLayers=3 "
-                            "(5 DoG scales/octave), numOctaves=3, upscale=false, numFeatures=5000; frames HBM-resident",
-                "frames_per_step_per_gpu": 1,
+                "workload": f"C2: detectAndCompute on 1920x1200 frames, {B} per step per GPU (one launch per stage "
+                            "for the batch), numOctaveLayers=3 (5 DoG scales/octave), numOctaves=3, upscale=false, "
+                            "numFeatures=5000; frames HBM-resident",
+                "frames_per_step_per_gpu": B,
+                "frames_per_launch": B,
                 "streams_per_gpu": a.streams,
                 "parallelism": f"frame-sharded x{world}, no data-path collective",
                 "keypoints_per_frame": kcount,
             },
             "roofline": rl["roofline"],
             "cpu_baseline": cpu,
-            "pipeline_hbm_frac": round(88.0 * sum_px / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "ms_per_frame": round(ms_per_frame, 4),
+            "pipeline_hbm_frac": round(88.0 * sum_px / (ms_per_frame / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             "sync_ms_per_frame": round(sync_ms, 4),
             "single_stream": {"value": round(single_value, 2), "ms_per_frame": round(single / n1 * 1e3, 4)},
             "host_input": host_input,

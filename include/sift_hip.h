@@ -97,6 +97,35 @@ int sift_hip_detect_device_fmt(sift_hip_t h, const void* dev_img, size_t row_str
                                void* stream);
 int sift_hip_sync(sift_hip_t h);
 
+/* Frame batches (C4: many frames per GPU).  sift_hip_set_batch(h, B), called
+ * before sift_hip_warmup, gives the handle B frame arenas (pyramid, keypoint
+ * lists, counters and result slots per frame) and a pipeline graph whose every
+ * launch processes all B frames: B x the workgroups per launch and 1/B of the
+ * dispatches per frame.  Results per frame are those of the single-frame call
+ * on the same frame, bit for bit.  B = 1 (default) is the single-frame handle;
+ * every single-frame entry point keeps working on a batch handle (frame 0's
+ * arena, a one-frame graph).  Replaces the per-frame loop of
+ * /root/reference/tool/extract_and_match_example.cc:69-101 over
+ * Detector::detectAndCompute (Detector.cu:133-233). */
+int sift_hip_set_batch(sift_hip_t h, int frames);
+int sift_hip_batch_capacity(sift_hip_t h, int* frames);
+
+/* n (1..B) device frames, frame i at dev_frames + i * frame_stride_bytes (0 =
+ * row_stride * height), enqueued on `stream` (NULL = internal), NOT
+ * synchronised (sift_hip_sync).  The batch becomes the current launch group. */
+int sift_hip_detect_batch_device(sift_hip_t h, const void* dev_frames, int n, size_t row_stride_bytes,
+                                 size_t frame_stride_bytes, int format, void* stream);
+/* Frames in the current launch group (1 after a single-frame call). */
+int sift_hip_batch_frames(sift_hip_t h, int* n);
+/* Frame i of the current group: count / overflow flags (valid after
+ * sift_hip_sync) and its device result arrays (layouts as
+ * sift_hip_results_device). */
+int sift_hip_batch_results_device(sift_hip_t h, int i, int* count, int* overflow, const float** kpts3,
+                                  const float** feats4, const uint16_t** desc);
+/* Copies min(count, cap) results of frame i to host memory (desc nullable). */
+int sift_hip_batch_copy_to_host(sift_hip_t h, int i, float* kpts3, float* feats4, uint16_t* desc, int cap,
+                                int* count);
+
 /* Pipelined host input (replaces the synchronous upload of CudaImage.cu:97-105
  * and the per-frame loop of extract_and_match_example.cc:69-101).
  * sift_hip_submit copies the frame into a pinned staging ring (the caller's

@@ -136,3 +136,24 @@ def test_python_surface_mirrors_reference(sift):
     for f in ["col_width", "row_width", "numFeatures", "numOctaveLayers", "contrastThreshould", "edgeThreshould",
               "sigma", "upscale"]:
         assert hasattr(sift.CudaSiftConfig(col_width=8, row_width=8), f)
+
+
+def test_batch_host_logic(sift):
+    """sift_hip_set_batch limits and call order (no GPU work involved)."""
+    L = sift.lib()
+    h = ctypes.c_void_p()
+    c = sift._Config()
+    L.sift_hip_default_config(ctypes.byref(c), 64, 64)
+    assert L.sift_hip_create(ctypes.byref(c), 0, ctypes.byref(h)) == 0
+    try:
+        assert L.sift_hip_set_batch(h, 0) == -1
+        assert L.sift_hip_set_batch(h, 65) == -1
+        assert L.sift_hip_set_batch(h, 4) == 0
+        n = ctypes.c_int()
+        assert L.sift_hip_batch_capacity(h, ctypes.byref(n)) == 0 and n.value == 4
+        # before sift_hip_warmup: out of order, refused before any device call
+        assert L.sift_hip_detect_batch_device(h, ctypes.c_void_p(16), 2, 0, 0, 0, None) == -3
+        assert L.sift_hip_batch_results_device(h, 0, None, None, None, None, None) == -3
+    finally:
+        L.sift_hip_destroy(h)
+    assert L.sift_hip_set_batch(None, 2) == -1

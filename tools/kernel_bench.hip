@@ -15,6 +15,7 @@
 #include "sift_kernels.h"
 
 using namespace sift_amd;
+static const Frames kOne{1, 0};  // one frame per launch
 
 
 #define CK(x)                                                                              \
@@ -208,17 +209,17 @@ int main(int argc, char** argv) {
         lt[i] = taps_for(std::sqrt(st * st - sp * sp));
     }
     const Taps init = taps_for(std::sqrt(sigma * sigma - 0.25));
-    launch_blur(dIn, W0, 1, W0, H0, pyr.oct[0].base, pyr.oct[0].pitch, nullptr, init, s);
+    launch_blur(dIn, W0, 1, W0, H0, pyr.oct[0].base, pyr.oct[0].pitch, nullptr, init, kOne, 0, s);
     for (int o = 0; o < 3; o++) {
         const OctGeom& g = pyr.oct[o];
         for (int i = 1; i < L + 3; i++) {
             float* dst = g.base + (size_t)i * g.planeStride;
             if (i == 1 && o > 0) {
                 const OctGeom& p = pyr.oct[o - 1];
-                launch_blur(p.base + (size_t)L * p.planeStride, p.pitch, 2, g.W, g.H, dst, g.pitch, g.base, lt[i], s);
+                launch_blur(p.base + (size_t)L * p.planeStride, p.pitch, 2, g.W, g.H, dst, g.pitch, g.base, lt[i], kOne, 0, s);
             } else {
                 launch_blur(g.base + (size_t)(i - 1) * g.planeStride, g.pitch, 1, g.W, g.H, dst, g.pitch, nullptr,
-                            lt[i], s);
+                            lt[i], kOne, 0, s);
             }
         }
     }
@@ -235,7 +236,7 @@ int main(int argc, char** argv) {
             float* src = g.base + (size_t)(i - 1) * g.planeStride;
             float* dst = g.base + (size_t)i * g.planeStride;
             const double bytes = 8.0 * g.W * g.H;
-            us = time_us(iters, s, [&] { launch_blur(src, g.pitch, 1, g.W, g.H, dst, g.pitch, nullptr, lt[i], s); });
+            us = time_us(iters, s, [&] { launch_blur(src, g.pitch, 1, g.W, g.H, dst, g.pitch, nullptr, lt[i], kOne, 0, s); });
             std::printf("{\"kernel\": \"k_blur<%d>\", \"octave\": %d, \"W\": %d, \"H\": %d, \"us\": %.3f, \"GBps\": %.1f}\n",
                         lt[i].n / 2, o, g.W, g.H, us, bytes / us / 1e3);
         }
@@ -250,7 +251,7 @@ int main(int argc, char** argv) {
         for (int o = 0; o < 3; o++) bytes += 4.0 * (L + 3) * pyr.oct[o].W * pyr.oct[o].H;
         us = time_us(iters, s, [&] {
             CK(hipMemsetAsync(dCtr, 0, sizeof(Counters), s));
-            launch_extrema_all(pyr, thr, dCand, dCtr, 1u << 20, s);
+            launch_extrema_all(pyr, thr, dCand, dCtr, 1u << 20, kOne, s);
         });
         std::printf("{\"kernel\": \"k_extrema_all (3 octaves)+memset\", \"us\": %.3f, \"GBps\": %.1f}\n", us,
                     bytes / us / 1e3);

@@ -1,9 +1,12 @@
 #!/bin/bash
 # PMC counter passes (kernel-trace only, no sys/runtime trace) over
 # tools/profile_frames.py, plus the FETCH_SIZE/WRITE_SIZE calibration binary.
-# Usage: tools/pmc.sh TAG   -> gpurun_out/TAG_p{1..4}/, gpurun_out/TAG_calib_{fetch,write}/
+# Usage: tools/pmc.sh TAG [profile_frames.py args, e.g. --batch 8]
+#   -> gpurun_out/TAG_p{1..4}/, gpurun_out/TAG_calib_{fetch,write}/
 set -o pipefail
 TAG=${1:-pmc}
+shift
+PF_ARGS="$*"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY"
@@ -13,7 +16,7 @@ P4="WRITE_SIZE"
 i=0
 for P in "$P1" "$P2" "$P3" "$P4"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $P --kernel-trace -d gpurun_out/${TAG}_p$i -o run --output-format csv -- python3 tools/profile_frames.py --frames 5 > gpurun_out/${TAG}_p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/${TAG}_p$i.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $P --kernel-trace -d gpurun_out/${TAG}_p$i -o run --output-format csv -- python3 tools/profile_frames.py --frames 5 $PF_ARGS > gpurun_out/${TAG}_p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/${TAG}_p$i.log; exit 1; }
 done
 if [ -x tools/hbm_calib ]; then
   for C in FETCH_SIZE WRITE_SIZE; do

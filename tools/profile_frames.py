@@ -5,6 +5,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "another-cuda-sift_amd"))
+import numpy as np  # noqa: E402
 import sift_amd as sift  # noqa: E402
 
 ap = argparse.ArgumentParser()
@@ -14,14 +15,20 @@ ap.add_argument("--height", type=int, default=1200)
 ap.add_argument("--octaves", type=int, default=3)
 ap.add_argument("--upscale", action="store_true")
 ap.add_argument("--eager", action="store_true", help="timing mode: un-graphed launches")
+ap.add_argument("--batch", type=int, default=1, help="frames per launch (sift_hip_set_batch)")
 a = ap.parse_args()
 cfg = sift.CudaSiftConfig(col_width=a.width, row_width=a.height, numOctaves=a.octaves, upscale=a.upscale)
-det = sift.Detector(cfg, device=0)
+det = sift.Detector(cfg, device=0, batch=a.batch)
 det.gpuWarmUpAndAllocate()
 det.set_timing(a.eager)
 img = sift.synth_frame(0, a.width, a.height)
+if a.batch > 1:  # B copies of the frame, device-resident
+    buf = sift.DeviceArray.from_numpy(np.ascontiguousarray(np.broadcast_to(img, (a.batch,) + img.shape)))
 for _ in range(a.frames):
-    det.detectAndCompute(img)
+    if a.batch > 1:
+        det.detectBatchDevice(buf.value, a.batch, a.width * 4, a.width * a.height * 4)
+    else:
+        det.detectAndCompute(img)
 print("keypoints", det.total_size)
 if a.eager:
     for k, v in sorted(det.timing().items(), key=lambda kv: -kv[1]["ms"]):
