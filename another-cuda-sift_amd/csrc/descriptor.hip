@@ -183,6 +183,10 @@ __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ 
     const float range = (decode_range_key(kmax) + decode_range_key(knmn)) * 1.001f;
     const float bins_per_rad = kN / 360.f;
 
+    // Plain round-robin keypoint -> workgroup (-> XCD): keypoints are in
+    // (octave, layer, row) order and their cost grows with scale, so handing
+    // each XCD a contiguous run (L2 locality) unbalances the XCDs -- measured
+    // 10-30 % slower frames.
     for (unsigned p = blockIdx.x; p < n; p += gridDim.x) {
         const DescJob jb = load_job(jobs, p);
         DescGeom G;

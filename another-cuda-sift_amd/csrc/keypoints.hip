@@ -103,7 +103,7 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
     const unsigned n = min(ctr->refined, kp.capRefined);
     const int fo = pyr.firstOctave;
-    for (unsigned k = blockIdx.x; k < n; k += gridDim.x) {
+    for (unsigned k = blockIdx.x; k < n; k += gridDim.x) {  // round-robin (see k_descriptor)
         const RefKpt kpt = load_ref(in, k);
         const int o = kpt.o, layer = kpt.layer, r = kpt.rc >> 16, c = kpt.rc & 0xffff;
         const OctGeom& g = octave_geom(pyr, o);

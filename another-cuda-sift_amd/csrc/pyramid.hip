@@ -60,9 +60,10 @@ void launch_upsample2x_u8(const uint8_t* src, int spitch, int W, int H, float* d
 }
 
 // ---------------------------------------------------------------------------
-// Separable Gaussian blur, one 64 x 32 output tile per 256-thread workgroup,
+// Separable Gaussian blur, one 64 x BLUR_TH output tile per workgroup of
+// BLUR_TH / 8 waves,
 // instantiated per radius R (taps 2R+1) so every tap loop is fully unrolled.
-// The (32+2R) x (64+2R) input tile (reflect-101 borders, optional stride-2
+// The (BLUR_TH+2R) x (64+2R) input tile (reflect-101 borders, optional stride-2
 // read = INTER_NEAREST octave decimation fused in) is staged once in LDS.
 // Row pass: 16 threads per row, each keeps a (2R+4)-float register window
 // (ds_read_b128) and runs 4 independent fma chains (4 adjacent outputs).
@@ -82,7 +83,13 @@ __device__ __forceinline__ f32x2 pk_mov_hi_lo(f32x2 a, f32x2 b) {
     return r;
 }
 constexpr int BLUR_TW = 64;
-constexpr int BLUR_TH = 32;
+#ifndef SIFT_BLUR_TH  // tile height: 64 (8 waves) beat 32 by 3-5 % of frame time (A/B builds: -DSIFT_BLUR_TH=32)
+#define SIFT_BLUR_TH 64
+#endif
+constexpr int BLUR_TH = SIFT_BLUR_TH;
+constexpr int BLUR_NW = BLUR_TH / 8;       // waves per workgroup: 8 output rows each in the column pass
+constexpr int BLUR_THREADS = 64 * BLUR_NW;
+static_assert(BLUR_TH % 8 == 0 && BLUR_NW <= 16, "blur tile height");
 
 // One blur launch's job: plane src (stride-sstep read = fused INTER_NEAREST
 // decimation) -> dst, optional decimated base copy, pixel range, counters.
@@ -139,7 +146,7 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
     // loads are issued before the first LDS store.
     {
         constexpr int RW = BLUR_TW + 2 * R;  // <= 128: two column chunks
-        constexpr int RPW = (IH + 3) / 4;    // rows per wave
+        constexpr int RPW = (IH + BLUR_NW - 1) / BLUR_NW;  // rows per wave
         const int wv = __builtin_amdgcn_readfirstlane(wave);
         const bool single = W > R + 1 && H > R + 1;  // one reflection suffices
         auto refl = [&](int p, int len) {
@@ -161,7 +168,7 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
         float v0[RPW], v1[RPW];
 #pragma unroll
         for (int i = 0; i < RPW; i++) {
-            const int ly = min(wv + 4 * i, IH - 1);
+            const int ly = min(wv + BLUR_NW * i, IH - 1);
             const int roff = __builtin_amdgcn_readfirstlane(refl(y0 - R + ly, H) * spitch * sstep * ES);
             if constexpr (ES == 1) {
                 v0[i] = (float)__builtin_amdgcn_raw_buffer_load_b8(rsrc, c0, roff, 0);
@@ -173,7 +180,7 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
         }
 #pragma unroll
         for (int i = 0; i < RPW; i++) {
-            const int ly = wv + 4 * i;
+            const int ly = wv + BLUR_NW * i;
             if (ly < IH) {
                 in[ly * IW + lane] = v0[i];
                 if (lane < RW - 64) in[ly * IW + 64 + lane] = v1[i];
@@ -182,7 +189,7 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
         if (ES == 4 && copy_out) {  // decimated base plane of this octave = the tile's interior inputs
 #pragma unroll
             for (int i = 0; i < RPW; i++) {
-                const int ly = wv + 4 * i, gy = y0 - R + ly;
+                const int ly = wv + BLUR_NW * i, gy = y0 - R + ly;
                 if (ly >= R && ly < R + BLUR_TH && gy < H) {
                     float* row = copy_out + (size_t)gy * dpitch + x0 - R;
                     if (lane >= R && x0 - R + lane < W) row[lane] = v0[i];
@@ -202,7 +209,7 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
         const bool grpB = (l >= 4 && l < 12) || (l >= 16 && l < 20) || l >= 28;
         const int blk = grpB ? (l < 12 ? l - 4 : (l < 20 ? l - 8 : l - 16)) : (l < 4 ? l : (l < 16 ? l - 8 : l - 12));
         const int xq = blk * 4;
-        for (int ly = wave * 4 + (lane >> 5) * 2 + (grpB ? 1 : 0); ly < IH; ly += 16) {
+        for (int ly = wave * 4 + (lane >> 5) * 2 + (grpB ? 1 : 0); ly < IH; ly += 4 * BLUR_NW) {
             float win[4 * NW];
             const f32x4* p = reinterpret_cast<const f32x4*>(in + ly * IW + xq);
 #pragma unroll
@@ -293,20 +300,25 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
             __syncthreads();  // reuse `mid` for the per-wave partials
             if (lane == 0) {
                 mid[wave] = mx;
-                mid[4 + wave] = nmn;
+                mid[BLUR_NW + wave] = nmn;
             }
             __syncthreads();
             if (tid == 0) {  // spread over kRangeSlots address pairs: no single hot atomic
                 unsigned* slot = range_keys + 2 * (tile % kRangeSlots);
-                atomicMax(slot, range_key(fmaxf(fmaxf(mid[0], mid[1]), fmaxf(mid[2], mid[3]))));
-                atomicMax(slot + 1, range_key(fmaxf(fmaxf(mid[4], mid[5]), fmaxf(mid[6], mid[7]))));
+                float a = mid[0], b = mid[BLUR_NW];
+                for (int w = 1; w < BLUR_NW; w++) {
+                    a = fmaxf(a, mid[w]);
+                    b = fmaxf(b, mid[BLUR_NW + w]);
+                }
+                atomicMax(slot, range_key(a));
+                atomicMax(slot + 1, range_key(b));
             }
         }
     }
 }
 
 template <int R, typename T = float>
-__global__ __launch_bounds__(256) void k_blur(BlurJob J) {
+__global__ __launch_bounds__(BLUR_THREADS) void k_blur(BlurJob J) {
     __shared__ __attribute__((aligned(16))) float in[blur_lds_floats<R>()];
     blur_tile<R, T>(J, blockIdx.x, in);
 }
@@ -317,7 +329,7 @@ __global__ __launch_bounds__(256) void k_blur(BlurJob J) {
 // dispatch) and small-octave tiles fill CUs the larger
 // job leaves idle.
 template <int RA, int RB>
-__global__ __launch_bounds__(256) void k_blur2(BlurJob A, BlurJob B) {
+__global__ __launch_bounds__(BLUR_THREADS) void k_blur2(BlurJob A, BlurJob B) {
     constexpr int NA = blur_lds_floats<RA>(), NB = blur_lds_floats<RB>();
     __shared__ __attribute__((aligned(16))) float in[NA > NB ? NA : NB];
     const int na = A.ntiles * A.nf;
@@ -353,7 +365,7 @@ using BlurLaunch = void (*)(const BlurJob&, hipStream_t);
 
 template <int R>
 void blur_launch_r(const BlurJob& j, hipStream_t s) {
-    hipLaunchKernelGGL(k_blur<R>, dim3(j.ntiles * j.nf), dim3(256), 0, s, j);
+    hipLaunchKernelGGL(k_blur<R>, dim3(j.ntiles * j.nf), dim3(BLUR_THREADS), 0, s, j);
 }
 
 template <int... Rs>
@@ -366,7 +378,7 @@ static const std::array<BlurLaunch, kMaxTaps / 2> kBlurTable = blur_table(std::m
 // 5, 6, 8, 10, 13), larger radius first.  Other pairs launch separately.
 template <int RA, int RB>
 void blur2_launch(const BlurJob& a, const BlurJob& b, hipStream_t s) {
-    hipLaunchKernelGGL((k_blur2<RA, RB>), dim3(a.ntiles * a.nf + b.ntiles * b.nf), dim3(256), 0, s, a, b);
+    hipLaunchKernelGGL((k_blur2<RA, RB>), dim3(a.ntiles * a.nf + b.ntiles * b.nf), dim3(BLUR_THREADS), 0, s, a, b);
 }
 bool launch_blur_pair_jobs(const BlurJob& a, const BlurJob& b, hipStream_t s) {
     const int ra = a.taps.n >> 1, rb = b.taps.n >> 1;
@@ -408,8 +420,8 @@ bool launch_blur_u8(const uint8_t* src, int spitch, int W, int H, float* dst, in
                     const Frames& fr, long sfs, hipStream_t s, unsigned* range_keys, Counters* zero_ctr) {
     const BlurJob j = make_job(src, spitch, 1, W, H, dst, dpitch, nullptr, taps, range_keys, zero_ctr, fr, sfs);
     switch (taps.n >> 1) {
-        case 5: hipLaunchKernelGGL((k_blur<5, uint8_t>), dim3(j.ntiles * j.nf), dim3(256), 0, s, j); return true;
-        case 6: hipLaunchKernelGGL((k_blur<6, uint8_t>), dim3(j.ntiles * j.nf), dim3(256), 0, s, j); return true;
+        case 5: hipLaunchKernelGGL((k_blur<5, uint8_t>), dim3(j.ntiles * j.nf), dim3(BLUR_THREADS), 0, s, j); return true;
+        case 6: hipLaunchKernelGGL((k_blur<6, uint8_t>), dim3(j.ntiles * j.nf), dim3(BLUR_THREADS), 0, s, j); return true;
         default: return false;
     }
 }

@@ -349,7 +349,9 @@ def main():
     det2 = sift.Detector(make_config(numOctaves=0), device=local)
     det2.gpuWarmUpAndAllocate()
     sets = []
-    for i in range(2):
+    # C3 uses sets 0 and 1; C5 uses set k on rank k (world > 1), or all 8 on
+    # one GPU (world == 1 rehearsal).
+    for i in range(8 if world == 1 else max(2, world)):
         det2.detectAndCompute(sift.synth_frame(77 + i, W, H))
         det2.copyToHost(True)
         d = det2.descriptors[:2000]
@@ -393,8 +395,37 @@ def main():
     n_matches = int((out_m >= 0).sum().item())
 
     # ---- C5: 8-way (world-way) all-gather + pairwise match -------------------
+    def run_c5_single_gpu(K=8):
+        """world == 1: the 8 sets are already on this GPU (no exchange); all
+        K * (K - 1) ordered pairs in ONE batched MFMA launch."""
+        pairs = [(i, j) for i in range(K) for j in range(K) if i != j]
+        P = len(pairs)
+        bm = sift.Matcher(nq, nq, max_pairs=P, device=local)
+        bi = torch.empty((P * nq, 2), dtype=torch.int32, device=dev)
+
+        def batched():
+            bm.match_batched([sets[i].data_ptr() for i, _ in pairs], [nq] * P, [sets[j].data_ptr() for _, j in pairs],
+                             [nq] * P, idx2_ptr=bi.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+
+        for _ in range(5):
+            batched()
+        torch.cuda.synchronize()
+        m0, m1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 20
+        m0.record()
+        for _ in range(reps):
+            batched()
+        m1.record()
+        torch.cuda.synchronize()
+        ms = m0.elapsed_time(m1) / reps
+        fl = 2.0 * nq * nq * 128 * P
+        return {"virtual_ranks": K, "pairs_per_gpu": P, "batched_match_ms": round(ms, 4), "allgather_us": None,
+                "tflops": round(fl / ms / 1e9, 2), "mfma_frac": round(fl / ms / 1e9 / FP16_MFMA_PEAK_TFLOPS, 4),
+                "note": "one-GPU rehearsal of C5: all 8 sets resident, the 56 ordered 2000x2000x128 pairs in one "
+                        "batched launch (no collective on one GPU)"}
+
     def run_c5():
-        mine = sets[rank % 2].contiguous()
+        mine = sets[rank].contiguous()
 
         def gather():
             g, c = multi.all_gather_sets(mine.to(cdev), nq, world)
@@ -428,16 +459,17 @@ def main():
             batched()
         m1.record()
         torch.cuda.synchronize()
+        bms = max_over_ranks(m0.elapsed_time(m1) / 50)
+        fl = 2.0 * nq * nq * 128 * P
         return {"allgather_us": round(ag_us, 2), "pairs_per_gpu": P,
-              "batched_match_ms": round(max_over_ranks(m0.elapsed_time(m1) / 50), 4),
+              "batched_match_ms": round(bms, 4), "tflops_per_gpu": round(fl / bms / 1e9, 2),
+              "mfma_frac": round(fl / bms / 1e9 / FP16_MFMA_PEAK_TFLOPS, 4),
               "collective": f"all_gather ({a.dist_backend}; nccl = RCCL all_gather_into_tensor), sift_amd/multi.py"}
 
-    c5 = None
-    if world > 1:
-        try:
-            c5 = run_c5()
-        except Exception as e:  # keep the C2 line even if the C5 side measurement fails
-            c5 = {"error": repr(e)[:300]}
+    try:
+        c5 = run_c5() if world > 1 else run_c5_single_gpu()
+    except Exception as e:  # keep the C2 line even if the C5 side measurement fails
+        c5 = {"error": repr(e)[:300]}
 
     # ---- CPU baseline: the oracle on the host cores (rank 0, N=1 only) -------
     cpu = None
