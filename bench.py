@@ -103,10 +103,14 @@ def pmc_traffic(summary_path, kernel_names):
     cal = summ.get("calibration_counter_over_true_bytes", {})
     fetch_scale = 1.0 / cal.get("copy4:FETCH_SIZE", 0.5)
     write_scale = 1.0 / cal.get("copy4:WRITE_SIZE", 1.0)
+    rows = [k for k in summ.get("kernels", [])
+            if k["kernel"].split("<")[0].split("::")[-1] in kernel_names and "FETCH_SIZE" in k and "WRITE_SIZE" in k]
+    # The handle's warm-up launches (single-frame grids, a few per kernel) are
+    # left out: only (kernel, grid) groups dispatched as often as the timed frames.
+    top = max((k["dispatches"] for k in rows), default=0)
     tot, n = 0.0, 0
-    for k in summ.get("kernels", []):
-        base = k["kernel"].split("<")[0].split("::")[-1]
-        if base in kernel_names and "FETCH_SIZE" in k and "WRITE_SIZE" in k:
+    for k in rows:
+        if k["dispatches"] >= top // 2:
             tot += (k["FETCH_SIZE"] * fetch_scale + k["WRITE_SIZE"] * write_scale) * 1024 * k["dispatches"]
             n += k["dispatches"]
     return {"bytes_per_launch": round(tot / n), "launches": n, "source": os.path.relpath(summary_path, ROOT)} if n else None

@@ -4,7 +4,7 @@ set -o pipefail
 TAG=${1:-run}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests/ -q -m gpu -x > gpurun_out/pytest_$TAG.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/ -q -m gpu -x --timeout 120 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_$TAG.log
 # A fault, abort or time limit ends the session (no further GPU step).

@@ -15,7 +15,8 @@ def main(bench_json, trace_csv):
     groups = {}
     for r in csv.DictReader(open(trace_csv)):
         if "k_blur" in r["Kernel_Name"]:
-            key = (r["Kernel_Name"], r.get("Grid_Size", ""))
+            key = (r["Kernel_Name"], r.get("Grid_Size", ""), r.get("Grid_Size_X", ""), r.get("Grid_Size_Y", ""),
+                   r.get("Grid_Size_Z", ""))
             groups.setdefault(key, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     # The timed launches (steps x repetitions per (kernel, grid)); the handle's
     # warm-up frames (a few launches per grid, incl. one-frame grids of a
