@@ -43,8 +43,31 @@ __global__ __launch_bounds__(256) void k_refine(PyrDesc pyr, const uint2* __rest
     bitmap = fptr(bitmap, foff);
     out = fptr(out, foff);
     const unsigned n = min(ctr->cand, capCand);
-    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        refine_candidate(pyr, cand[i], ctr, bitmap, out, kp, foff);
+    const int lane = threadIdx.x & 63;
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    // Wave-uniform loop (the append below is a wave collective).
+    for (unsigned i0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < n; i0 += gridDim.x * blockDim.x) {
+        const unsigned i = i0 + lane;
+        RefKpt k;
+        long bit = 0;
+        const bool acc = i < n && refine_candidate(pyr, cand[i], bitmap, kp, foff, k, bit);
+        // One counter atomic per wave (a per-lane atomic on one address
+        // serialises in L2).
+        const unsigned long long mask = __ballot(acc);
+        if (!mask) continue;
+        unsigned wbase = 0;
+        if (lane == 0) wbase = atomicAdd(&ctr->refined, (unsigned)__popcll(mask));
+        wbase = __shfl(wbase, 0);
+        if (acc) {
+            const unsigned slot = wbase + (unsigned)__popcll(mask & lt_mask);
+            if (slot < kp.capRefined) {
+                out[slot] = k;
+            } else {
+                atomicOr(&ctr->overflow, 2u);
+                atomicAnd(&bitmap[bit >> 5], ~(1u << (bit & 31)));  // every set bit belongs to a stored keypoint
+            }
+        }
+    }
 }
 
 // Workgroups per frame of the keypoint kernels: a single frame gets `one`

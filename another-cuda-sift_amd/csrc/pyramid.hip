@@ -165,11 +165,9 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
         const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<T*>(src), 0, (int)min((long)spitch * sstep * H * ES, 0x7fffffffL), 0x00020000);
         const unsigned c0 = (unsigned)(gx0 * sstep) * ES, c1 = (unsigned)(gx1 * sstep) * ES;
+        const int rowB = spitch * sstep * ES;  // bytes per source row
         float v0[RPW], v1[RPW];
-#pragma unroll
-        for (int i = 0; i < RPW; i++) {
-            const int ly = min(wv + BLUR_NW * i, IH - 1);
-            const int roff = __builtin_amdgcn_readfirstlane(refl(y0 - R + ly, H) * spitch * sstep * ES);
+        auto ld = [&](int i, int roff) {
             if constexpr (ES == 1) {
                 v0[i] = (float)__builtin_amdgcn_raw_buffer_load_b8(rsrc, c0, roff, 0);
                 v1[i] = (float)__builtin_amdgcn_raw_buffer_load_b8(rsrc, c1, roff, 0);
@@ -177,14 +175,31 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
                 v0[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, c0, roff, 0));
                 v1[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, c1, roff, 0));
             }
-        }
+        };
+        if (y0 - R >= 0 && y0 - R + IH <= H) {
+            // Interior rows (most tiles): the row offset advances by a constant,
+            // one s_add per row.  Rows past IH of the last step read in-range
+            // data (or 0 past the buffer end) and are never stored.
+            const int rb = __builtin_amdgcn_readfirstlane((y0 - R + wv) * rowB), rs = BLUR_NW * rowB;
 #pragma unroll
-        for (int i = 0; i < RPW; i++) {
-            const int ly = wv + BLUR_NW * i;
-            if (ly < IH) {
-                in[ly * IW + lane] = v0[i];
-                if (lane < RW - 64) in[ly * IW + 64 + lane] = v1[i];
+            for (int i = 0; i < RPW; i++) ld(i, rb + i * rs);
+        } else {
+#pragma unroll
+            for (int i = 0; i < RPW; i++) {
+                const int ly = min(wv + BLUR_NW * i, IH - 1);
+                ld(i, __builtin_amdgcn_readfirstlane(refl(y0 - R + ly, H) * rowB));
             }
+        }
+        // LDS row of step i: one base address + an immediate offset per row;
+        // only the last step can fall past IH.
+        float* const irow = in + wv * IW + lane;
+#pragma unroll
+        for (int i = 0; i < RPW; i++)
+            if (i < RPW - 1 || wv + BLUR_NW * i < IH) irow[BLUR_NW * i * IW] = v0[i];
+        if (lane < RW - 64) {
+#pragma unroll
+            for (int i = 0; i < RPW; i++)
+                if (i < RPW - 1 || wv + BLUR_NW * i < IH) irow[BLUR_NW * i * IW + 64] = v1[i];
         }
         if (ES == 4 && copy_out) {  // decimated base plane of this octave = the tile's interior inputs
 #pragma unroll
@@ -269,7 +284,6 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
 #pragma unroll
         for (int j = 0; j < 4 + 2 * R; j++) cp[j] = (f32x2){vmid[j * IW], vmid[(j + 4) * IW]};
         const int gx = x0 + lx;
-        float mx = -FLT_MAX, nmn = -FLT_MAX;
         float out[8];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
@@ -279,20 +293,34 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
             out[q] = a[0];
             out[q + 4] = a[1];
         }
+        if (y0 + BLUR_TH <= H && x0 + BLUR_TW <= W) {
+            // Full tile: unconditional buffer stores, the row step in the
+            // scalar offset (no per-row address arithmetic or exec masking).
+            const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
+                dst, 0, (int)min((long)dpitch * H * 4, 0x7fffffffL), 0x00020000);
+            const unsigned voff = (unsigned)((y0 + yb) * dpitch + gx) * 4u;
 #pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const float s = out[q];
-            const int gy = y0 + yb + q;
-            if (gy < H && gx < W) {
-                dst[(size_t)gy * dpitch + gx] = s;
-                mx = fmaxf(mx, s);
-                nmn = fmaxf(nmn, -s);
+            for (int q = 0; q < 8; q++)
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, out[q]), drs, voff, q * dpitch * 4, 0);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const int gy = y0 + yb + q;
+                if (gy < H && gx < W) dst[(size_t)gy * dpitch + gx] = out[q];
             }
         }
         // Pixel range of the plane (requested for octave 0 / plane 0 only: every
         // later plane is a convex combination of it).  The descriptor sizes its
         // fixed-point histogram scale from it.
         if (range_keys) {
+            float mx = -FLT_MAX, nmn = -FLT_MAX;
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                if (y0 + yb + q < H && gx < W) {
+                    mx = fmaxf(mx, out[q]);
+                    nmn = fmaxf(nmn, -out[q]);
+                }
+            }
             for (int off = 32; off > 0; off >>= 1) {
                 mx = fmaxf(mx, __shfl_xor(mx, off));
                 nmn = fmaxf(nmn, __shfl_xor(nmn, off));

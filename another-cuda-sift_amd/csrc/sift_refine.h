@@ -1,9 +1,9 @@
-// adjustLocalExtrema (OpenCV 4.x sift.simd.hpp) for one 3x3x3 candidate, shared
-// by k_refine (keypoints.hip) and the extrema kernel's epilogue (pyramid.hip).
-// DoG values are re-formed from the Gaussian planes (G_{l+1} - G_l: the same
-// single rounding as a stored DoG).  Accepted keypoints are de-duplicated by
-// final grid position with a bitmap (OpenCV removes the same duplicates later
-// in removeDuplicatedSorted) and compacted with an atomic.
+// adjustLocalExtrema (OpenCV 4.x sift.simd.hpp) for one 3x3x3 candidate, used
+// by k_refine (keypoints.hip).  DoG values are re-formed from the Gaussian
+// planes (G_{l+1} - G_l: the same single rounding as a stored DoG).  Accepted
+// keypoints are de-duplicated by final grid position with a bitmap (OpenCV
+// removes the same duplicates later in removeDuplicatedSorted); k_refine
+// compacts them with one counter atomic per wave.
 // Reference: SiftOps.cu:63-208 + collectKpts SiftOps.cu:210-235.
 #pragma once
 #include <climits>
@@ -21,9 +21,10 @@ __device__ __forceinline__ const OctGeom& octave_geom(const PyrDesc& pyr, int o)
 // q = {octave << 8 | layer, r << 16 | c} as the extrema kernels emit it.
 // foff: byte offset of the candidate's frame arena (ctr / bitmap / out are
 // already that frame's).
-__device__ __forceinline__ void refine_candidate(const PyrDesc& pyr, uint2 q, Counters* __restrict__ ctr,
-                                                 uint32_t* __restrict__ bitmap, RefKpt* __restrict__ out,
-                                                 const KeypointParams& kp, long foff) {
+// Returns true for an accepted, first-of-its-position keypoint `k` (its
+// dedupe bit `bit` is set); the caller appends it (wave-aggregated).
+__device__ __forceinline__ bool refine_candidate(const PyrDesc& pyr, uint2 q, uint32_t* __restrict__ bitmap,
+                                                 const KeypointParams& kp, long foff, RefKpt& k, long& bit) {
     const int L = pyr.L;
     const float img_scale = 1.f / 255.f;
     const float deriv_scale = img_scale * 0.5f;
@@ -37,26 +38,28 @@ __device__ __forceinline__ void refine_candidate(const PyrDesc& pyr, uint2 q, Co
     const long ps = g.planeStride;
     const int pitch = g.pitch;
     // The 3x3 neighbourhood of Gaussian planes layer-1 .. layer+2 around
-    // (r, c): 12 row segments of 3 floats, one 12-byte buffer load each (all
-    // in flight together), instead of ~30 scattered dword loads per Newton
-    // step.  DoG values are formed from it exactly as a stored DoG
-    // (G_{l+1} - G_l, one rounding).  The block of the converged position
-    // stays in registers for the contrast and edge tests.
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(G), 0, (int)min((long)(L + 3) * ps * 4, 0x7fffffffL), 0x00020000);
+    // (r, c): 12 row segments of 3 floats, one 12-byte load each (all in
+    // flight together), instead of ~30 scattered dword loads per Newton step.
+    // The octave (hence the plane base) differs between the lanes of a wave,
+    // so these are 64-bit-address global loads: a buffer resource would be
+    // divergent and cost a readfirstlane waterfall loop per load.  Every
+    // block is inside the plane (|offset| <= 1 from a position >= kBorder
+    // from the edges, layers 0 .. L+2).  DoG values are formed from it
+    // exactly as a stored DoG (G_{l+1} - G_l, one rounding).  The block of the
+    // converged position stays in registers for the contrast and edge tests.
     float D[3][3][3];  // D[s][dy][dx] = DoG at (layer - 1 + s, r - 1 + dy, c - 1 + dx)
     auto load_block = [&]() {
-        typedef unsigned u32x3 __attribute__((ext_vector_type(3)));
         float v[4][3][3];
+        typedef const __attribute__((address_space(1))) float* gptr;  // global_load, not flat
+        const gptr b = (gptr)(G + (long)(layer - 1) * ps + (long)(r - 1) * pitch + (c - 1));
 #pragma unroll
         for (int p = 0; p < 4; p++)
 #pragma unroll
             for (int dy = 0; dy < 3; dy++) {
-                const unsigned off = (unsigned)((long)(layer - 1 + p) * ps + (long)(r - 1 + dy) * pitch + c - 1) * 4u;
-                const u32x3 w = __builtin_amdgcn_raw_buffer_load_b96(rsrc, off, 0, 0);
-                v[p][dy][0] = __uint_as_float(w.x);
-                v[p][dy][1] = __uint_as_float(w.y);
-                v[p][dy][2] = __uint_as_float(w.z);
+                const gptr e = b + p * ps + dy * pitch;
+                v[p][dy][0] = e[0];
+                v[p][dy][1] = e[1];
+                v[p][dy][2] = e[2];
             }
 #pragma unroll
         for (int p = 0; p < 3; p++)
@@ -114,7 +117,7 @@ __device__ __forceinline__ void refine_candidate(const PyrDesc& pyr, uint2 q, Co
             break;
         }
     }
-    if (!ok || it >= kMaxInterpSteps) return;
+    if (!ok || it >= kMaxInterpSteps) return false;
 
     // D still holds the block of the converged (layer, r, c).
     const float c0 = D[1][1][1];
@@ -129,7 +132,7 @@ __device__ __forceinline__ void refine_candidate(const PyrDesc& pyr, uint2 q, Co
     t += dD1 * xr;
     t += dD2 * xi;
     const float contr = c0 * img_scale + t * 0.5f;
-    if (fabsf(contr) * L < kp.contrastThreshold) return;
+    if (fabsf(contr) * L < kp.contrastThreshold) return false;
     const float v2 = c0 * 2.f;
     const float dxx = (cr + cl - v2) * second_deriv_scale;
     const float dyy = (cd + cu - v2) * second_deriv_scale;
@@ -137,14 +140,13 @@ __device__ __forceinline__ void refine_candidate(const PyrDesc& pyr, uint2 q, Co
     const float tr = dxx + dyy;
     const float det = dxx * dyy - dxy * dxy;
     const float et = kp.edgeThreshold;
-    if (det <= 0 || tr * tr * et >= (et + 1) * (et + 1) * det) return;
+    if (det <= 0 || tr * tr * et >= (et + 1) * (et + 1) * det) return false;
 
     // Duplicate (same final octave/layer/r/c) -> identical keypoint: keep one.
-    const long bit = g.bitBase + ((long)(layer - 1) * g.H + r) * g.W + c;
+    bit = g.bitBase + ((long)(layer - 1) * g.H + r) * g.W + c;
     const uint32_t m = 1u << (bit & 31);
-    if (atomicOr(&bitmap[bit >> 5], m) & m) return;
+    if (atomicOr(&bitmap[bit >> 5], m) & m) return false;
 
-    RefKpt k;
     k.x = ((float)c + xc) * (float)(1 << o);
     k.y = ((float)r + xr) * (float)(1 << o);
     k.octave = o + (layer << 8) + ((int)rint(((double)xi + 0.5) * 255) << 16);
@@ -153,13 +155,7 @@ __device__ __forceinline__ void refine_candidate(const PyrDesc& pyr, uint2 q, Co
     k.o = o;
     k.layer = layer;
     k.rc = r << 16 | c;
-    const unsigned slot = atomicAdd(&ctr->refined, 1u);
-    if (slot < kp.capRefined) {
-        out[slot] = k;
-    } else {
-        atomicOr(&ctr->overflow, 2u);
-        atomicAnd(&bitmap[bit >> 5], ~m);  // every set bit belongs to a stored keypoint
-    }
+    return true;
 }
 
 }  // namespace sift_amd
