@@ -45,9 +45,8 @@ namespace sift_amd {
 constexpr int kD = 4, kN = 8;
 constexpr int kCells = (kD + 2) * (kD + 2);  // 36 spatial cells incl. the border ring
 constexpr int kMaxRows = kDescMaxRows;       // enumerated windows: side = 2R+1 <= kMaxRows
-constexpr int kGroup = 4;                    // samples whose loads are in flight together
-constexpr int kDT = 256;                     // threads (4 waves) per keypoint
-constexpr int kPer = kDT >= 128 ? 1 : 128 / kDT;  // descriptor entries per thread in the epilogue
+constexpr int kGroup = 4;                    // samples whose loads are in flight together (raster path)
+constexpr int kItem = 2;                     // consecutive samples of one row per work item (enumerated path)
 
 struct DescGeom {
     float cos_t, sin_t, exp_scale;
@@ -84,13 +83,14 @@ __device__ __forceinline__ void trilinear(float mag, float rbf, float cbf, float
 // Shrink [lo, hi] to a superset of the integers j with -1 < j*s + b < kD
 // (margin 1e-4 in bin units and one sample each side, so float rounding of the
 // exact per-sample test can never fall outside the enumerated range).
-__device__ __forceinline__ void clip_interval(int& lo, int& hi, double s, double b, int R) {
+// inv_s = 1 / s (computed once per keypoint; an ulp of it is far inside the margins).
+__device__ __forceinline__ void clip_interval(int& lo, int& hi, double s, double inv_s, double b, int R) {
     constexpr double lb = -1.0 - 1e-4, ub = kD + 1e-4;
     if (fabs(s) < 1e-12) {
         if (b <= lb || b >= ub) hi = lo - 1;
         return;
     }
-    double x1 = (lb - b) / s, x2 = (ub - b) / s;
+    double x1 = (lb - b) * inv_s, x2 = (ub - b) * inv_s;
     if (x1 > x2) {
         const double t = x1;
         x1 = x2;
@@ -128,25 +128,26 @@ __device__ __forceinline__ float desc_magnitude(float x, float y) {
 }
 __device__ __forceinline__ float desc_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
 
-// DescJob read with scalar loads from the constant address space: every field
-// is uniform and lives in SGPRs.
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 struct JobWords {
     u32x4 w[4];
 };
 
-__device__ __forceinline__ DescJob load_job(const DescJob* jobs, unsigned p) {
-    const __attribute__((address_space(4))) u32x4* c = (const __attribute__((address_space(4))) u32x4*)(jobs + p);
-    JobWords r;
-#pragma unroll
-    for (int i = 0; i < 4; i++) r.w[i] = c[i];
-    return __builtin_bit_cast(DescJob, r);
-}
+#ifdef SIFT_DESC_STAMPS
+__device__ unsigned long long g_desc_stamps[8];
+#endif
 
-__global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ jobs, const Counters* __restrict__ ctr,
+// kDT threads per keypoint: 4 waves for a single frame (few keypoints, the
+// chip needs the parallelism inside each), 2 waves for frame batches (more
+// keypoints in flight per CU: 296 vs 311 us per 8-frame launch, tools/ab_*).
+#ifndef SIFT_DESC_WAVES
+#define SIFT_DESC_WAVES 6  // min waves per SIMD (VGPR budget <= 80): 198 us vs 208 (5) and 211 (8) per 8-frame launch
+#endif
+template <int kDT>
+__global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJob* __restrict__ jobs, const Counters* __restrict__ ctr,
                                                    const unsigned* __restrict__ range_keys,
                                                    uint16_t* __restrict__ desc, Counters* __restrict__ host_ctr,
-                                                   long fs) {
+                                                   long fs, unsigned nf) {
     // Two u32 fixed-point histograms so that each sample's orientation pair
     // (o0, o0+1) is one naturally aligned ds_add_u64 (low word o0, high word
     // o0+1): even o0 -> histE[cell*8 + o], odd o0 -> histO[cell*10 + 1 + o]
@@ -155,20 +156,26 @@ __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ 
     __shared__ __attribute__((aligned(16))) unsigned histE[kCells * 8 + kCells * 10];
     unsigned* histO = histE + kCells * 8;
     __shared__ __attribute__((aligned(16))) float sq[128];
-    __shared__ int rowpre[kMaxRows + 4], rowlo[kMaxRows];
+    __shared__ int rowpre[kMaxRows + 4], rowlo[kMaxRows], rowln[kMaxRows];
     __shared__ float s_norm[12];
+    constexpr int kPer = kDT >= 128 ? 1 : 128 / kDT;  // descriptor entries per thread in the epilogue
 
     const int tid = threadIdx.x, lane = tid & 63;
-    const long foff = blockIdx.y * fs;  // frame blockIdx.y
+    // 1-D grid, frame = block % nf: consecutive workgroups are dispatched to
+    // consecutive XCDs, so with 8 frames each frame's keypoints run on one
+    // XCD (its L2 serves neighbouring keypoints' overlapping windows, in
+    // row order) instead of every XCD fetching lines of every frame.
+    const unsigned frame = blockIdx.x % nf, wg = blockIdx.x / nf, nwg = gridDim.x / nf;
+    const long foff = frame * fs;
     jobs = fptr(jobs, foff);
     ctr = fptr(ctr, foff);
     range_keys = fptr(range_keys, foff);
     desc = fptr(desc, foff);
-    host_ctr += blockIdx.y;
+    host_ctr += frame;
     const unsigned n = ctr->final_n;
     // The frame's counters are final before this (last) kernel starts: hand
     // them to the host's pinned copy directly (no D2H copy node in the graph).
-    if (blockIdx.x == 0 && tid < (int)(sizeof(Counters) / 4))
+    if (wg == 0 && tid < (int)(sizeof(Counters) / 4))
         reinterpret_cast<unsigned*>(host_ctr)[tid] = reinterpret_cast<const unsigned*>(ctr)[tid];
     // Pixel range of the frame; it bounds every Gaussian plane (convex blurs).
     unsigned kmax = 0, knmn = 0;
@@ -187,8 +194,35 @@ __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ 
     // (octave, layer, row) order and their cost grows with scale, so handing
     // each XCD a contiguous run (L2 locality) unbalances the XCDs -- measured
     // 10-30 % slower frames.
-    for (unsigned p = blockIdx.x; p < n; p += gridDim.x) {
-        const DescJob jb = load_job(jobs, p);
+#ifndef SIFT_DESC_VARIANT
+#define SIFT_DESC_VARIANT 0
+#endif
+    unsigned sink = 0;  // timing variant 2 only
+    // Jobs are prefetched one keypoint ahead as vector loads (lanes 0-15, one
+    // dword each) and moved to SGPRs with v_readlane: a scalar load at the
+    // top of each keypoint would expose a memory latency per keypoint, and a
+    // scalar prefetch would be waited for by the body's first lgkmcnt(0).
+    const unsigned* __restrict__ jw = reinterpret_cast<const unsigned*>(jobs);
+    unsigned jnext = n ? jw[min(wg, n - 1) * 16u + (lane & 15)] : 0u;
+#ifdef SIFT_DESC_STAMPS  // in-kernel phase timing (tools only): s_memtime deltas per phase, summed
+    unsigned long long st_acc[4] = {0, 0, 0, 0}, st_prev = __builtin_amdgcn_s_memtime();
+#define SIFT_STAMP(ph)                                              \
+    do {                                                            \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        st_acc[ph] += t_ - st_prev;                                 \
+        st_prev = t_;                                               \
+    } while (0)
+#else
+#define SIFT_STAMP(ph) (void)0
+#endif
+    for (unsigned p = wg; p < n; p += nwg) {
+        SIFT_STAMP(0);
+        const unsigned jcur = jnext;
+        jnext = jw[min(p + nwg, n - 1) * 16u + (lane & 15)];
+        JobWords jwd;
+#pragma unroll
+        for (int q = 0; q < 16; q++) jwd.w[q >> 2][q & 3] = __builtin_amdgcn_readlane(jcur, q);
+        const DescJob jb = __builtin_bit_cast(DescJob, jwd);
         DescGeom G;
         G.cos_t = jb.cos_t;
         G.sin_t = jb.sin_t;
@@ -204,14 +238,17 @@ __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ 
 
         for (int i = tid; i < kCells * 18; i += kDT) histE[i] = 0u;
         if (enumerated) {
+            const double inv_sin = 1.0 / (double)G.sin_t, inv_cos = 1.0 / (double)G.cos_t;
             for (int t = tid; t < side; t += kDT) {
                 const int i = t - radius, r = G.pty + i;
                 int lo = max(-radius, 1 - G.ptx), hi = min(radius, G.cols - 2 - G.ptx);
                 if (r <= 0 || r >= G.rows - 1) hi = lo - 1;
-                clip_interval(lo, hi, (double)G.sin_t, (double)i * G.cos_t + (kD / 2 - 0.5), radius);
-                clip_interval(lo, hi, (double)G.cos_t, -(double)i * G.sin_t + (kD / 2 - 0.5), radius);
+                clip_interval(lo, hi, (double)G.sin_t, inv_sin, (double)i * G.cos_t + (kD / 2 - 0.5), radius);
+                clip_interval(lo, hi, (double)G.cos_t, inv_cos, -(double)i * G.sin_t + (kD / 2 - 0.5), radius);
+                const int len = max(hi - lo + 1, 0);
                 rowlo[t] = lo;
-                rowpre[t + 1] = max(hi - lo + 1, 0);
+                rowln[t] = len;
+                rowpre[t + 1] = (len + kItem - 1) / kItem;  // items of kItem consecutive samples
             }
             if (tid == 0) rowpre[0] = 0;
             lds_barrier();
@@ -237,14 +274,16 @@ __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ 
         const int S = min(31 - e, 40);
         const float fxs = ldexpf(1.f, S);
         lds_barrier();
+        SIFT_STAMP(1);
 
         // One sample from its four neighbours (l, r, u, d).
         // One sample from its four neighbours (l, r, u, d).  Branch-free so
         // that the kGroup samples of a group interleave (ILP): a rejected
         // sample keeps in-range bin indices and adds zeros.
-        auto accumulate = [&](int i, int j, bool in, float l, float r, float u, float d) {
-            float rbin, cbin, c_rot, r_rot;
-            const bool valid = desc_sample(G, i, j, rbin, cbin, c_rot, r_rot) && in;
+        auto accum_rot = [&](float c_rot, float r_rot, bool valid, float l, float r, float u, float d) {
+            float rbin = r_rot + (float)(kD / 2) - 0.5f;
+            float cbin = c_rot + (float)(kD / 2) - 0.5f;
+            valid = valid && rbin > -1 && rbin < kD && cbin > -1 && cbin < kD;
             const float dx = r - l, dy = u - d;
             const float wgt = desc_exp((c_rot * c_rot + r_rot * r_rot) * G.exp_scale);
             const float gori = desc_atan2(dy, dx);
@@ -271,9 +310,18 @@ __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ 
                 const int off = (q & 4 ? (kD + 2) * stride : 0) + (q & 2 ? stride : 0);
                 const unsigned lo = (unsigned)v[q];  // truncation: < 2^-S per contribution
                 const unsigned hi = (unsigned)v[q + 1];
+#if SIFT_DESC_VARIANT == 2  // timing variant: no LDS atomics
+                sink += lo ^ hi ^ (unsigned)(uintptr_t)(hb + off);
+#else
                 atomicAdd(reinterpret_cast<unsigned long long*>(hb + off),
                           ((unsigned long long)hi << 32) | (unsigned long long)lo);
+#endif
             }
+        };
+        auto accumulate = [&](int i, int j, bool in, float l, float r, float u, float d) {
+            float rbin, cbin, c_rot, r_rot;
+            const bool valid = desc_sample(G, i, j, rbin, cbin, c_rot, r_rot) && in;
+            accum_rot(c_rot, r_rot, valid, l, r, u, d);
         };
         // Gradient loads of up to kGroup samples, then their accumulation.
         // Samples outside the plane read 0 (buffer range check) and are
@@ -283,6 +331,10 @@ __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ 
 #pragma unroll
             for (int t = 0; t < kGroup; t++) {
                 const unsigned o = (unsigned)((G.pty + gi[t]) * jb.pitch + G.ptx + gj[t]) * 4u;
+#if SIFT_DESC_VARIANT == 3  // timing variant: no gradient loads
+                l[t] = (float)(o & 255); r[t] = (float)((o >> 3) & 255); u[t] = (float)((o >> 5) & 255); d[t] = (float)((o >> 7) & 255);
+                continue;
+#endif
                 l[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o - 4u, 0, 0));
                 r[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o + 4u, 0, 0));
                 u[t] = __builtin_bit_cast(float,
@@ -295,7 +347,17 @@ __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ 
         };
 
         if (enumerated) {
+            // Work items of kItem (2) consecutive samples of one row: their
+            // neighbours come in as one 16-byte and two 8-byte loads instead of
+            // four dword loads per sample, and i * sin / i * cos are shared.  Each thread takes a contiguous run
+            // of items.  Rows hold only in-image samples (the intervals are
+            // clipped to 1 .. cols-2 / rows 1 .. rows-2), so validity is the
+            // oracle's bin-range test alone.
+#if SIFT_DESC_VARIANT == 1
+            const int N = 0;
+#else
             const int N = rowpre[side];
+#endif
             const int run = (N + kDT - 1) / kDT;
             const int k0 = min(N, tid * run), k1 = min(N, k0 + run);
             if (k0 < k1) {
@@ -306,22 +368,40 @@ __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ 
                     else hi = mid - 1;
                 }
                 int row = lo;
-                int j = rowlo[row] + (k0 - rowpre[row]);
-                int jend = rowlo[row] + (rowpre[row + 1] - rowpre[row]) - 1;
-                for (int q = k0; q < k1; q += kGroup) {
-                    int gi[kGroup], gj[kGroup];
+                int jj = rowlo[row] + kItem * (k0 - rowpre[row]);
+                int jend = rowlo[row] + rowln[row];  // exclusive
+                typedef float f32x4d __attribute__((ext_vector_type(4)));
+                typedef float f32x2d __attribute__((ext_vector_type(2)));
+                const int pitch4 = 4 * jb.pitch;
+                for (int k = k0; k < k1; k++) {
+                    const int i = row - radius;
+                    const int cnt = jend - jj;
+                    const unsigned o = (unsigned)((G.pty + i) * jb.pitch + G.ptx + jj) * 4u;
+                    static_assert(kItem == 2, "item loads below are for pairs");
+                    // (x-1 .. x+2) of the row, (x, x+1) of the rows above and below.
+                    const f32x4d cm = __builtin_bit_cast(f32x4d, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o - 4u, 0, 0));
+                    const f32x2d up = __builtin_bit_cast(f32x2d, __builtin_amdgcn_raw_buffer_load_b64(rsrc, o - pitch4, 0, 0));
+                    const f32x2d dn = __builtin_bit_cast(f32x2d, __builtin_amdgcn_raw_buffer_load_b64(rsrc, o + pitch4, 0, 0));
+                    const float fi = (float)i, is = fi * G.sin_t, ic = fi * G.cos_t;
+                    const float row6[4] = {cm[0], cm[1], cm[2], cm[3]};
 #pragma unroll
-                    for (int t = 0; t < kGroup; t++) {
-                        gi[t] = row - radius;
-                        gj[t] = j;
-                        if (q + t + 1 < k1 && ++j > jend) {
-                            do row++;
-                            while (rowpre[row + 1] == rowpre[row]);
-                            j = rowlo[row];
-                            jend = j + (rowpre[row + 1] - rowpre[row]) - 1;
-                        }
+                    for (int t = 0; t < kItem; t++) {
+                        const float fj = (float)(jj + t);
+                        // desc_sample's rotation, operation for operation.
+                        const float c_rot = fj * G.cos_t - is;
+                        const float r_rot = fj * G.sin_t + ic;
+                        accum_rot(c_rot, r_rot, t < cnt, row6[t], row6[t + 2], up[t], dn[t]);
+                        // One sample at a time: interleaving the four keeps
+                        // ~90 VGPRs live (occupancy 5 instead of 8 waves/SIMD).
+                        __builtin_amdgcn_sched_barrier(0);
                     }
-                    group(gi, gj, k1 - q);
+                    jj += kItem;
+                    if (k + 1 < k1 && jj >= jend) {  // next non-empty row
+                        do row++;
+                        while (rowpre[row + 1] == rowpre[row]);
+                        jj = rowlo[row];
+                        jend = jj + rowln[row];
+                    }
                 }
             }
         } else {  // huge window: the full raster, rejected samples included
@@ -338,6 +418,7 @@ __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ 
             }
         }
         lds_barrier();
+        SIFT_STAMP(2);
 
         // Wrap, L2 norm (8 fma lanes, then v_reduce_sum's pairing), 0.2 clip.
         const float inv = ldexpf(1.f, -S);
@@ -388,18 +469,37 @@ __global__ __launch_bounds__(kDT) void k_descriptor(const DescJob* __restrict__ 
             int v = cv_round(val[h] * scale);
             v = v < 0 ? 0 : (v > 255 ? 255 : v);
             const _Float16 hv = (_Float16)(float)v;
-            if (tid + kDT * h < 128) desc[(size_t)p * 128 + tid + kDT * h] = __builtin_bit_cast(uint16_t, hv);
+            if (tid + kDT * h < 128) desc[(size_t)p * 128 + tid + kDT * h] = __builtin_bit_cast(uint16_t, hv) + (uint16_t)(sink == 0x12345u);
         }
         lds_barrier();  // sq / histograms are rewritten by the next keypoint
+        SIFT_STAMP(3);
     }
+#ifdef SIFT_DESC_STAMPS
+    if (tid == 0) {
+        for (int q = 0; q < 4; q++) atomicAdd(&g_desc_stamps[q], st_acc[q]);
+        atomicAdd(&g_desc_stamps[4], (unsigned long long)((n > wg) ? (n - wg + nwg - 1) / nwg : 0));
+        atomicAdd(&g_desc_stamps[5], 1ull);
+    }
+#endif
 }
+
+#ifdef SIFT_DESC_STAMPS
+extern "C" int sift_hip_debug_desc_stamps(unsigned long long* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_desc_stamps), sizeof(g_desc_stamps));
+}
+#endif
 
 void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned* range_keys, uint16_t* desc,
                        Counters* host_ctr, const KeypointParams& kp, const Frames& fr, hipStream_t s) {
     (void)kp;
-    const int per = fr.nf <= 1 ? 8192 : std::max(2048, 16384 / fr.nf);  // workgroups per frame
-    hipLaunchKernelGGL(k_descriptor, dim3(per, fr.nf), dim3(kDT), 0, s, jobs, ctr, range_keys, desc, host_ctr,
-                       fr.stride);
+    if (fr.nf <= 1) {
+        hipLaunchKernelGGL(k_descriptor<256>, dim3(8192), dim3(256), 0, s, jobs, ctr, range_keys, desc, host_ctr,
+                           fr.stride, 1u);
+    } else {
+        const int per = std::max(2048, 16384 / fr.nf) * 2;  // workgroups per frame
+        hipLaunchKernelGGL(k_descriptor<128>, dim3(per * fr.nf), dim3(128), 0, s, jobs, ctr, range_keys, desc,
+                           host_ctr, fr.stride, (unsigned)fr.nf);
+    }
 }
 
 }  // namespace sift_amd
