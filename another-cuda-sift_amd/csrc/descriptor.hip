@@ -46,7 +46,10 @@ constexpr int kD = 4, kN = 8;
 constexpr int kCells = (kD + 2) * (kD + 2);  // 36 spatial cells incl. the border ring
 constexpr int kMaxRows = kDescMaxRows;       // enumerated windows: side = 2R+1 <= kMaxRows
 constexpr int kGroup = 4;                    // samples whose loads are in flight together (raster path)
-constexpr int kItem = 2;                     // consecutive samples of one row per work item (enumerated path)
+#ifndef SIFT_DESC_ITEM
+#define SIFT_DESC_ITEM 2
+#endif
+constexpr int kItem = SIFT_DESC_ITEM;        // consecutive samples of one row per work item (enumerated path)
 
 struct DescGeom {
     float cos_t, sin_t, exp_scale;
@@ -377,13 +380,26 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
                     const int i = row - radius;
                     const int cnt = jend - jj;
                     const unsigned o = (unsigned)((G.pty + i) * jb.pitch + G.ptx + jj) * 4u;
-                    static_assert(kItem == 2, "item loads below are for pairs");
-                    // (x-1 .. x+2) of the row, (x, x+1) of the rows above and below.
-                    const f32x4d cm = __builtin_bit_cast(f32x4d, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o - 4u, 0, 0));
-                    const f32x2d up = __builtin_bit_cast(f32x2d, __builtin_amdgcn_raw_buffer_load_b64(rsrc, o - pitch4, 0, 0));
-                    const f32x2d dn = __builtin_bit_cast(f32x2d, __builtin_amdgcn_raw_buffer_load_b64(rsrc, o + pitch4, 0, 0));
+                    // (x-1 .. x+kItem) of the row, (x .. x+kItem-1) of the rows above and below.
+                    float row6[kItem + 2], up[kItem], dn[kItem];
+                    {
+                        const f32x4d cm = __builtin_bit_cast(f32x4d, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o - 4u, 0, 0));
+                        if constexpr (kItem == 2) {
+                            const f32x2d u2 = __builtin_bit_cast(f32x2d, __builtin_amdgcn_raw_buffer_load_b64(rsrc, o - pitch4, 0, 0));
+                            const f32x2d d2 = __builtin_bit_cast(f32x2d, __builtin_amdgcn_raw_buffer_load_b64(rsrc, o + pitch4, 0, 0));
+                            for (int t = 0; t < 2; t++) up[t] = u2[t], dn[t] = d2[t];
+                        } else {
+                            static_assert(kItem == 4, "items of 2 or 4 samples");
+                            const f32x2d ce = __builtin_bit_cast(f32x2d, __builtin_amdgcn_raw_buffer_load_b64(rsrc, o + 12u, 0, 0));
+                            const f32x4d u4 = __builtin_bit_cast(f32x4d, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o - pitch4, 0, 0));
+                            const f32x4d d4 = __builtin_bit_cast(f32x4d, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o + pitch4, 0, 0));
+                            for (int t = 0; t < 4; t++) up[t] = u4[t], dn[t] = d4[t];
+                            row6[4] = ce[0];
+                            row6[5] = ce[1];
+                        }
+                        for (int t = 0; t < 4; t++) row6[t] = cm[t];
+                    }
                     const float fi = (float)i, is = fi * G.sin_t, ic = fi * G.cos_t;
-                    const float row6[4] = {cm[0], cm[1], cm[2], cm[3]};
 #pragma unroll
                     for (int t = 0; t < kItem; t++) {
                         const float fj = (float)(jj + t);
