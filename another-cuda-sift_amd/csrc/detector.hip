@@ -1058,14 +1058,14 @@ int sift_hip_debug_candidates(sift_hip_t d, int* quads, int cap, int* count) {
 struct sift_hip_matcher {
     int device = 0;
     int maxQ = 0, maxT = 0, maxP = 0;
-    float4* dPart = nullptr;
-    float* dQnorm = nullptr;
+    unsigned long long* dKeys = nullptr;  // running top-2 keys per (pair, query), all ones between calls
+    unsigned* dDone = nullptr;            // finished splits per (pair, 32-query block), zero between calls
     int* dMatch = nullptr;
     static constexpr int kMaxSplits = 256;
     ~sift_hip_matcher() {
         (void)hipSetDevice(device);
-        if (dPart) (void)hipFree(dPart);
-        if (dQnorm) (void)hipFree(dQnorm);
+        if (dKeys) (void)hipFree(dKeys);
+        if (dDone) (void)hipFree(dDone);
         if (dMatch) (void)hipFree(dMatch);
     }
 };
@@ -1085,11 +1085,13 @@ int sift_hip_matcher_create(int device, int max_query, int max_train, int max_pa
     m->maxQ = max_query;
     m->maxT = max_train;
     m->maxP = max_pairs;
+    const size_t nkeys = 2 * (size_t)max_pairs * max_query, nblk = (size_t)max_pairs * ((max_query + 31) / 32);
     if (hipSetDevice(m->device) != hipSuccess ||
-        hipMalloc((void**)&m->dPart, sizeof(float4) * (size_t)max_pairs * sift_hip_matcher::kMaxSplits * max_query) !=
-            hipSuccess ||
-        hipMalloc((void**)&m->dQnorm, sizeof(float) * (size_t)max_pairs * max_query) != hipSuccess ||
-        hipMalloc((void**)&m->dMatch, sizeof(int) * (size_t)max_pairs * max_query) != hipSuccess) {
+        hipMalloc((void**)&m->dKeys, sizeof(unsigned long long) * nkeys) != hipSuccess ||
+        hipMalloc((void**)&m->dDone, sizeof(unsigned) * nblk) != hipSuccess ||
+        hipMalloc((void**)&m->dMatch, sizeof(int) * (size_t)max_pairs * max_query) != hipSuccess ||
+        hipMemset(m->dKeys, 0xff, sizeof(unsigned long long) * nkeys) != hipSuccess ||
+        hipMemset(m->dDone, 0, sizeof(unsigned) * nblk) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
         delete m;
         return fail(SIFT_HIP_ERR_NOMEM, "matcher allocation failed");
     }
@@ -1120,7 +1122,7 @@ int sift_hip_match_batched(sift_hip_matcher_t m, int P, const uint16_t* const* q
     }
     HIPCHK(hipSetDevice(m->device));
     const int S = std::min(match_splits(maxq, maxt, P), (int)sift_hip_matcher::kMaxSplits);
-    launch_match(b, S, m->maxQ, m->dPart, m->dQnorm, ratio, ratio_on_squared, idx2, d2, match, (hipStream_t)stream);
+    launch_match(b, S, m->maxQ, m->dKeys, m->dDone, ratio, ratio_on_squared, idx2, d2, match, (hipStream_t)stream);
     HIPCHK(hipGetLastError());
     return SIFT_HIP_OK;
 }

@@ -62,23 +62,46 @@ __device__ __forceinline__ half8 load_frag(const uint16_t* row, int koff) {
     return *reinterpret_cast<const half8*>(row + koff);
 }
 
-__device__ __forceinline__ float sumsq(const half8& v) {
-    float s = 0.f;
+constexpr int kNone = 0x7fffffff;
+
+// |v|^2 over a lane's eight 8-element fragments: v_dot2_f32_f16 in four
+// independent chains (exact: integer products, partial sums < 2^24).
+__device__ __forceinline__ float sumsq8(const half8 (&v)[8]) {
+    typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+    float c[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-        const float f = (float)v[j];
-        s = __fmaf_rn(f, f, s);
-    }
-    return s;
+    for (int s = 0; s < 8; s++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const half2v x = {v[s][2 * j], v[s][2 * j + 1]};
+            c[j] = __builtin_amdgcn_fdot2(x, x, c[j], false);
+        }
+    return (c[0] + c[1]) + (c[2] + c[3]);
 }
 
-constexpr int kNone = 0x7fffffff;
+// Global top-2 of a query across the S split workgroups, by 64-bit atomicMin
+// on keys (d^2 bits << 32 | train index): d^2 >= 0 orders like its bits, and
+// the index breaks ties to the lower train row (OpenCV's order).  A split
+// min's its best into K1; whatever it displaced (or its best, if that lost)
+// and its runner-up are candidates for K2, of which the smaller is min'ed in
+// (the larger can never be second).  Every key except the final K1 reaches
+// K2 this way, so K2 ends as the true second.  All exchange goes through
+// device-scope atomics (coherent across XCDs, no cache write-back fences);
+// the last split of a query block (a counter) decodes, writes the outputs
+// and resets keys and counter for the next call.
+__device__ __forceinline__ unsigned long long match_key(float d2, int idx) {
+    return idx == kNone ? ~0ull : ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)idx;
+}
 
 // grid = (query blocks of 32, train splits, pairs); 4 waves per workgroup share
 // the query block and stride over the split's 32-row train tiles.
-__global__ __launch_bounds__(256) void k_match_partial(MatchBatch batch, int S, int nq_stride, float4* __restrict__ part,
-                                                       float* __restrict__ qnorm) {
+__global__ __launch_bounds__(256) void k_match_partial(MatchBatch batch, int S, int nq_stride,
+                                                       unsigned long long* __restrict__ keys,
+                                                       unsigned* __restrict__ done, float ratio, int ratio_on_squared,
+                                                       int* __restrict__ idx2, float* __restrict__ d2out,
+                                                       int* __restrict__ match) {
     __shared__ Top2 wtop[4][32];
+    __shared__ unsigned s_last;
     const int p = blockIdx.z;
     const MatchPair& pr = batch.pair[p];
     const int q0 = blockIdx.x * 32;
@@ -90,12 +113,9 @@ __global__ __launch_bounds__(256) void k_match_partial(MatchBatch batch, int S, 
     const int qrow = q0 + col;
     const bool qvalid = qrow < pr.nq;
     half8 bq[8];
-    float qn = 0.f;
 #pragma unroll
-    for (int s = 0; s < 8; s++) {
-        bq[s] = qvalid ? load_frag(pr.q + (size_t)qrow * 128, 16 * s + 8 * h) : half8{};
-        qn += sumsq(bq[s]);
-    }
+    for (int s = 0; s < 8; s++) bq[s] = qvalid ? load_frag(pr.q + (size_t)qrow * 128, 16 * s + 8 * h) : half8{};
+    float qn = sumsq8(bq);
     qn += __shfl_xor(qn, 32);
 
     const int ntiles = (pr.nt + 31) / 32;
@@ -108,16 +128,19 @@ __global__ __launch_bounds__(256) void k_match_partial(MatchBatch batch, int S, 
         const int trow = t0 + col;
         const bool tvalid = trow < pr.nt;
         half8 a[8];
-        float tn = 0.f;
 #pragma unroll
-        for (int s = 0; s < 8; s++) {
-            a[s] = tvalid ? load_frag(pr.t + (size_t)trow * 128, 16 * s + 8 * h) : half8{};
-            tn += sumsq(a[s]);
-        }
+        for (int s = 0; s < 8; s++) a[s] = tvalid ? load_frag(pr.t + (size_t)trow * 128, 16 * s + 8 * h) : half8{};
+        float tn = sumsq8(a);
         tn += __shfl_xor(tn, 32);
-        f32x16 acc = {};
+        // Two independent accumulation chains (even / odd K blocks), summed:
+        // exact for integer descriptors (every partial sum < 2^24).
+        f32x16 acc = {}, acc2 = {};
 #pragma unroll
-        for (int s = 0; s < 8; s++) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[s], bq[s], acc, 0, 0, 0);
+        for (int s = 0; s < 8; s += 2) {
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[s], bq[s], acc, 0, 0, 0);
+            acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[s + 1], bq[s + 1], acc2, 0, 0, 0);
+        }
+        acc += acc2;
 #pragma unroll
         for (int i = 0; i < 16; i++) {
             const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
@@ -148,32 +171,28 @@ __global__ __launch_bounds__(256) void k_match_partial(MatchBatch batch, int S, 
         r = merge_top2(r, wtop[2][col]);
         r = merge_top2(r, wtop[3][col]);
         if (qvalid) {
-            part[((size_t)p * S + split) * nq_stride + qrow] =
-                make_float4(r.d1, __int_as_float(r.i1), r.d2, __int_as_float(r.i2));
-            if (split == 0) qnorm[(size_t)p * nq_stride + qrow] = qn;
+            unsigned long long* K = keys + 2 * ((size_t)p * nq_stride + qrow);
+            const unsigned long long a1 = match_key(r.d1 + qn, r.i1), a2 = match_key(r.d2 + qn, r.i2);
+            if (a1 != ~0ull) {
+                const unsigned long long o1 = atomicMin(&K[0], a1);
+                const unsigned long long c = a1 < o1 ? o1 : a1;
+                const unsigned long long o2 = atomicMin(&K[1], c < a2 ? c : a2);
+                __asm__ volatile("" ::"v"(o2));  // returned: the min is performed before the count below
+            }
         }
     }
-}
-
-__global__ __launch_bounds__(256) void k_match_merge(MatchBatch batch, int S, int nq_stride, const float4* __restrict__ part,
-                                                     const float* __restrict__ qnorm, float ratio, int ratio_on_squared,
-                                                     int* __restrict__ idx2, float* __restrict__ d2out,
-                                                     int* __restrict__ match) {
-    const int p = blockIdx.y;
-    const MatchPair& pr = batch.pair[p];
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= pr.nq) return;
-    const int ntiles = (pr.nt + 31) / 32;
-    const int tps = (ntiles + S - 1) / S;
-    Top2 r{INFINITY, INFINITY, kNone, kNone};
-    for (int s = 0; s < S; s++) {
-        if (s * tps >= ntiles) break;
-        const float4 v = part[((size_t)p * S + s) * nq_stride + q];
-        r = merge_top2(r, Top2{v.x, v.z, __float_as_int(v.y), __float_as_int(v.w)});
-    }
-    const float qn = qnorm[(size_t)p * nq_stride + q];
-    const int i1 = r.i1 == kNone ? -1 : r.i1, i2 = r.i2 == kNone ? -1 : r.i2;
-    const float e1 = i1 >= 0 ? r.d1 + qn : FLT_MAX, e2 = i2 >= 0 ? r.d2 + qn : FLT_MAX;
+    __syncthreads();
+    unsigned* cnt = done + (size_t)p * gridDim.x + blockIdx.x;
+    if (threadIdx.x == 0) s_last = atomicAdd(cnt, 1u) == (unsigned)(S - 1);
+    __syncthreads();
+    if (!s_last || threadIdx.x >= 32 || q0 + (int)threadIdx.x >= pr.nq) return;
+    const int q = q0 + threadIdx.x;
+    unsigned long long* K = keys + 2 * ((size_t)p * nq_stride + q);
+    const unsigned long long k1 = atomicExch(&K[0], ~0ull), k2 = atomicExch(&K[1], ~0ull);
+    if (threadIdx.x == 0) atomicExch(cnt, 0u);
+    const int i1 = k1 == ~0ull ? -1 : (int)(unsigned)k1, i2 = k2 == ~0ull ? -1 : (int)(unsigned)k2;
+    const float e1 = i1 >= 0 ? __uint_as_float((unsigned)(k1 >> 32)) : FLT_MAX;
+    const float e2 = i2 >= 0 ? __uint_as_float((unsigned)(k2 >> 32)) : FLT_MAX;
     const size_t o = (size_t)pr.out_off + q;
     if (idx2) {
         idx2[2 * o] = i1;
@@ -207,14 +226,12 @@ int match_splits(int max_nq, int max_nt, int P) {
     return S;
 }
 
-void launch_match(const MatchBatch& batch, int S, int nq_stride, float4* part, float* qnorm, float ratio,
+void launch_match(const MatchBatch& batch, int S, int nq_stride, unsigned long long* keys, unsigned* done, float ratio,
                   int ratio_on_squared, int* idx2, float* d2, int* match, hipStream_t s) {
     int max_nq = 1;
     for (int p = 0; p < batch.P; p++) max_nq = max(max_nq, batch.pair[p].nq);
     dim3 g1((max_nq + 31) / 32, S, batch.P);
-    hipLaunchKernelGGL(k_match_partial, g1, dim3(256), 0, s, batch, S, nq_stride, part, qnorm);
-    dim3 g2((max_nq + 255) / 256, batch.P);
-    hipLaunchKernelGGL(k_match_merge, g2, dim3(256), 0, s, batch, S, nq_stride, part, qnorm, ratio, ratio_on_squared,
+    hipLaunchKernelGGL(k_match_partial, g1, dim3(256), 0, s, batch, S, nq_stride, keys, done, ratio, ratio_on_squared,
                        idx2, d2, match);
 }
 

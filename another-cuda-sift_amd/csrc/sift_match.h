@@ -22,7 +22,9 @@ struct MatchBatch {
 };
 
 int match_splits(int max_nq, int max_nt, int P);
-void launch_match(const MatchBatch& batch, int S, int nq_stride, float4* part, float* qnorm, float ratio,
+// keys: 2 x u64 per (pair, query), all ones between calls; done: a counter per
+// (pair, 32-query block), zero between calls (the merging workgroup resets both).
+void launch_match(const MatchBatch& batch, int S, int nq_stride, unsigned long long* keys, unsigned* done, float ratio,
                   int ratio_on_squared, int* idx2, float* d2, int* match, hipStream_t s);
 
 }  // namespace sift_amd
