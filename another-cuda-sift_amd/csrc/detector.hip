@@ -566,8 +566,12 @@ void enqueue_body(sift_hip_detector* d, int slot, int nf) {
                  [&] { launch_bucket_scatter(d->dOri, d->dCtr, d->dBoff, d->dSlot, d->dOrder, d->kp, fr, s); });
     }
     d->timed("bucket_rank", 0, [&] {
-        launch_bucket_rank(d->pyr, d->dOri, d->dBcount, d->dBoff, d->dOrder, d->dCtr, d->dJobs, d->dKpts3[slot],
-                           d->dFeats4[slot], d->kp, fr, s);
+        if (d->kp.numBuckets <= kOrderMaxBuckets)
+            launch_rank_final(d->pyr, d->dOri, d->dBcount, d->dBoff, d->dOrder, d->dCtr, d->dJobs, d->dKpts3[slot],
+                              d->dFeats4[slot], d->kp, fr, s);
+        else  // bucket_count needs zeroed counts: the bucket-parallel ranking re-zeroes them
+            launch_bucket_rank(d->pyr, d->dOri, d->dBcount, d->dBoff, d->dOrder, d->dCtr, d->dJobs, d->dKpts3[slot],
+                               d->dFeats4[slot], d->kp, fr, s);
     });
     d->timed("descriptor", 0, [&] {
         launch_descriptor(d->dJobs, d->dCtr, range_keys(d, parity), d->dDesc[slot], d->hCtrDev + (size_t)slot * d->B,

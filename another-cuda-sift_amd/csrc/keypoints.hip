@@ -554,6 +554,7 @@ __global__ __launch_bounds__(1024) void k_order(const OriKpt* __restrict__ kpts,
         }
         if (tid == 0) {
             ctr->final_n = min(total, kp.capFinal);
+            ctr->pad[0] = total;  // entries of `order` (k_rank_final)
             if (total > kp.capFinal) atomicOr(&ctr->overflow, 8u);
         }
     }
@@ -659,6 +660,54 @@ __global__ __launch_bounds__(256) void k_bucket_rank(PyrDesc pyr, const OriKpt* 
         }
         if (lane == 0) bcount[b] = 0u;  // zero for the next frame (no memset node)
     }
+}
+
+// The same final order, parallel over keypoints instead of buckets (k_order
+// path, where bcount/boff are rewritten every frame for every non-empty bucket
+// and nothing reads an empty one): thread per position of `order`; its
+// keypoint's rank inside its row bucket = bucket entries with a smaller sub
+// key (buckets hold a few keypoints).  Every keypoint's chain of dependent
+// loads runs at once instead of one bucket after another per wave.
+__global__ __launch_bounds__(256) void k_rank_final(PyrDesc pyr, const OriKpt* __restrict__ kpts,
+                                                    const unsigned* __restrict__ bcount,
+                                                    const unsigned* __restrict__ boff, const int* __restrict__ order,
+                                                    const Counters* __restrict__ ctr, DescJob* __restrict__ jobs,
+                                                    float* __restrict__ kpts3, float* __restrict__ feats4,
+                                                    KeypointParams kp, long fs) {
+    const long foff = blockIdx.y * fs;  // frame blockIdx.y
+    kpts = fptr(kpts, foff);
+    bcount = fptr(bcount, foff);
+    boff = fptr(boff, foff);
+    order = fptr(order, foff);
+    ctr = fptr(ctr, foff);
+    jobs = fptr(jobs, foff);
+    kpts3 = fptr(kpts3, foff);
+    feats4 = fptr(feats4, foff);
+    // Every entry of `order` (a bucket straddling capFinal still has
+    // positions below it); positions >= capFinal are dropped.
+    const unsigned n = ctr->pad[0];
+    const unsigned cap = kp.capFinal;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const OriKpt k = kpts[order[i]];
+        const unsigned base = boff[k.bucket], cnt = bcount[k.bucket];
+        unsigned rank = 0;
+        for (unsigned f = 0; f < cnt; f++) rank += (unsigned)(kpts[order[base + f]].sub < k.sub);
+        const unsigned pos = base + rank;
+        if (pos < cap) {
+            jobs[pos] = make_desc_job(pyr, k, foff);
+            kpts3[3 * (size_t)pos + 0] = k.x;
+            kpts3[3 * (size_t)pos + 1] = k.y;
+            kpts3[3 * (size_t)pos + 2] = (float)((k.octave >> 8) & 255);
+            reinterpret_cast<float4*>(feats4)[pos] = make_float4((float)k.octave, k.size, k.response, k.angle);
+        }
+    }
+}
+
+void launch_rank_final(const PyrDesc& pyr, const OriKpt* kpts, const unsigned* bcount, const unsigned* boff,
+                       const int* order, const Counters* ctr, DescJob* jobs, float* kpts3, float* feats4,
+                       const KeypointParams& kp, const Frames& fr, hipStream_t s) {
+    hipLaunchKernelGGL(k_rank_final, dim3(64, fr.nf), dim3(256), 0, s, pyr, kpts, bcount, boff, order, ctr, jobs, kpts3,
+                       feats4, kp, fr.stride);
 }
 
 void launch_bucket_rank(const PyrDesc& pyr, const OriKpt* kpts, unsigned* bcount, const unsigned* boff,

@@ -73,7 +73,7 @@ struct Counters {
     unsigned final_n;    // after retainBest (written by the bucket scan)
     unsigned overflow;   // bit 0 cand, 1 refined, 2 oriented, 3 final
     unsigned thr_bits;   // retainBest response threshold (float bits)
-    unsigned pad[2];
+    unsigned pad[2];     // pad[0]: entries of the order list (k_order path)
 };
 
 // --- launch wrappers (implemented in pyramid.hip / keypoints.hip / match.hip) --
@@ -160,6 +160,9 @@ struct DescJob {
 };
 static_assert(sizeof(DescJob) == 64, "DescJob is one 64-byte scalar load");
 
+void launch_rank_final(const PyrDesc& pyr, const OriKpt* kpts, const unsigned* bcount, const unsigned* boff,
+                       const int* order, const Counters* ctr, DescJob* jobs, float* kpts3, float* feats4,
+                       const KeypointParams& kp, const Frames& fr, hipStream_t s);
 void launch_bucket_rank(const PyrDesc& pyr, const OriKpt* kpts, unsigned* bcount, const unsigned* boff,
                         const int* order, const Counters* ctr, DescJob* jobs, float* kpts3, float* feats4,
                         const KeypointParams& kp, const Frames& fr, hipStream_t s);
