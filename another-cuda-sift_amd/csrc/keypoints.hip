@@ -205,12 +205,17 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
                 }
                 return eq;
             };
-            int less_s;
-            const unsigned long long eq_s = rank_of(bin, less_s);
-            if (valid) chunk[less_s + __popcll(eq_s & lt_mask)] = w * mag;
             int start;  // lanes >= 36 query bins no sample has: cb = 0
-            const int cb = __popcll(rank_of(lane, start));
+            const unsigned long long eq_l = rank_of(lane, start);
+            const int cb = __popcll(eq_l);
             const int incl = start + cb;
+            // A sample's less(bin) and eq(bin) are those lane `bin` just
+            // computed for its own key: three shuffles instead of a second
+            // radix rank per sample.
+            const int less_s = __shfl(start, bin);
+            const unsigned long long eq_s = ((unsigned long long)(unsigned)__shfl((int)(eq_l >> 32), bin) << 32) |
+                                            (unsigned)__shfl((int)(unsigned)eq_l, bin);
+            if (valid) chunk[less_s + __popcll(eq_s & lt_mask)] = w * mag;
             lds_barrier();
             // Lane b (< 36; others have cb = 0) adds its bin's values in order,
             // four LDS reads in flight at a time.
