@@ -44,6 +44,7 @@ namespace sift_amd {
 
 constexpr int kD = 4, kN = 8;
 constexpr int kCells = (kD + 2) * (kD + 2);  // 36 spatial cells incl. the border ring
+constexpr int kCellW = 10;                   // dwords per cell in each fixed-point histogram
 constexpr int kMaxRows = kDescMaxRows;       // enumerated windows: side = 2R+1 <= kMaxRows
 constexpr int kGroup = 4;                    // samples whose loads are in flight together (raster path)
 #ifndef SIFT_DESC_ITEM
@@ -69,18 +70,25 @@ __device__ __forceinline__ bool desc_sample(const DescGeom& G, int i, int j, flo
 }
 
 // The 8 contributions of one sample, OpenCV's order and names (v_rco[r][c][o]).
+// Independent pairs go through v_pk_mul_f32 / v_pk_add_f32 (each half an IEEE
+// op, so every value is the oracle's): 8 VALU instead of 14.
+typedef float f32x2t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void trilinear(float mag, float rbf, float cbf, float obf, float v[8]) {
     const float v_r1 = mag * rbf, v_r0 = mag - v_r1;
-    const float v_rc11 = v_r1 * cbf, v_rc10 = v_r1 - v_rc11;
-    const float v_rc01 = v_r0 * cbf, v_rc00 = v_r0 - v_rc01;
-    v[7] = v_rc11 * obf;
-    v[6] = v_rc11 - v[7];
-    v[5] = v_rc10 * obf;
-    v[4] = v_rc10 - v[5];
-    v[3] = v_rc01 * obf;
-    v[2] = v_rc01 - v[3];
-    v[1] = v_rc00 * obf;
-    v[0] = v_rc00 - v[1];
+    const f32x2t r10 = {v_r1, v_r0};
+    const f32x2t rc_1 = r10 * (f32x2t){cbf, cbf};  // (v_rc11, v_rc01)
+    const f32x2t rc_0 = r10 - rc_1;                // (v_rc10, v_rc00)
+    const f32x2t ob = {obf, obf};
+    const f32x2t hi_a = rc_1 * ob, hi_b = rc_0 * ob;  // (v7, v3), (v5, v1)
+    const f32x2t lo_a = rc_1 - hi_a, lo_b = rc_0 - hi_b;  // (v6, v2), (v4, v0)
+    v[7] = hi_a[0];
+    v[3] = hi_a[1];
+    v[5] = hi_b[0];
+    v[1] = hi_b[1];
+    v[6] = lo_a[0];
+    v[2] = lo_a[1];
+    v[4] = lo_b[0];
+    v[0] = lo_b[1];
 }
 
 // Shrink [lo, hi] to a superset of the integers j with -1 < j*s + b < kD
@@ -153,11 +161,11 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
                                                    long fs, unsigned nf) {
     // Two u32 fixed-point histograms so that each sample's orientation pair
     // (o0, o0+1) is one naturally aligned ds_add_u64 (low word o0, high word
-    // o0+1): even o0 -> histE[cell*8 + o], odd o0 -> histO[cell*10 + 1 + o]
+    // o0+1): even o0 -> histE[cell*10 + o], odd o0 -> histO[cell*10 + 1 + o]
     // (slot 9 = orientation 8, wrapped into 0 at the end).  The per-keypoint
     // scale keeps every bin below 2^31, so no carry crosses the word boundary.
-    __shared__ __attribute__((aligned(16))) unsigned histE[kCells * 8 + kCells * 10];
-    unsigned* histO = histE + kCells * 8;
+    __shared__ __attribute__((aligned(16))) unsigned histE[2 * kCells * kCellW];
+    unsigned* histO = histE + kCells * kCellW;
     __shared__ __attribute__((aligned(16))) float sq[128];
     __shared__ int rowpre[kMaxRows + 4], rowlo[kMaxRows], rowln[kMaxRows];
     __shared__ float s_norm[12];
@@ -239,7 +247,7 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
         const __amdgpu_buffer_rsrc_t rsrc =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(jb.img), 0, jb.rows * jb.pitch * 4, 0x00020000);
 
-        for (int i = tid; i < kCells * 18; i += kDT) histE[i] = 0u;
+        for (int i = tid; i < 2 * kCells * kCellW; i += kDT) histE[i] = 0u;
         if (enumerated) {
             const double inv_sin = 1.0 / (double)G.sin_t, inv_cos = 1.0 / (double)G.cos_t;
             for (int t = tid; t < side; t += kDT) {
@@ -284,33 +292,41 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
         // that the kGroup samples of a group interleave (ILP): a rejected
         // sample keeps in-range bin indices and adds zeros.
         auto accum_rot = [&](float c_rot, float r_rot, bool valid, float l, float r, float u, float d) {
-            float rbin = r_rot + (float)(kD / 2) - 0.5f;
-            float cbin = c_rot + (float)(kD / 2) - 0.5f;
+            // (cbin, rbin) and the squared radius as packed pairs (IEEE per half).
+            const f32x2t rot = {c_rot, r_rot};
+            const f32x2t bins = (rot + (f32x2t){(float)(kD / 2), (float)(kD / 2)}) - (f32x2t){0.5f, 0.5f};
+            float cbin = bins[0], rbin = bins[1];
             valid = valid && rbin > -1 && rbin < kD && cbin > -1 && cbin < kD;
             const float dx = r - l, dy = u - d;
-            const float wgt = desc_exp((c_rot * c_rot + r_rot * r_rot) * G.exp_scale);
+            const f32x2t sq = rot * rot;
+            const float wgt = desc_exp((sq[0] + sq[1]) * G.exp_scale);
             const float gori = desc_atan2(dy, dx);
             const float gmag = desc_magnitude(dx, dy);
             float obin = (gori - jb.angle) * bins_per_rad;
             // x 2^S (exact): the trilinear parts come out in fixed-point units.
             const float mag = valid ? gmag * wgt * fxs : 0.f;
-            const int r0 = min(max(cv_floor(rbin), -1), kD - 1), c0 = min(max(cv_floor(cbin), -1), kD - 1);
-            int o0 = cv_floor(obin);
-            rbin -= (float)r0;
-            cbin -= (float)c0;
-            obin -= (float)o0;
+            // cvFloor in the float domain (the clamp only guards rejected
+            // samples): r - floor(r) is the oracle's r - (float)cvFloor(r).
+            const float r0f = fminf(fmaxf(floorf(rbin), -1.f), (float)(kD - 1));
+            const float c0f = fminf(fmaxf(floorf(cbin), -1.f), (float)(kD - 1));
+            const float o0f = floorf(obin);
+            rbin -= r0f;
+            cbin -= c0f;
+            obin -= o0f;
+            int o0 = (int)o0f;
             if (o0 < 0) o0 += kN;
             if (o0 >= kN) o0 -= kN;
             o0 &= kN - 1;  // no-op for valid samples (o0 in [0, 8) already)
-            const int cell = (r0 + 1) * (kD + 2) + c0 + 1;
-            const bool odd = o0 & 1;
-            const int stride = odd ? 10 : 8;  // dwords per cell
-            unsigned* hb = odd ? histO + cell * 10 + 1 + o0 : histE + cell * 8 + o0;
+            const int cell = ((int)r0f + 1) * (kD + 2) + (int)c0f + 1;
+            const int odd = o0 & 1;
+            // Both histograms have 10 dwords per cell, so the four u64 adds of
+            // a sample sit at constant offsets from hb (immediate offsets).
+            unsigned* hb = (odd ? histO : histE) + cell * kCellW + o0 + odd;
             float v[8];
             trilinear(mag, rbin, cbin, obin, v);
 #pragma unroll
             for (int q = 0; q < 8; q += 2) {
-                const int off = (q & 4 ? (kD + 2) * stride : 0) + (q & 2 ? stride : 0);
+                const int off = (q & 4 ? (kD + 2) * kCellW : 0) + (q & 2 ? kCellW : 0);
                 const unsigned lo = (unsigned)v[q];  // truncation: < 2^-S per contribution
                 const unsigned hi = (unsigned)v[q + 1];
 #if SIFT_DESC_VARIANT == 2  // timing variant: no LDS atomics
@@ -403,10 +419,11 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
 #pragma unroll
                     for (int t = 0; t < kItem; t++) {
                         const float fj = (float)(jj + t);
-                        // desc_sample's rotation, operation for operation.
-                        const float c_rot = fj * G.cos_t - is;
-                        const float r_rot = fj * G.sin_t + ic;
-                        accum_rot(c_rot, r_rot, t < cnt, row6[t], row6[t + 2], up[t], dn[t]);
+                        // desc_sample's rotation, operation for operation
+                        // (c = j*cos - i*sin, r = j*sin + i*cos), packed.
+                        const f32x2t pr = (f32x2t){fj, fj} * (f32x2t){G.cos_t, G.sin_t};
+                        const f32x2t rot = pr + (f32x2t){-is, ic};
+                        accum_rot(rot[0], rot[1], t < cnt, row6[t], row6[t + 2], up[t], dn[t]);
                         // One sample at a time: interleaving the four keeps
                         // ~90 VGPRs live (occupancy 5 instead of 8 waves/SIMD).
                         __builtin_amdgcn_sched_barrier(0);
@@ -444,8 +461,8 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
             const int t = min(tid + kDT * h, 127);  // threads past 128 mirror entry 127 (never stored)
             const int ii = t >> 5, jj = (t >> 3) & 3, kk = t & 7;
             const int cell = (ii + 1) * (kD + 2) + (jj + 1);
-            unsigned long long hv = (unsigned long long)histE[cell * 8 + kk] + histO[cell * 10 + 1 + kk];
-            if (kk == 0) hv += histO[cell * 10 + 9];
+            unsigned long long hv = (unsigned long long)histE[cell * kCellW + kk] + histO[cell * kCellW + 1 + kk];
+            if (kk == 0) hv += histO[cell * kCellW + 9];
             val[h] = (float)((double)hv * (double)inv);
             if (tid + kDT * h < 128) sq[t] = val[h];
         }
