@@ -90,9 +90,13 @@ constexpr int BLUR_TW = 64;
 #define SIFT_BLUR_TH 64
 #endif
 constexpr int BLUR_TH = SIFT_BLUR_TH;
-constexpr int BLUR_NW = BLUR_TH / 8;       // waves per workgroup: 8 output rows each in the column pass
+#ifndef SIFT_BLUR_NW
+#define SIFT_BLUR_NW (SIFT_BLUR_TH / 8)
+#endif
+constexpr int BLUR_NW = SIFT_BLUR_NW;      // waves per workgroup
+constexpr int BLUR_CB = BLUR_TH / (8 * BLUR_NW);  // 8-row column-pass blocks per wave
 constexpr int BLUR_THREADS = 64 * BLUR_NW;
-static_assert(BLUR_TH % 8 == 0 && BLUR_NW <= 16, "blur tile height");
+static_assert(BLUR_TH % (8 * BLUR_NW) == 0 && BLUR_NW <= 16, "blur tile height");
 
 // One blur launch's job: plane src (stride-sstep read = fused INTER_NEAREST
 // decimation) -> dst, optional decimated base copy, pixel range, counters.
@@ -296,8 +300,11 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
     __syncthreads();
     BLUR_STAMP(2);  // row pass + barrier
 
-    {
-        const int lx = lane, yb = wave * 8;
+    float mx = -FLT_MAX, nmn = -FLT_MAX;  // pixel range (range_keys only)
+    const int gx = x0 + lane;
+#pragma unroll
+    for (int cbk = 0; cbk < BLUR_CB; cbk++) {
+        const int lx = lane, yb = (wave + cbk * BLUR_NW) * 8;
         // Column pairs (c[i], c[i+4]), one ds_read2st64_b32 each: output rows
         // (q, q+4) share every v_pk_add/v_pk_fma_f32 and no pair is assembled
         // from two loads.
@@ -318,7 +325,6 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
 #pragma unroll
         for (int j = 0; j < 4 + 2 * R; j++) cp[j] = (f32x2){vmid[j * IW], vmid[(j + 4) * IW]};
 #endif
-        const int gx = x0 + lx;
         float out[8];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
@@ -344,16 +350,7 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
                 if (gy < H && gx < W) dst[(size_t)gy * dpitch + gx] = out[q];
             }
         }
-        BLUR_STAMP(3);  // column pass, stores issued
-#ifdef SIFT_BLUR_STAMPS
-        __builtin_amdgcn_s_waitcnt(0);
-        BLUR_STAMP(4);  // stores done
-#endif
-        // Pixel range of the plane (requested for octave 0 / plane 0 only: every
-        // later plane is a convex combination of it).  The descriptor sizes its
-        // fixed-point histogram scale from it.
         if (range_keys) {
-            float mx = -FLT_MAX, nmn = -FLT_MAX;
 #pragma unroll
             for (int q = 0; q < 8; q++) {
                 if (y0 + yb + q < H && gx < W) {
@@ -361,6 +358,18 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
                     nmn = fmaxf(nmn, -out[q]);
                 }
             }
+        }
+    }
+    BLUR_STAMP(3);  // column pass, stores issued
+#ifdef SIFT_BLUR_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+    BLUR_STAMP(4);  // stores done
+#endif
+    {
+        // Pixel range of the plane (requested for octave 0 / plane 0 only: every
+        // later plane is a convex combination of it).  The descriptor sizes its
+        // fixed-point histogram scale from it.
+        if (range_keys) {
             for (int off = 32; off > 0; off >>= 1) {
                 mx = fmaxf(mx, __shfl_xor(mx, off));
                 nmn = fmaxf(nmn, __shfl_xor(nmn, off));
