@@ -189,6 +189,30 @@ def test_matcher_exact(sift, oracle, nq, nt):
     assert np.array_equal(gm, exp)
 
 
+def test_matcher_cross_split_ties_and_reuse(sift, oracle):
+    """Ties between train rows in different split workgroups (the 64-bit key
+    merge must keep the lower index), and repeated calls on one matcher (the
+    merging workgroup restores keys and counters for the next call)."""
+    nq, nt = 300, 2000
+    rng = np.random.default_rng(11)
+    t = rng.integers(0, 256, (nt, 128)).astype(np.float32)
+    t[1990] = t[7]  # same row far apart: different splits
+    t[1500] = t[7]
+    q = rng.integers(0, 256, (nq, 128)).astype(np.float32)
+    q[0] = t[7]
+    q[1] = t[7] + 1
+    dq, dt = sift.DeviceArray.from_numpy(_half_rows(q)), sift.DeviceArray.from_numpy(_half_rows(t))
+    m = sift.Matcher(nq, nt)
+    oi, od = oracle.knn2(q, t)
+    assert tuple(oi[0]) == (7, 1500)
+    for rep in range(4):
+        idx2, d2 = sift.DeviceArray(nq * 8), sift.DeviceArray(nq * 8)
+        n = nq if rep % 2 == 0 else 137  # smaller call in between
+        m.match_device(dq.value, n, dt.value, nt, 0.8, False, idx2.value, d2.value, 0)
+        gi = idx2.to_numpy(np.int32, (nq, 2))[:n]
+        assert np.array_equal(gi, oi[:n]), rep
+
+
 def test_match_batched_equals_pairs(sift, oracle):
     rng = np.random.default_rng(5)
     sets = [rng.integers(0, 256, (n, 128)).astype(np.float32) for n in (300, 257, 64, 500)]
