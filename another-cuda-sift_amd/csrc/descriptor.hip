@@ -529,7 +529,12 @@ void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned*
         hipLaunchKernelGGL(k_descriptor<256>, dim3(8192), dim3(256), 0, s, jobs, ctr, range_keys, desc, host_ctr,
                            fr.stride, 1u);
     } else {
-        const int per = std::max(2048, 16384 / fr.nf) * 2;  // workgroups per frame
+        // Workgroups per frame: 2048 at 8 frames (16384 in all).  The bigger
+        // grids this kernel once had filled every CU slot and kept the other
+        // stream's pyramid kernels out; with fewer workgroups (each looping
+        // over more keypoints) the two co-reside: +2-3 % frame rate
+        // (tools/grid_sweep.sh).
+        const int per = std::max(1024, 16384 / fr.nf);
         hipLaunchKernelGGL(k_descriptor<128>, dim3(per * fr.nf), dim3(128), 0, s, jobs, ctr, range_keys, desc,
                            host_ctr, fr.stride, (unsigned)fr.nf);
     }

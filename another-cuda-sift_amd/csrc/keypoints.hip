@@ -281,7 +281,11 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
 
 void launch_orientation(const PyrDesc& pyr, const RefKpt* in, Counters* ctr, OriKpt* out, uint32_t* bitmap,
                         const KeypointParams& kp, const Frames& fr, hipStream_t s) {
-    hipLaunchKernelGGL(k_orientation, dim3(per_frame_blocks(8192, fr.nf), fr.nf), dim3(64), 0, s, pyr, in, ctr, out,
+    // One-wave workgroups per frame: 8192 for a single frame, 1024 at 8 frames.
+    // Grids that fill every wave slot keep the other stream's pyramid kernels
+    // out; this size lets them co-reside (+2-4 % frame rate, tools/grid_sweep.sh).
+    const int per = fr.nf <= 1 ? 8192 : std::max(256, 8192 / fr.nf);
+    hipLaunchKernelGGL(k_orientation, dim3(per, fr.nf), dim3(64), 0, s, pyr, in, ctr, out,
                        bitmap, kp, fr.stride);
 }
 
