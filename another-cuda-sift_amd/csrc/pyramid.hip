@@ -61,7 +61,7 @@ void launch_upsample2x_u8(const uint8_t* src, int spitch, int W, int H, float* d
 
 // ---------------------------------------------------------------------------
 // Separable Gaussian blur, one 64 x BLUR_TH output tile per workgroup of
-// BLUR_TH / 8 waves,
+// BLUR_NW waves (each BLUR_TH / BLUR_NW rows of the column pass),
 // instantiated per radius R (taps 2R+1) so every tap loop is fully unrolled.
 // The (BLUR_TH+2R) x (64+2R) input tile (reflect-101 borders, optional stride-2
 // read = INTER_NEAREST octave decimation fused in) is staged once in LDS.
@@ -90,8 +90,8 @@ constexpr int BLUR_TW = 64;
 #define SIFT_BLUR_TH 64
 #endif
 constexpr int BLUR_TH = SIFT_BLUR_TH;
-#ifndef SIFT_BLUR_NW
-#define SIFT_BLUR_NW (SIFT_BLUR_TH / 8)
+#ifndef SIFT_BLUR_NW  // 4 waves (16 column-pass rows each): the blur holds half of a CU's wave
+#define SIFT_BLUR_NW 4   // slots, so the other stream's keypoint kernels co-reside (+0.7 % frame rate vs 8)
 #endif
 constexpr int BLUR_NW = SIFT_BLUR_NW;      // waves per workgroup
 constexpr int BLUR_CB = BLUR_TH / (8 * BLUR_NW);  // 8-row column-pass blocks per wave
