@@ -534,7 +534,11 @@ void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned*
         // stream's pyramid kernels out; with fewer workgroups (each looping
         // over more keypoints) the two co-reside: +2-3 % frame rate
         // (tools/grid_sweep.sh).
+#ifdef SIFT_DESC_PER  // tools A/B builds
+        const int per = SIFT_DESC_PER;
+#else
         const int per = std::max(1024, 16384 / fr.nf);
+#endif
         hipLaunchKernelGGL(k_descriptor<128>, dim3(per * fr.nf), dim3(128), 0, s, jobs, ctr, range_keys, desc,
                            host_ctr, fr.stride, (unsigned)fr.nf);
     }

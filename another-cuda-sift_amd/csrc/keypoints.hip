@@ -284,7 +284,11 @@ void launch_orientation(const PyrDesc& pyr, const RefKpt* in, Counters* ctr, Ori
     // One-wave workgroups per frame: 8192 for a single frame, 1024 at 8 frames.
     // Grids that fill every wave slot keep the other stream's pyramid kernels
     // out; this size lets them co-reside (+2-4 % frame rate, tools/grid_sweep.sh).
+#ifdef SIFT_ORI_PER  // tools A/B builds
+    const int per = fr.nf <= 1 ? 8192 : SIFT_ORI_PER;
+#else
     const int per = fr.nf <= 1 ? 8192 : std::max(256, 8192 / fr.nf);
+#endif
     hipLaunchKernelGGL(k_orientation, dim3(per, fr.nf), dim3(64), 0, s, pyr, in, ctr, out,
                        bitmap, kp, fr.stride);
 }
