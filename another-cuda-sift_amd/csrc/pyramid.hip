@@ -90,13 +90,16 @@ constexpr int BLUR_TW = 64;
 #define SIFT_BLUR_TH 64
 #endif
 constexpr int BLUR_TH = SIFT_BLUR_TH;
-#ifndef SIFT_BLUR_NW  // 4 waves (16 column-pass rows each): the blur holds half of a CU's wave
-#define SIFT_BLUR_NW 4   // slots, so the other stream's keypoint kernels co-reside (+0.7 % frame rate vs 8)
+// Waves per workgroup NW (a template parameter): 4 for launches of >= 2048
+// tiles (octave-0 launches of frame batches: 2-8 % faster per launch, and a
+// workgroup pair holds half of a CU's wave slots, so the other stream's
+// keypoint kernels co-reside), 8 for the small launches (more waves per tile
+// hide their latency better).
+#ifndef SIFT_BLUR_BIG_TILES
+#define SIFT_BLUR_BIG_TILES 2048
 #endif
-constexpr int BLUR_NW = SIFT_BLUR_NW;      // waves per workgroup
-constexpr int BLUR_CB = BLUR_TH / (8 * BLUR_NW);  // 8-row column-pass blocks per wave
-constexpr int BLUR_THREADS = 64 * BLUR_NW;
-static_assert(BLUR_TH % (8 * BLUR_NW) == 0 && BLUR_NW <= 16, "blur tile height");
+static_assert(BLUR_TH % 32 == 0, "blur tile height: 8-row column blocks for 4 or 8 waves");
+static int blur_waves(int tiles) { return tiles >= SIFT_BLUR_BIG_TILES ? 4 : 8; }
 
 // One blur launch's job: plane src (stride-sstep read = fused INTER_NEAREST
 // decimation) -> dst, optional decimated base copy, pixel range, counters.
@@ -137,8 +140,10 @@ extern "C" int sift_hip_debug_blur_stamps(unsigned long long* out) {
 #define BLUR_STAMP(ph) (void)0
 #endif
 
-template <int R, typename T>
+template <int R, typename T, int NWAVES>
 __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __restrict__ in) {
+    constexpr int BLUR_NW = NWAVES;                   // waves per workgroup
+    constexpr int BLUR_CB = BLUR_TH / (8 * BLUR_NW);  // 8-row column-pass blocks per wave
 #ifdef SIFT_BLUR_STAMPS
     unsigned long long bst_prev = __builtin_amdgcn_s_memtime();
     if (threadIdx.x == 0) atomicAdd(&g_blur_stamps[R][5], 1ull);
@@ -394,10 +399,10 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
     }
 }
 
-template <int R, typename T = float>
-__global__ __launch_bounds__(BLUR_THREADS) void k_blur(BlurJob J) {
+template <int R, typename T, int NW>
+__global__ __launch_bounds__(64 * NW) void k_blur(BlurJob J) {
     __shared__ __attribute__((aligned(16))) float in[blur_lds_floats<R>()];
-    blur_tile<R, T>(J, blockIdx.x, in);
+    blur_tile<R, T, NW>(J, blockIdx.x, in);
 }
 
 // Two independent blur jobs in one launch (blocks [0, A.ntiles) take A): the
@@ -405,15 +410,15 @@ __global__ __launch_bounds__(BLUR_THREADS) void k_blur(BlurJob J) {
 // do not depend on, so a frame needs fewer launches (each costs ~0.7-1.5 us of
 // dispatch) and small-octave tiles fill CUs the larger
 // job leaves idle.
-template <int RA, int RB>
-__global__ __launch_bounds__(BLUR_THREADS) void k_blur2(BlurJob A, BlurJob B) {
+template <int RA, int RB, int NW>
+__global__ __launch_bounds__(64 * NW) void k_blur2(BlurJob A, BlurJob B) {
     constexpr int NA = blur_lds_floats<RA>(), NB = blur_lds_floats<RB>();
     __shared__ __attribute__((aligned(16))) float in[NA > NB ? NA : NB];
     const int na = A.ntiles * A.nf;
     if ((int)blockIdx.x < na)
-        blur_tile<RA, float>(A, blockIdx.x, in);
+        blur_tile<RA, float, NW>(A, blockIdx.x, in);
     else
-        blur_tile<RB, float>(B, blockIdx.x - na, in);
+        blur_tile<RB, float, NW>(B, blockIdx.x - na, in);
 }
 
 static BlurJob make_job(const void* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, float* copy_out,
@@ -442,7 +447,11 @@ using BlurLaunch = void (*)(const BlurJob&, hipStream_t);
 
 template <int R>
 void blur_launch_r(const BlurJob& j, hipStream_t s) {
-    hipLaunchKernelGGL(k_blur<R>, dim3(j.ntiles * j.nf), dim3(BLUR_THREADS), 0, s, j);
+    const int tiles = j.ntiles * j.nf;
+    if (blur_waves(tiles) == 4)
+        hipLaunchKernelGGL((k_blur<R, float, 4>), dim3(tiles), dim3(256), 0, s, j);
+    else
+        hipLaunchKernelGGL((k_blur<R, float, 8>), dim3(tiles), dim3(512), 0, s, j);
 }
 
 template <int... Rs>
@@ -455,7 +464,11 @@ static const std::array<BlurLaunch, kMaxTaps / 2> kBlurTable = blur_table(std::m
 // 5, 6, 8, 10, 13), larger radius first.  Other pairs launch separately.
 template <int RA, int RB>
 void blur2_launch(const BlurJob& a, const BlurJob& b, hipStream_t s) {
-    hipLaunchKernelGGL((k_blur2<RA, RB>), dim3(a.ntiles * a.nf + b.ntiles * b.nf), dim3(BLUR_THREADS), 0, s, a, b);
+    const int tiles = a.ntiles * a.nf + b.ntiles * b.nf;
+    if (blur_waves(tiles) == 4)
+        hipLaunchKernelGGL((k_blur2<RA, RB, 4>), dim3(tiles), dim3(256), 0, s, a, b);
+    else
+        hipLaunchKernelGGL((k_blur2<RA, RB, 8>), dim3(tiles), dim3(512), 0, s, a, b);
 }
 bool launch_blur_pair_jobs(const BlurJob& a, const BlurJob& b, hipStream_t s) {
     const int ra = a.taps.n >> 1, rb = b.taps.n >> 1;
@@ -496,9 +509,17 @@ bool launch_blur_pair(const BlurDesc& a, const BlurDesc& b, const Frames& fr, hi
 bool launch_blur_u8(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, const Taps& taps,
                     const Frames& fr, long sfs, hipStream_t s, unsigned* range_keys, Counters* zero_ctr) {
     const BlurJob j = make_job(src, spitch, 1, W, H, dst, dpitch, nullptr, taps, range_keys, zero_ctr, fr, sfs);
+    const int tiles = j.ntiles * j.nf;
+    const bool big = blur_waves(tiles) == 4;
     switch (taps.n >> 1) {
-        case 5: hipLaunchKernelGGL((k_blur<5, uint8_t>), dim3(j.ntiles * j.nf), dim3(BLUR_THREADS), 0, s, j); return true;
-        case 6: hipLaunchKernelGGL((k_blur<6, uint8_t>), dim3(j.ntiles * j.nf), dim3(BLUR_THREADS), 0, s, j); return true;
+        case 5:
+            if (big) hipLaunchKernelGGL((k_blur<5, uint8_t, 4>), dim3(tiles), dim3(256), 0, s, j);
+            else hipLaunchKernelGGL((k_blur<5, uint8_t, 8>), dim3(tiles), dim3(512), 0, s, j);
+            return true;
+        case 6:
+            if (big) hipLaunchKernelGGL((k_blur<6, uint8_t, 4>), dim3(tiles), dim3(256), 0, s, j);
+            else hipLaunchKernelGGL((k_blur<6, uint8_t, 8>), dim3(tiles), dim3(512), 0, s, j);
+            return true;
         default: return false;
     }
 }
