@@ -539,8 +539,11 @@ void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned*
 #else
         const int per = std::max(1024, 16384 / fr.nf);
 #endif
-        hipLaunchKernelGGL(k_descriptor<128>, dim3(per * fr.nf), dim3(128), 0, s, jobs, ctr, range_keys, desc,
-                           host_ctr, fr.stride, (unsigned)fr.nf);
+#ifndef SIFT_DESC_BATCH_DT
+#define SIFT_DESC_BATCH_DT 128  // threads per keypoint for frame batches (tools A/B builds vary it)
+#endif
+        hipLaunchKernelGGL(k_descriptor<SIFT_DESC_BATCH_DT>, dim3(per * fr.nf), dim3(SIFT_DESC_BATCH_DT), 0, s, jobs,
+                           ctr, range_keys, desc, host_ctr, fr.stride, (unsigned)fr.nf);
     }
 }
 
