@@ -178,7 +178,11 @@ int sift_hip_debug_candidates(sift_hip_t h, int* quads, int cap, int* count);
 
 /* --- Brute-force matcher (replaces sift_cuda::matchBruteForce, Match.cuh:9-25) */
 
-/* Scratch for up to max_query x max_train per pair and max_pairs pairs. */
+/* Scratch for up to max_query x max_train per pair and max_pairs pairs.  One
+ * launch per match call: the split workgroups merge their top-2 through
+ * device-scope atomics in this scratch, so calls on ONE matcher must be
+ * ordered (same stream, or synchronised); use one matcher per stream for
+ * concurrent matching. */
 int sift_hip_matcher_create(int device, int max_query, int max_train, int max_pairs,
                             sift_hip_matcher_t* out);
 int sift_hip_matcher_destroy(sift_hip_matcher_t m);
