@@ -111,6 +111,19 @@ __device__ __forceinline__ RefKpt load_ref(const RefKpt* in, unsigned k) {  // s
     return __builtin_bit_cast(RefKpt, r);
 }
 
+// Inclusive prefix sum over the 64 lanes of a wave with gfx9 DPP: row_shr
+// 1/2/4/8 inside each 16-lane row, then row_bcast:15 / row_bcast:31 carry the
+// row totals into the following rows (masked rows keep 0 and add nothing).
+__device__ __forceinline__ int wave_incl_scan(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
 __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* __restrict__ in,
                                                     Counters* __restrict__ ctr, OriKpt* __restrict__ out,
                                                     uint32_t* __restrict__ bitmap, KeypointParams kp, long fs) {
@@ -124,6 +137,9 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
     const int lane = threadIdx.x;
     s_exptab[lane] = c_exptab[lane];
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    unsigned long long lane_nb[6];  // all ones where bit k of the lane index is 0
+#pragma unroll
+    for (int bit = 0; bit < 6; bit++) lane_nb[bit] = ((lane >> bit) & 1) ? 0ull : ~0ull;
     const unsigned n = min(ctr->refined, kp.capRefined);
     const int fo = pyr.firstOctave;
     for (unsigned k = blockIdx.x; k < n; k += gridDim.x) {  // round-robin (see k_descriptor)
@@ -191,24 +207,15 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
 #pragma unroll
             for (int bit = 0; bit < 6; bit++) m[bit] = __ballot(valid && ((bin >> bit) & 1));
             const unsigned long long vmask = __ballot(valid);
-            auto rank_of = [&](int key, int& less) {
-                unsigned long long eq = vmask;
-                less = 0;
+            // Lane b's bin mask eq(b) from the ballots (bit k of b selects m[k]
+            // or its complement), its count cb and, since bins are lane
+            // indices, start = the exclusive prefix of cb over lanes (DPP scan).
+            unsigned long long eq_l = vmask;
 #pragma unroll
-                for (int bit = 5; bit >= 0; bit--) {
-                    if ((key >> bit) & 1) {
-                        less += __popcll(eq & ~m[bit]);
-                        eq &= m[bit];
-                    } else {
-                        eq &= ~m[bit];
-                    }
-                }
-                return eq;
-            };
-            int start;  // lanes >= 36 query bins no sample has: cb = 0
-            const unsigned long long eq_l = rank_of(lane, start);
-            const int cb = __popcll(eq_l);
-            const int incl = start + cb;
+            for (int bit = 0; bit < 6; bit++) eq_l &= m[bit] ^ lane_nb[bit];
+            const int cb = __popcll(eq_l);  // lanes >= 36: no sample has that bin
+            const int incl = wave_incl_scan(cb);
+            const int start = incl - cb;
             // A sample's less(bin) and eq(bin) are those lane `bin` just
             // computed for its own key: three shuffles instead of a second
             // radix rank per sample.
