@@ -709,7 +709,10 @@ __global__ __launch_bounds__(256) void k_extrema(OctGeom g, int Lrt, int o, floa
 // ---------------------------------------------------------------------------
 constexpr int EX4_LIST = 2048;  // per-workgroup candidate list (LDS): a 256 x 32 x L block can hold
                                 // ~7 % extrema on textured frames; overflow spills to HBM
-constexpr int EX4_COLS = 256;  // columns per wave
+#ifndef SIFT_EX_CPL
+#define SIFT_EX_CPL 4  // columns per lane of the extrema strips (2 or 4)
+#endif
+constexpr int EX4_COLS = 64 * SIFT_EX_CPL;  // columns per wave
 
 __device__ __forceinline__ float dpp_left_or(float own, float v) {  // lane i <- lane i-1, lane 0 <- own
     return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own), __float_as_int(v), 0x138, 0xf, 0xf, false));
@@ -720,26 +723,27 @@ __device__ __forceinline__ float dpp_right_or(float own, float v) {  // lane i <
 
 // One workgroup = 4 waves stacked vertically over a 256-column strip: block
 // `tile` of the octave (strips across; the caller picks the XCD order).
-template <int LT, int EX4_TR, int EX4_AHEAD>
+template <int LT, int EX4_TR, int EX4_AHEAD, int CPL = SIFT_EX_CPL>
 __device__ __forceinline__ void extrema_block(const OctGeom& g, int o, float thr, uint2* __restrict__ cand,
                                               Counters* __restrict__ ctr, unsigned cap, int tile, int strips,
                                               uint2* s_list, unsigned& s_cnt, unsigned& s_base) {
     constexpr int NG = LT + 3, ND = LT + 2;
-    static_assert(4 * LT <= 31, "hit bits per row");
-    typedef float f4 __attribute__((ext_vector_type(4)));
+    static_assert(CPL * LT <= 31 && (CPL == 2 || CPL == 4), "hit bits per row");
+    typedef float f4 __attribute__((ext_vector_type(CPL)));  // CPL columns of one lane
+    constexpr int EX4_COLS = 64 * CPL;                          // columns per wave
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int x0 = (tile % strips) * EX4_COLS, y0 = ((tile / strips) * 4 + wave) * EX4_TR;
     const int W = g.W, H = g.H, pitch = g.pitch;
-    const int xl = x0 + 4 * lane;
+    const int xl = x0 + CPL * lane;
     const int xe = min(max(lane == 0 ? x0 - 1 : x0 + EX4_COLS, 0), W - 1);
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         g.base, 0, (int)min((long)NG * g.planeStride * 4, 0x7fffffffL), 0x00020000);
     if (tid == 0) s_cnt = 0;
     __syncthreads();
 
-    bool colOK[4];
+    bool colOK[CPL];
 #pragma unroll
-    for (int c = 0; c < 4; c++) colOK[c] = xl + c >= 5 && xl + c < W - 5;
+    for (int c = 0; c < CPL; c++) colOK[c] = xl + c >= 5 && xl + c < W - 5;
 
     // Ring slot: DoG of the lane's 4 columns and of its outer column, per plane.
     f4 rd[3][ND];
@@ -754,7 +758,10 @@ __device__ __forceinline__ void extrema_block(const OctGeom& g, int o, float thr
 #pragma unroll
         for (int d = 0; d < NG; d++) {
             const int so = (int)((long)d * g.planeStride * 4);
-            v[d] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off4, so, 0));
+            if constexpr (CPL == 4)
+                v[d] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off4, so, 0));
+            else
+                v[d] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off4, so, 0));
             e[d] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, offe, so, 0));
         }
     };
@@ -775,7 +782,7 @@ __device__ __forceinline__ void extrema_block(const OctGeom& g, int o, float thr
         if (lane == 0) base = atomicAdd(&s_cnt, tot);
         unsigned pos = __builtin_amdgcn_readfirstlane(base) + excl;
         for (unsigned m = hits; m; m &= m - 1u, pos++) {
-            const int f = __builtin_ctz(m), l = f / 4 + 1, c = f & 3;
+            const int f = __builtin_ctz(m), l = f / CPL + 1, c = f % CPL;
             const uint2 q = make_uint2((unsigned)(o << 8 | l), (unsigned)(r << 16 | (xl + c)));
             if (pos < EX4_LIST) {
                 s_list[pos] = q;
@@ -795,35 +802,36 @@ __device__ __forceinline__ void extrema_block(const OctGeom& g, int o, float thr
         for (int d = 0; d < ND; d++) {
             f4 vx, vn;
 #pragma unroll
-            for (int c = 0; c < 4; c++) {
+            for (int c = 0; c < CPL; c++) {
                 vx[c] = fmaxf(fmaxf(rd[A][d][c], rd[B][d][c]), rd[C][d][c]);
                 vn[c] = fminf(fminf(rd[A][d][c], rd[B][d][c]), rd[C][d][c]);
             }
             const float ex = fmaxf(fmaxf(re[A][d], re[B][d]), re[C][d]);
             const float en = fminf(fminf(re[A][d], re[B][d]), re[C][d]);
-            const float lx = dpp_left_or(ex, vx[3]), ln = dpp_left_or(en, vn[3]);
+            const float lx = dpp_left_or(ex, vx[CPL - 1]), ln = dpp_left_or(en, vn[CPL - 1]);
             const float rx = dpp_right_or(ex, vx[0]), rn = dpp_right_or(en, vn[0]);
-            hx[d][0] = fmaxf(fmaxf(lx, vx[0]), vx[1]);
-            hx[d][1] = fmaxf(fmaxf(vx[0], vx[1]), vx[2]);
-            hx[d][2] = fmaxf(fmaxf(vx[1], vx[2]), vx[3]);
-            hx[d][3] = fmaxf(fmaxf(vx[2], vx[3]), rx);
-            hn[d][0] = fminf(fminf(ln, vn[0]), vn[1]);
-            hn[d][1] = fminf(fminf(vn[0], vn[1]), vn[2]);
-            hn[d][2] = fminf(fminf(vn[1], vn[2]), vn[3]);
-            hn[d][3] = fminf(fminf(vn[2], vn[3]), rn);
+            // Column c's horizontal neighbours: c-1 and c+1 (across the lane
+            // edges: the DPP values), max/min in the same operation order.
+#pragma unroll
+            for (int c = 0; c < CPL; c++) {
+                const float xa = c == 0 ? lx : vx[c - 1], xb = c == CPL - 1 ? rx : vx[c + 1];
+                const float na = c == 0 ? ln : vn[c - 1], nb = c == CPL - 1 ? rn : vn[c + 1];
+                hx[d][c] = fmaxf(fmaxf(xa, vx[c]), xb);
+                hn[d][c] = fminf(fminf(na, vn[c]), nb);
+            }
         }
-        unsigned hits = 0;  // bit (l - 1) * 4 + c
+        unsigned hits = 0;  // bit (l - 1) * CPL + c
 #pragma unroll
         for (int l = 1; l <= LT; l++)
 #pragma unroll
-            for (int c = 0; c < 4; c++) {
+            for (int c = 0; c < CPL; c++) {
                 const float v = rd[B][l][c];
                 const float M = fmaxf(fmaxf(hx[l - 1][c], hx[l][c]), hx[l + 1][c]);
                 const float m = fminf(fminf(hn[l - 1][c], hn[l][c]), hn[l + 1][c]);
                 // M >= v >= m always (v is one of the 27), so "v >= all" is v == M;
                 // |v| > thr >= 0 excludes v == 0, and the sign picks the test.
                 const bool h = rowOK && colOK[c] && fabsf(v) > thr && v == (v > 0 ? M : m);
-                hits |= (unsigned)h << ((l - 1) * 4 + c);
+                hits |= (unsigned)h << ((l - 1) * CPL + c);
             }
         return hits;
     };
