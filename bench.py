@@ -9,7 +9,7 @@ Workload (BASELINE.json configs[1], "C2"): synthetic 1920x1200 frames,
 detectAndCompute with numOctaveLayers=3 (5 DoG scales per octave), 3 octaves,
 upscale=false, numFeatures=5000; frames are resident in HBM when the timed
 region starts (H2D excluded, like the reference's readme.md:11).  A step is one
-batch of --batch frames (default 8) through a frame-batch detector: every
+batch of --batch frames (default 16) through a frame-batch detector: every
 pipeline launch processes the whole batch (sift_hip_set_batch), and steps
 rotate over --streams detectors (default 2, each its own HIP stream + graphs)
 so consecutive batches overlap.  Every frame is fully processed (results are
@@ -66,7 +66,7 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) on the 8-GPU node; gloo to rehearse N > 1 on one GPU")
     ap.add_argument("--streams", type=int, default=2, help="detectors (HIP streams) steps rotate over")
-    ap.add_argument("--batch", type=int, default=8,
+    ap.add_argument("--batch", type=int, default=16,
                     help="frames per step: one launch per pipeline stage processes the whole batch "
                          "(sift_hip_set_batch); 1 = single-frame graphs")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-oracle sample length")
