@@ -70,6 +70,17 @@ def test_batch_c2_workload_u8(sift):
     assert_equal_results(got, single_results(sift, cfg, frames))
 
 
+@pytest.mark.parametrize("B,n", [(16, 16), (16, 5)])
+def test_batch_c2_workload_16(sift, B, n):
+    """bench.py's default launch group: 16 frames of the C2 workload per launch
+    (4-wave blur tiles, batch-sized keypoint grids), a full and a partial batch."""
+    w, h = 1920, 1200
+    cfg = sift.CudaSiftConfig(col_width=w, row_width=h, numFeatures=5000, numOctaves=3)
+    frames = [sift.synth_frame(80 + i, w, h) for i in range(n)]
+    _, got = batch_results(sift, cfg, frames, B)
+    assert_equal_results(got, single_results(sift, cfg, frames))
+
+
 def test_batch_upscale(sift):
     w, h = 320, 240
     cfg = sift.CudaSiftConfig(col_width=w, row_width=h, upscale=True, numFeatures=0)
