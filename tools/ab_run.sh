@@ -6,7 +6,7 @@ set -o pipefail
 mkdir -p gpurun_out
 for rep in 1 2; do
   for N in "$@"; do
-    SIFT_HIP_LIB=ab/$N.so timeout -k 10 120 python tools/batch_sweep.py --batches 8 --streams 2 --frames 800 > gpurun_out/ab_$N.$rep.json 2>&1 || { echo "$N failed"; tail -5 gpurun_out/ab_$N.$rep.json; exit 1; }
+    SIFT_HIP_LIB=ab/$N.so timeout -k 10 120 python tools/batch_sweep.py --batches ${AB_BATCH:-16} --streams 2 --frames 800 > gpurun_out/ab_$N.$rep.json 2>&1 || { echo "$N failed"; tail -5 gpurun_out/ab_$N.$rep.json; exit 1; }
     echo "$N rep$rep $(tail -1 gpurun_out/ab_$N.$rep.json)"
   done
 done
