@@ -127,7 +127,7 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* __restrict__ in,
                                                     Counters* __restrict__ ctr, OriKpt* __restrict__ out,
                                                     uint32_t* __restrict__ bitmap, KeypointParams kp, long fs) {
-    __shared__ float chunk[64];
+    __shared__ __attribute__((aligned(16))) float chunk[64 + 3 * kOriBins];  // bin runs padded to 4
     const long foff = blockIdx.y * fs;  // frame blockIdx.y
     in = fptr(in, foff);
     ctr = fptr(ctr, foff);
@@ -214,8 +214,12 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
 #pragma unroll
             for (int bit = 0; bit < 6; bit++) eq_l &= m[bit] ^ lane_nb[bit];
             const int cb = __popcll(eq_l);  // lanes >= 36: no sample has that bin
-            const int incl = wave_incl_scan(cb);
-            const int start = incl - cb;
+            // Bins start on 16-byte boundaries (runs padded to a multiple of 4
+            // with +0.0, which leaves a non-negative sum unchanged), so lane b
+            // reads its run with ds_read_b128 and no bounds tests.
+            const int c4 = (cb + 3) & ~3;
+            const int start = wave_incl_scan(c4) - c4;
+            for (int q = cb; q < c4; q++) chunk[start + q] = 0.f;
             // A sample's less(bin) and eq(bin) are those lane `bin` just
             // computed for its own key: three shuffles instead of a second
             // radix rank per sample.
@@ -224,15 +228,13 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
                                             (unsigned)__shfl((int)(unsigned)eq_l, bin);
             if (valid) chunk[less_s + __popcll(eq_s & lt_mask)] = w * mag;
             lds_barrier();
-            // Lane b (< 36; others have cb = 0) adds its bin's values in order,
-            // four LDS reads in flight at a time.
-            for (int t0 = start; t0 < incl; t0 += 4) {
-                const float v0 = chunk[t0], v1 = chunk[min(t0 + 1, 63)], v2 = chunk[min(t0 + 2, 63)],
-                            v3 = chunk[min(t0 + 3, 63)];
-                acc = acc + v0;
-                if (t0 + 1 < incl) acc = acc + v1;
-                if (t0 + 2 < incl) acc = acc + v2;
-                if (t0 + 3 < incl) acc = acc + v3;
+            // Lane b (< 36; others have cb = 0) adds its bin's values in order.
+            for (int t0 = start; t0 < start + c4; t0 += 4) {
+                const float4 v = *reinterpret_cast<const float4*>(chunk + t0);
+                acc = acc + v.x;
+                acc = acc + v.y;
+                acc = acc + v.z;
+                acc = acc + v.w;
             }
             lds_barrier();  // chunk is rewritten by the next 64 samples
         }
