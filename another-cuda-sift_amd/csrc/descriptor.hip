@@ -266,11 +266,7 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
             if (tid < 64) {  // inclusive scan of row counts (entries 2l+1, 2l+2 of rowpre per lane)
                 const int a = 2 * lane + 1 <= side ? rowpre[2 * lane + 1] : 0;
                 const int b = 2 * lane + 2 <= side ? rowpre[2 * lane + 2] : 0;
-                int sum = a + b;
-                for (int off = 1; off < 64; off <<= 1) {
-                    const int t = __shfl_up(sum, off);
-                    if (lane >= off) sum += t;
-                }
+                const int sum = wave_incl_scan(a + b);
                 if (2 * lane + 1 <= side) rowpre[2 * lane + 1] = sum - b;
                 if (2 * lane + 2 <= side) rowpre[2 * lane + 2] = sum;
             }

@@ -111,19 +111,6 @@ __device__ __forceinline__ RefKpt load_ref(const RefKpt* in, unsigned k) {  // s
     return __builtin_bit_cast(RefKpt, r);
 }
 
-// Inclusive prefix sum over the 64 lanes of a wave with gfx9 DPP: row_shr
-// 1/2/4/8 inside each 16-lane row, then row_bcast:15 / row_bcast:31 carry the
-// row totals into the following rows (masked rows keep 0 and add nothing).
-__device__ __forceinline__ int wave_incl_scan(int x) {
-    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
-    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
-    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
-    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
-    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
-    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
-    return x;
-}
-
 __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* __restrict__ in,
                                                     Counters* __restrict__ ctr, OriKpt* __restrict__ out,
                                                     uint32_t* __restrict__ bitmap, KeypointParams kp, long fs) {
@@ -404,12 +391,7 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(const unsigned* __restrict
     for (int base = 0; base < kp.numBuckets; base += 1024) {
         const int i = base + tid;
         const unsigned v = i < kp.numBuckets ? bcount[i] : 0u;
-        unsigned x = v;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const unsigned y = __shfl_up(x, off);
-            if (lane >= off) x += y;
-        }
+        const unsigned x = (unsigned)wave_incl_scan((int)v);
         if (lane == 63) wsum[w] = x;
         __syncthreads();
         unsigned wpre = 0, tot = 0;
@@ -552,12 +534,7 @@ __global__ __launch_bounds__(1024) void k_order(const OriKpt* __restrict__ kpts,
         const int b0 = min(tid * per, nb), b1 = min(b0 + per, nb);
         unsigned sum = 0;
         for (int b = b0; b < b1; b++) sum += s_bucket[b];
-        unsigned x = sum;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const unsigned y = __shfl_up(x, off);
-            if (lane >= off) x += y;
-        }
+        const unsigned x = (unsigned)wave_incl_scan((int)sum);
         if (lane == 63) wsum[w] = x;
         __syncthreads();
         unsigned run = x - sum, total = 0;

@@ -89,6 +89,19 @@ __device__ __forceinline__ int xcd_tile(int b, int ntiles) {
 // Workgroup barrier ordering LDS only.  __syncthreads() also fences global
 // memory, i.e. waits for every outstanding global load (vmcnt(0)) -- which
 // would drain loads deliberately issued ahead across the barrier.
+// Inclusive prefix sum over the 64 lanes of a wave with gfx9 DPP: row_shr
+// 1/2/4/8 inside each 16-lane row, then row_bcast:15 / row_bcast:31 carry the
+// row totals into the following rows (masked rows keep 0 and add nothing).
+__device__ __forceinline__ int wave_incl_scan(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
 __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
