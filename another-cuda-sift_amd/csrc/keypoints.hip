@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void k_refine(PyrDesc pyr, const uint2* __rest
         if (!mask) continue;
         unsigned wbase = 0;
         if (lane == 0) wbase = atomicAdd(&ctr->refined, (unsigned)__popcll(mask));
-        wbase = __shfl(wbase, 0);
+        wbase = __builtin_amdgcn_readfirstlane(wbase);
         if (acc) {
             const unsigned slot = wbase + (unsigned)__popcll(mask & lt_mask);
             if (slot < kp.capRefined) {
@@ -233,9 +233,7 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
         const float tp1 = __shfl(acc, (bl + 1) % kOriBins);
         const float tp2 = __shfl(acc, (bl + 2) % kOriBins);
         const float h = __fmaf_rn(tm2 + tp2, 1.f / 16.f, __fmaf_rn(tm1 + tp1, 4.f / 16.f, acc * (6.f / 16.f)));
-        float mx = lane < kOriBins ? h : -INFINITY;
-#pragma unroll
-        for (int d = 32; d > 0; d >>= 1) mx = fmaxf(mx, __shfl_xor(mx, d));
+        const float mx = wave_max(lane < kOriBins ? h : -INFINITY);
         const float mag_thr = (float)(mx * kOriPeakRatio);
         const float hl = __shfl(h, (bl + kOriBins - 1) % kOriBins);
         const float hr = __shfl(h, (bl + 1) % kOriBins);
@@ -244,7 +242,7 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
         if (!mask) continue;
         unsigned basepos = 0;
         if (lane == 0) basepos = atomicAdd(&ctr->oriented, (unsigned)__popcll(mask));
-        basepos = __shfl(basepos, 0);
+        basepos = __builtin_amdgcn_readfirstlane(basepos);
         if (peak) {
             float bin = (float)lane + 0.5f * (hl - hr) / (hl - 2 * h + hr);
             bin = bin < 0 ? kOriBins + bin : bin >= kOriBins ? bin - kOriBins : bin;

@@ -102,6 +102,20 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
     return x;
 }
 
+// Maximum over the 64 lanes of a wave, returned to every lane: DPP row_shr
+// 1/2/4/8, row_bcast:15/31 (identity -inf in masked / out-of-row lanes), then
+// lane 63 broadcast through an SGPR.  No LDS round trips.
+__device__ __forceinline__ float wave_max(float x) {
+    const int ninf = __float_as_int(-INFINITY);
+    x = fmaxf(x, __int_as_float(__builtin_amdgcn_update_dpp(ninf, __float_as_int(x), 0x111, 0xf, 0xf, false)));
+    x = fmaxf(x, __int_as_float(__builtin_amdgcn_update_dpp(ninf, __float_as_int(x), 0x112, 0xf, 0xf, false)));
+    x = fmaxf(x, __int_as_float(__builtin_amdgcn_update_dpp(ninf, __float_as_int(x), 0x114, 0xf, 0xf, false)));
+    x = fmaxf(x, __int_as_float(__builtin_amdgcn_update_dpp(ninf, __float_as_int(x), 0x118, 0xf, 0xf, false)));
+    x = fmaxf(x, __int_as_float(__builtin_amdgcn_update_dpp(ninf, __float_as_int(x), 0x142, 0xa, 0xf, false)));
+    x = fmaxf(x, __int_as_float(__builtin_amdgcn_update_dpp(ninf, __float_as_int(x), 0x143, 0xc, 0xf, false)));
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+}
+
 __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
