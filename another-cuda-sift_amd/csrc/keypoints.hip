@@ -31,8 +31,7 @@ constexpr float kOriPeakRatio = 0.8f;
 
 
 // ---------------------------------------------------------------------------
-// adjustLocalExtrema, one thread per candidate of the global list (pyramids
-// with L > 6; otherwise the extrema kernel refines its own candidates).
+// adjustLocalExtrema, one thread per candidate of the extrema kernel's list.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_refine(PyrDesc pyr, const uint2* __restrict__ cand, unsigned capCand,
                                                 Counters* __restrict__ ctr, uint32_t* __restrict__ bitmap,
@@ -88,13 +87,14 @@ void launch_refine(const PyrDesc& pyr, const uint2* cand, unsigned capCand, Coun
 // the window's samples in raster order, so that order is kept exactly:
 // samples are produced 64 at a time in raster order (lane = sample; gradients
 // by bounds-checked buffer loads straight from the plane); six ballots on the
-// bin bits give every sample its radix rank (samples of smaller bins + its
-// lane rank inside its bin), which packs the chunk's values bin by bin (lane
-// order inside a bin) into a 64-entry LDS buffer, and lane b (< 36) -- whose
-// range is the radix rank of key b -- adds its bin's values in that order to
-// its running sum --
-// OpenCV's sequential sum, carried in a register across chunks.  <1 KB of LDS
-// per keypoint.  Smoothing, max and peak interpolation use wave shuffles.
+// bin bits give lane b the mask and count of bin b, a DPP wave scan of the
+// counts (rounded up to 4) the start of bin b's run in an LDS buffer, and every
+// sample its slot (start of its bin + its lane rank inside the bin, fetched
+// from lane `bin` by shuffles); pads hold +0.0.  Lane b (< 36) then adds its
+// bin's values in that order to its running sum -- OpenCV's sequential sum,
+// carried in a register across chunks.  <1 KB of LDS per keypoint.
+// Smoothing and peak interpolation use wave shuffles, the maximum a DPP
+// reduction.
 // Reference: SiftOps.cu:237-376 (DoG plane, 32-lane LDS atomics, floor bins,
 // no interpolation, SURVEY A-9).
 // ---------------------------------------------------------------------------
