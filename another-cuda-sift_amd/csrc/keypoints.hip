@@ -294,6 +294,40 @@ void launch_orientation(const PyrDesc& pyr, const RefKpt* in, Counters* ctr, Ori
 // which is exactly the set OpenCV's nth_element + partition keeps.
 // Reference: keeps the first numFeatures in octave order (CudaMemcpyUtils.cu:38-49).
 // ---------------------------------------------------------------------------
+// Radix-select digit step (wave 0 of the workgroup, all 64 lanes): the
+// largest digit d with sum(hist[d' > d]) + hist[d] >= k, and k minus the
+// count above it -- the sequential top-down scan of KeyPointsFilter's
+// nth_element threshold, done with 4 bins per lane and a DPP scan (no
+// 256-step dependent LDS loop).  No such digit: (0, k), as the loop gives.
+__device__ __forceinline__ void radix_digit(const unsigned* hist, unsigned k, int lane, int& digit, unsigned& newk) {
+    unsigned h[4], bsum = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        h[j] = hist[255 - 4 * lane - j];  // descending digits
+        bsum += h[j];
+    }
+    unsigned cum = (unsigned)wave_incl_scan((int)bsum) - bsum;  // counts of the higher digits
+    int dl = -1;
+    unsigned kl = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        if (dl < 0 && cum + h[j] >= k) {
+            dl = 255 - 4 * lane - j;
+            kl = k - cum;
+        }
+        cum += h[j];
+    }
+    const unsigned long long hit = __ballot(dl >= 0);
+    if (!hit) {
+        digit = 0;
+        newk = k;
+        return;
+    }
+    const int src = __builtin_ctzll(hit);
+    digit = __builtin_amdgcn_readlane(dl, src);
+    newk = (unsigned)__builtin_amdgcn_readlane((int)kl, src);
+}
+
 __global__ __launch_bounds__(1024) void k_select(const OriKpt* __restrict__ kpts, Counters* __restrict__ ctr,
                                                  unsigned* __restrict__ zero_range, KeypointParams kp, long fs) {
     __shared__ unsigned hist[256];
@@ -303,7 +337,7 @@ __global__ __launch_bounds__(1024) void k_select(const OriKpt* __restrict__ kpts
     ctr = fptr(ctr, foff);
     zero_range = fptr(zero_range, foff);
     const unsigned n = min(ctr->oriented, kp.capOriented);
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
     for (int i = tid; i < 2 * kRangeSlots; i += 1024) zero_range[i] = 0u;  // next frame's range keys
     if (kp.numFeatures <= 0 || n <= (unsigned)kp.numFeatures) {
         if (tid == 0) ctr->thr_bits = 0u;
@@ -323,19 +357,14 @@ __global__ __launch_bounds__(1024) void k_select(const OriKpt* __restrict__ kpts
             if ((b & pmask) == prefix) atomicAdd(&hist[(b >> shift) & 255u], 1u);
         }
         __syncthreads();
-        if (tid == 0) {
-            unsigned k = s_k, cum = 0;
-            int digit = 0;
-            for (int d = 255; d >= 0; d--) {
-                if (cum + hist[d] >= k) {
-                    digit = d;
-                    k -= cum;
-                    break;
-                }
-                cum += hist[d];
+        if (tid < 64) {
+            int digit;
+            unsigned k;
+            radix_digit(hist, s_k, lane, digit, k);
+            if (tid == 0) {
+                s_k = k;
+                s_prefix = prefix | ((unsigned)digit << shift);
             }
-            s_k = k;
-            s_prefix = prefix | ((unsigned)digit << shift);
         }
         pmask |= 255u << shift;
         __syncthreads();
@@ -485,19 +514,14 @@ __global__ __launch_bounds__(1024) void k_order(const OriKpt* __restrict__ kpts,
                 if ((b & pmask) == prefix) atomicAdd(&hist[(b >> shift) & 255u], 1u);
             }
             __syncthreads();
-            if (tid == 0) {
-                unsigned k = s_k, cum = 0;
-                int digit = 0;
-                for (int d = 255; d >= 0; d--) {
-                    if (cum + hist[d] >= k) {
-                        digit = d;
-                        k -= cum;
-                        break;
-                    }
-                    cum += hist[d];
+            if (tid < 64) {
+                int digit;
+                unsigned k;
+                radix_digit(hist, s_k, lane, digit, k);
+                if (tid == 0) {
+                    s_k = k;
+                    s_prefix = prefix | ((unsigned)digit << shift);
                 }
-                s_k = k;
-                s_prefix = prefix | ((unsigned)digit << shift);
             }
             pmask |= 255u << shift;
             __syncthreads();
