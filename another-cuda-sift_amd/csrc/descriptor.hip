@@ -51,6 +51,28 @@ constexpr int kGroup = 4;                    // samples whose loads are in fligh
 #define SIFT_DESC_ITEM 2
 #endif
 constexpr int kItem = SIFT_DESC_ITEM;        // consecutive samples of one row per work item (enumerated path)
+// Histogram copies: lane l adds into copy l % kCopies, so lanes working on
+// the same (cell, orientation) -- same LDS address, serialised atomics -- are
+// spread over kCopies addresses (banks 16 apart); the epilogue sums them.
+#ifndef SIFT_DESC_COPIES
+#define SIFT_DESC_COPIES 1
+#endif
+constexpr int kCopies = SIFT_DESC_COPIES;
+static_assert(kCopies == 1 || kCopies == 2 || kCopies == 4, "histogram copies: 1, 2 or 4");
+constexpr int kHistWords = 2 * kCells * kCellW;  // one copy: the even- and the odd-orientation histogram
+// Lane -> run permutation (odd multiplier, 1 = identity): a wave's lanes take
+// runs spread over the window instead of neighbouring runs, so fewer lanes of
+// one atomic instruction share a cell.
+#ifndef SIFT_DESC_PERM
+#define SIFT_DESC_PERM 1
+#endif
+static_assert(SIFT_DESC_PERM % 2 == 1, "lane permutation multiplier must be odd");
+// Transcendentals: 0 = native v_rcp / v_sqrt / v_exp (+-1 ulp); 1 = the
+// oracle's correctly rounded division / sqrt and OpenCV's exp32f table
+// polynomial (fewer +-1 descriptor flips, more VALU).
+#ifndef SIFT_DESC_PRECISE
+#define SIFT_DESC_PRECISE 0
+#endif
 
 struct DescGeom {
     float cos_t, sin_t, exp_scale;
@@ -120,7 +142,15 @@ __device__ __forceinline__ void clip_interval(int& lo, int& hi, double s, double
 // differences move a descriptor entry by ~1e-7 relative and flip its rounding
 // only at a .5 boundary: inside the |diff| <= 1 bar, at the same rate as the
 // summation-order difference.  The fastAtan2 polynomial itself is kept.
+__constant__ float c_exptab_desc[64];  // OpenCV expTab_f (SIFT_DESC_PRECISE)
+void upload_exp_table_desc(const float* tab64) {
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_exptab_desc), tab64, sizeof(float) * 64);
+}
+
 __device__ __forceinline__ float desc_atan2(float y, float x) {
+#if SIFT_DESC_PRECISE
+    return cv_fast_atan2(y, x);
+#endif
     const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
     const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
     const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
@@ -135,9 +165,20 @@ __device__ __forceinline__ float desc_atan2(float y, float x) {
     return a;
 }
 __device__ __forceinline__ float desc_magnitude(float x, float y) {
+#if SIFT_DESC_PRECISE
+    return cv_magnitude(x, y);
+#else
     return __builtin_amdgcn_sqrtf(__fmaf_rn(x, x, y * y));
+#endif
 }
-__device__ __forceinline__ float desc_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
+__device__ __forceinline__ float desc_exp(float x, const float* tab) {
+#if SIFT_DESC_PRECISE
+    return cv_exp32f(x, tab);
+#else
+    (void)tab;
+    return __builtin_amdgcn_exp2f(x * 1.44269504088896341f);
+#endif
+}
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 struct JobWords {
@@ -164,9 +205,14 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
     // o0+1): even o0 -> histE[cell*10 + o], odd o0 -> histO[cell*10 + 1 + o]
     // (slot 9 = orientation 8, wrapped into 0 at the end).  The per-keypoint
     // scale keeps every bin below 2^31, so no carry crosses the word boundary.
-    __shared__ __attribute__((aligned(16))) unsigned histE[2 * kCells * kCellW];
-    unsigned* histO = histE + kCells * kCellW;
+    __shared__ __attribute__((aligned(16))) unsigned histE[kCopies * kHistWords];  // copy c at c * kHistWords
     __shared__ __attribute__((aligned(16))) float sq[128];
+#if SIFT_DESC_PRECISE
+    __shared__ float s_tab[64];
+    for (int i = threadIdx.x; i < 64; i += kDT) s_tab[i] = c_exptab_desc[i];
+#else
+    float* const s_tab = nullptr;
+#endif
     __shared__ int rowpre[kMaxRows + 4], rowlo[kMaxRows], rowln[kMaxRows];
     __shared__ float s_norm[12];
     constexpr int kPer = kDT >= 128 ? 1 : 128 / kDT;  // descriptor entries per thread in the epilogue
@@ -247,7 +293,7 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
         const __amdgpu_buffer_rsrc_t rsrc =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(jb.img), 0, jb.rows * jb.pitch * 4, 0x00020000);
 
-        for (int i = tid; i < 2 * kCells * kCellW; i += kDT) histE[i] = 0u;
+        for (int i = tid; i < kCopies * kHistWords; i += kDT) histE[i] = 0u;
         if (enumerated) {
             const double inv_sin = 1.0 / (double)G.sin_t, inv_cos = 1.0 / (double)G.cos_t;
             for (int t = tid; t < side; t += kDT) {
@@ -295,7 +341,7 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
             valid = valid && rbin > -1 && rbin < kD && cbin > -1 && cbin < kD;
             const float dx = r - l, dy = u - d;
             const f32x2t sq = rot * rot;
-            const float wgt = desc_exp((sq[0] + sq[1]) * G.exp_scale);
+            const float wgt = desc_exp((sq[0] + sq[1]) * G.exp_scale, s_tab);
             const float gori = desc_atan2(dy, dx);
             const float gmag = desc_magnitude(dx, dy);
             float obin = (gori - jb.angle) * bins_per_rad;
@@ -317,7 +363,8 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
             const int odd = o0 & 1;
             // Both histograms have 10 dwords per cell, so the four u64 adds of
             // a sample sit at constant offsets from hb (immediate offsets).
-            unsigned* hb = (odd ? histO : histE) + cell * kCellW + o0 + odd;
+            unsigned* hb = histE + (lane & (kCopies - 1)) * kHistWords + (odd ? kCells * kCellW : 0) + cell * kCellW +
+                           o0 + odd;
             float v[8];
             trilinear(mag, rbin, cbin, obin, v);
 #pragma unroll
@@ -374,7 +421,8 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
             const int N = rowpre[side];
 #endif
             const int run = (N + kDT - 1) / kDT;
-            const int k0 = min(N, tid * run), k1 = min(N, k0 + run);
+            const int tq = (tid & ~63) | ((lane * SIFT_DESC_PERM) & 63);  // this thread's run
+            const int k0 = min(N, tq * run), k1 = min(N, k0 + run);
             if (k0 < k1) {
                 int lo = 0, hi = side - 1;  // last row with rowpre[row] <= k0 (non-empty)
                 while (lo < hi) {
@@ -457,8 +505,14 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
             const int t = min(tid + kDT * h, 127);  // threads past 128 mirror entry 127 (never stored)
             const int ii = t >> 5, jj = (t >> 3) & 3, kk = t & 7;
             const int cell = (ii + 1) * (kD + 2) + (jj + 1);
-            unsigned long long hv = (unsigned long long)histE[cell * kCellW + kk] + histO[cell * kCellW + 1 + kk];
-            if (kk == 0) hv += histO[cell * kCellW + 9];
+            unsigned long long hv = 0;
+#pragma unroll
+            for (int c = 0; c < kCopies; c++) {
+                const unsigned* hE = histE + c * kHistWords;
+                const unsigned* hO = hE + kCells * kCellW;
+                hv += (unsigned long long)hE[cell * kCellW + kk] + hO[cell * kCellW + 1 + kk];
+                if (kk == 0) hv += hO[cell * kCellW + 9];
+            }
             val[h] = (float)((double)hv * (double)inv);
             if (tid + kDT * h < 128) sq[t] = val[h];
         }

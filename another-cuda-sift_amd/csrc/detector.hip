@@ -64,6 +64,78 @@ Taps gaussian_taps(double sigma) {
     return t;
 }
 
+// Compile-time A/B and instrumentation switches of the kernels (tools/ab_*.sh
+// builds pass them through EXTRA_HIPFLAGS to every translation unit).  Any
+// of them makes this a non-default build: sift_hip_version() lists them
+// ("build=ab ..."), and bench.py and __graft_entry__.smoke() refuse such a
+// library, so a measured or tested line always names the code it ran.
+#define SIFT_XSTR(x) #x
+#define SIFT_STR(x) SIFT_XSTR(x)
+const char* build_flags() {
+    return ""
+#ifdef SIFT_SKIP_STAGES
+           " SIFT_SKIP_STAGES=" SIFT_SKIP_STAGES
+#endif
+#ifdef SIFT_DESC_VARIANT
+           " SIFT_DESC_VARIANT=" SIFT_STR(SIFT_DESC_VARIANT)
+#endif
+#ifdef SIFT_DESC_STAMPS
+           " SIFT_DESC_STAMPS"
+#endif
+#ifdef SIFT_BLUR_STAMPS
+           " SIFT_BLUR_STAMPS"
+#endif
+#ifdef SIFT_BLUR_COL_UNIQUE
+           " SIFT_BLUR_COL_UNIQUE=" SIFT_STR(SIFT_BLUR_COL_UNIQUE)
+#endif
+#ifdef SIFT_BLUR_TH
+           " SIFT_BLUR_TH=" SIFT_STR(SIFT_BLUR_TH)
+#endif
+#ifdef SIFT_BLUR_BIG_TILES
+           " SIFT_BLUR_BIG_TILES=" SIFT_STR(SIFT_BLUR_BIG_TILES)
+#endif
+#ifdef SIFT_BLUR_IW16
+           " SIFT_BLUR_IW16=" SIFT_STR(SIFT_BLUR_IW16)
+#endif
+#ifdef SIFT_BLUR_X4LD
+           " SIFT_BLUR_X4LD=" SIFT_STR(SIFT_BLUR_X4LD)
+#endif
+#ifdef SIFT_BLUR_X4ST
+           " SIFT_BLUR_X4ST=" SIFT_STR(SIFT_BLUR_X4ST)
+#endif
+#ifdef SIFT_ORI_PER
+           " SIFT_ORI_PER=" SIFT_STR(SIFT_ORI_PER)
+#endif
+#ifdef SIFT_DESC_PER
+           " SIFT_DESC_PER=" SIFT_STR(SIFT_DESC_PER)
+#endif
+#ifdef SIFT_DESC_BATCH_DT
+           " SIFT_DESC_BATCH_DT=" SIFT_STR(SIFT_DESC_BATCH_DT)
+#endif
+#ifdef SIFT_DESC_WAVES
+           " SIFT_DESC_WAVES=" SIFT_STR(SIFT_DESC_WAVES)
+#endif
+#ifdef SIFT_DESC_ITEM
+           " SIFT_DESC_ITEM=" SIFT_STR(SIFT_DESC_ITEM)
+#endif
+#ifdef SIFT_DESC_PERM
+           " SIFT_DESC_PERM=" SIFT_STR(SIFT_DESC_PERM)
+#endif
+#ifdef SIFT_DESC_COPIES
+           " SIFT_DESC_COPIES=" SIFT_STR(SIFT_DESC_COPIES)
+#endif
+#ifdef SIFT_DESC_PRECISE
+           " SIFT_DESC_PRECISE=" SIFT_STR(SIFT_DESC_PRECISE)
+#endif
+#ifdef SIFT_EX_CPL
+           " SIFT_EX_CPL=" SIFT_STR(SIFT_EX_CPL)
+#endif
+#ifdef SIFT_MATCH_WG_TARGET
+           " SIFT_MATCH_WG_TARGET=" SIFT_STR(SIFT_MATCH_WG_TARGET)
+#endif
+        ;
+}
+
 struct TimingRec {
     int name;
     hipEvent_t e0, e1;
@@ -144,6 +216,7 @@ struct sift_hip_detector {
     float* dFeats4[kSlots] = {};
     uint16_t* dDesc[kSlots] = {};
     int cur = 0, count = 0, prevCount = 0;  // slot_of(current) and the counts of current, current - 1
+    bool countsValid = true;  // count / prevCount / the slot's host counters read after the frame completed
 
     hipGraphExec_t exec[kSlots] = {};   // B frames per launch
     hipGraphExec_t exec1[kSlots] = {};  // one frame (B > 1 only; exec when B = 1)
@@ -623,6 +696,7 @@ int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEven
 void make_current(sift_hip_detector* d, long long f) {
     d->current = f;
     d->cur = d->slot_of(f);
+    d->countsValid = false;
 }
 
 void complete_counts(sift_hip_detector* d) {
@@ -633,6 +707,17 @@ void complete_counts(sift_hip_detector* d) {
     };
     d->count = n(f);
     d->prevCount = n(f - 1);
+    d->countsValid = true;
+}
+
+// Counts of the current launch group are read from the pinned host copies its
+// last kernel writes: an accessor called before sift_hip_sync / sift_hip_wait
+// (e.g. straight after sift_hip_detect_device) first waits for that group.
+int ensure_counts(sift_hip_detector* d) {
+    if (d->countsValid) return SIFT_HIP_OK;
+    if (d->current >= d->firstFrame) HIPCHK(hipEventSynchronize(d->evFrame[d->cur]));
+    complete_counts(d);
+    return SIFT_HIP_OK;
 }
 
 int finish_frame(sift_hip_detector* d) {
@@ -724,10 +809,12 @@ void sift_hip_default_config(sift_hip_config* c, int w, int h) {
 }
 
 const char* sift_hip_version(void) {
-    static char buf[96];
+    static char buf[512];
     int rt = 0;
     (void)hipRuntimeGetVersion(&rt);
-    snprintf(buf, sizeof buf, "abi=%d arch=gfx950 hip=%d", SIFT_HIP_ABI_VERSION, rt);
+    const char* ab = build_flags();
+    snprintf(buf, sizeof buf, "abi=%d arch=gfx950 hip=%d build=%s%s", SIFT_HIP_ABI_VERSION, rt, ab[0] ? "ab" : "default",
+             ab);
     return buf;
 }
 
@@ -911,6 +998,8 @@ int sift_hip_batch_results_device(sift_hip_t d, int i, int* count, int* overflow
     CHECK_HANDLE(d);
     if (d->current < d->firstFrame || i < 0 || i >= d->nfOf[d->cur])
         return fail(SIFT_HIP_ERR_INVALID, "no such frame in the current batch");
+    if (count || overflow)
+        if (int rc = ensure_counts(d)) return rc;
     const Counters& c = d->hCtr[(size_t)d->cur * d->B + i];
     const long o = (long)i * d->afs;
     if (count) *count = (int)std::min<unsigned>(c.final_n, d->kp.capFinal);
@@ -947,12 +1036,20 @@ int sift_hip_sync(sift_hip_t d) {
 
 int sift_hip_num_keypoints(sift_hip_t d, int* n) {
     if (!d || !n) return fail(SIFT_HIP_ERR_INVALID, "null argument");
+    if (d->allocated) {
+        HIPCHK(hipSetDevice(d->device));
+        if (int rc = ensure_counts(d)) return rc;
+    }
     *n = d->count;
     return SIFT_HIP_OK;
 }
 
 int sift_hip_overflow_flags(sift_hip_t d, int* flags) {
     if (!d || !flags) return fail(SIFT_HIP_ERR_INVALID, "null argument");
+    if (d->allocated) {
+        HIPCHK(hipSetDevice(d->device));
+        if (int rc = ensure_counts(d)) return rc;
+    }
     *flags = d->hCtr ? (int)d->hCtr[(size_t)d->cur * d->B].overflow : 0;
     return SIFT_HIP_OK;
 }
@@ -960,6 +1057,8 @@ int sift_hip_overflow_flags(sift_hip_t d, int* flags) {
 int sift_hip_results_device(sift_hip_t d, const float** k3, const float** f4, const uint16_t** desc,
                             const uint16_t** prev, int* prevCount, int* capacity) {
     CHECK_HANDLE(d);
+    if (prevCount)
+        if (int rc = ensure_counts(d)) return rc;
     if (k3) *k3 = d->dKpts3[d->cur];
     if (f4) *f4 = d->dFeats4[d->cur];
     if (desc) *desc = d->dDesc[d->cur];
@@ -971,6 +1070,7 @@ int sift_hip_results_device(sift_hip_t d, const float** k3, const float** f4, co
 
 int sift_hip_copy_to_host(sift_hip_t d, float* k3, float* f4, uint16_t* desc, int cap) {
     CHECK_HANDLE(d);
+    if (int rc = ensure_counts(d)) return rc;
     const int n = std::min(d->count, cap);
     // On the copy stream, ordered after the current frame only: frames
     // submitted after it keep running.
@@ -989,6 +1089,7 @@ int sift_hip_copy_to_host(sift_hip_t d, float* k3, float* f4, uint16_t* desc, in
 
 int sift_hip_copy_descriptors_device(sift_hip_t d, uint16_t* dst, int cap, void* stream) {
     CHECK_HANDLE(d);
+    if (int rc = ensure_counts(d)) return rc;
     const int n = std::min(d->count, cap);
     hipStream_t s = stream ? (hipStream_t)stream : d->stream;
     if (s != d->stream) HIPCHK(hipStreamWaitEvent(s, d->evFrame[d->cur], 0));
@@ -1037,6 +1138,7 @@ int sift_hip_debug_gaussian(sift_hip_t d, int o, int layer, float* out) {
 
 int sift_hip_debug_candidates(sift_hip_t d, int* quads, int cap, int* count) {
     CHECK_HANDLE(d);
+    if (int rc = ensure_counts(d)) return rc;
     const Counters& c = d->hCtr[(size_t)d->cur * d->B];
     const int n = (int)std::min<unsigned>(c.cand, d->capCand);
     if (count) *count = (int)c.cand;
@@ -1063,14 +1165,17 @@ struct sift_hip_matcher {
     int device = 0;
     int maxQ = 0, maxT = 0, maxP = 0;
     unsigned long long* dKeys = nullptr;  // running top-2 keys per (pair, query), all ones between calls
-    unsigned* dDone = nullptr;            // finished splits per (pair, 32-query block), zero between calls
+    unsigned* dDone = nullptr;            // finished splits per (pair, 256-query block), zero between calls
     int* dMatch = nullptr;
-    static constexpr int kMaxSplits = 256;
+    int8_t* dCodes = nullptr;             // int8 codes of a call's distinct sets (k_match_prep)
+    int* dNorms = nullptr;                // |code|^2 per code row
+    unsigned* dFlags = nullptr;           // per set slot: == epoch if the set is not all integers 0..255
+    long codeRows = 0;
+    unsigned epoch = 0;
     ~sift_hip_matcher() {
         (void)hipSetDevice(device);
-        if (dKeys) (void)hipFree(dKeys);
-        if (dDone) (void)hipFree(dDone);
-        if (dMatch) (void)hipFree(dMatch);
+        for (void* p : {(void*)dKeys, (void*)dDone, (void*)dMatch, (void*)dCodes, (void*)dNorms, (void*)dFlags})
+            if (p) (void)hipFree(p);
     }
 };
 
@@ -1089,13 +1194,21 @@ int sift_hip_matcher_create(int device, int max_query, int max_train, int max_pa
     m->maxQ = max_query;
     m->maxT = max_train;
     m->maxP = max_pairs;
-    const size_t nkeys = 2 * (size_t)max_pairs * max_query, nblk = (size_t)max_pairs * ((max_query + 31) / 32);
+    // Distinct sets of a call: at most 2 per pair, each at most max(maxQ, maxT) rows.
+    m->codeRows = 2L * max_pairs * std::max(max_query, max_train);
+    const size_t nkeys = 2 * (size_t)max_pairs * max_query;
+    const size_t nblk = (size_t)max_pairs * ((max_query + kMatchQB - 1) / kMatchQB);
     if (hipSetDevice(m->device) != hipSuccess ||
         hipMalloc((void**)&m->dKeys, sizeof(unsigned long long) * nkeys) != hipSuccess ||
         hipMalloc((void**)&m->dDone, sizeof(unsigned) * nblk) != hipSuccess ||
         hipMalloc((void**)&m->dMatch, sizeof(int) * (size_t)max_pairs * max_query) != hipSuccess ||
+        hipMalloc((void**)&m->dCodes, (size_t)m->codeRows * 128) != hipSuccess ||
+        hipMalloc((void**)&m->dNorms, sizeof(int) * (size_t)m->codeRows) != hipSuccess ||
+        hipMalloc((void**)&m->dFlags, sizeof(unsigned) * 2 * kMaxMatchPairs) != hipSuccess ||
         hipMemset(m->dKeys, 0xff, sizeof(unsigned long long) * nkeys) != hipSuccess ||
-        hipMemset(m->dDone, 0, sizeof(unsigned) * nblk) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        hipMemset(m->dDone, 0, sizeof(unsigned) * nblk) != hipSuccess ||
+        hipMemset(m->dFlags, 0, sizeof(unsigned) * 2 * kMaxMatchPairs) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess) {
         delete m;
         return fail(SIFT_HIP_ERR_NOMEM, "matcher allocation failed");
     }
@@ -1113,20 +1226,45 @@ int sift_hip_match_batched(sift_hip_matcher_t m, int P, const uint16_t* const* q
                            float* d2, int* match, void* stream) {
     if (!m || P <= 0 || P > m->maxP || !q || !nq || !t || !nt) return fail(SIFT_HIP_ERR_INVALID, "bad batch");
     MatchBatch b{};
+    MatchSets sets{};
     b.P = P;
+    // Distinct sets by pointer (a set used by several pairs is prepared once).
+    auto set_of = [&](const uint16_t* ptr, int n) {
+        for (int k = 0; k < sets.nsets; k++)
+            if (sets.set[k].src == ptr) {
+                sets.set[k].n = std::max(sets.set[k].n, n);
+                return k;
+            }
+        sets.set[sets.nsets] = MatchSet{ptr, n, 0};
+        return sets.nsets++;
+    };
     int off = 0, maxq = 1, maxt = 1;
     for (int p = 0; p < P; p++) {
         if (nq[p] < 0 || nt[p] < 0 || nq[p] > m->maxQ || nt[p] > m->maxT)
             return fail(SIFT_HIP_ERR_INVALID, "pair size exceeds matcher limits");
         if ((nq[p] && !q[p]) || (nt[p] && !t[p])) return fail(SIFT_HIP_ERR_INVALID, "null descriptor pointer");
-        b.pair[p] = MatchPair{q[p], t[p], nq[p], nt[p], off, 0};
+        const int qs = set_of(q[p], nq[p]), ts = set_of(t[p], nt[p]);
+        b.pair[p] = MatchPair{q[p], t[p], nq[p], nt[p], off, qs, ts, 0, 0, 0};
         off += nq[p];
         maxq = std::max(maxq, nq[p]);
         maxt = std::max(maxt, nt[p]);
     }
+    long row = 0;
+    for (int k = 0; k < sets.nsets; k++) {
+        sets.set[k].row0 = (int)row;
+        row += sets.set[k].n;
+        sets.maxn = std::max(sets.maxn, sets.set[k].n);
+    }
+    if (row > m->codeRows) return fail(SIFT_HIP_ERR_INVALID, "descriptor sets exceed the matcher's code buffer");
+    for (int p = 0; p < P; p++) {
+        b.pair[p].qrow0 = sets.set[b.pair[p].qset].row0;
+        b.pair[p].trow0 = sets.set[b.pair[p].tset].row0;
+    }
+    m->epoch = m->epoch + 1 == 0 ? 1 : m->epoch + 1;  // flags from earlier calls never equal it
     HIPCHK(hipSetDevice(m->device));
-    const int S = std::min(match_splits(maxq, maxt, P), (int)sift_hip_matcher::kMaxSplits);
-    launch_match(b, S, m->maxQ, m->dKeys, m->dDone, ratio, ratio_on_squared, idx2, d2, match, (hipStream_t)stream);
+    const int S = match_splits(maxq, maxt, P);
+    launch_match(sets, b, S, m->maxQ, m->dCodes, m->dNorms, m->dFlags, m->epoch, m->dKeys, m->dDone, ratio,
+                 ratio_on_squared, idx2, d2, match, (hipStream_t)stream);
     HIPCHK(hipGetLastError());
     return SIFT_HIP_OK;
 }

@@ -2,27 +2,64 @@
 //
 // Replaces /root/reference/sift_cuda/sift_func/Match.cu:8-177 (32 lanes per
 // query, half2 diff^2, an N x M fp32 score matrix written to and re-read from
-// HBM, allocated per call).  Here the distance is a GEMM: for a tile of 32 train
-// rows x 32 queries one wave issues 8 v_mfma_f32_32x32x16_f16 over K = 128 and
-// gets dot(t, q) in fp32; d^2 = |t|^2 + |q|^2 - 2 dot is formed in registers and
-// folded into a per-lane running top-2 in the epilogue, so the N x M matrix never
-// leaves the register file.  Operand roles are chosen so that the accumulator's
-// column (lane) is the query and its 16 registers are train rows: each lane
-// scans train rows in increasing index order, giving OpenCV's batchDistance
-// tie-break (lower train index first) with a strict '<' insert.
+// HBM and allocated per call).  Here the distance matrix never leaves the
+// register file.  Two launches per call:
 //
-// Exactness: SIFT descriptors from this library are integers 0..255 stored in
-// fp16; products are exact in fp32 and every partial sum is < 2^24, so d^2 is
-// exact and the top-2 is identical to the oracle's (sift_oracle_knn2).
+//  k_match_prep  every distinct descriptor set of the call (fp16 rows) becomes
+//                int8 codes c = v - 128 (128 B per row) and |c|^2 per row, once
+//                per set (the 8-way match: 8 sets for 56 pairs).  A set holding
+//                a value that is not an integer 0..255 is flagged.
+//  k_match       the distance GEMM on v_mfma_i32_32x32x32_i8.  A workgroup owns
+//                256 queries (4 waves x 64; a wave keeps its two 32-query B
+//                operands in registers for the whole launch) and streams its
+//                split of the train rows through LDS in 32-row tiles, double
+//                buffered (one 16-byte load per thread per tile, the next
+//                tile in flight while this one computes): a tile is read from
+//                L2 once per 256 queries and feeds 8 MFMAs per wave.
+//
+// Exactness: d^2 = sum (t - q)^2 = |c_t|^2 + |c_q|^2 - 2 c_t.c_q for the
+// shifted codes (translation invariant); |c|^2 <= 2^21 and |c_t.c_q| <= 2^21, so
+// the int32 accumulator and every key below are exact.  A lane folds the 16
+// train rows of its accumulator into a running top-2 with three VALU per
+// element: key = 256 dot - (128 |c_t|^2 + r) (v_lshl_add_u32), where r is the
+// row's index inside a group of 4 tiles, orders (e = d^2 - |c_q|^2, train row)
+// in reverse, and the top-2 of the keys is v_max_i32 + v_med3_i32.  Every 4
+// tiles the group's top-2 is decoded into (e, train index) and merged into the
+// running pair.  Ties keep the lower train index -- OpenCV's batchDistance /
+// knnMatch order and the oracle's (sift_oracle_knn2).
+//
+// A pair with a flagged set (non-integer or out-of-range fp16 values, e.g. the
+// reference's own unrounded x512 descriptors) runs the general path in the
+// same launch: v_mfma_f32_32x32x16_f16 dot products (exact products, fp32
+// sums), fp32 norms, a float top-2 in train order.
+//
+// Splits of the train rows merge through 64-bit atomicMin keys (d^2 bits << 32 |
+// train index) in the matcher's scratch; the last split of a query block (a
+// counter) writes the outputs and restores the scratch.  With one split the
+// workgroup writes the outputs itself.
 #include <float.h>
+#include <limits.h>
 
 #include "sift_kernels.h"
 #include "sift_match.h"
+#include "sift_math.h"
+
+#ifndef SIFT_MATCH_WG_TARGET
+#define SIFT_MATCH_WG_TARGET 512  // workgroups a launch aims for (2 per CU) when choosing train splits
+#endif
 
 namespace sift_amd {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kNone = 0x7fffffff;
+constexpr int kRowPad = 144;  // LDS bytes per code row: rows 36 dwords apart -> conflict-free ds_read_b128
+constexpr int kGroupTiles = 4;  // tiles per key group: local row r < 128 in the key's low 7 bits
+constexpr int kInvalidKey = -(1 << 30);  // keys <= this are padding rows (or none)
+constexpr int kPadBias = -(3 << 29);     // key bias of a padding row (codes 0: key = bias <= kInvalidKey)
 
 struct Top2 {
     float d1, d2;
@@ -58,14 +95,91 @@ __device__ __forceinline__ Top2 shfl_top2(const Top2& t, int mask) {
     return r;
 }
 
+// ---------------------------------------------------------------------------
+// Set preparation: 8 threads per row (16 halves each).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_match_prep(MatchSets sets, int8_t* __restrict__ codes,
+                                                    int* __restrict__ norms, unsigned* __restrict__ flags,
+                                                    unsigned epoch) {
+    const MatchSet& st = sets.set[blockIdx.y];
+    if ((int)blockIdx.x * 32 >= st.n) return;
+    const int row = blockIdx.x * 32 + (threadIdx.x >> 3), part = threadIdx.x & 7;
+    const bool in = row < st.n;
+    const uint4* src = reinterpret_cast<const uint4*>(st.src + (size_t)min(row, st.n - 1) * 128 + part * 16);
+    const uint4 a = src[0], b = src[1];
+    const unsigned w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    unsigned pk[4] = {0u, 0u, 0u, 0u};
+    int nrm = 0;
+    bool bad = false;
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+        const float v = (float)__builtin_bit_cast(_Float16, (unsigned short)(w[e >> 1] >> (16 * (e & 1))));
+        bad |= !(v >= 0.f && v <= 255.f && v == __builtin_rintf(v));  // NaN fails every test
+        const int c = (int)fminf(fmaxf(v, 0.f), 255.f) - 128;
+        nrm += c * c;
+        pk[e >> 2] |= (unsigned)(c & 255) << (8 * (e & 3));
+    }
+    nrm += __shfl_xor(nrm, 1);
+    nrm += __shfl_xor(nrm, 2);
+    nrm += __shfl_xor(nrm, 4);
+    if (in) {
+        *reinterpret_cast<uint4*>(codes + ((size_t)st.row0 + row) * 128 + part * 16) =
+            make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        if (part == 0) norms[st.row0 + row] = nrm;
+        if (bad) flags[blockIdx.y] = epoch;  // every writer stores the same word
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Integer path helpers.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int med3_i32(int a, int b, int c) {
+    int r;
+    __asm__("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+struct Best {
+    int e1, i1, e2, i2;  // e = d^2 - |c_q|^2 (kNone: no entry), i = train index
+};
+
+// Merge a key group's top-2 (max-keys m1 >= m2 of the group starting at train
+// row t0) into the running pair.  The running entries come from earlier groups
+// (lower train indices), so they win ties.
+__device__ __forceinline__ void fold_group(Best& b, int m1, int m2, int t0) {
+    const bool v1 = m1 > kInvalidKey, v2 = m2 > kInvalidKey;
+    const int s1 = v1 ? -m1 : 0, s2 = v2 ? -m2 : 0;  // 128 e + r
+    const int te1 = v1 ? (s1 >> 7) : kNone, ti1 = t0 + (s1 & 127);
+    const int te2 = v2 ? (s2 >> 7) : kNone, ti2 = t0 + (s2 & 127);
+    const bool c1 = te1 < b.e1;
+    const bool c2 = c1 ? te2 < b.e1 : te1 < b.e2;
+    const int ne2 = c1 ? (c2 ? te2 : b.e1) : (c2 ? te1 : b.e2);
+    const int ni2 = c1 ? (c2 ? ti2 : b.i1) : (c2 ? ti1 : b.i2);
+    b.e1 = c1 ? te1 : b.e1;
+    b.i1 = c1 ? ti1 : b.i1;
+    b.e2 = ne2;
+    b.i2 = ni2;
+}
+
+__device__ __forceinline__ bool lt_ei(int ea, int ia, int eb, int ib) { return ea < eb || (ea == eb && ia < ib); }
+
+__device__ __forceinline__ Best merge_best(const Best a, const Best b) {
+    const bool bf = lt_ei(b.e1, b.i1, a.e1, a.i1);
+    const int we = bf ? b.e1 : a.e1, wi = bf ? b.i1 : a.i1;
+    const int le = bf ? a.e1 : b.e1, li = bf ? a.i1 : b.i1;  // head of the other list
+    const int ne = bf ? b.e2 : a.e2, ni = bf ? b.i2 : a.i2;  // runner-up of the winner's list
+    const bool ls = lt_ei(le, li, ne, ni);
+    return Best{we, wi, ls ? le : ne, ls ? li : ni};
+}
+
+// ---------------------------------------------------------------------------
+// General (fp16) path helpers.
+// ---------------------------------------------------------------------------
 __device__ __forceinline__ half8 load_frag(const uint16_t* row, int koff) {
     return *reinterpret_cast<const half8*>(row + koff);
 }
 
-constexpr int kNone = 0x7fffffff;
-
-// |v|^2 over a lane's eight 8-element fragments: v_dot2_f32_f16 in four
-// independent chains (exact: integer products, partial sums < 2^24).
+// |v|^2 over a lane's eight 8-element fragments: v_dot2_f32_f16 in four chains.
 __device__ __forceinline__ float sumsq8(const half8 (&v)[8]) {
     typedef _Float16 half2v __attribute__((ext_vector_type(2)));
     float c[4] = {0.f, 0.f, 0.f, 0.f};
@@ -79,37 +193,11 @@ __device__ __forceinline__ float sumsq8(const half8 (&v)[8]) {
     return (c[0] + c[1]) + (c[2] + c[3]);
 }
 
-// Global top-2 of a query across the S split workgroups, by 64-bit atomicMin
-// on keys (d^2 bits << 32 | train index): d^2 >= 0 orders like its bits, and
-// the index breaks ties to the lower train row (OpenCV's order).  A split
-// min's its best into K1; whatever it displaced (or its best, if that lost)
-// and its runner-up are candidates for K2, of which the smaller is min'ed in
-// (the larger can never be second).  Every key except the final K1 reaches
-// K2 this way, so K2 ends as the true second.  All exchange goes through
-// device-scope atomics (coherent across XCDs, no cache write-back fences);
-// the last split of a query block (a counter) decodes, writes the outputs
-// and resets keys and counter for the next call.
-__device__ __forceinline__ unsigned long long match_key(float d2, int idx) {
-    return idx == kNone ? ~0ull : ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)idx;
-}
-
-// grid = (query blocks of 32, train splits, pairs); 4 waves per workgroup share
-// the query block and stride over the split's 32-row train tiles.
-__global__ __launch_bounds__(256) void k_match_partial(MatchBatch batch, int S, int nq_stride,
-                                                       unsigned long long* __restrict__ keys,
-                                                       unsigned* __restrict__ done, float ratio, int ratio_on_squared,
-                                                       int* __restrict__ idx2, float* __restrict__ d2out,
-                                                       int* __restrict__ match) {
-    __shared__ Top2 wtop[4][32];
-    __shared__ unsigned s_last;
-    const int p = blockIdx.z;
-    const MatchPair& pr = batch.pair[p];
-    const int q0 = blockIdx.x * 32;
-    if (q0 >= pr.nq) return;
-    const int split = blockIdx.y;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int col = lane & 31, h = lane >> 5;
-
+// One wave's 32 queries (rows q0 + col of the pair) against train tiles
+// [tbeg, tend): f16 MFMA (train rows as A, queries as B, so the accumulator's
+// lane is the query and its 16 registers are train rows in increasing order),
+// float top-2 with a strict '<' insert.  Returns the full d^2.
+__device__ Top2 match_f16_block(const MatchPair& pr, int q0, int tbeg, int tend, int col, int h) {
     const int qrow = q0 + col;
     const bool qvalid = qrow < pr.nq;
     half8 bq[8];
@@ -117,23 +205,15 @@ __global__ __launch_bounds__(256) void k_match_partial(MatchBatch batch, int S, 
     for (int s = 0; s < 8; s++) bq[s] = qvalid ? load_frag(pr.q + (size_t)qrow * 128, 16 * s + 8 * h) : half8{};
     float qn = sumsq8(bq);
     qn += __shfl_xor(qn, 32);
-
-    const int ntiles = (pr.nt + 31) / 32;
-    const int tps = (ntiles + S - 1) / S;
-    const int tbeg = split * tps, tend = min(ntiles, tbeg + tps);
-
     Top2 best{INFINITY, INFINITY, kNone, kNone};
-    for (int tile = tbeg + w; tile < tend; tile += 4) {
-        const int t0 = tile * 32;
-        const int trow = t0 + col;
+    for (int tile = tbeg; tile < tend; tile++) {
+        const int t0 = tile * kMatchTileRows, trow = t0 + col;
         const bool tvalid = trow < pr.nt;
         half8 a[8];
 #pragma unroll
         for (int s = 0; s < 8; s++) a[s] = tvalid ? load_frag(pr.t + (size_t)trow * 128, 16 * s + 8 * h) : half8{};
         float tn = sumsq8(a);
         tn += __shfl_xor(tn, 32);
-        // Two independent accumulation chains (even / odd K blocks), summed:
-        // exact for integer descriptors (every partial sum < 2^24).
         f32x16 acc = {}, acc2 = {};
 #pragma unroll
         for (int s = 0; s < 8; s += 2) {
@@ -144,56 +224,32 @@ __global__ __launch_bounds__(256) void k_match_partial(MatchBatch batch, int S, 
 #pragma unroll
         for (int i = 0; i < 16; i++) {
             const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
-            const float tnr = __shfl(tn, row);
-            const int tr = t0 + row;
-            const float d = tnr - 2.f * acc[i];
-            if (tr < pr.nt) {
-                if (d < best.d2) {
-                    if (d < best.d1) {
-                        best.d2 = best.d1;
-                        best.i2 = best.i1;
-                        best.d1 = d;
-                        best.i1 = tr;
-                    } else {
-                        best.d2 = d;
-                        best.i2 = tr;
-                    }
+            const float d = __shfl(tn, row) - 2.f * acc[i];
+            if (t0 + row < pr.nt && d < best.d2) {
+                if (d < best.d1) {
+                    best.d2 = best.d1;
+                    best.i2 = best.i1;
+                    best.d1 = d;
+                    best.i1 = t0 + row;
+                } else {
+                    best.d2 = d;
+                    best.i2 = t0 + row;
                 }
             }
         }
     }
     best = merge_top2(best, shfl_top2(best, 32));
-    if (h == 0) wtop[w][col] = best;
-    __syncthreads();
-    if (w == 0 && h == 0) {
-        Top2 r = wtop[0][col];
-        r = merge_top2(r, wtop[1][col]);
-        r = merge_top2(r, wtop[2][col]);
-        r = merge_top2(r, wtop[3][col]);
-        if (qvalid) {
-            unsigned long long* K = keys + 2 * ((size_t)p * nq_stride + qrow);
-            const unsigned long long a1 = match_key(r.d1 + qn, r.i1), a2 = match_key(r.d2 + qn, r.i2);
-            if (a1 != ~0ull) {
-                const unsigned long long o1 = atomicMin(&K[0], a1);
-                const unsigned long long c = a1 < o1 ? o1 : a1;
-                const unsigned long long o2 = atomicMin(&K[1], c < a2 ? c : a2);
-                __asm__ volatile("" ::"v"(o2));  // returned: the min is performed before the count below
-            }
-        }
-    }
-    __syncthreads();
-    unsigned* cnt = done + (size_t)p * gridDim.x + blockIdx.x;
-    if (threadIdx.x == 0) s_last = atomicAdd(cnt, 1u) == (unsigned)(S - 1);
-    __syncthreads();
-    if (!s_last || threadIdx.x >= 32 || q0 + (int)threadIdx.x >= pr.nq) return;
-    const int q = q0 + threadIdx.x;
-    unsigned long long* K = keys + 2 * ((size_t)p * nq_stride + q);
-    const unsigned long long k1 = atomicExch(&K[0], ~0ull), k2 = atomicExch(&K[1], ~0ull);
-    if (threadIdx.x == 0) atomicExch(cnt, 0u);
-    const int i1 = k1 == ~0ull ? -1 : (int)(unsigned)k1, i2 = k2 == ~0ull ? -1 : (int)(unsigned)k2;
-    const float e1 = i1 >= 0 ? __uint_as_float((unsigned)(k1 >> 32)) : FLT_MAX;
-    const float e2 = i2 >= 0 ? __uint_as_float((unsigned)(k2 >> 32)) : FLT_MAX;
-    const size_t o = (size_t)pr.out_off + q;
+    best.d1 += qn;
+    best.d2 += qn;
+    return best;
+}
+
+__device__ __forceinline__ unsigned long long match_key(float d2, int idx) {
+    return idx == kNone ? ~0ull : ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)idx;
+}
+
+__device__ __forceinline__ void write_match(int i1, float e1, int i2, float e2, size_t o, float ratio,
+                                            int ratio_on_squared, int* idx2, float* d2out, int* match) {
     if (idx2) {
         idx2[2 * o] = i1;
         idx2[2 * o + 1] = i2;
@@ -216,23 +272,191 @@ __global__ __launch_bounds__(256) void k_match_partial(MatchBatch batch, int S, 
     }
 }
 
-int match_splits(int max_nq, int max_nt, int P) {
-    const int qblocks = (max_nq + 31) / 32;
-    const int ntiles = (max_nt + 31) / 32;
-    int S = (1024 + qblocks * P - 1) / (qblocks * P);
-    S = S < 1 ? 1 : S;
-    const int maxS = (ntiles + 3) / 4;  // keep >= 4 tiles (one per wave) per split
-    if (S > maxS) S = maxS < 1 ? 1 : maxS;
-    return S;
+// grid = (256-query blocks, train splits, pairs), 256 threads.
+__global__ __launch_bounds__(256, 2) void k_match(MatchBatch batch, int S, int nq_stride,
+                                                  const int8_t* __restrict__ codes, const int* __restrict__ norms,
+                                                  const unsigned* __restrict__ flags, unsigned epoch,
+                                                  unsigned long long* __restrict__ keys, unsigned* __restrict__ done,
+                                                  float ratio, int ratio_on_squared, int* __restrict__ idx2,
+                                                  float* __restrict__ d2out, int* __restrict__ match) {
+    __shared__ __attribute__((aligned(16))) int8_t s_tile[2][kMatchTileRows * kRowPad];
+    __shared__ __attribute__((aligned(16))) int s_ntk[2][kMatchTileRows];
+    __shared__ Top2 s_res[kMatchQB];
+    __shared__ unsigned s_last;
+    const int p = blockIdx.z;
+    const MatchPair& pr = batch.pair[p];
+    const int q0 = blockIdx.x * kMatchQB;
+    if (q0 >= pr.nq) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, col = lane & 31, h = lane >> 5;
+    const int ntiles = (pr.nt + kMatchTileRows - 1) / kMatchTileRows, tps = (ntiles + S - 1) / S;
+    const int tbeg = min(ntiles, (int)blockIdx.y * tps), tend = min(ntiles, tbeg + tps);
+    const int q0w = q0 + 64 * w;
+    Top2 res[2];
+    if (flags[pr.qset] != epoch && flags[pr.tset] != epoch) {
+        // ---- integer path ----
+        const int8_t* __restrict__ qc = codes + (size_t)pr.qrow0 * 128;
+        const int8_t* __restrict__ tc = codes + (size_t)pr.trow0 * 128;
+        const int* __restrict__ tn = norms + pr.trow0;
+        // B operands: lane (col, h) holds bytes [64h, 64h + 64) of query row
+        // q0w + 32 qb + col, one 16-byte fragment per MFMA; the A fragments
+        // take the same bytes of the train rows, so both sides pair the same
+        // descriptor dimensions in every K slot.
+        i32x4 bq[2][4];
+        int qn[2];
+#pragma unroll
+        for (int qb = 0; qb < 2; qb++) {
+            const int row = min(q0w + 32 * qb + col, pr.nq - 1);
+            const i32x4* src = reinterpret_cast<const i32x4*>(qc + (size_t)row * 128 + 64 * h);
+#pragma unroll
+            for (int kb = 0; kb < 4; kb++) bq[qb][kb] = src[kb];
+            qn[qb] = norms[pr.qrow0 + row];
+        }
+        // Tile loader: thread -> 16 bytes (row tid >> 3, part tid & 7) of a
+        // 4 KiB tile; thread r < 32 -> row r's negated key bias.
+        const int lrow = tid >> 3, lpart = tid & 7;
+        i32x4 nv = {0, 0, 0, 0};
+        int nk = 0;
+        auto fetch = [&](int tile) {
+            const int r = tile * kMatchTileRows + lrow;
+            const i32x4 v = *reinterpret_cast<const i32x4*>(tc + (size_t)min(r, pr.nt - 1) * 128 + 16 * lpart);
+            nv = r < pr.nt ? v : (i32x4){0, 0, 0, 0};
+            const int rr = tile * kMatchTileRows + (tid & 31);
+            const int n2 = tn[min(rr, pr.nt - 1)];
+            const int lr = ((tile - tbeg) & (kGroupTiles - 1)) * kMatchTileRows + (tid & 31);  // row in the key group
+            nk = rr < pr.nt ? -(128 * n2 + lr) : kPadBias;
+        };
+        auto stash = [&](int buf) {
+            *reinterpret_cast<i32x4*>(s_tile[buf] + lrow * kRowPad + 16 * lpart) = nv;
+            if (tid < kMatchTileRows) s_ntk[buf][tid] = nk;
+        };
+        Best best[2] = {{kNone, kNone, kNone, kNone}, {kNone, kNone, kNone, kNone}};
+        int m1[2] = {INT_MIN, INT_MIN}, m2[2] = {INT_MIN, INT_MIN};
+        if (tbeg < tend) {
+            fetch(tbeg);
+            stash(0);
+            if (tbeg + 1 < tend) fetch(tbeg + 1);
+        }
+        for (int tile = tbeg; tile < tend; tile++) {
+            const int buf = (tile - tbeg) & 1;
+            lds_barrier();  // tile `tile` is in s_tile[buf]; every wave is done with s_tile[buf ^ 1]
+            i32x4 a[4], tk[4];
+            const int8_t* ta = s_tile[buf] + col * kRowPad + 64 * h;
+#pragma unroll
+            for (int kb = 0; kb < 4; kb++) a[kb] = *reinterpret_cast<const i32x4*>(ta + 16 * kb);
+            // accumulator register i holds train row (i & 3) + 8 (i >> 2) + 4 h
+#pragma unroll
+            for (int g = 0; g < 4; g++) tk[g] = *reinterpret_cast<const i32x4*>(s_ntk[buf] + 8 * g + 4 * h);
+            if (tile + 1 < tend) {
+                stash(buf ^ 1);
+                if (tile + 2 < tend) fetch(tile + 2);
+            }
+#pragma unroll
+            for (int qb = 0; qb < 2; qb++) {
+                i32x16 acc = {};
+#pragma unroll
+                for (int kb = 0; kb < 4; kb++) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[kb], bq[qb][kb], acc, 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    const int key = (acc[i] << 8) + tk[i >> 2][i & 3];
+                    m2[qb] = med3_i32(m1[qb], key, m2[qb]);  // second largest of {m1 >= m2, key}
+                    m1[qb] = max(m1[qb], key);
+                }
+            }
+            const int gi = tile - tbeg;
+            if ((gi & (kGroupTiles - 1)) == kGroupTiles - 1 || tile + 1 == tend) {
+                const int t0 = (tile - (gi & (kGroupTiles - 1))) * kMatchTileRows;
+#pragma unroll
+                for (int qb = 0; qb < 2; qb++) {
+                    fold_group(best[qb], m1[qb], m2[qb], t0);
+                    m1[qb] = m2[qb] = INT_MIN;
+                }
+            }
+        }
+#pragma unroll
+        for (int qb = 0; qb < 2; qb++) {
+            Best o;  // the other half of the train rows (lane ^ 32)
+            o.e1 = __shfl_xor(best[qb].e1, 32);
+            o.i1 = __shfl_xor(best[qb].i1, 32);
+            o.e2 = __shfl_xor(best[qb].e2, 32);
+            o.i2 = __shfl_xor(best[qb].i2, 32);
+            const Best r = merge_best(best[qb], o);
+            res[qb].d1 = r.e1 == kNone ? INFINITY : (float)(r.e1 + qn[qb]);
+            res[qb].i1 = r.e1 == kNone ? kNone : r.i1;
+            res[qb].d2 = r.e2 == kNone ? INFINITY : (float)(r.e2 + qn[qb]);
+            res[qb].i2 = r.e2 == kNone ? kNone : r.i2;
+        }
+    } else {
+        // ---- general path: fp16 values that are not integers 0..255 ----
+        res[0] = match_f16_block(pr, q0w, tbeg, tend, col, h);
+        res[1] = match_f16_block(pr, q0w + 32, tbeg, tend, col, h);
+    }
+    if (h == 0) {
+        s_res[64 * w + col] = res[0];
+        s_res[64 * w + 32 + col] = res[1];
+    }
+    __syncthreads();
+    const int q = q0 + tid;
+    const bool qv = q < pr.nq;
+    const size_t o = (size_t)pr.out_off + q;
+    if (S == 1) {
+        if (qv) {
+            const Top2 r = s_res[tid];
+            const int i1 = r.i1 == kNone ? -1 : r.i1, i2 = r.i2 == kNone ? -1 : r.i2;
+            write_match(i1, i1 >= 0 ? r.d1 : FLT_MAX, i2, i2 >= 0 ? r.d2 : FLT_MAX, o, ratio, ratio_on_squared, idx2,
+                        d2out, match);
+        }
+        return;
+    }
+    // Global top-2 of a query across the S splits: 64-bit atomicMin on keys.
+    // A split min's its best into K1; whatever that displaced (or its best, if
+    // it lost) and its runner-up are candidates for K2, of which the smaller is
+    // min'ed in (the larger can never be second).  Every key except the final
+    // K1 reaches K2 this way, so K2 ends as the true second.  Device-scope
+    // atomics only (coherent across XCDs, no cache write-back fences).
+    unsigned long long* K = keys + 2 * ((size_t)p * nq_stride + q);
+    if (qv) {
+        const Top2 r = s_res[tid];
+        const unsigned long long a1 = match_key(r.d1, r.i1), a2 = match_key(r.d2, r.i2);
+        if (a1 != ~0ull) {
+            const unsigned long long o1 = atomicMin(&K[0], a1);
+            const unsigned long long c = a1 < o1 ? o1 : a1;
+            const unsigned long long o2 = atomicMin(&K[1], c < a2 ? c : a2);
+            __asm__ volatile("" ::"v"(o2));  // returned: the min is performed before the count below
+        }
+    }
+    __syncthreads();
+    unsigned* cnt = done + (size_t)p * gridDim.x + blockIdx.x;
+    if (tid == 0) s_last = atomicAdd(cnt, 1u) == (unsigned)(S - 1);
+    __syncthreads();
+    if (!s_last || !qv) return;
+    const unsigned long long k1 = atomicExch(&K[0], ~0ull), k2 = atomicExch(&K[1], ~0ull);
+    if (tid == 0) atomicExch(cnt, 0u);
+    const int i1 = k1 == ~0ull ? -1 : (int)(unsigned)k1, i2 = k2 == ~0ull ? -1 : (int)(unsigned)k2;
+    const float e1 = i1 >= 0 ? __uint_as_float((unsigned)(k1 >> 32)) : FLT_MAX;
+    const float e2 = i2 >= 0 ? __uint_as_float((unsigned)(k2 >> 32)) : FLT_MAX;
+    write_match(i1, e1, i2, e2, o, ratio, ratio_on_squared, idx2, d2out, match);
 }
 
-void launch_match(const MatchBatch& batch, int S, int nq_stride, unsigned long long* keys, unsigned* done, float ratio,
+int match_splits(int max_nq, int max_nt, int P) {
+    const int qblocks = (max_nq + kMatchQB - 1) / kMatchQB;
+    const int ntiles = (max_nt + kMatchTileRows - 1) / kMatchTileRows;
+    int S = (SIFT_MATCH_WG_TARGET + qblocks * P - 1) / (qblocks * P);
+    const int maxS = ntiles / 2 > 1 ? ntiles / 2 : 1;  // >= 2 tiles per split
+    S = S < maxS ? S : maxS;
+    return S < 1 ? 1 : S;
+}
+
+void launch_match(const MatchSets& sets, const MatchBatch& batch, int S, int nq_stride, int8_t* codes, int* norms,
+                  unsigned* flags, unsigned epoch, unsigned long long* keys, unsigned* done, float ratio,
                   int ratio_on_squared, int* idx2, float* d2, int* match, hipStream_t s) {
+    if (sets.maxn > 0)
+        hipLaunchKernelGGL(k_match_prep, dim3((sets.maxn + 31) / 32, sets.nsets), dim3(256), 0, s, sets, codes, norms,
+                           flags, epoch);
     int max_nq = 1;
     for (int p = 0; p < batch.P; p++) max_nq = max(max_nq, batch.pair[p].nq);
-    dim3 g1((max_nq + 31) / 32, S, batch.P);
-    hipLaunchKernelGGL(k_match_partial, g1, dim3(256), 0, s, batch, S, nq_stride, keys, done, ratio, ratio_on_squared,
-                       idx2, d2, match);
+    dim3 g((max_nq + kMatchQB - 1) / kMatchQB, S, batch.P);
+    hipLaunchKernelGGL(k_match, g, dim3(256), 0, s, batch, S, nq_stride, codes, norms, flags, epoch, keys, done, ratio,
+                       ratio_on_squared, idx2, d2, match);
 }
 
 }  // namespace sift_amd

@@ -115,9 +115,41 @@ struct BlurJob {
     Taps taps;
 };
 
+// LDS row pitch of a blur tile (floats).  The row pass stores each lane's 4
+// outputs with ds_write_b128, whose 8-lane groups put blocks of one row
+// beside the same blocks of the next row: conflict-free exactly when the pitch
+// is 16 mod 32 dwords (the old pitch, 64 + 2R rounded up to 4, was only for
+// R = 8: SQ_LDS_BANK_CONFLICT 16-21 % of the LDS cycles at R = 5, 6, 10, 13).
+// A multiple-of-16 pitch also lets the column pass fetch (y, y + 4) pairs with
+// one ds_read2st64_b32.
+#ifndef SIFT_BLUR_IW16
+#define SIFT_BLUR_IW16 1
+#endif
+// Tiles with every input in the image read their staging rows as aligned
+// 16-byte loads of columns x0 - 8 .. x0 + 71 (radius <= 8): a quarter of the
+// load instructions of the per-column dword staging.  The LDS tile then starts
+// at column x0 - 8 for every radius <= 8 (ORG), whichever staging ran.
+#ifndef SIFT_BLUR_X4LD
+#define SIFT_BLUR_X4LD 0
+#endif
+// Full tiles store their output rows as 16-byte stores (each wave's 8-row
+// blocks transposed through the freed LDS tile) instead of one dword per
+// lane and row: a quarter of the store instructions.
+#ifndef SIFT_BLUR_X4ST
+#define SIFT_BLUR_X4ST 0
+#endif
+template <int R>
+constexpr int blur_org() {  // tile column 0 = image column x0 - ORG
+    return SIFT_BLUR_X4LD && R <= 8 ? 8 : R;
+}
+template <int R>
+constexpr int blur_iw() {
+    return SIFT_BLUR_IW16 ? ((BLUR_TW + 2 * blur_org<R>() + 15) / 32) * 32 + 16
+                          : (BLUR_TW + 2 * blur_org<R>() + 3) & ~3;
+}
 template <int R>
 constexpr int blur_lds_floats() {
-    return (BLUR_TW + 2 * R + 3 & ~3) * (BLUR_TH + 2 * R) + 4;
+    return blur_iw<R>() * (BLUR_TH + 2 * R) + 4;
 }
 
 // Tile `blk` of job J's nf * ntiles (64 x 32 outputs; frame-major, XCD order)
@@ -148,9 +180,12 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
     unsigned long long bst_prev = __builtin_amdgcn_s_memtime();
     if (threadIdx.x == 0) atomicAdd(&g_blur_stamps[R][5], 1ull);
 #endif
-    constexpr int IW = (BLUR_TW + 2 * R + 3) & ~3;  // row stride, multiple of 4 floats
+    constexpr int IW = blur_iw<R>();                 // LDS row stride (floats)
     constexpr int IH = BLUR_TH + 2 * R;
-    constexpr int NW = (2 * R + 4 + 3) / 4;          // float4 reads per row window
+    constexpr int ORG = blur_org<R>();               // LDS column 0 = image column x0 - ORG
+    constexpr int SA = (ORG - R) & ~3, SS = (ORG - R) & 3;  // row window: aligned start, shift
+    constexpr int NW = (SS + 2 * R + 4 + 3) / 4;     // float4 reads per row window
+    static_assert(BLUR_TW - 4 + SA + 4 * NW <= IW, "row window inside the LDS row");
     const int t = xcd_tile(blk, J.ntiles * J.nf);
     const int f = t / J.ntiles, tile = t - f * J.ntiles;
     const T* __restrict__ src = fptr(static_cast<const T*>(J.src), f * J.sfs);
@@ -207,7 +242,26 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
                 v1[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, c1, roff, 0));
             }
         };
-        if (y0 - R >= 0 && y0 - R + IH <= H) {
+        const bool x4 = ES == 4 && ORG == 8 && sstep == 1 && x0 >= 8 && x0 + BLUR_TW + 8 <= W && y0 - R >= 0 &&
+                        y0 - R + IH <= H;  // uniform
+        if (x4) {
+            // Interior tile: 16-byte loads of the 80-column rows (IW = 80, so the
+            // LDS tile is one contiguous run of float4s), all in flight before
+            // the first LDS store.
+            static_assert(ES != 4 || ORG != 8 || IW == 80, "x4 staging assumes 80-float LDS rows");
+            constexpr int NQ = 20 * IH, NT = 64 * BLUR_NW, QPT = (NQ + NT - 1) / NT;
+            typedef unsigned u32x4s __attribute__((ext_vector_type(4)));
+            u32x4s q4[QPT];
+            const int rb0 = (y0 - R) * spitch + x0 - 8;
+#pragma unroll
+            for (int u = 0; u < QPT; u++) {
+                const int idx = min(tid + NT * u, NQ - 1), row = idx / 20, qq = idx - row * 20;
+                q4[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (unsigned)(rb0 + row * spitch + 4 * qq) * 4u, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < QPT; u++)
+                if (u < QPT - 1 || tid + NT * u < NQ) *reinterpret_cast<u32x4s*>(in + 4 * (tid + NT * u)) = q4[u];
+        } else if (y0 - R >= 0 && y0 - R + IH <= H) {
             // Interior rows (most tiles): the row offset advances by a constant,
             // one s_add per row.  Rows past IH of the last step read in-range
             // data (or 0 past the buffer end) and are never stored.
@@ -223,14 +277,16 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
         }
         // LDS row of step i: one base address + an immediate offset per row;
         // only the last step can fall past IH.
-        float* const irow = in + wv * IW + lane;
-#pragma unroll
-        for (int i = 0; i < RPW; i++)
-            if (i < RPW - 1 || wv + BLUR_NW * i < IH) irow[BLUR_NW * i * IW] = v0[i];
-        if (lane < RW - 64) {
+        float* const irow = in + wv * IW + lane + (ORG - R);
+        if (!x4) {
 #pragma unroll
             for (int i = 0; i < RPW; i++)
-                if (i < RPW - 1 || wv + BLUR_NW * i < IH) irow[BLUR_NW * i * IW + 64] = v1[i];
+                if (i < RPW - 1 || wv + BLUR_NW * i < IH) irow[BLUR_NW * i * IW] = v0[i];
+            if (lane < RW - 64) {
+#pragma unroll
+                for (int i = 0; i < RPW; i++)
+                    if (i < RPW - 1 || wv + BLUR_NW * i < IH) irow[BLUR_NW * i * IW + 64] = v1[i];
+            }
         }
         BLUR_STAMP(0);  // loads landed, LDS written
         if (ES == 4 && copy_out) {  // decimated base plane of this octave = the tile's interior inputs
@@ -259,7 +315,9 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
         const int xq = blk * 4;
         for (int ly = wave * 4 + (lane >> 5) * 2 + (grpB ? 1 : 0); ly < IH; ly += 4 * BLUR_NW) {
             float win[4 * NW];
-            const f32x4* p = reinterpret_cast<const f32x4*>(in + ly * IW + xq);
+            // The row's window starts at LDS column xq + ORG - R: read from the
+            // aligned column xq + SA, the first SS values are skipped.
+            const f32x4* p = reinterpret_cast<const f32x4*>(in + ly * IW + xq + SA);
 #pragma unroll
             for (int v = 0; v < NW; v++) {
                 f32x4 f = p[v];
@@ -281,7 +339,10 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
             for (int j = 0; j < 2 * NW; j++) pe[j] = (f32x2){win[2 * j], win[2 * j + 1]};
 #pragma unroll
             for (int j = 0; j < 2 * NW - 1; j++) po[j] = pk_mov_hi_lo(pe[j], pe[j + 1]);
-            auto pr = [&](int i) -> f32x2 { return (i & 1) ? po[i >> 1] : pe[i >> 1]; };  // (win[i], win[i+1])
+            auto pr = [&](int i) -> f32x2 {  // (window[i], window[i+1]) = (win[SS+i], win[SS+i+1])
+                i += SS;
+                return (i & 1) ? po[i >> 1] : pe[i >> 1];
+            };
             f32x2 s2[2];
 #pragma unroll
             for (int h = 0; h < 2; h++) {
@@ -307,6 +368,8 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
 
     float mx = -FLT_MAX, nmn = -FLT_MAX;  // pixel range (range_keys only)
     const int gx = x0 + lane;
+    const bool full = y0 + BLUR_TH <= H && x0 + BLUR_TW <= W;  // uniform
+    float outs[BLUR_CB][8];  // SIFT_BLUR_X4ST: full-tile rows kept for the widened stores
 #pragma unroll
     for (int cbk = 0; cbk < BLUR_CB; cbk++) {
         const int lx = lane, yb = (wave + cbk * BLUR_NW) * 8;
@@ -339,7 +402,10 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
             out[q] = a[0];
             out[q + 4] = a[1];
         }
-        if (y0 + BLUR_TH <= H && x0 + BLUR_TW <= W) {
+        if (SIFT_BLUR_X4ST && full) {
+#pragma unroll
+            for (int q = 0; q < 8; q++) outs[cbk][q] = out[q];
+        } else if (full) {
             // Full tile: unconditional buffer stores, the row step in the
             // scalar offset (no per-row address arithmetic or exec masking).
             const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
@@ -362,6 +428,33 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
                     mx = fmaxf(mx, out[q]);
                     nmn = fmaxf(nmn, -out[q]);
                 }
+            }
+        }
+    }
+    if (SIFT_BLUR_X4ST && full) {
+        // Widened stores: every wave's column pass has read `mid` (barrier);
+        // each wave writes its 8-row blocks into the free LDS tile as a plain
+        // 64-float-pitch image and reads back its own rows as float4s (the
+        // same wave, in-order LDS: no second barrier), one 16-byte store per
+        // 4 columns.  ds_read_b128 groups then cover 64 distinct banks.
+        __syncthreads();
+#pragma unroll
+        for (int cbk = 0; cbk < BLUR_CB; cbk++) {
+            const int yb = (wave + cbk * BLUR_NW) * 8;
+#pragma unroll
+            for (int q = 0; q < 8; q++) in[(yb + q) * BLUR_TW + lane] = outs[cbk][q];
+        }
+        typedef unsigned u32x4t __attribute__((ext_vector_type(4)));
+        const __amdgpu_buffer_rsrc_t drs =
+            __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)min((long)dpitch * H * 4, 0x7fffffffL), 0x00020000);
+#pragma unroll
+        for (int cbk = 0; cbk < BLUR_CB; cbk++) {
+            const int yb = (wave + cbk * BLUR_NW) * 8;
+#pragma unroll
+            for (int hh = 0; hh < 2; hh++) {
+                const int row = yb + 4 * hh + (lane >> 4), c4 = 4 * (lane & 15);
+                const u32x4t v = *reinterpret_cast<const u32x4t*>(in + row * BLUR_TW + c4);
+                __builtin_amdgcn_raw_buffer_store_b128(v, drs, (unsigned)((y0 + row) * dpitch + x0 + c4) * 4u, 0, 0);
             }
         }
     }

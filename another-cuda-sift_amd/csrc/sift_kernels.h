@@ -181,7 +181,9 @@ __device__ __forceinline__ float decode_range_key(unsigned u) {
     return __uint_as_float(u & 0x80000000u ? u & 0x7fffffffu : ~u);
 }
 
-// Exp table (OpenCV expTab_f) uploaded once per device.
+// Exp table (OpenCV expTab_f) uploaded once per device (orientation and
+// descriptor translation units each hold a copy).
 void upload_exp_table(const float* tab64);
+void upload_exp_table_desc(const float* tab64);
 
 }  // namespace sift_amd

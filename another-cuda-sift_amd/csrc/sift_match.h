@@ -6,25 +6,44 @@
 namespace sift_amd {
 
 constexpr int kMaxMatchPairs = 64;
+constexpr int kMatchQB = 256;       // queries per workgroup: 4 waves x 64
+constexpr int kMatchTileRows = 32;  // train rows per LDS tile
 
 struct MatchPair {
     const uint16_t* q;  // nq x 128 half, row-major
     const uint16_t* t;  // nt x 128 half, row-major
     int nq, nt;
     int out_off;        // output row offset of this pair
+    int qset, tset;     // this call's prepared sets (k_match_prep) holding q and t
+    int qrow0, trow0;   // their first int8 code row
     int pad;
 };
 
-// Passed by value: lives in the kernarg segment (64 x 32 B = 2 KiB).
+// Passed by value: lives in the kernarg segment (64 x 48 B = 3 KiB).
 struct MatchBatch {
     MatchPair pair[kMaxMatchPairs];
     int P;
 };
 
+// A distinct descriptor set of one call (sets are deduplicated by pointer: the
+// 8-way match has 8 sets for 56 pairs): n rows at src -> codes row0 ...
+struct MatchSet {
+    const uint16_t* src;
+    int n, row0;
+};
+struct MatchSets {
+    MatchSet set[2 * kMaxMatchPairs];
+    int nsets, maxn;
+};
+
 int match_splits(int max_nq, int max_nt, int P);
+// codes / norms: int8 code rows (128 B) and |code|^2 per row, capacity for the
+// call's sets; flags: one word per set slot, == epoch when that set holds a
+// value that is not an integer 0..255 (matched by the general f16 path).
 // keys: 2 x u64 per (pair, query), all ones between calls; done: a counter per
-// (pair, 32-query block), zero between calls (the merging workgroup resets both).
-void launch_match(const MatchBatch& batch, int S, int nq_stride, unsigned long long* keys, unsigned* done, float ratio,
+// (pair, 256-query block), zero between calls (the merging workgroup resets both).
+void launch_match(const MatchSets& sets, const MatchBatch& batch, int S, int nq_stride, int8_t* codes, int* norms,
+                  unsigned* flags, unsigned epoch, unsigned long long* keys, unsigned* done, float ratio,
                   int ratio_on_squared, int* idx2, float* d2, int* match, hipStream_t s);
 
 }  // namespace sift_amd

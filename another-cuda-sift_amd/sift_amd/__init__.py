@@ -125,7 +125,14 @@ def _ptr(a: np.ndarray) -> int:
 
 
 def version() -> str:
+    """'abi=<n> arch=gfx950 hip=<ver> build=default' or 'build=ab <A/B macros>'."""
     return lib().sift_hip_version().decode()
+
+
+def is_default_build() -> bool:
+    """False for a library built with kernel A/B or instrumentation macros
+    (tools/ab_variant.sh): bench.py and smoke() refuse to report from one."""
+    return "build=default" in version()
 
 
 def device_count() -> int:

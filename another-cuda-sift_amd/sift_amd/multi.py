@@ -31,16 +31,13 @@ def peer_pairs(rank: int, world: int) -> List[Tuple[int, int]]:
     return [(rank, j) for j in range(world) if j != rank]
 
 
-def all_gather_sets(local: torch.Tensor, count: int, world: int, group=None) -> Tuple[torch.Tensor, List[int]]:
-    """All-gather every rank's (n, 128) descriptor set (same n on all ranks) and
-    its valid row count.  Returns (world, n, 128) and the per-rank counts."""
+def all_gather_rows(local: torch.Tensor, world: int, group=None) -> torch.Tensor:
+    """All-gather every rank's (n, 128) descriptor rows (same n on all ranks):
+    (world, n, 128).  16-bit descriptor bits travel as int32 (RCCL and gloo
+    have no int16); on "nccl" (= RCCL over xGMI) one all_gather_into_tensor."""
     if world == 1:
-        return local.unsqueeze(0), [count]
-    cnt = torch.tensor([count], dtype=torch.int64, device=local.device)
-    counts = [torch.empty_like(cnt) for _ in range(world)]
-    dist.all_gather(counts, cnt, group=group)
+        return local.unsqueeze(0)
     local = local.contiguous()
-    # 16-bit descriptor bits travel as int32 (NCCL/RCCL and gloo have no int16).
     wide = local.view(torch.int32) if local.dtype in (torch.int16, torch.float16) else local
     if dist.get_backend(group) == "nccl":
         out = torch.empty((world,) + tuple(wide.shape), dtype=wide.dtype, device=wide.device)
@@ -49,8 +46,24 @@ def all_gather_sets(local: torch.Tensor, count: int, world: int, group=None) -> 
         parts = [torch.empty_like(wide) for _ in range(world)]
         dist.all_gather(parts, wide, group=group)
         out = torch.stack(parts)
-    out = out.view(local.dtype)
-    return out, [int(c.item()) for c in counts]
+    return out.view(local.dtype)
+
+
+def all_gather_counts(count: int, world: int, device, group=None) -> List[int]:
+    """Every rank's valid row count (once per set size change, not per exchange)."""
+    if world == 1:
+        return [count]
+    cnt = torch.tensor([count], dtype=torch.int64, device=device)
+    counts = [torch.empty_like(cnt) for _ in range(world)]
+    dist.all_gather(counts, cnt, group=group)
+    return [int(c.item()) for c in counts]
+
+
+def all_gather_sets(local: torch.Tensor, count: int, world: int, group=None) -> Tuple[torch.Tensor, List[int]]:
+    """All-gather every rank's (n, 128) descriptor set (same n on all ranks) and
+    its valid row count.  Returns (world, n, 128) and the per-rank counts."""
+    counts = all_gather_counts(count, world, local.device, group)
+    return all_gather_rows(local, world, group), counts
 
 
 MatchFn = Callable[[Sequence[torch.Tensor], Sequence[int], Sequence[torch.Tensor], Sequence[int]], List[torch.Tensor]]

@@ -76,7 +76,65 @@ def parse():
                          "rocprofv3 --kernel-trace --stats summary is committed beside the roofline numbers")
     ap.add_argument("--traffic-summary", default=os.path.join(ROOT, "profiles", "round1", "pmc_summary.json"),
                     help="PMC summary (tools/pmc_summary.py) with FETCH_SIZE/WRITE_SIZE of this code")
+    ap.add_argument("--allow-ab-build", action="store_true",
+                    help="run on a library built with A/B or instrumentation macros (never for reported numbers)")
+    ap.add_argument("--launcher-selftest", action="store_true",
+                    help="CPU test of the N-rank launcher: the ranks join a gloo group and report; no GPU work")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`python bench.py --gpus N` without a torchrun parent: start N rank
+    processes (LOCAL_RANK = RANK = r, one per GPU) with the torch.distributed
+    environment and wait for them.  This process only parses arguments -- it
+    never touches the GPU -- so the ranks are plain fresh child processes.
+    Rank 0 inherits stdout and prints the JSON line; if a rank fails the
+    others are terminated (by PID) and the exit code is non-zero."""
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc, live = 0, list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks", file=sys.stderr)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def launcher_selftest(world, rank):
+    """The N > 1 plumbing without a GPU: gloo group, barrier, max over ranks."""
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.tensor([float(rank + 1)])
+    if world > 1:
+        dist.barrier()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "n_gpus": world, "selftest": True, "max_rank_plus_1": t.item()}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def make_config(**kw):
@@ -171,11 +229,126 @@ def measure_roofline(det, frames, stride, traffic_summary, nt=20, warm=3, batch=
     return {"roofline": roof, "timing": timing, "frames": nt}
 
 
+def cpu_threads():
+    """Threads for the CPU legs: OMP_NUM_THREADS when set (the GPU box sets it to
+    this job's CPU share), else every CPU in this process's affinity mask."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    return (int(env) if env.isdigit() and int(env) > 0 else aff), aff, env or None
+
+
+def _median_ms(fn, reps, warm=1):
+    for _ in range(warm):
+        fn()
+    ts = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t)
+    return float(np.median(ts) * 1e3)
+
+
+def cpu_baseline(a, cfg, c3_sets):
+    """The CPU oracle (oracle/sift_oracle.cpp, OpenMP; a restatement of OpenCV
+    4.x SIFT + BFMatcher knn-2, test infrastructure) on this host's cores, on
+    bounded samples: C2 (the headline workload) for ~a.cpu_seconds, C1 (the
+    reference's CPU plumbing, tool/extract_and_match_example.cc:62-100: detect
+    two 752x480 frames with OpenCV defaults, knn-2 + ratio 0.8) and the C3
+    knn-2 on the GPU bench's 2000 x 2000 sets."""
+    import oracle_binding as oracle
+
+    threads, aff, env = cpu_threads()
+    p = oracle.from_config(cfg)
+    imgs = [sift.synth_frame(i, W, H) for i in range(4)]
+    oracle.detect_and_compute(imgs[0], p, threads=threads)  # warm
+    n, t = 0, time.perf_counter()
+    while True:
+        oracle.detect_and_compute(imgs[n % 4], p, threads=threads)
+        n += 1
+        if time.perf_counter() - t > a.cpu_seconds and n >= 3:
+            break
+    dt = time.perf_counter() - t
+    cpu = {"value": round(n * W * H / 1e6 / dt, 2), "unit": "Mpix/s", "cores": threads, "kind": "port",
+           "sample": f"{n} frames of the C2 workload (1920x1200, 3 octaves, numFeatures 5000) in {dt:.1f}s, "
+                     f"oracle/sift_oracle.cpp OpenMP {threads} threads",
+           "cpu_model": cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": aff, "omp_num_threads": env}
+    # C1: 752x480, cv::SIFT defaults (firstOctave -1, nfeatures 0), frames 0 and 1, knn-2 + ratio 0.8.
+    p1 = oracle.params(nfeatures=0, firstOctave=-1)
+    f0, f1 = sift.synth_frame(0, 752, 480), sift.synth_frame(1, 752, 480)
+    res = {}
+
+    def c1():
+        _, d0 = oracle.detect_and_compute(f0, p1, threads=threads)
+        _, d1 = oracle.detect_and_compute(f1, p1, threads=threads)
+        idx, dist = oracle.knn2(d0, d1, threads=threads)
+        res.update(k0=len(d0), k1=len(d1), matches=int((dist[:, 0] < 0.8 * dist[:, 1]).sum()))
+
+    c1_ms = _median_ms(c1, 5)
+    cpu["c1_752x480_detect2_match_ms"] = round(c1_ms, 2)
+    cpu["c1"] = {"keypoints": [res["k0"], res["k1"]], "matches": res["matches"],
+                 "note": "two detectAndCompute calls (OpenCV defaults) + knn-2 + ratio 0.8 on distances, per frame pair"}
+    q, tr = (np.ascontiguousarray(x, np.float32) for x in c3_sets)
+    cpu["c3_knn2_2000x2000_ms"] = round(_median_ms(lambda: oracle.knn2(q, tr, threads=threads), 5), 2)
+    try:  # OpenCV itself, when the box has it (BASELINE.md section 2, secondary)
+        import cv2
+
+        cv2.setNumThreads(threads)
+        sift_cv = cv2.SIFT_create(nfeatures=5000, nOctaveLayers=3)
+        u8 = imgs[0].astype(np.uint8)
+        sift_cv.detectAndCompute(u8, None)
+        m, t = 0, time.perf_counter()
+        while time.perf_counter() - t < 5.0 or m < 3:
+            sift_cv.detectAndCompute(imgs[m % 4].astype(np.uint8), None)
+            m += 1
+        cpu["opencv"] = {"version": cv2.__version__, "value": round(m * W * H / 1e6 / (time.perf_counter() - t), 2),
+                         "note": "cv2.SIFT_create defaults (firstOctave -1), not the C2 octave count"}
+    except ImportError:
+        cpu["opencv"] = "cv2 not importable on this box"
+    return cpu
+
+
+def run_c1_gpu(local):
+    """C1's pipeline on the GPU for comparison: two synchronous 752x480 frames
+    through one Detector (OpenCV defaults), then matchBruteForce of the
+    previous frame's descriptors against the current (ratio 0.8 on distances),
+    host frames in, match indices out -- the reference tool's per-frame loop."""
+    cfg1 = sift.CudaSiftConfig(col_width=752, row_width=480, numFeatures=0, upscale=True)
+    det = sift.Detector(cfg1, device=local)
+    det.gpuWarmUpAndAllocate()
+    f = [sift.synth_frame(0, 752, 480), sift.synth_frame(1, 752, 480)]
+    m = sift.Matcher(8192, 8192, device=local)
+    out = {}
+
+    def once():
+        det.detectAndCompute(f[0])
+        det.detectAndCompute(f[1])
+        r = m.match_host(det.prev_descriptor.data(), det.prev_size, det.device_descriptor.data(), det.total_size,
+                         0.8, False)
+        out["matches"] = int((r >= 0).sum())
+        out["k"] = [det.prev_size, det.total_size]
+
+    ms = _median_ms(once, 20, warm=3)
+    return {"ms": round(ms, 4), "keypoints": out["k"], "matches": out["matches"],
+            "note": "host f32 frames, synchronous detectAndCompute x2 + matchBruteForce (prev vs current), median of 20"}
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus))  # before any GPU call in this process
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    if a.launcher_selftest:
+        launcher_selftest(world, rank)
+        return
+    if not sift.is_default_build() and not a.allow_ab_build:
+        print(f"bench.py: {sift.LIB_PATH} is a non-default build ({sift.version()}); rebuild with `make`",
+              file=sys.stderr)
+        sys.exit(3)
     local = local % max(torch.cuda.device_count(), 1)  # one rank per GPU on the driver's node
     torch.cuda.set_device(local)
     if world > 1:
@@ -430,21 +603,23 @@ def main():
 
     def run_c5():
         mine = sets[rank].contiguous()
+        counts = multi.all_gather_counts(nq, world, cdev)  # once; the exchange itself is the rows
 
         def gather():
-            g, c = multi.all_gather_sets(mine.to(cdev), nq, world)
-            return g.to(dev), c
+            return multi.all_gather_rows(mine.to(cdev), world).to(dev)
 
         for _ in range(5):
-            gathered, counts = gather()
+            gathered = gather()
         torch.cuda.synchronize()
+        barrier()
         ag0, ag1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ag0.record()
         for _ in range(20):
-            gathered, counts = gather()
+            gathered = gather()
         ag1.record()
         torch.cuda.synchronize()
         ag_us = max_over_ranks(ag0.elapsed_time(ag1) / 20 * 1e3)
+        assert counts == [nq] * world
         peers = [j for _, j in multi.peer_pairs(rank, world)]
         P = len(peers)
         bi = torch.empty((P * nq, 2), dtype=torch.int32, device=dev)
@@ -465,7 +640,7 @@ def main():
         torch.cuda.synchronize()
         bms = max_over_ranks(m0.elapsed_time(m1) / 50)
         fl = 2.0 * nq * nq * 128 * P
-        return {"allgather_us": round(ag_us, 2), "pairs_per_gpu": P,
+        return {"allgather_us": round(ag_us, 2), "allgather_bytes_per_rank": nq * 128 * 2, "pairs_per_gpu": P,
               "batched_match_ms": round(bms, 4), "tflops_per_gpu": round(fl / bms / 1e9, 2),
               "mfma_frac": round(fl / bms / 1e9 / FP16_MFMA_PEAK_TFLOPS, 4),
               "collective": f"all_gather ({a.dist_backend}; nccl = RCCL all_gather_into_tensor), sift_amd/multi.py"}
@@ -478,38 +653,8 @@ def main():
     # ---- CPU baseline: the oracle on the host cores (rank 0, N=1 only) -------
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        import oracle_binding as oracle
-
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-        p = oracle.from_config(cfg)
-        imgs = [sift.synth_frame(1000 * rank + i, W, H) for i in range(nframes)]
-        oracle.detect_and_compute(imgs[0], p, threads=threads)  # warm
-        n, t = 0, time.perf_counter()
-        while True:
-            oracle.detect_and_compute(imgs[n % nframes], p, threads=threads)
-            n += 1
-            if time.perf_counter() - t > a.cpu_seconds and n >= 3:
-                break
-        dt = time.perf_counter() - t
-        cpu = {"value": round(n * W * H / 1e6 / dt, 2), "unit": "Mpix/s", "cores": threads, "kind": "port",
-               "sample": f"{n} frames of the C2 workload (1920x1200, 3 octaves, numFeatures 5000) in {dt:.1f}s, "
-                         f"oracle/sift_oracle.cpp OpenMP {threads} threads",
-               "cpu_model": cpu_model()}
-        try:  # OpenCV itself, when the box has it (secondary)
-            import cv2
-
-            cv2.setNumThreads(threads)
-            sift_cv = cv2.SIFT_create(nfeatures=5000, nOctaveLayers=3)
-            u8 = imgs[0].astype(np.uint8)
-            sift_cv.detectAndCompute(u8, None)
-            m, t = 0, time.perf_counter()
-            while time.perf_counter() - t < 5.0 or m < 3:
-                sift_cv.detectAndCompute(imgs[m % nframes].astype(np.uint8), None)
-                m += 1
-            cpu["opencv"] = {"version": cv2.__version__, "value": round(m * W * H / 1e6 / (time.perf_counter() - t), 2),
-                             "note": "cv2.SIFT_create defaults (firstOctave -1), not the C2 octave count"}
-        except ImportError:
-            cpu["opencv"] = "cv2 not importable on this box"
+        cpu = cpu_baseline(a, cfg, [s.cpu().view(torch.float16).float().numpy() for s in sets[:2]])
+    c1_gpu = run_c1_gpu(local) if rank == 0 else None
 
     if rank == 0:
         line = {
@@ -525,6 +670,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
+            "library": sift.version(),
             "config": {
                 "workload": f"C2: detectAndCompute on 1920x1200 frames, {B} per step per GPU (one launch per stage "
                             "for the batch), numOctaveLayers=3 (5 DoG scales/octave), numOctaves=3, upscale=false, "
@@ -550,6 +696,7 @@ def main():
                          "matches": n_matches, "ratio": 0.8},
             "c4_256_frames_1600x900": c4,
             "c5_allgather_match": c5,
+            "c1_gpu": c1_gpu,
             "ref_published": {"detect_1920x1200_ms": 3.1, "match_2k_ms": "just under 1", "hardware": "RTX 4070 Super",
                               "note": "reference readme.md:11-15; config not stated (tool default upscale=false, auto octaves)"},
         }

@@ -78,6 +78,7 @@ def test_headers_compile_without_hip(tmp_path):
 def test_version_and_default_config(sift):
     v = sift.version()
     assert "abi=1" in v and "gfx950" in v
+    assert "build=default" in v and sift.is_default_build(), v  # no A/B macros in the shipped library
     cfg = sift.CudaSiftConfig(col_width=640, row_width=480)
     # Reference defaults (CudaSiftConfig.hh:3-14).
     assert (cfg.numFeatures, cfg.numOctaveLayers, cfg.contrastThreshould, cfg.edgeThreshould, cfg.sigma) == \

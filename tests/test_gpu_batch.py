@@ -10,6 +10,7 @@ single-frame call on a batch handle, and one frame against the CPU oracle.
 import numpy as np
 import pytest
 import torch
+from parity_bar import assert_descriptor_bar
 
 
 pytestmark = pytest.mark.gpu
@@ -105,5 +106,4 @@ def test_single_frame_call_on_batch_handle(sift, oracle):
     o = np.stack([ok["x"], ok["y"], ok["size"], ok["angle"]], 1)
     gi, oi = np.lexsort(gk[:, :4].T[::-1]), np.lexsort(o.T[::-1])
     assert np.array_equal(gk[gi, :4], o[oi])
-    diff = np.abs(got[2][2].view(np.float16).astype(np.float32)[gi] - od[oi])
-    assert diff.max() <= 1 and (diff == 0).mean() >= 0.995
+    assert_descriptor_bar(got[2][2].view(np.float16).astype(np.float32)[gi], od[oi], "batch frame 2")

@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 
 from test_gpu_parity import assert_same_keypoints, gpu_keypoints, make_detector, sort_keys
+from parity_bar import assert_descriptor_bar
 
 pytestmark = pytest.mark.gpu
 
@@ -50,8 +51,7 @@ def test_u8_other_sigma_vs_oracle(sift, oracle):
     gk, gd, _ = gpu_keypoints(det)
     ok, od = oracle.detect_and_compute(img, oracle.from_config(cfg))
     assert_same_keypoints(gk, ok)
-    diff = np.abs(gd[sort_keys(gk)] - od[sort_keys(ok)])
-    assert diff.max() <= 1.0 and (diff == 0).mean() >= 0.995
+    assert_descriptor_bar(gd[sort_keys(gk)], od[sort_keys(ok)], "u8 sigma 2")
 
 
 def test_u8_device_and_strided_host(sift):
