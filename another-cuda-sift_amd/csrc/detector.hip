@@ -8,7 +8,10 @@
 // per frame is the final 32-byte counter readback.
 #include <hip/hip_runtime.h>
 
+#include <sys/stat.h>
+
 #include <algorithm>
+#include <cerrno>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -222,6 +225,11 @@ struct sift_hip_detector {
     hipGraphExec_t exec1[kSlots] = {};  // one frame (B > 1 only; exec when B = 1)
     bool useGraph = true;
 
+    // Stage dumps (sift_hip_set_datagen): directory, and a device copy of the
+    // frame's input as float (the caller's buffer may change before the dump).
+    std::string dgDir;
+    float* dDg = nullptr;
+
     bool timing = false;
     int blurReps = 1;  // timing mode: each blur launch repeated back to back inside its event pair
     std::vector<TimingRec> trecs;
@@ -291,6 +299,7 @@ struct sift_hip_detector {
                 if (evRead[k]) (void)hipEventDestroy(evRead[k]);
             }
             if (hCtr) (void)hipHostFree(hCtr);
+            if (dDg) (void)hipFree(dDg);
             for (auto e : evPool) (void)hipEventDestroy(e);
             if (evIn) (void)hipEventDestroy(evIn);
             if (evOut) (void)hipEventDestroy(evOut);
@@ -671,12 +680,28 @@ int build_graphs(sift_hip_detector* d) {
     return SIFT_HIP_OK;
 }
 
+int dump_stage_files(sift_hip_detector* d);
+void complete_counts(sift_hip_detector* d);
+
 // Enqueues launch group d->submitted (nf frames at byte stride sfs) on
 // d->stream; `consumed` (nullable) is recorded once the input has been read.
+// With stage dumps on (single frames after warm-up) the frame's input is kept
+// as float, the frame is completed synchronously and dumped.
 int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEvent_t consumed, int nf = 1,
               long sfs = 0) {
     const long long f = d->submitted;
     const int slot = d->slot_of(f);
+    const bool dump = !d->dgDir.empty() && nf == 1 && d->firstFrame > 0;
+    const int W = d->cfg.col_width, H = d->cfg.row_width;
+    if (dump) {
+        if (!d->dDg && hipMalloc((void**)&d->dDg, sizeof(float) * (size_t)W * H) != hipSuccess)
+            return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc of the stage-dump input failed");
+        if (fmt == SIFT_HIP_U8)
+            launch_u8_to_f32((const uint8_t*)img, pitch, W, H, d->dDg, W, Frames{1, 0}, 0, d->stream);
+        else
+            HIPCHK(hipMemcpy2DAsync(d->dDg, sizeof(float) * W, img, sizeof(float) * (size_t)pitch, sizeof(float) * W,
+                                    H, hipMemcpyDeviceToDevice, d->stream));
+    }
     enqueue_head(d, img, pitch, fmt, slot & 1, nf, sfs);
     if (consumed) HIPCHK(hipEventRecord(consumed, d->stream));
     hipGraphExec_t g = nf == d->B ? d->exec[slot] : (nf == 1 ? d->exec1[slot] : nullptr);
@@ -688,6 +713,14 @@ int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEven
     HIPCHK(hipEventRecord(d->evFrame[slot], d->stream));
     d->nfOf[slot] = nf;
     d->submitted = f + 1;
+    if (dump) {
+        HIPCHK(hipStreamSynchronize(d->stream));
+        if (d->timing) d->collect_timing();
+        d->current = f;
+        d->cur = slot;
+        complete_counts(d);
+        return dump_stage_files(d);
+    }
     return SIFT_HIP_OK;
 }
 
@@ -782,6 +815,84 @@ int wait_frame(sift_hip_detector* d, long long f) {
     make_current(d, f);
     complete_counts(d);
     return SIFT_HIP_OK;
+}
+
+// Stage dumps of the current frame (Detector::setDataGen, reference
+// Detector.cu:145-229 / PerfData.cuh): raw little-endian row-major files plus a
+// meta.json describing them; tests/stage_check.py replays them against the CPU
+// oracle (and against this library).
+int write_file(const std::string& path, const void* data, size_t bytes) {
+    FILE* fp = fopen(path.c_str(), "wb");
+    if (!fp) return fail(SIFT_HIP_ERR_INVALID, "cannot write " + path);
+    const size_t n = bytes ? fwrite(data, 1, bytes, fp) : 0;
+    fclose(fp);
+    if (n != bytes) return fail(SIFT_HIP_ERR_INVALID, "short write to " + path);
+    return SIFT_HIP_OK;
+}
+
+int dump_stage_files(sift_hip_detector* d) {
+    const std::string& dir = d->dgDir;
+    if (mkdir(dir.c_str(), 0755) != 0 && errno != EEXIST) return fail(SIFT_HIP_ERR_INVALID, "cannot create " + dir);
+    const int W = d->cfg.col_width, H = d->cfg.row_width;
+    std::vector<float> buf((size_t)W * H);
+    HIPCHK(hipMemcpy(buf.data(), d->dDg, sizeof(float) * buf.size(), hipMemcpyDeviceToHost));
+    if (int rc = write_file(dir + "/input.f32", buf.data(), sizeof(float) * buf.size())) return rc;
+    std::string octs;
+    for (int o = 0; o < d->nOct; o++) {
+        const OctGeom& g = d->pyr.oct[o];
+        std::vector<float> plane((size_t)g.W * g.H);
+        for (int l = 0; l < d->L + 3; l++) {
+            HIPCHK(hipMemcpy2D(plane.data(), sizeof(float) * g.W, g.base + (size_t)l * g.planeStride,
+                               sizeof(float) * g.pitch, sizeof(float) * g.W, g.H, hipMemcpyDeviceToHost));
+            char name[64];
+            snprintf(name, sizeof name, "/gauss_o%d_l%d.f32", o, l);
+            if (int rc = write_file(dir + name, plane.data(), sizeof(float) * plane.size())) return rc;
+        }
+        char e[64];
+        snprintf(e, sizeof e, "%s[%d, %d]", o ? ", " : "", g.W, g.H);
+        octs += e;
+    }
+    const Counters& c = d->hCtr[(size_t)d->cur * d->B];
+    const int nc = (int)std::min<unsigned>(c.cand, d->capCand);
+    std::vector<uint2> cand(nc);
+    std::vector<int> quads(4 * (size_t)nc);
+    if (nc) HIPCHK(hipMemcpy(cand.data(), d->dCand, sizeof(uint2) * nc, hipMemcpyDeviceToHost));
+    for (int i = 0; i < nc; i++) {
+        quads[4 * i] = (int)(cand[i].x >> 8);
+        quads[4 * i + 1] = (int)(cand[i].x & 255);
+        quads[4 * i + 2] = (int)(cand[i].y >> 16);
+        quads[4 * i + 3] = (int)(cand[i].y & 0xffff);
+    }
+    if (int rc = write_file(dir + "/candidates.i32", quads.data(), sizeof(int) * quads.size())) return rc;
+    const int n = d->count;
+    std::vector<float> k3(3 * (size_t)n), f4(4 * (size_t)n);
+    std::vector<uint16_t> desc(128 * (size_t)n);
+    if (n) {
+        HIPCHK(hipMemcpy(k3.data(), d->dKpts3[d->cur], sizeof(float) * k3.size(), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(f4.data(), d->dFeats4[d->cur], sizeof(float) * f4.size(), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(desc.data(), d->dDesc[d->cur], sizeof(uint16_t) * desc.size(), hipMemcpyDeviceToHost));
+    }
+    if (int rc = write_file(dir + "/kpts3.f32", k3.data(), sizeof(float) * k3.size())) return rc;
+    if (int rc = write_file(dir + "/feats4.f32", f4.data(), sizeof(float) * f4.size())) return rc;
+    if (int rc = write_file(dir + "/desc.f16", desc.data(), sizeof(uint16_t) * desc.size())) return rc;
+    const sift_hip_config& g = d->cfg;
+    char meta[2048];
+    snprintf(meta, sizeof meta,
+             "{\n \"format\": \"sift_hip stage dump 1\",\n \"frame\": %lld,\n \"width\": %d,\n \"height\": %d,\n"
+             " \"config\": {\"numFeatures\": %d, \"numOctaveLayers\": %d, \"contrastThreshould\": %.17g,"
+             " \"edgeThreshould\": %.17g, \"sigma\": %.17g, \"upscale\": %d, \"numOctaves\": %d},\n"
+             " \"octaves\": [%s],\n \"planes_per_octave\": %d,\n \"candidates\": %d,\n \"keypoints\": %d,\n"
+             " \"overflow\": %u,\n"
+             " \"files\": {\"input.f32\": \"float32 [height][width], the frame as the pipeline read it\",\n"
+             "  \"gauss_o<o>_l<l>.f32\": \"float32 [h_o][w_o], Gaussian plane l of octave o\",\n"
+             "  \"candidates.i32\": \"int32 [candidates][4] (octave, layer, row, col) of the 3x3x3 extrema, unordered\",\n"
+             "  \"kpts3.f32\": \"float32 [keypoints][3] {x, y, layer}\",\n"
+             "  \"feats4.f32\": \"float32 [keypoints][4] {packed octave, size, response, angle}\",\n"
+             "  \"desc.f16\": \"float16 [keypoints][128], integers 0..255\"}\n}\n",
+             d->current - d->firstFrame, g.col_width, g.row_width, g.numFeatures, g.numOctaveLayers,
+             g.contrastThreshould, g.edgeThreshould, g.sigma, g.upscale, d->nOct, octs.c_str(), d->L + 3, nc, n,
+             c.overflow);
+    return write_file(dir + "/meta.json", meta, strlen(meta));
 }
 
 #define CHECK_HANDLE(h)                                                                       \
@@ -1095,6 +1206,12 @@ int sift_hip_copy_descriptors_device(sift_hip_t d, uint16_t* dst, int cap, void*
     if (s != d->stream) HIPCHK(hipStreamWaitEvent(s, d->evFrame[d->cur], 0));
     if (n > 0) HIPCHK(hipMemcpyAsync(dst, d->dDesc[d->cur], sizeof(uint16_t) * 128 * n, hipMemcpyDeviceToDevice, s));
     if (!stream) HIPCHK(hipStreamSynchronize(s));
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_set_datagen(sift_hip_t d, const char* dir) {
+    if (!d) return fail(SIFT_HIP_ERR_INVALID, "null handle");
+    d->dgDir = dir ? dir : "";
     return SIFT_HIP_OK;
 }
 

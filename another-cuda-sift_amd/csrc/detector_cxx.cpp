@@ -142,6 +142,11 @@ void Detector::detectAndComputeDevice(const float* dev, size_t stride, void* str
     refreshViews();
 }
 
+void Detector::setDataGen(const std::string& path) {
+    m_debug_path = path;
+    if (m_handle) check(sift_hip_set_datagen(m_handle, path.c_str()), "setDataGen");
+}
+
 void Detector::copyToHost(bool descriptor) {
     if (!m_initialized) return;
     final_kpts.resize((size_t)total_size);

@@ -40,6 +40,8 @@
 #include <float.h>
 #include <limits.h>
 
+#include <type_traits>
+
 #include "sift_kernels.h"
 #include "sift_match.h"
 #include "sift_math.h"
@@ -146,19 +148,20 @@ struct Best {
 // Merge a key group's top-2 (max-keys m1 >= m2 of the group starting at train
 // row t0) into the running pair.  The running entries come from earlier groups
 // (lower train indices), so they win ties.
-__device__ __forceinline__ void fold_group(Best& b, int m1, int m2, int t0) {
+__device__ __forceinline__ Best fold_group(const Best b, int m1, int m2, int t0) {
+    const int be1 = b.e1, bi1 = b.i1, be2 = b.e2, bi2 = b.i2;  // values: no member-address selects (scratch)
     const bool v1 = m1 > kInvalidKey, v2 = m2 > kInvalidKey;
     const int s1 = v1 ? -m1 : 0, s2 = v2 ? -m2 : 0;  // 128 e + r
     const int te1 = v1 ? (s1 >> 7) : kNone, ti1 = t0 + (s1 & 127);
     const int te2 = v2 ? (s2 >> 7) : kNone, ti2 = t0 + (s2 & 127);
-    const bool c1 = te1 < b.e1;
-    const bool c2 = c1 ? te2 < b.e1 : te1 < b.e2;
-    const int ne2 = c1 ? (c2 ? te2 : b.e1) : (c2 ? te1 : b.e2);
-    const int ni2 = c1 ? (c2 ? ti2 : b.i1) : (c2 ? ti1 : b.i2);
-    b.e1 = c1 ? te1 : b.e1;
-    b.i1 = c1 ? ti1 : b.i1;
-    b.e2 = ne2;
-    b.i2 = ni2;
+    const bool c1 = te1 < be1;
+    const bool c2 = c1 ? te2 < be1 : te1 < be2;
+    Best r;
+    r.e2 = c1 ? (c2 ? te2 : be1) : (c2 ? te1 : be2);
+    r.i2 = c1 ? (c2 ? ti2 : bi1) : (c2 ? ti1 : bi2);
+    r.e1 = c1 ? te1 : be1;
+    r.i1 = c1 ? ti1 : bi1;
+    return r;
 }
 
 __device__ __forceinline__ bool lt_ei(int ea, int ia, int eb, int ib) { return ea < eb || (ea == eb && ia < ib); }
@@ -312,65 +315,86 @@ __global__ __launch_bounds__(256, 2) void k_match(MatchBatch batch, int S, int n
             qn[qb] = norms[pr.qrow0 + row];
         }
         // Tile loader: thread -> 16 bytes (row tid >> 3, part tid & 7) of a
-        // 4 KiB tile; thread r < 32 -> row r's negated key bias.
+        // 4 KiB tile; thread r < 32 -> row r's negated key bias.  Loads run two
+        // tiles ahead through a ring of two register slots (tile k in slot
+        // k & 1), so a tile's global load has two iterations to land before
+        // it is stored to its LDS buffer (k & 1) for iteration k.
         const int lrow = tid >> 3, lpart = tid & 7;
-        i32x4 nv = {0, 0, 0, 0};
-        int nk = 0;
-        auto fetch = [&](int tile) {
+        i32x4 nv[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+        int nk[2] = {0, 0};
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        auto fetch = [&](int tile, auto slot) {
+            constexpr int SL = decltype(slot)::value;
             const int r = tile * kMatchTileRows + lrow;
             const i32x4 v = *reinterpret_cast<const i32x4*>(tc + (size_t)min(r, pr.nt - 1) * 128 + 16 * lpart);
-            nv = r < pr.nt ? v : (i32x4){0, 0, 0, 0};
+            nv[SL] = r < pr.nt ? v : (i32x4){0, 0, 0, 0};
             const int rr = tile * kMatchTileRows + (tid & 31);
             const int n2 = tn[min(rr, pr.nt - 1)];
             const int lr = ((tile - tbeg) & (kGroupTiles - 1)) * kMatchTileRows + (tid & 31);  // row in the key group
-            nk = rr < pr.nt ? -(128 * n2 + lr) : kPadBias;
+            nk[SL] = rr < pr.nt ? -(128 * n2 + lr) : kPadBias;
         };
-        auto stash = [&](int buf) {
-            *reinterpret_cast<i32x4*>(s_tile[buf] + lrow * kRowPad + 16 * lpart) = nv;
-            if (tid < kMatchTileRows) s_ntk[buf][tid] = nk;
+        auto stash = [&](auto slot) {  // slot k & 1 -> LDS buffer k & 1
+            constexpr int SL = decltype(slot)::value;
+            *reinterpret_cast<i32x4*>(s_tile[SL] + lrow * kRowPad + 16 * lpart) = nv[SL];
+            if (tid < kMatchTileRows) s_ntk[SL][tid] = nk[SL];
         };
         Best best[2] = {{kNone, kNone, kNone, kNone}, {kNone, kNone, kNone, kNone}};
-        int m1[2] = {INT_MIN, INT_MIN}, m2[2] = {INT_MIN, INT_MIN};
+        // Running key top-2 per query block in two chains (even / odd
+        // accumulator registers): half the dependent v_max / v_med3 chain.
+        int m1e[2] = {INT_MIN, INT_MIN}, m2e[2] = {INT_MIN, INT_MIN};  // even registers
+        int m1o[2] = {INT_MIN, INT_MIN}, m2o[2] = {INT_MIN, INT_MIN};  // odd registers
         if (tbeg < tend) {
-            fetch(tbeg);
-            stash(0);
-            if (tbeg + 1 < tend) fetch(tbeg + 1);
+            fetch(tbeg, I0{});
+            stash(I0{});
+            if (tbeg + 1 < tend) fetch(tbeg + 1, I1{});
+            if (tbeg + 2 < tend) fetch(tbeg + 2, I0{});
         }
-        for (int tile = tbeg; tile < tend; tile++) {
-            const int buf = (tile - tbeg) & 1;
-            lds_barrier();  // tile `tile` is in s_tile[buf]; every wave is done with s_tile[buf ^ 1]
+        auto step = [&](int tile, auto par) {  // par = (tile - tbeg) & 1
+            constexpr int PB = decltype(par)::value;
+            lds_barrier();  // tile `tile` is in s_tile[PB]; every wave is done with s_tile[PB ^ 1]
             i32x4 a[4], tk[4];
-            const int8_t* ta = s_tile[buf] + col * kRowPad + 64 * h;
+            const int8_t* ta = s_tile[PB] + col * kRowPad + 64 * h;
 #pragma unroll
             for (int kb = 0; kb < 4; kb++) a[kb] = *reinterpret_cast<const i32x4*>(ta + 16 * kb);
             // accumulator register i holds train row (i & 3) + 8 (i >> 2) + 4 h
 #pragma unroll
-            for (int g = 0; g < 4; g++) tk[g] = *reinterpret_cast<const i32x4*>(s_ntk[buf] + 8 * g + 4 * h);
+            for (int g = 0; g < 4; g++) tk[g] = *reinterpret_cast<const i32x4*>(s_ntk[PB] + 8 * g + 4 * h);
             if (tile + 1 < tend) {
-                stash(buf ^ 1);
-                if (tile + 2 < tend) fetch(tile + 2);
+                stash(std::integral_constant<int, PB ^ 1>{});
+                if (tile + 3 < tend) fetch(tile + 3, std::integral_constant<int, PB ^ 1>{});
             }
+            i32x16 acc[2] = {{}, {}};
 #pragma unroll
-            for (int qb = 0; qb < 2; qb++) {
-                i32x16 acc = {};
+            for (int qb = 0; qb < 2; qb++)
 #pragma unroll
-                for (int kb = 0; kb < 4; kb++) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[kb], bq[qb][kb], acc, 0, 0, 0);
+                for (int kb = 0; kb < 4; kb++)
+                    acc[qb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[kb], bq[qb][kb], acc[qb], 0, 0, 0);
 #pragma unroll
-                for (int i = 0; i < 16; i++) {
-                    const int key = (acc[i] << 8) + tk[i >> 2][i & 3];
-                    m2[qb] = med3_i32(m1[qb], key, m2[qb]);  // second largest of {m1 >= m2, key}
-                    m1[qb] = max(m1[qb], key);
+            for (int qb = 0; qb < 2; qb++)
+#pragma unroll
+                for (int i = 0; i < 16; i += 2) {
+                    const int ke = (acc[qb][i] << 8) + tk[i >> 2][i & 3];
+                    const int ko = (acc[qb][i + 1] << 8) + tk[i >> 2][(i & 3) + 1];
+                    m2e[qb] = med3_i32(m1e[qb], ke, m2e[qb]);  // second largest of {m1 >= m2, key}
+                    m1e[qb] = max(m1e[qb], ke);
+                    m2o[qb] = med3_i32(m1o[qb], ko, m2o[qb]);
+                    m1o[qb] = max(m1o[qb], ko);
                 }
-            }
             const int gi = tile - tbeg;
             if ((gi & (kGroupTiles - 1)) == kGroupTiles - 1 || tile + 1 == tend) {
                 const int t0 = (tile - (gi & (kGroupTiles - 1))) * kMatchTileRows;
 #pragma unroll
                 for (int qb = 0; qb < 2; qb++) {
-                    fold_group(best[qb], m1[qb], m2[qb], t0);
-                    m1[qb] = m2[qb] = INT_MIN;
+                    const int a1 = m1e[qb], a2 = m2e[qb], b1 = m1o[qb], b2 = m2o[qb];
+                    best[qb] = fold_group(best[qb], max(a1, b1), max(min(a1, b1), max(a2, b2)), t0);
+                    m1e[qb] = m2e[qb] = m1o[qb] = m2o[qb] = INT_MIN;
                 }
             }
+        };
+        for (int tile = tbeg; tile < tend; tile += 2) {
+            step(tile, I0{});
+            if (tile + 1 < tend) step(tile + 1, I1{});
         }
 #pragma unroll
         for (int qb = 0; qb < 2; qb++) {

@@ -130,22 +130,22 @@ struct BlurJob {
 // load instructions of the per-column dword staging.  The LDS tile then starts
 // at column x0 - 8 for every radius <= 8 (ORG), whichever staging ran.
 #ifndef SIFT_BLUR_X4LD
-#define SIFT_BLUR_X4LD 0
+#define SIFT_BLUR_X4LD 1
 #endif
 // Full tiles store their output rows as 16-byte stores (each wave's 8-row
 // blocks transposed through the freed LDS tile) instead of one dword per
 // lane and row: a quarter of the store instructions.
 #ifndef SIFT_BLUR_X4ST
-#define SIFT_BLUR_X4ST 0
+#define SIFT_BLUR_X4ST 1
 #endif
 template <int R>
 constexpr int blur_org() {  // tile column 0 = image column x0 - ORG
     return SIFT_BLUR_X4LD && R <= 8 ? 8 : R;
 }
 template <int R>
-constexpr int blur_iw() {
-    return SIFT_BLUR_IW16 ? ((BLUR_TW + 2 * blur_org<R>() + 15) / 32) * 32 + 16
-                          : (BLUR_TW + 2 * blur_org<R>() + 3) & ~3;
+constexpr int blur_iw() {  // radius > 8: the next 16-mod-32 pitch (112) costs a workgroup per CU -- kept at 64 + 2R
+    return SIFT_BLUR_IW16 && R <= 8 ? ((BLUR_TW + 2 * blur_org<R>() + 15) / 32) * 32 + 16
+                                    : (BLUR_TW + 2 * blur_org<R>() + 3) & ~3;
 }
 template <int R>
 constexpr int blur_lds_floats() {

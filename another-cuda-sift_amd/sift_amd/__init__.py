@@ -87,6 +87,7 @@ def lib() -> ctypes.CDLL:
         "sift_hip_results_device": (i, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), ip, ip]),
         "sift_hip_copy_to_host": (i, [vp, vp, vp, vp, i]),
         "sift_hip_copy_descriptors_device": (i, [vp, vp, i, vp]),
+        "sift_hip_set_datagen": (i, [vp, ctypes.c_char_p]),
         "sift_hip_set_timing": (i, [vp, i]),
         "sift_hip_timing_count": (i, [vp, ip]),
         "sift_hip_timing_entry": (i, [vp, i, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(d), ip, ctypes.POINTER(d)]),
@@ -350,6 +351,11 @@ class Detector:
         cnt = ctypes.c_int()
         _check(lib().sift_hip_debug_candidates(self._h, _ptr(q), cap, ctypes.byref(cnt)), "debug_candidates")
         return q[: min(cnt.value, cap)]
+
+    def setDataGen(self, path: str) -> None:
+        """Detector.hh:48-51: from now on every single-frame detect writes its stage
+        dumps into `path` (sift_hip_set_datagen; "" switches them off)."""
+        _check(lib().sift_hip_set_datagen(self._h, (path or "").encode()), "setDataGen")
 
     # --- stage timing (roofline) ---------------------------------------------
     def set_timing(self, enable, blur_reps: int = 1) -> None:

@@ -44,8 +44,11 @@ public:
     // Detector.cu:606-634: copies total_size results (+ descriptors) to host.
     void copyToHost(bool descriptor);
 
-    // Detector.hh:48-51 debug snapshot switch: accepted, snapshots not produced.
-    void setDataGen(const std::string& path) { m_debug_path = path; }
+    // Detector.hh:48-51 debug snapshot switch: every following detectAndCompute
+    // writes its stage dumps into `path` (sift_hip_set_datagen: meta.json,
+    // input, every Gaussian plane, candidates, keypoints, descriptors);
+    // tests/stage_check.py replays them.  An empty path switches it off.
+    void setDataGen(const std::string& path);
 
     int numOctaves() const { return m_nOctaves; }
     sift_hip_detector* handle() const { return m_handle; }

@@ -160,6 +160,17 @@ int sift_hip_copy_to_host(sift_hip_t h, float* kpts3, float* feats4, uint16_t* d
  * for an RCCL all-gather).  Copies min(count, cap) rows, pads nothing. */
 int sift_hip_copy_descriptors_device(sift_hip_t h, uint16_t* dst, int cap, void* stream);
 
+/* Detector::setDataGen(path) (Detector.hh:48-51; the reference dumps each
+ * stage's octave-0 inputs/outputs as msgpack+zlib, Detector.cu:145-229,
+ * PerfData.cuh:12-155).  With a non-empty dir every following single-frame
+ * detect completes synchronously and writes this build's stage dumps of the
+ * frame into dir (overwritten per frame; dir is created): meta.json (config,
+ * octave geometry, counts, file layouts), input.f32, gauss_o<o>_l<l>.f32 (every
+ * Gaussian plane), candidates.i32, kpts3.f32, feats4.f32, desc.f16 -- raw
+ * little-endian row-major arrays.  tests/stage_check.py replays a dump against
+ * the CPU oracle and this library.  NULL or "" switches the dumps off. */
+int sift_hip_set_datagen(sift_hip_t h, const char* dir);
+
 /* Stage timing for roofline reporting: when enabled, the next detect calls run
  * un-graphed with HIP events around every kernel; names are stable strings.
  * enable >= 2 also repeats each (pure) blur launch `enable` times back to back

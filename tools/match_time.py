@@ -1,5 +1,7 @@
-"""2000 x 2000 x 128 match latency (bench.py's match_2k timing: 200 back-to-back
-calls between HIP events) for A/B of library builds (SIFT_HIP_LIB)."""
+"""Matcher timings for A/B of library builds (SIFT_HIP_LIB): the C3 single
+2000 x 2000 x 128 pair (bench.py's match_2k: 200 back-to-back calls between HIP
+events) and the C5 rehearsal (8 sets, all 56 ordered pairs in one batched
+call), each checked against torch fp32 (exact for integer descriptors)."""
 import json
 import os
 import sys
@@ -12,11 +14,14 @@ import sift_amd as sift  # noqa: E402
 
 nq = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
 rng = np.random.default_rng(1)
-sets = [torch.from_numpy(rng.integers(0, 256, (nq, 128)).astype(np.float16).view(np.int16)).cuda() for _ in range(2)]
-m = sift.Matcher(nq, nq, max_pairs=8, device=0)
-oi = torch.empty((nq, 2), dtype=torch.int32, device="cuda")
-od = torch.empty((nq, 2), dtype=torch.float32, device="cuda")
-om = torch.empty(nq, dtype=torch.int32, device="cuda")
+K = 8
+sets = [torch.from_numpy(rng.integers(0, 256, (nq, 128)).astype(np.float16).view(np.int16)).cuda() for _ in range(K)]
+pairs = [(i, j) for i in range(K) for j in range(K) if i != j]
+P = len(pairs)
+m = sift.Matcher(nq, nq, max_pairs=P, device=0)
+oi = torch.empty((P * nq, 2), dtype=torch.int32, device="cuda")
+od = torch.empty((P * nq, 2), dtype=torch.float32, device="cuda")
+om = torch.empty(P * nq, dtype=torch.int32, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 
 
@@ -25,19 +30,40 @@ def one():
                    om.data_ptr(), st)
 
 
-for _ in range(20):
-    one()
-torch.cuda.synchronize()
-e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-e0.record()
-for _ in range(200):
-    one()
-e1.record()
-torch.cuda.synchronize()
-ms = e0.elapsed_time(e1) / 200
-# check against torch fp32 (exact for integer descriptors)
-q, t = sets[0].view(torch.float16).float(), sets[1].view(torch.float16).float()
-d2 = (q * q).sum(1, keepdim=True) + (t * t).sum(1)[None] - 2 * q @ t.T
-ref = torch.topk(d2, 2, dim=1, largest=False)
-ok = bool((oi[:, 0].long() == ref.indices[:, 0]).float().mean() > 0.999)
-print(json.dumps({"lib": os.environ.get("SIFT_HIP_LIB", "default"), "nq": nq, "ms": round(ms, 4), "top1_ok": ok}))
+def batched():
+    m.match_batched([sets[i].data_ptr() for i, _ in pairs], [nq] * P, [sets[j].data_ptr() for _, j in pairs], [nq] * P,
+                    idx2_ptr=oi.data_ptr(), d2_ptr=od.data_ptr(), stream=st)
+
+
+def timed(fn, reps):
+    for _ in range(10):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def ref_top2(q, t):
+    q, t = q.view(torch.float16).float(), t.view(torch.float16).float()
+    d2 = (q * q).sum(1, keepdim=True) + (t * t).sum(1)[None] - 2 * q @ t.T
+    return torch.topk(d2, 2, dim=1, largest=False)
+
+
+ms1 = timed(one, 200)
+r = ref_top2(sets[0], sets[1])
+ok1 = bool((oi[:nq, 0].long() == r.indices[:, 0]).float().mean() > 0.999)
+ms56 = timed(batched, 50)
+ok56 = True
+for p in (0, 17, 55):
+    i, j = pairs[p]
+    r = ref_top2(sets[i], sets[j])
+    ok56 &= bool((oi[p * nq:(p + 1) * nq, 0].long() == r.indices[:, 0]).float().mean() > 0.999)
+fl1, fl56 = 2.0 * nq * nq * 128, 2.0 * nq * nq * 128 * P
+print(json.dumps({"lib": os.environ.get("SIFT_HIP_LIB", "default"), "nq": nq, "ms": round(ms1, 4),
+                  "top1_ok": ok1, "c5_56_pairs_ms": round(ms56, 4), "c5_top1_ok": ok56,
+                  "c5_tops": round(fl56 / ms56 / 1e9, 1), "c3_tops": round(fl1 / ms1 / 1e9, 1)}))
