@@ -18,7 +18,8 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
             -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -I$(SRC) -Wall -Wno-unused-result $(EXTRA_HIPFLAGS)
 CXXFLAGS := -O2 -std=c++17 -fPIC -Iinclude -Wall -Wextra
 
-HIP_SRCS := $(SRC)/detector.hip $(SRC)/pyramid.hip $(SRC)/keypoints.hip $(SRC)/descriptor.hip $(SRC)/match.hip
+HIP_SRCS := $(SRC)/detector.hip $(SRC)/pyramid.hip $(SRC)/keypoints.hip $(SRC)/descriptor.hip $(SRC)/match.hip \
+            $(SRC)/multi.hip
 HIP_OBJS := $(patsubst $(SRC)/%.hip,$(OUT)/obj/%.o,$(HIP_SRCS)) $(OUT)/obj/synth_frame.o
 
 all: $(OUT)/libsift_hip.so $(OUT)/libsift_cuda.so tools
@@ -32,15 +33,17 @@ $(OUT)/obj/synth_frame.o: $(SRC)/synth_frame.cpp include/sift_hip.h
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
 $(OUT)/libsift_hip.so: $(HIP_OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HIP_OBJS) -Wl,-soname,libsift_hip.so
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HIP_OBJS) -ldl -Wl,-soname,libsift_hip.so
 
-$(OUT)/libsift_cuda.so: $(SRC)/detector_cxx.cpp $(wildcard include/sift_cuda/*.hh) $(OUT)/libsift_hip.so
-	$(CXX) $(CXXFLAGS) -shared -o $@ $(SRC)/detector_cxx.cpp -L$(OUT) -lsift_hip -Wl,-rpath,'$$ORIGIN'
+CXX_SRCS := $(SRC)/detector_cxx.cpp $(SRC)/multi_cxx.cpp
 
-tools: $(OUT)/detection_example $(OUT)/extract_and_match_example
+$(OUT)/libsift_cuda.so: $(CXX_SRCS) $(wildcard include/sift_cuda/*.hh) include/sift_hip.h $(OUT)/libsift_hip.so
+	$(CXX) $(CXXFLAGS) -pthread -shared -o $@ $(CXX_SRCS) -L$(OUT) -lsift_hip -Wl,-rpath,'$$ORIGIN'
+
+tools: $(OUT)/detection_example $(OUT)/extract_and_match_example $(OUT)/multi_gpu_example
 
 $(OUT)/%: tools/%.cpp $(OUT)/libsift_cuda.so
-	$(CXX) $(CXXFLAGS) -o $@ $< -L$(OUT) -lsift_cuda -lsift_hip -Wl,-rpath,'$$ORIGIN'
+	$(CXX) $(CXXFLAGS) -pthread -o $@ $< -L$(OUT) -lsift_cuda -lsift_hip -Wl,-rpath,'$$ORIGIN'
 
 oracle:
 	$(MAKE) -C oracle

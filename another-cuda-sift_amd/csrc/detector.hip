@@ -154,6 +154,8 @@ struct TimingAgg {
 
 }  // namespace
 
+void sift_amd::set_last_error(const std::string& msg) { g_err = msg; }
+
 struct sift_hip_detector {
     sift_hip_config cfg{};
     int device = 0;

@@ -44,10 +44,12 @@ sift_hip_config toAbi(const CudaSiftConfig& c) {
 
 }  // namespace
 
-Detector::Detector(const CudaSiftConfig& config) : m_config(config) {
+Detector::Detector(const CudaSiftConfig& config) : Detector(config, -1) {}
+
+Detector::Detector(const CudaSiftConfig& config, int device) : m_config(config) {
     if (config.col_width > 0 && config.row_width > 0) {
         const sift_hip_config a = toAbi(config);
-        check(sift_hip_create(&a, -1, &m_handle), "Detector::Detector");
+        check(sift_hip_create(&a, device, &m_handle), "Detector::Detector");
         sift_hip_num_octaves(m_handle, &m_nOctaves);
     }
     max_kpts = config.numFeatures;

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 namespace sift_amd {
 
 constexpr int kMaxOctaves = 16;
@@ -180,6 +182,10 @@ __device__ __forceinline__ unsigned range_key(float f) {
 __device__ __forceinline__ float decode_range_key(unsigned u) {
     return __uint_as_float(u & 0x80000000u ? u & 0x7fffffffu : ~u);
 }
+
+// The C ABI's thread-local error message (sift_hip_last_error), shared by
+// the translation units that implement entry points.
+void set_last_error(const std::string& msg);
 
 // Exp table (OpenCV expTab_f) uploaded once per device (orientation and
 // descriptor translation units each hold a copy).

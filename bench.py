@@ -44,7 +44,7 @@ from sift_amd import multi  # noqa: E402
 METRIC = "detectAndCompute Mpix/s + 2kx2k 128-D match ms at 1/2/4/8 MI355X"
 W, H = 1920, 1200
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
-FP16_MFMA_PEAK_TFLOPS = 2500.0  # dense
+I8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA (MI355X_MICROARCH.md: 2x the 2.5 PF bf16 rate); the matcher's dtype
 
 
 def cpu_model():
@@ -332,6 +332,115 @@ def run_c1_gpu(local):
             "note": "host f32 frames, synchronous detectAndCompute x2 + matchBruteForce (prev vs current), median of 20"}
 
 
+
+def pmc_kernel(summary_path, kernel_names):
+    """Per-dispatch means of a kernel family's counters in a committed PMC
+    summary (the timed-launch groups only, as pmc_traffic): corrected HBM
+    bytes and the VALU busy fraction (2 cycles per wave64 VALU instruction on
+    a SIMD32, over the dispatch's wall cycles x 1024 SIMDs; GRBM_GUI_ACTIVE
+    sums the 8 XCDs)."""
+    try:
+        with open(summary_path) as f:
+            summ = json.load(f)
+    except (OSError, ValueError):
+        return None
+    cal = summ.get("calibration_counter_over_true_bytes", {})
+    fetch_scale = 1.0 / cal.get("copy4:FETCH_SIZE", 0.5)
+    write_scale = 1.0 / cal.get("copy4:WRITE_SIZE", 1.0)
+    rows = [k for k in summ.get("kernels", []) if k["kernel"].split("<")[0].split("::")[-1] in kernel_names]
+    if not rows:
+        return None
+    top = max(k["dispatches"] for k in rows)
+    rows = [k for k in rows if k["dispatches"] >= top // 2]
+    n = sum(k["dispatches"] for k in rows)
+
+    def mean(c):
+        v = [(k[c], k["dispatches"]) for k in rows if c in k]
+        return sum(x * d for x, d in v) / sum(d for _, d in v) if v else None
+
+    out = {"dispatches": n, "source": os.path.relpath(summary_path, ROOT)}
+    fs, ws = mean("FETCH_SIZE"), mean("WRITE_SIZE")
+    if fs is not None and ws is not None:
+        out["hbm_bytes"] = round((fs * fetch_scale + ws * write_scale) * 1024)
+    valu, gui = mean("SQ_INSTS_VALU"), mean("GRBM_GUI_ACTIVE")
+    if valu and gui:
+        out["valu_busy_frac"] = round(2.0 * valu / (gui / 8.0 * 1024), 4)
+    conf, lds = mean("SQ_LDS_BANK_CONFLICT"), mean("SQ_ACTIVE_INST_LDS")
+    if conf is not None and lds:
+        out["lds_bank_conflict_over_active_lds"] = round(conf / lds, 4)
+    return out
+
+
+def window_bytes(kpts3, feats4, first_octave=0):
+    """Algorithmic (unique input) bytes of the keypoint kernels for one frame's
+    final keypoints (SURVEY.md 8d keypoint term): orientation reads the
+    (2r+3)^2 pixels of its r = round(4.5 scl) window plus gradient neighbours,
+    once per refined keypoint (= distinct (x, y, size, octave)); the
+    descriptor reads the (5 hist_width + 3)^2 pixels of its rotated 4x4-cell
+    square (at most the (2r+1)^2 window, r = round(hist_width * sqrt2 * 2.5))
+    and writes 256 B of descriptor + reads its 64-B job."""
+    oct_ = feats4[:, 0].astype(np.int64) & 255
+    oct_ = np.where(oct_ >= 128, oct_ - 256, oct_)
+    size_o = feats4[:, 1] / np.exp2(oct_.astype(np.float64))  # size in its octave's pixels
+    hw = 1.5 * size_o
+    r_desc = np.round(hw * np.sqrt(2.0) * 2.5)
+    desc = 4.0 * np.minimum((2 * r_desc + 1) ** 2, (5 * hw + 3) ** 2) + 256 + 64
+    uniq = np.unique(np.stack([kpts3[:, 0], kpts3[:, 1], feats4[:, 1], feats4[:, 0]], 1), axis=0)
+    o_u = uniq[:, 3].astype(np.int64) & 255
+    o_u = np.where(o_u >= 128, o_u - 256, o_u) - first_octave
+    r_ori = np.round(4.5 * uniq[:, 2] * 0.5 / np.exp2(o_u.astype(np.float64) + first_octave))
+    ori = 4.0 * (2 * r_ori + 3) ** 2 + 32 + 32
+    return float(ori.sum()), float(desc.sum()), len(uniq)
+
+
+def kernel_rooflines(det, timing, steps, B, pmc_path):
+    """Per-kernel roofline entries of the C2 step (eager timing pass, HIP
+    events on the detector's stream): algorithmic bytes per launch / average
+    launch time against the 8 TB/s HBM peak, with the committed PMC summary's
+    measured HBM bytes and VALU busy fraction beside it."""
+    per_frame = [det.batch_copy_to_host(i, descriptor=False) for i in range(B)]
+    ori_b = desc_b = 0.0
+    refined = 0
+    for k3, f4, _ in per_frame:
+        o, d, n = window_bytes(k3, f4)
+        ori_b += o
+        desc_b += d
+        refined += n
+    out = {}
+
+    def entry(names, bytes_per_launch, pmc_names, note):
+        ms = sum(timing[n]["ms"] for n in names if n in timing)
+        launches = sum(timing[n]["launches"] for n in names if n in timing)
+        if not launches:
+            return None
+        us = ms / launches * 1e3
+        achieved = bytes_per_launch / (us * 1e-6) / 1e9
+        e = {"bound": "hbm", "algo_bytes_per_launch": round(bytes_per_launch), "avg_launch_us": round(us, 3),
+             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": round(achieved / HBM_PEAK_GBS, 4), "note": note}
+        p = pmc_kernel(pmc_path, pmc_names)
+        if p:
+            e["pmc"] = p
+            if "hbm_bytes" in p:
+                e["traffic"] = p["hbm_bytes"]
+                e["traffic_over_algo"] = round(p["hbm_bytes"] / bytes_per_launch, 3)
+        return e
+
+    blurs = [k for k in timing if k.startswith("blur_")]
+    bl = sum(timing[k]["launches"] for k in blurs)
+    out["blur"] = entry(blurs, sum(timing[k]["bytes"] for k in blurs) / bl, ("k_blur", "k_blur2"),
+                        "all blur launches of a step, each x10 back to back between events; read + write of "
+                        "every plane (+ the decimated base copy)")
+    out["extrema"] = entry(["extrema"], timing["extrema"]["bytes"] / timing["extrema"]["launches"],
+                           ("k_extrema_all",), "reads the L+3 Gaussian planes of every octave once (24 B/px)")
+    out["orientation"] = entry(["orientation"], ori_b, ("k_orientation",),
+                               f"window model over {refined} refined keypoints of the {B}-frame step "
+                               "(L2-served windows: latency/VALU-bound, frac vs HBM is not its limit)")
+    out["descriptor"] = entry(["descriptor"], desc_b, ("k_descriptor",),
+                              "rotated-square window model + 256 B out + 64 B job per keypoint "
+                              "(L2-served windows: latency/VALU-bound)")
+    return {k: v for k, v in out.items() if v}
+
 def main():
     a = parse()
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
@@ -517,6 +626,10 @@ def main():
     # ---- per-kernel roofline: HIP events on the detector's own stream --------
     rl = measure_roofline(detb, frames, stride, a.traffic_summary, batch=fb if B > 1 else None)
     timing, nt = rl["timing"], rl["frames"] * B
+    try:
+        rk = kernel_rooflines(detb, timing, rl["frames"], B, a.traffic_summary) if B > 1 else {}
+    except Exception as e:  # keep the line if a model input is missing
+        rk = {"error": repr(e)[:300]}
     del detb
     stages = stage_table(timing, nt)
     total_ms = sum(stages.values()) * nt / 1e3
@@ -597,7 +710,7 @@ def main():
         ms = m0.elapsed_time(m1) / reps
         fl = 2.0 * nq * nq * 128 * P
         return {"virtual_ranks": K, "pairs_per_gpu": P, "batched_match_ms": round(ms, 4), "allgather_us": None,
-                "tflops": round(fl / ms / 1e9, 2), "mfma_frac": round(fl / ms / 1e9 / FP16_MFMA_PEAK_TFLOPS, 4),
+                "tops": round(fl / ms / 1e9, 2), "mfma_frac": round(fl / ms / 1e9 / I8_MFMA_PEAK_TOPS, 4),
                 "note": "one-GPU rehearsal of C5: all 8 sets resident, the 56 ordered 2000x2000x128 pairs in one "
                         "batched launch (no collective on one GPU)"}
 
@@ -641,14 +754,21 @@ def main():
         bms = max_over_ranks(m0.elapsed_time(m1) / 50)
         fl = 2.0 * nq * nq * 128 * P
         return {"allgather_us": round(ag_us, 2), "allgather_bytes_per_rank": nq * 128 * 2, "pairs_per_gpu": P,
-              "batched_match_ms": round(bms, 4), "tflops_per_gpu": round(fl / bms / 1e9, 2),
-              "mfma_frac": round(fl / bms / 1e9 / FP16_MFMA_PEAK_TFLOPS, 4),
+              "batched_match_ms": round(bms, 4), "tops_per_gpu": round(fl / bms / 1e9, 2),
+              "mfma_frac": round(fl / bms / 1e9 / I8_MFMA_PEAK_TOPS, 4),
               "collective": f"all_gather ({a.dist_backend}; nccl = RCCL all_gather_into_tensor), sift_amd/multi.py"}
 
     try:
         c5 = run_c5() if world > 1 else run_c5_single_gpu()
     except Exception as e:  # keep the C2 line even if the C5 side measurement fails
         c5 = {"error": repr(e)[:300]}
+    if isinstance(rk, dict) and "batched_match_ms" in c5:
+        ops = 2.0 * nq * nq * 128 * c5["pairs_per_gpu"]
+        rk["matcher"] = {"bound": "mfma", "kernel": "k_match_prep + k_match (C5 batched launch)",
+                         "algo_ops_per_launch": ops, "avg_launch_us": round(c5["batched_match_ms"] * 1e3, 3),
+                         "achieved": round(ops / c5["batched_match_ms"] / 1e9, 1), "peak": I8_MFMA_PEAK_TOPS,
+                         "unit": "TOPS", "frac": round(ops / c5["batched_match_ms"] / 1e9 / I8_MFMA_PEAK_TOPS, 4),
+                         "c3_single_pair_frac": round(flops / match_ms / 1e9 / I8_MFMA_PEAK_TOPS, 5)}
 
     # ---- CPU baseline: the oracle on the host cores (rank 0, N=1 only) -------
     cpu = None
@@ -682,6 +802,7 @@ def main():
                 "keypoints_per_frame": kcount,
             },
             "roofline": rl["roofline"],
+            "roofline_kernels": rk,
             "cpu_baseline": cpu,
             "ms_per_frame": round(ms_per_frame, 4),
             "pipeline_hbm_frac": round(88.0 * sum_px / (ms_per_frame / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -692,7 +813,8 @@ def main():
             "stage_sum_us_eager": round(total_ms / nt * 1e3, 1),
             "dominant_stage": dom,
             "match_2k": {"ms": round(match_ms, 4), "ms_sync_host": round(match_sync_ms, 4),
-                         "tflops": round(flops / match_ms / 1e9, 2), "mfma_frac": round(flops / match_ms / 1e9 / FP16_MFMA_PEAK_TFLOPS, 5),
+                         "tops": round(flops / match_ms / 1e9, 2), "mfma_frac": round(flops / match_ms / 1e9 / I8_MFMA_PEAK_TOPS, 5),
+                         "dtype": "int8 codes (v - 128) on v_mfma_i32_32x32x32_i8, exact int32 d^2",
                          "matches": n_matches, "ratio": 0.8},
             "c4_256_frames_1600x900": c4,
             "c5_allgather_match": c5,

@@ -17,6 +17,10 @@ namespace sift_cuda {
 class Detector {
 public:
     explicit Detector(const CudaSiftConfig& config);
+    // Extra: bound to an explicit device instead of the calling thread's
+    // current one (one Detector per GPU, each driven by its own host thread:
+    // sift_cuda/MultiDetector.hh).
+    Detector(const CudaSiftConfig& config, int device);
     ~Detector();
     Detector(const Detector&) = delete;
     Detector& operator=(const Detector&) = delete;

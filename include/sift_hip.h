@@ -223,6 +223,30 @@ int sift_hip_match_host(sift_hip_matcher_t m, const uint16_t* query, int nq,
                         const uint16_t* train, int nt, float ratio, int ratio_on_squared,
                         int* out);
 
+/* --- Multi-GPU (the reference binds one Detector to the current
+ * device, Detector.hh:26-29, and has no multi-GPU path) ----------------------- */
+
+/* Binds the calling host thread to `device` (a thread per GPU drives its own
+ * Detector; sift_hip_malloc & co. then allocate there). */
+int sift_hip_set_device(int device);
+/* Any-to-any device copy (peer or same device) on `stream` (NULL: synchronous). */
+int sift_hip_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
+
+/* Node-local communicator over RCCL (xGMI): one rank per entry of `devices`
+ * (distinct GPUs), created with ncclCommInitAll.  RCCL is loaded with dlopen on
+ * first use (no link-time dependency). */
+typedef struct sift_hip_comm* sift_hip_comm_t;
+int sift_hip_comm_create(int ndev, const int* devices, sift_hip_comm_t* out);
+int sift_hip_comm_destroy(sift_hip_comm_t c);
+int sift_hip_comm_size(sift_hip_comm_t c, int* n);
+/* All-gather: recv[k] (device k) receives ndev * bytes, rank r's send[r] at
+ * offset r * bytes (the C5 exchange of descriptor sets).  One ncclAllGather per
+ * rank inside an ncclGroupStart/End; streams[k] may be NULL for the
+ * communicator's own stream, and with streams == NULL the call returns after
+ * every rank's copy has completed. */
+int sift_hip_comm_allgather(sift_hip_comm_t c, const void* const* send, void* const* recv, size_t bytes,
+                            void* const* streams);
+
 /* --- Utilities -------------------------------------------------------------- */
 
 /* Deterministic synthetic frame, fp32 0..255 integers. */
