@@ -575,9 +575,12 @@ extern "C" int sift_hip_debug_desc_stamps(unsigned long long* out) {
 void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned* range_keys, uint16_t* desc,
                        Counters* host_ctr, const KeypointParams& kp, const Frames& fr, hipStream_t s) {
     (void)kp;
+#ifndef SIFT_DESC_SINGLE_DT
+#define SIFT_DESC_SINGLE_DT 256  // threads per keypoint for a single frame (tools A/B builds vary it)
+#endif
     if (fr.nf <= 1) {
-        hipLaunchKernelGGL(k_descriptor<256>, dim3(8192), dim3(256), 0, s, jobs, ctr, range_keys, desc, host_ctr,
-                           fr.stride, 1u);
+        hipLaunchKernelGGL(k_descriptor<SIFT_DESC_SINGLE_DT>, dim3(8192), dim3(SIFT_DESC_SINGLE_DT), 0, s, jobs, ctr,
+                           range_keys, desc, host_ctr, fr.stride, 1u);
     } else {
         // Workgroups per frame: 2048 at 8 frames (16384 in all).  The bigger
         // grids this kernel once had filled every CU slot and kept the other

@@ -103,8 +103,20 @@ const char* build_flags() {
 #ifdef SIFT_BLUR_X4LD
            " SIFT_BLUR_X4LD=" SIFT_STR(SIFT_BLUR_X4LD)
 #endif
+#ifdef SIFT_BLUR_CHAIN
+           " SIFT_BLUR_CHAIN=" SIFT_STR(SIFT_BLUR_CHAIN)
+#endif
+#ifdef SIFT_CHAIN_NW
+           " SIFT_CHAIN_NW=" SIFT_STR(SIFT_CHAIN_NW)
+#endif
 #ifdef SIFT_BLUR_X4ST
            " SIFT_BLUR_X4ST=" SIFT_STR(SIFT_BLUR_X4ST)
+#endif
+#ifdef SIFT_ORI_AHEAD
+           " SIFT_ORI_AHEAD=" SIFT_STR(SIFT_ORI_AHEAD)
+#endif
+#ifdef SIFT_DESC_SINGLE_DT
+           " SIFT_DESC_SINGLE_DT=" SIFT_STR(SIFT_DESC_SINGLE_DT)
 #endif
 #ifdef SIFT_ORI_PER
            " SIFT_ORI_PER=" SIFT_STR(SIFT_ORI_PER)
@@ -233,6 +245,10 @@ struct sift_hip_detector {
     float* dDg = nullptr;
 
     bool timing = false;
+#ifndef SIFT_BLUR_CHAIN
+#define SIFT_BLUR_CHAIN 0  // measured slower: A/B builds -DSIFT_BLUR_CHAIN=1
+#endif
+    bool blurChains = SIFT_BLUR_CHAIN;  // chained blur units (launch_blur_chain)
     int blurReps = 1;  // timing mode: each blur launch repeated back to back inside its event pair
     std::vector<TimingRec> trecs;
     std::vector<TimingAgg> tagg;
@@ -591,13 +607,38 @@ void enqueue_body(sift_hip_detector* d, int slot, int nf) {
             jobs.push_back(j);
         }
     }
-    std::vector<bool> done(jobs.size(), false);
     auto idx = [&](int o, int i) { return o * (L + 2) + (i - 1); };
+    // Launch units: a chain of planes (i, i+1) of one octave in one tile pass
+    // (plane i written, not re-read: launch_blur_chain) where an instantiation
+    // exists for their radii, else single planes.  With L = 3 and sigma 1.6
+    // (radii 5, 6, 8, 10, 13): units (1,2), (3,4), 5 per octave.
+    struct Unit {
+        int o, i, n;  // planes i .. i + n - 1 of octave o
+    };
+    std::vector<Unit> units;
+    for (int o = 0; o < d->nOct; o++) {
+        const OctGeom& g = d->pyr.oct[o];
+        for (int i = 1; i < L + 3;) {
+            const bool chain = d->blurChains && i + 1 < L + 3 &&
+                               blur_chain_supported(d->layerTaps[i].n >> 1, d->layerTaps[i + 1].n >> 1, g.W, g.H);
+            units.push_back(Unit{o, i, chain ? 2 : 1});
+            i += chain ? 2 : 1;
+        }
+    }
+    std::vector<bool> planeDone(jobs.size(), false), unitDone(units.size(), false);
     auto ready = [&](size_t k) {
-        const Job& j = jobs[k];
-        if (done[k]) return false;
-        if (j.i >= 2) return (bool)done[idx(j.o, j.i - 1)];
-        return j.o == 0 || (bool)done[idx(j.o - 1, L)];
+        const Unit& u = units[k];
+        if (unitDone[k]) return false;
+        if (u.i >= 2) return (bool)planeDone[idx(u.o, u.i - 1)];
+        return u.o == 0 || (bool)planeDone[idx(u.o - 1, L)];
+    };
+    auto finish = [&](size_t k) {
+        unitDone[k] = true;
+        for (int q = 0; q < units[k].n; q++) planeDone[idx(units[k].o, units[k].i + q)] = true;
+    };
+    auto unit_bytes = [&](const Unit& u) {  // algorithmic: one read of the input, a write per plane (+ base copy)
+        const Job& j = jobs[idx(u.o, u.i)];
+        return u.n == 1 ? j.bytes : j.bytes + (double)j.b.W * j.b.H * 4 * nf;
     };
     auto single = [&](const Job& j) {
         d->timed(blurNames[j.o], j.bytes, [&] {
@@ -605,24 +646,48 @@ void enqueue_body(sift_hip_detector* d, int slot, int nf) {
                         d->afs, s);
         });
     };
-    for (size_t left = jobs.size(); left > 0;) {
+    for (size_t left = units.size(); left > 0;) {
         int a = -1, b = -1;
-        for (size_t k = 0; k < jobs.size() && b < 0; k++)
+        for (size_t k = 0; k < units.size() && b < 0; k++)
             if (ready(k)) (a < 0 ? a : b) = (int)k;
-        const Job& ja = jobs[a];
+        const Unit& ua = units[a];
         bool paired = false;
         if (b >= 0) {
-            const Job& jb = jobs[b];
+            const Unit& ub = units[b];
             char name[16];
-            snprintf(name, sizeof name, "blur_o%d+o%d", ja.o, jb.o);
-            d->timed(name, ja.bytes + jb.bytes, [&] { paired = launch_blur_pair(ja.b, jb.b, fr, s); });
+            snprintf(name, sizeof name, "blur_o%d+o%d", ua.o, ub.o);
+            const double bytes = unit_bytes(ua) + unit_bytes(ub);
+            if (ua.n == 1 && ub.n == 1) {
+                d->timed(name, bytes,
+                         [&] { paired = launch_blur_pair(jobs[idx(ua.o, ua.i)].b, jobs[idx(ub.o, ub.i)].b, fr, s); });
+            } else if (ua.n + ub.n == 3) {
+                const Unit& uc = ua.n == 2 ? ua : ub;
+                const Unit& us = ua.n == 2 ? ub : ua;
+                d->timed(name, bytes, [&] {
+                    paired = launch_blur_chain(jobs[idx(uc.o, uc.i)].b, jobs[idx(uc.o, uc.i + 1)].b,
+                                               &jobs[idx(us.o, us.i)].b, fr, s);
+                });
+            }
             if (paired) {
-                done[b] = true;
+                finish(b);
                 left--;
             }
         }
-        if (!paired) single(ja);
-        done[a] = true;
+        if (!paired) {
+            if (ua.n == 2) {
+                bool ok = false;
+                d->timed(blurNames[ua.o], unit_bytes(ua), [&] {
+                    ok = launch_blur_chain(jobs[idx(ua.o, ua.i)].b, jobs[idx(ua.o, ua.i + 1)].b, nullptr, fr, s);
+                });
+                if (!ok) {  // (unit built only where supported)
+                    single(jobs[idx(ua.o, ua.i)]);
+                    single(jobs[idx(ua.o, ua.i + 1)]);
+                }
+            } else {
+                single(jobs[idx(ua.o, ua.i)]);
+            }
+        }
+        finish(a);
         left--;
     }
     double exBytes = 0;

@@ -112,6 +112,199 @@ __device__ __forceinline__ RefKpt load_ref(const RefKpt* in, unsigned k) {  // s
     return __builtin_bit_cast(RefKpt, r);
 }
 
+// Gradients of one 64-sample chunk of the window (lane = sample, raster
+// order); the next chunk's loads are issued before a chunk is processed.
+struct OriFetch {
+    int i, j;
+    bool valid;
+    float xl, xr, yu, yd;
+};
+struct OriWin {
+    __amdgpu_buffer_rsrc_t rsrc;
+    int r, c, radius, side, total, pitch, W, H;
+    unsigned mside;  // idx / side == umulhi(idx, mside)
+    float expf_scale;
+};
+__device__ __forceinline__ OriFetch ori_fetch(const OriWin& wn, int base, int lane) {
+    OriFetch f;
+    const int idx = base + lane;
+    f.i = (int)__umulhi((unsigned)idx, wn.mside);
+    f.j = idx - f.i * wn.side;
+    const int y = wn.r + f.i - wn.radius, x = wn.c + f.j - wn.radius;
+    f.valid = idx < wn.total && y > 0 && y < wn.H - 1 && x > 0 && x < wn.W - 1;
+    const unsigned o0 = f.valid ? (unsigned)(y * wn.pitch + x) * 4u : 0x80000000u;
+    f.xl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wn.rsrc, o0 - 4u, 0, 0));
+    f.xr = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wn.rsrc, o0 + 4u, 0, 0));
+    f.yu = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wn.rsrc, o0 - 4u * wn.pitch, 0, 0));
+    f.yd = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wn.rsrc, o0 + 4u * wn.pitch, 0, 0));
+    return f;
+}
+
+// One chunk's weighted magnitudes sorted into bin runs in `buf` (bin b's run
+// starts at the returned lane-b value, 16-byte aligned, padded with +0.0 to a
+// multiple of 4; lanes >= 36 get the end of the last run).
+__device__ __forceinline__ int ori_sort_chunk(const OriWin& wn, const OriFetch& cur, int lane, const float* s_exptab,
+                                              const unsigned long long (&lane_nb)[6], float* buf, int& c4out) {
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    const int i = cur.i, j = cur.j;
+    const bool valid = cur.valid;
+    const int ii = i - wn.radius, jj = j - wn.radius;
+    const float dx = cur.xr - cur.xl, dy = cur.yu - cur.yd;
+    const float w = cv_exp32f((float)(ii * ii + jj * jj) * wn.expf_scale, s_exptab);
+    const float ori = cv_fast_atan2(dy, dx);
+    const float mag = cv_magnitude(dx, dy);
+    int bin = cv_round((kOriBins / 360.f) * ori);
+    if (bin >= kOriBins) bin -= kOriBins;
+    if (bin < 0) bin += kOriBins;
+    // Radix ranks from six ballots on the bin bits (MSB first): for each
+    // key k, `less(k)` = valid samples with a smaller bin and `eq(k)` =
+    // those with bin k.  A sample's slot is less(bin) + its lane rank
+    // inside eq(bin) (raster order); lane b < 36 sums slots
+    // [less(b), less(b) + |eq(b)|) -- no LDS counts, no scan.
+    unsigned long long m[6];
+#pragma unroll
+    for (int bit = 0; bit < 6; bit++) m[bit] = __ballot(valid && ((bin >> bit) & 1));
+    const unsigned long long vmask = __ballot(valid);
+    // Lane b's bin mask eq(b) from the ballots (bit k of b selects m[k]
+    // or its complement), its count cb and, since bins are lane
+    // indices, start = the exclusive prefix of cb over lanes (DPP scan).
+    unsigned long long eq_l = vmask;
+#pragma unroll
+    for (int bit = 0; bit < 6; bit++) eq_l &= m[bit] ^ lane_nb[bit];
+    const int cb = __popcll(eq_l);  // lanes >= 36: no sample has that bin
+    // Bins start on 16-byte boundaries (runs padded to a multiple of 4
+    // with +0.0, which leaves a non-negative sum unchanged), so lane b
+    // reads its run with ds_read_b128 and no bounds tests.
+    const int c4 = (cb + 3) & ~3;
+    const int start = wave_incl_scan(c4) - c4;
+    for (int q = cb; q < c4; q++) buf[start + q] = 0.f;
+    c4out = c4;
+    // A sample's less(bin) and eq(bin) are those lane `bin` just
+    // computed for its own key: three shuffles instead of a second
+    // radix rank per sample.
+    const int less_s = __shfl(start, bin);
+    const unsigned long long eq_s = ((unsigned long long)(unsigned)__shfl((int)(eq_l >> 32), bin) << 32) |
+                                    (unsigned)__shfl((int)(unsigned)eq_l, bin);
+    if (valid) buf[less_s + __popcll(eq_s & lt_mask)] = w * mag;
+    return start;
+}
+
+// Lane b adds its bin's run [start, end) in order (OpenCV's sequential sum).
+// (Reading four float4s per LDS round trip, with +0.0 past the run, measured
+// 5 % slower on 16-frame batches and equal on one frame.)
+__device__ __forceinline__ float ori_add_run(float acc, const float* buf, int start, int end) {
+    for (int t0 = start; t0 < end; t0 += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(buf + t0);
+        acc = acc + v.x;
+        acc = acc + v.y;
+        acc = acc + v.z;
+        acc = acc + v.w;
+    }
+    return acc;
+}
+
+__device__ __forceinline__ OriWin ori_window(const PyrDesc& pyr, const RefKpt& kpt, long foff, const OctGeom*& gout) {
+    const int o = kpt.o, layer = kpt.layer;
+    const OctGeom& g = octave_geom(pyr, o);
+    gout = &g;
+    OriWin wn;
+    wn.r = kpt.rc >> 16;
+    wn.c = kpt.rc & 0xffff;
+    const float* img = fptr(g.base, foff) + (size_t)layer * g.planeStride;
+    wn.pitch = g.pitch;
+    wn.W = g.W;
+    wn.H = g.H;
+    const float scl_octv = kpt.size * 0.5f / (float)(1 << o);
+    wn.radius = cv_round(kOriRadius * scl_octv);
+    const float sigma = kOriSigFctr * scl_octv;
+    wn.expf_scale = -1.f / (2.f * sigma * sigma);
+    wn.side = 2 * wn.radius + 1;
+    wn.total = wn.side * wn.side;
+    wn.mside = (unsigned)(4294967296.0 / wn.side) + 1u;
+    wn.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(img), 0, wn.H * wn.pitch * 4, 0x00020000);
+    return wn;
+}
+
+// Entries of the oriented list (refined slots + appended peaks, holes included).
+__device__ __forceinline__ unsigned oriented_count(const Counters* ctr, const KeypointParams& kp) {
+    return min(min(ctr->refined, kp.capRefined) + ctr->oriented, kp.capOriented);
+}
+
+// Smoothing, peaks and the oriented keypoints of one histogram (lane b < 36
+// holds bin b's sum), written by the calling wave: the first peak into the
+// keypoint's own slot k, the others appended after the n_ref refined slots
+// (one atomic per keypoint with several peaks: a per-keypoint atomic on the
+// frame's one counter serialised a single frame's 4.4k waves, 40 us).
+__device__ __forceinline__ void ori_emit(float acc, const RefKpt& kpt, const OctGeom& g, int fo, int lane, unsigned k,
+                                         unsigned n_ref, Counters* __restrict__ ctr, OriKpt* __restrict__ out,
+                                         const KeypointParams& kp) {
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    // Circular [1 4 6 4 1]/16 smoothing (SIMD body, fma form).
+    const int bl = lane < kOriBins ? lane : 0;
+    const float tm2 = __shfl(acc, (bl + kOriBins - 2) % kOriBins);
+    const float tm1 = __shfl(acc, (bl + kOriBins - 1) % kOriBins);
+    const float tp1 = __shfl(acc, (bl + 1) % kOriBins);
+    const float tp2 = __shfl(acc, (bl + 2) % kOriBins);
+    const float h = __fmaf_rn(tm2 + tp2, 1.f / 16.f, __fmaf_rn(tm1 + tp1, 4.f / 16.f, acc * (6.f / 16.f)));
+    const float mx = wave_max(lane < kOriBins ? h : -INFINITY);
+    const float mag_thr = (float)(mx * kOriPeakRatio);
+    const float hl = __shfl(h, (bl + kOriBins - 1) % kOriBins);
+    const float hr = __shfl(h, (bl + 1) % kOriBins);
+    const bool peak = lane < kOriBins && h > hl && h > hr && h >= mag_thr;
+    const unsigned long long mask = __ballot(peak);
+    if (!mask) {
+        if (lane == 0) {
+            OriKpt hole{};
+            hole.bucket = kHoleBucket;
+            out[k] = hole;
+        }
+        return;
+    }
+    const int npk = __popcll(mask), first = __builtin_ctzll(mask);
+    unsigned basepos = 0;
+    if (lane == 0 && npk > 1) basepos = atomicAdd(&ctr->oriented, (unsigned)(npk - 1));
+    basepos = __builtin_amdgcn_readfirstlane(basepos);
+    if (peak) {
+        const int layer = kpt.layer, r = kpt.rc >> 16, c = kpt.rc & 0xffff;
+        float bin = (float)lane + 0.5f * (hl - hr) / (hl - 2 * h + hr);
+        bin = bin < 0 ? kOriBins + bin : bin >= kOriBins ? bin - kOriBins : bin;
+        float angle = 360.f - (float)((360.f / kOriBins) * bin);
+        if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+        OriKpt ok;
+        ok.x = kpt.x;
+        ok.y = kpt.y;
+        ok.size = kpt.size;
+        ok.angle = angle;
+        ok.response = kpt.response;
+        ok.octave = kpt.octave;
+        if (fo < 0) {
+            const float scale = 1.f / (float)(1 << -fo);
+            ok.octave = (kpt.octave & ~255) | ((kpt.octave + fo) & 255);
+            ok.x *= scale;
+            ok.y *= scale;
+            ok.size *= scale;
+        }
+        ok.bucket = g.rowBase + (layer - 1) * g.H + r;
+        ok.sub = (c << 6) | lane;
+        const unsigned pos = lane == first ? k : n_ref + basepos + (unsigned)__popcll(mask & lt_mask) - 1u;
+        if (pos < kp.capOriented)
+            out[pos] = ok;
+        else
+            atomicOr(&ctr->overflow, 4u);
+    }
+}
+
+__device__ __forceinline__ void ori_clear_bit(uint32_t* bitmap, const OctGeom& g, const RefKpt& kpt) {
+    // the keypoint's dedupe bit, for the next frame (no memset node)
+    const int layer = kpt.layer, r = kpt.rc >> 16, c = kpt.rc & 0xffff;
+    const long bit = g.bitBase + ((long)(layer - 1) * g.H + r) * g.W + c;
+    atomicAnd(&bitmap[bit >> 5], ~(1u << (bit & 31)));
+}
+
+#ifndef SIFT_ORI_AHEAD
+#define SIFT_ORI_AHEAD 1  // 2, 3, 4 measured equal on one frame and on batches (A/B builds)
+#endif
+constexpr int kOriAhead = SIFT_ORI_AHEAD;  // chunks whose gradient loads are in flight
 __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* __restrict__ in,
                                                     Counters* __restrict__ ctr, OriKpt* __restrict__ out,
                                                     uint32_t* __restrict__ bitmap, KeypointParams kp, long fs) {
@@ -124,7 +317,6 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
     __shared__ float s_exptab[64];
     const int lane = threadIdx.x;
     s_exptab[lane] = c_exptab[lane];
-    const unsigned long long lt_mask = (1ull << lane) - 1ull;
     unsigned long long lane_nb[6];  // all ones where bit k of the lane index is 0
 #pragma unroll
     for (int bit = 0; bit < 6; bit++) lane_nb[bit] = ((lane >> bit) & 1) ? 0ull : ~0ull;
@@ -132,145 +324,29 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
     const int fo = pyr.firstOctave;
     for (unsigned k = blockIdx.x; k < n; k += gridDim.x) {  // round-robin (see k_descriptor)
         const RefKpt kpt = load_ref(in, k);
-        const int o = kpt.o, layer = kpt.layer, r = kpt.rc >> 16, c = kpt.rc & 0xffff;
-        const OctGeom& g = octave_geom(pyr, o);
-        if (lane == 0) {  // clear the keypoint's dedupe bit for the next frame (no memset node)
-            const long bit = g.bitBase + ((long)(layer - 1) * g.H + r) * g.W + c;
-            atomicAnd(&bitmap[bit >> 5], ~(1u << (bit & 31)));
-        }
-        const float* img = fptr(g.base, foff) + (size_t)layer * g.planeStride;
-        const int pitch = g.pitch, W = g.W, H = g.H;
-        const float scl_octv = kpt.size * 0.5f / (float)(1 << o);
-        const int radius = cv_round(kOriRadius * scl_octv);
-        const float sigma = kOriSigFctr * scl_octv;
-        const float expf_scale = -1.f / (2.f * sigma * sigma);
-        const int side = 2 * radius + 1, total = side * side;
-        const unsigned mside = (unsigned)(4294967296.0 / side) + 1u;  // idx / side == umulhi(idx, mside)
-        const __amdgpu_buffer_rsrc_t rsrc =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(img), 0, H * pitch * 4, 0x00020000);
-
-        // Chunk geometry + its four gradient loads; the next chunk's loads are
-        // issued before this chunk is processed (one chunk of latency hidden).
-        struct Fetch {
-            int i, j;
-            bool valid;
-            float xl, xr, yu, yd;
-        };
-        auto fetch = [&](int base) {
-            Fetch f;
-            const int idx = base + lane;
-            f.i = (int)__umulhi((unsigned)idx, mside);
-            f.j = idx - f.i * side;
-            const int y = r + f.i - radius, x = c + f.j - radius;
-            f.valid = idx < total && y > 0 && y < H - 1 && x > 0 && x < W - 1;
-            const unsigned o0 = f.valid ? (unsigned)(y * pitch + x) * 4u : 0x80000000u;
-            f.xl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o0 - 4u, 0, 0));
-            f.xr = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o0 + 4u, 0, 0));
-            f.yu = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o0 - 4u * pitch, 0, 0));
-            f.yd = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o0 + 4u * pitch, 0, 0));
-            return f;
-        };
+        const OctGeom* gp;
+        const OriWin wn = ori_window(pyr, kpt, foff, gp);
+        if (lane == 0) ori_clear_bit(bitmap, *gp, kpt);
         float acc = 0.f;  // temphist[lane] for lane < 36
-        Fetch nxt = fetch(0);
-        for (int base = 0; base < total; base += 64) {
-            const Fetch cur = nxt;
-            if (base + 64 < total) nxt = fetch(base + 64);
-            const int i = cur.i, j = cur.j;
-            const bool valid = cur.valid;
-            const float xl = cur.xl, xr = cur.xr, yu = cur.yu, yd = cur.yd;
-            const int ii = i - radius, jj = j - radius;
-            const float dx = xr - xl, dy = yu - yd;
-            const float w = cv_exp32f((float)(ii * ii + jj * jj) * expf_scale, s_exptab);
-            const float ori = cv_fast_atan2(dy, dx);
-            const float mag = cv_magnitude(dx, dy);
-            int bin = cv_round((kOriBins / 360.f) * ori);
-            if (bin >= kOriBins) bin -= kOriBins;
-            if (bin < 0) bin += kOriBins;
-            // Radix ranks from six ballots on the bin bits (MSB first): for each
-            // key k, `less(k)` = valid samples with a smaller bin and `eq(k)` =
-            // those with bin k.  A sample's slot is less(bin) + its lane rank
-            // inside eq(bin) (raster order); lane b < 36 sums slots
-            // [less(b), less(b) + |eq(b)|) -- no LDS counts, no scan.
-            unsigned long long m[6];
+        // Loads run kOriAhead chunks ahead of the chunk being sorted (ring of
+        // fetches): a large keypoint's chunks are a dependent chain, and
+        // with one chunk in flight each waited for a memory round trip.
+        OriFetch ring[kOriAhead];
 #pragma unroll
-            for (int bit = 0; bit < 6; bit++) m[bit] = __ballot(valid && ((bin >> bit) & 1));
-            const unsigned long long vmask = __ballot(valid);
-            // Lane b's bin mask eq(b) from the ballots (bit k of b selects m[k]
-            // or its complement), its count cb and, since bins are lane
-            // indices, start = the exclusive prefix of cb over lanes (DPP scan).
-            unsigned long long eq_l = vmask;
+        for (int q = 0; q < kOriAhead; q++) ring[q] = ori_fetch(wn, 64 * q, lane);
+        for (int base = 0; base < wn.total; base += 64) {
+            const OriFetch cur = ring[0];
 #pragma unroll
-            for (int bit = 0; bit < 6; bit++) eq_l &= m[bit] ^ lane_nb[bit];
-            const int cb = __popcll(eq_l);  // lanes >= 36: no sample has that bin
-            // Bins start on 16-byte boundaries (runs padded to a multiple of 4
-            // with +0.0, which leaves a non-negative sum unchanged), so lane b
-            // reads its run with ds_read_b128 and no bounds tests.
-            const int c4 = (cb + 3) & ~3;
-            const int start = wave_incl_scan(c4) - c4;
-            for (int q = cb; q < c4; q++) chunk[start + q] = 0.f;
-            // A sample's less(bin) and eq(bin) are those lane `bin` just
-            // computed for its own key: three shuffles instead of a second
-            // radix rank per sample.
-            const int less_s = __shfl(start, bin);
-            const unsigned long long eq_s = ((unsigned long long)(unsigned)__shfl((int)(eq_l >> 32), bin) << 32) |
-                                            (unsigned)__shfl((int)(unsigned)eq_l, bin);
-            if (valid) chunk[less_s + __popcll(eq_s & lt_mask)] = w * mag;
+            for (int q = 0; q + 1 < kOriAhead; q++) ring[q] = ring[q + 1];
+            if (base + 64 * kOriAhead < wn.total) ring[kOriAhead - 1] = ori_fetch(wn, base + 64 * kOriAhead, lane);
+            int c4;
+            const int start = ori_sort_chunk(wn, cur, lane, s_exptab, lane_nb, chunk, c4);
             lds_barrier();
             // Lane b (< 36; others have cb = 0) adds its bin's values in order.
-            for (int t0 = start; t0 < start + c4; t0 += 4) {
-                const float4 v = *reinterpret_cast<const float4*>(chunk + t0);
-                acc = acc + v.x;
-                acc = acc + v.y;
-                acc = acc + v.z;
-                acc = acc + v.w;
-            }
+            acc = ori_add_run(acc, chunk, start, start + c4);
             lds_barrier();  // chunk is rewritten by the next 64 samples
         }
-
-        // Circular [1 4 6 4 1]/16 smoothing (SIMD body, fma form).
-        const int bl = lane < kOriBins ? lane : 0;
-        const float tm2 = __shfl(acc, (bl + kOriBins - 2) % kOriBins);
-        const float tm1 = __shfl(acc, (bl + kOriBins - 1) % kOriBins);
-        const float tp1 = __shfl(acc, (bl + 1) % kOriBins);
-        const float tp2 = __shfl(acc, (bl + 2) % kOriBins);
-        const float h = __fmaf_rn(tm2 + tp2, 1.f / 16.f, __fmaf_rn(tm1 + tp1, 4.f / 16.f, acc * (6.f / 16.f)));
-        const float mx = wave_max(lane < kOriBins ? h : -INFINITY);
-        const float mag_thr = (float)(mx * kOriPeakRatio);
-        const float hl = __shfl(h, (bl + kOriBins - 1) % kOriBins);
-        const float hr = __shfl(h, (bl + 1) % kOriBins);
-        const bool peak = lane < kOriBins && h > hl && h > hr && h >= mag_thr;
-        const unsigned long long mask = __ballot(peak);
-        if (!mask) continue;
-        unsigned basepos = 0;
-        if (lane == 0) basepos = atomicAdd(&ctr->oriented, (unsigned)__popcll(mask));
-        basepos = __builtin_amdgcn_readfirstlane(basepos);
-        if (peak) {
-            float bin = (float)lane + 0.5f * (hl - hr) / (hl - 2 * h + hr);
-            bin = bin < 0 ? kOriBins + bin : bin >= kOriBins ? bin - kOriBins : bin;
-            float angle = 360.f - (float)((360.f / kOriBins) * bin);
-            if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
-            OriKpt ok;
-            ok.x = kpt.x;
-            ok.y = kpt.y;
-            ok.size = kpt.size;
-            ok.angle = angle;
-            ok.response = kpt.response;
-            ok.octave = kpt.octave;
-            if (fo < 0) {
-                const float scale = 1.f / (float)(1 << -fo);
-                ok.octave = (kpt.octave & ~255) | ((kpt.octave + fo) & 255);
-                ok.x *= scale;
-                ok.y *= scale;
-                ok.size *= scale;
-            }
-            ok.bucket = g.rowBase + (layer - 1) * H + r;
-            ok.sub = (c << 6) | lane;
-            const unsigned pos = basepos + (unsigned)__popcll(mask & lt_mask);
-            if (pos < kp.capOriented)
-                out[pos] = ok;
-            else
-                atomicOr(&ctr->overflow, 4u);
-        }
+        ori_emit(acc, kpt, *gp, fo, lane, k, n, ctr, out, kp);
     }
 }
 
@@ -284,8 +360,7 @@ void launch_orientation(const PyrDesc& pyr, const RefKpt* in, Counters* ctr, Ori
 #else
     const int per = fr.nf <= 1 ? 8192 : std::max(256, 8192 / fr.nf);
 #endif
-    hipLaunchKernelGGL(k_orientation, dim3(per, fr.nf), dim3(64), 0, s, pyr, in, ctr, out,
-                       bitmap, kp, fr.stride);
+    hipLaunchKernelGGL(k_orientation, dim3(per, fr.nf), dim3(64), 0, s, pyr, in, ctr, out, bitmap, kp, fr.stride);
 }
 
 // ---------------------------------------------------------------------------
@@ -337,7 +412,7 @@ __global__ __launch_bounds__(1024) void k_select(const OriKpt* __restrict__ kpts
     kpts = fptr(kpts, foff);
     ctr = fptr(ctr, foff);
     zero_range = fptr(zero_range, foff);
-    const unsigned n = min(ctr->oriented, kp.capOriented);
+    const unsigned n = oriented_count(ctr, kp);
     const int tid = threadIdx.x, lane = tid & 63;
     for (int i = tid; i < 2 * kRangeSlots; i += 1024) zero_range[i] = 0u;  // next frame's range keys
     if (kp.numFeatures <= 0 || n <= (unsigned)kp.numFeatures) {
@@ -392,11 +467,11 @@ __global__ __launch_bounds__(256) void k_bucket_count(const OriKpt* __restrict__
     ctr = fptr(ctr, foff);
     bcount = fptr(bcount, foff);
     slot = fptr(slot, foff);
-    const unsigned n = min(ctr->oriented, kp.capOriented);
+    const unsigned n = oriented_count(ctr, kp);
     const float thr = __uint_as_float(ctr->thr_bits);
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const OriKpt k = kpts[i];
-        slot[i] = k.response >= thr ? (int)atomicAdd(&bcount[k.bucket], 1u) : -1;
+        slot[i] = k.bucket != kHoleBucket && k.response >= thr ? (int)atomicAdd(&bcount[k.bucket], 1u) : -1;
     }
 }
 
@@ -454,7 +529,7 @@ __global__ __launch_bounds__(256) void k_bucket_scatter(const OriKpt* __restrict
     boff = fptr(boff, foff);
     slot = fptr(slot, foff);
     order = fptr(order, foff);
-    const unsigned n = min(ctr->oriented, kp.capOriented);
+    const unsigned n = oriented_count(ctr, kp);
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int s = slot[i];
         if (s >= 0) order[boff[kpts[i].bucket] + (unsigned)s] = (int)i;
@@ -492,7 +567,7 @@ __global__ __launch_bounds__(1024) void k_order(const OriKpt* __restrict__ kpts,
     boff = fptr(boff, foff);
     slot = fptr(slot, foff);
     order = fptr(order, foff);
-    const unsigned n = min(ctr->oriented, kp.capOriented);
+    const unsigned n = oriented_count(ctr, kp);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nb = kp.numBuckets;
     for (int i = tid; i < 2 * kRangeSlots; i += 1024) zero_range[i] = 0u;  // next frame's range keys
@@ -545,7 +620,7 @@ __global__ __launch_bounds__(1024) void k_order(const OriKpt* __restrict__ kpts,
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const unsigned i = i0 + 1024u * u;
-            if (i < n) slot[i] = rs[u] >= thr ? (int)atomicAdd(&s_bucket[bk[u]], 1u) : -1;
+            if (i < n) slot[i] = (unsigned)bk[u] != kHoleBucket && rs[u] >= thr ? (int)atomicAdd(&s_bucket[bk[u]], 1u) : -1;
         }
     }
     __syncthreads();

@@ -71,12 +71,17 @@ struct OriKpt {
 struct Counters {
     unsigned cand;       // 3x3x3 extrema candidates
     unsigned refined;    // after adjustLocalExtrema + dedupe
-    unsigned oriented;   // after orientation peaks
+    unsigned oriented;   // orientation peaks beyond each keypoint's first (appended after the refined slots)
     unsigned final_n;    // after retainBest (written by the bucket scan)
     unsigned overflow;   // bit 0 cand, 1 refined, 2 oriented, 3 final
     unsigned thr_bits;   // retainBest response threshold (float bits)
     unsigned pad[2];     // pad[0]: entries of the order list (k_order path)
 };
+
+// Oriented keypoint list: refined keypoint k's first peak sits in slot k (no
+// atomic), further peaks are appended from slot min(refined, capRefined) on;
+// a keypoint without a peak leaves a hole (bucket kHoleBucket, response 0).
+constexpr unsigned kHoleBucket = 0xffffffffu;
 
 // --- launch wrappers (implemented in pyramid.hip / keypoints.hip / match.hip) --
 // sfs: byte stride between the nf source frames (the caller's frames or arenas).
@@ -102,6 +107,12 @@ struct BlurDesc {
     const Taps* taps;
 };
 bool launch_blur_pair(const BlurDesc& a, const BlurDesc& b, const Frames& fr, hipStream_t s);
+// Chained blurs: plane a.dst from a.src, then plane b.dst from a.dst (b.src
+// ignored), in one tile pass; optionally beside an independent single blur
+// in the same launch.  false (nothing launched) without an instantiation for
+// the radii, or for planes too small for one-bounce reflection.
+bool blur_chain_supported(int ra, int rb, int W, int H);
+bool launch_blur_chain(const BlurDesc& a, const BlurDesc& b, const BlurDesc* single, const Frames& fr, hipStream_t s);
 // 8-bit frames (pitches in bytes).  launch_blur_u8 returns false (nothing
 // launched) for an init radius without a fused 8-bit instantiation; the caller
 // then converts with launch_u8_to_f32 and uses launch_blur.
