@@ -346,7 +346,9 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
             const float gmag = desc_magnitude(dx, dy);
             float obin = (gori - jb.angle) * bins_per_rad;
             // x 2^S (exact): the trilinear parts come out in fixed-point units.
-            const float mag = valid ? gmag * wgt * fxs : 0.f;
+            // A select, not a branch around the product (every operand is
+            // finite: enumerated samples are in-image).
+            const float mag = (gmag * wgt * fxs) * (valid ? 1.f : 0.f);
             // cvFloor in the float domain (the clamp only guards rejected
             // samples): r - floor(r) is the oracle's r - (float)cvFloor(r).
             const float r0f = fminf(fmaxf(floorf(rbin), -1.f), (float)(kD - 1));
@@ -355,16 +357,18 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
             rbin -= r0f;
             cbin -= c0f;
             obin -= o0f;
-            int o0 = (int)o0f;
-            if (o0 < 0) o0 += kN;
-            if (o0 >= kN) o0 -= kN;
-            o0 &= kN - 1;  // no-op for valid samples (o0 in [0, 8) already)
-            const int cell = ((int)r0f + 1) * (kD + 2) + (int)c0f + 1;
+            // obin is in (-8, 8), so o0 & 7 is OpenCV's `o0 += n if < 0, -= n
+            // if >= n` wrap (two's complement).
+            const int o0 = (int)o0f & (kN - 1);
             const int odd = o0 & 1;
+            // Word of (cell, o0) in the parity's histogram: cell = (r0 + 1) *
+            // (kD + 2) + (c0 + 1), 10 words per cell -- formed in float (small
+            // exact integers, one fma chain) instead of integer multiplies.
             // Both histograms have 10 dwords per cell, so the four u64 adds of
             // a sample sit at constant offsets from hb (immediate offsets).
-            unsigned* hb = histE + (lane & (kCopies - 1)) * kHistWords + (odd ? kCells * kCellW : 0) + cell * kCellW +
-                           o0 + odd;
+            const unsigned cw = (unsigned)__fmaf_rn(r0f, (float)((kD + 2) * kCellW),
+                                                     __fmaf_rn(c0f, (float)kCellW, (float)((kD + 3) * kCellW)));
+            unsigned* hb = histE + (lane & (kCopies - 1)) * kHistWords + cw + (unsigned)(o0 + odd * (kCells * kCellW + 1));
             float v[8];
             trilinear(mag, rbin, cbin, obin, v);
 #pragma unroll

@@ -103,6 +103,9 @@ const char* build_flags() {
 #ifdef SIFT_BLUR_X4LD
            " SIFT_BLUR_X4LD=" SIFT_STR(SIFT_BLUR_X4LD)
 #endif
+#ifdef SIFT_BLUR_DMA
+           " SIFT_BLUR_DMA=" SIFT_STR(SIFT_BLUR_DMA)
+#endif
 #ifdef SIFT_BLUR_CHAIN
            " SIFT_BLUR_CHAIN=" SIFT_STR(SIFT_BLUR_CHAIN)
 #endif

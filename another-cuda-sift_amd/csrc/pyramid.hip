@@ -138,6 +138,11 @@ struct BlurJob {
 #ifndef SIFT_BLUR_X4ST
 #define SIFT_BLUR_X4ST 1
 #endif
+// Interior-tile staging by LDS-DMA (global_load_lds_dwordx4) instead of
+// 16-byte loads into VGPRs + ds_write_b128.
+#ifndef SIFT_BLUR_DMA
+#define SIFT_BLUR_DMA 1
+#endif
 template <int R>
 constexpr int blur_org() {  // tile column 0 = image column x0 - ORG
     return SIFT_BLUR_X4LD && R <= 8 ? 8 : R;
@@ -250,9 +255,26 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
             // the first LDS store.
             static_assert(ES != 4 || ORG != 8 || IW == 80, "x4 staging assumes 80-float LDS rows");
             constexpr int NQ = 20 * IH, NT = 64 * BLUR_NW, QPT = (NQ + NT - 1) / NT;
+            const int rb0 = (y0 - R) * spitch + x0 - 8;
+#if SIFT_BLUR_DMA
+            // LDS-DMA: float4 q of the tile goes from global memory straight
+            // to LDS float4 q (global_load_lds_dwordx4: a wave's 64 lanes fill
+            // 1 KiB at M0), no VGPR round trip and no ds_write_b128; the
+            // staging barrier below waits for vmcnt(0).
+            const float* fsrc = reinterpret_cast<const float*>(src);  // ES == 4 here
+#pragma unroll
+            for (int u = 0; u < QPT; u++) {
+                const int idx = tid + NT * u;
+                if (u < QPT - 1 || idx < NQ) {
+                    const int row = idx / 20, qq = idx - row * 20;
+                    __builtin_amdgcn_global_load_lds(
+                        (const void*)(fsrc + rb0 + row * spitch + 4 * qq),
+                        (__attribute__((address_space(3))) void*)(in + 4 * (NT * u + 64 * (tid >> 6))), 16, 0, 0);
+                }
+            }
+#else
             typedef unsigned u32x4s __attribute__((ext_vector_type(4)));
             u32x4s q4[QPT];
-            const int rb0 = (y0 - R) * spitch + x0 - 8;
 #pragma unroll
             for (int u = 0; u < QPT; u++) {
                 const int idx = min(tid + NT * u, NQ - 1), row = idx / 20, qq = idx - row * 20;
@@ -261,6 +283,7 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
 #pragma unroll
             for (int u = 0; u < QPT; u++)
                 if (u < QPT - 1 || tid + NT * u < NQ) *reinterpret_cast<u32x4s*>(in + 4 * (tid + NT * u)) = q4[u];
+#endif
         } else if (y0 - R >= 0 && y0 - R + IH <= H) {
             // Interior rows (most tiles): the row offset advances by a constant,
             // one s_add per row.  Rows past IH of the last step read in-range
