@@ -211,7 +211,7 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
     __shared__ float s_tab[64];
     for (int i = threadIdx.x; i < 64; i += kDT) s_tab[i] = c_exptab_desc[i];
 #else
-    float* const s_tab = nullptr;
+    [[maybe_unused]] float* const s_tab = nullptr;
 #endif
     __shared__ int rowpre[kMaxRows + 4], rowlo[kMaxRows], rowln[kMaxRows];
     __shared__ float s_norm[12];
@@ -341,7 +341,13 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
             valid = valid && rbin > -1 && rbin < kD && cbin > -1 && cbin < kD;
             const float dx = r - l, dy = u - d;
             const f32x2t sq = rot * rot;
+#if SIFT_DESC_PRECISE
             const float wgt = desc_exp((sq[0] + sq[1]) * G.exp_scale, s_tab);
+#else
+            // exp_scale = -1/8 is a power of two, so (r2 * -1/8) * log2(e)
+            // = r2 * (-log2(e) / 8) with the same single rounding: one multiply.
+            const float wgt = __builtin_amdgcn_exp2f((sq[0] + sq[1]) * (-1.44269504088896341f / (kD * kD * 0.5f)));
+#endif
             const float gori = desc_atan2(dy, dx);
             const float gmag = desc_magnitude(dx, dy);
             float obin = (gori - jb.angle) * bins_per_rad;
