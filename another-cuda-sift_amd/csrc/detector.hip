@@ -106,6 +106,9 @@ const char* build_flags() {
 #ifdef SIFT_BLUR_DMA
            " SIFT_BLUR_DMA=" SIFT_STR(SIFT_BLUR_DMA)
 #endif
+#ifdef SIFT_EX_TALL_MIN
+           " SIFT_EX_TALL_MIN=" SIFT_STR(SIFT_EX_TALL_MIN)
+#endif
 #ifdef SIFT_BLUR_CHAIN
            " SIFT_BLUR_CHAIN=" SIFT_STR(SIFT_BLUR_CHAIN)
 #endif

@@ -12,6 +12,8 @@
 
 #include <algorithm>
 
+#include <cstddef>
+
 #include "sift_kernels.h"
 #include "sift_math.h"
 #include "sift_refine.h"
@@ -606,21 +608,44 @@ __global__ __launch_bounds__(1024) void k_order(const OriKpt* __restrict__ kpts,
     const unsigned thr_bits = sel ? s_prefix : 0u;
     if (tid == 0) ctr->thr_bits = thr_bits;
     const float thr = __uint_as_float(thr_bits);
-    // counts (the slot order inside a bucket is re-ranked by k_bucket_rank);
-    // four keypoints' loads in flight per thread
-    for (unsigned i0 = tid; i0 < n; i0 += 4 * 1024) {
-        int bk[4];
-        float rs[4];
+    // counts (the slot order inside a bucket is re-ranked by k_bucket_rank).
+    // Up to kOrderRegs * 1024 entries (a frame's usual count) keep their
+    // bucket and slot in registers for the scatter below (one 16-byte load
+    // of {response, octave, bucket, sub} per entry, no slot[] round trip);
+    // larger lists go through slot[], four entries' loads in flight.
+    constexpr int kOrderRegs = 8;
+    static_assert(sizeof(OriKpt) == 32 && offsetof(OriKpt, response) == 16 && offsetof(OriKpt, bucket) == 24,
+                  "k_order reads {response, octave, bucket, sub} as the entry's second float4");
+    const bool inreg = n <= kOrderRegs * 1024u;
+    int rbk[kOrderRegs], rsl[kOrderRegs];
+    if (inreg) {
+        float4 q[kOrderRegs];
+        const float4* kq = reinterpret_cast<const float4*>(kpts);
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const unsigned i = min(i0 + 1024u * u, n - 1);
-            bk[u] = kpts[i].bucket;
-            rs[u] = kpts[i].response;
+        for (int u = 0; u < kOrderRegs; u++) q[u] = kq[2 * min(tid + 1024u * u, n - 1) + 1];
+#pragma unroll
+        for (int u = 0; u < kOrderRegs; u++) {
+            const unsigned i = tid + 1024u * u;
+            rbk[u] = __float_as_int(q[u].z);
+            rsl[u] = i < n && (unsigned)rbk[u] != kHoleBucket && q[u].x >= thr ? (int)atomicAdd(&s_bucket[rbk[u]], 1u)
+                                                                               : -1;
         }
+    } else {
+        for (unsigned i0 = tid; i0 < n; i0 += 4 * 1024) {
+            int bk[4];
+            float rs[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const unsigned i = i0 + 1024u * u;
-            if (i < n) slot[i] = (unsigned)bk[u] != kHoleBucket && rs[u] >= thr ? (int)atomicAdd(&s_bucket[bk[u]], 1u) : -1;
+            for (int u = 0; u < 4; u++) {
+                const unsigned i = min(i0 + 1024u * u, n - 1);
+                bk[u] = kpts[i].bucket;
+                rs[u] = kpts[i].response;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const unsigned i = i0 + 1024u * u;
+                if (i < n)
+                    slot[i] = (unsigned)bk[u] != kHoleBucket && rs[u] >= thr ? (int)atomicAdd(&s_bucket[bk[u]], 1u) : -1;
+            }
         }
     }
     __syncthreads();
@@ -657,9 +682,15 @@ __global__ __launch_bounds__(1024) void k_order(const OriKpt* __restrict__ kpts,
     }
     __syncthreads();
     // scatter (slot[i] was written by this same thread above)
-    for (unsigned i = tid; i < n; i += 1024) {
-        const int sl = slot[i];
-        if (sl >= 0) order[s_bucket[kpts[i].bucket] + (unsigned)sl] = (int)i;
+    if (inreg) {
+#pragma unroll
+        for (int u = 0; u < kOrderRegs; u++)
+            if (rsl[u] >= 0) order[s_bucket[rbk[u]] + (unsigned)rsl[u]] = (int)(tid + 1024u * u);
+    } else {
+        for (unsigned i = tid; i < n; i += 1024) {
+            const int sl = slot[i];
+            if (sl >= 0) order[s_bucket[kpts[i].bucket] + (unsigned)sl] = (int)i;
+        }
     }
 }
 
