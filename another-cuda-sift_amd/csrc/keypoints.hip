@@ -163,10 +163,11 @@ __device__ __forceinline__ int ori_sort_chunk(const OriWin& wn, const OriFetch& 
     // those with bin k.  A sample's slot is less(bin) + its lane rank
     // inside eq(bin) (raster order); lane b < 36 sums slots
     // [less(b), less(b) + |eq(b)|) -- no LDS counts, no scan.
+    // (The bin-bit ballots need not exclude invalid lanes: vmask does below.)
     unsigned long long m[6];
 #pragma unroll
-    for (int bit = 0; bit < 6; bit++) m[bit] = __ballot(valid && ((bin >> bit) & 1));
-    const unsigned long long vmask = __ballot(valid);
+    for (int bit = 0; bit < 6; bit++) m[bit] = __builtin_amdgcn_ballot_w64(((bin >> bit) & 1) != 0);
+    const unsigned long long vmask = __builtin_amdgcn_ballot_w64(valid);
     // Lane b's bin mask eq(b) from the ballots (bit k of b selects m[k]
     // or its complement), its count cb and, since bins are lane
     // indices, start = the exclusive prefix of cb over lanes (DPP scan).
@@ -179,7 +180,9 @@ __device__ __forceinline__ int ori_sort_chunk(const OriWin& wn, const OriFetch& 
     // reads its run with ds_read_b128 and no bounds tests.
     const int c4 = (cb + 3) & ~3;
     const int start = wave_incl_scan(c4) - c4;
-    for (int q = cb; q < c4; q++) buf[start + q] = 0.f;
+    // Pads: the run's last float4 zeroed first; the samples' stores below
+    // come later in this wave's LDS order and overwrite its non-pad slots.
+    if (c4 > cb) *reinterpret_cast<float4*>(buf + start + c4 - 4) = make_float4(0.f, 0.f, 0.f, 0.f);
     c4out = c4;
     // A sample's less(bin) and eq(bin) are those lane `bin` just
     // computed for its own key: three shuffles instead of a second
