@@ -4,6 +4,8 @@
   instead of the register-streaming all-octave one.
 * More than 16384 row buckets (tall, doubled images): retainBest select,
   bucket count, scan and scatter as four kernels instead of k_order.
+* More than 8192 oriented entries in k_order (a dense blob field): the
+  count/scatter go through slot[] instead of registers.
 * maxKeypoints below the keypoint count: results are the first maxKeypoints
   of the full, deterministic output order, and overflow bit 3 is raised.
 Same bar as test_gpu_parity.py: keypoints bit-exact, descriptors |diff| <= 1
@@ -61,3 +63,27 @@ def test_max_keypoints_truncates_in_order(sift):
     assert det.overflow_flags() & 8
     k, d, _ = gpu_keypoints(det)
     assert np.array_equal(k, fk[:cap]) and np.array_equal(d, fd[:cap])
+
+
+def blob_field(w, h, n, seed):
+    """128 grey with n random Gaussian blobs (sigma 1.2-3, +-40..110): ~11k
+    keypoints at 1280x960 (OpenCV defaults, no doubled base)."""
+    rng = np.random.default_rng(seed)
+    img = np.full((h, w), 128.0, np.float32)
+    ys, xs = rng.integers(8, h - 8, n), rng.integers(8, w - 8, n)
+    sig = rng.uniform(1.2, 3.0, n)
+    amp = rng.choice([-1, 1], n) * rng.uniform(40, 110, n)
+    yy, xx = np.mgrid[-7:8, -7:8]
+    for y, x, sg, a in zip(ys, xs, sig, amp):
+        img[y - 7:y + 8, x - 7:x + 8] += a * np.exp(-(xx * xx + yy * yy) / (2 * sg * sg))
+    return np.clip(img, 0, 255).astype(np.float32)
+
+
+def test_order_many_entries_slot_path(sift, oracle):
+    w, h = 1280, 960  # ~5.7k row buckets: k_order, with > 8192 oriented entries
+    img = blob_field(w, h, 50000, 1)
+    cfg, det = make_detector(sift, w, h, numFeatures=0, maxKeypoints=1 << 16)
+    det.detectAndCompute(img)
+    assert det.overflow_flags() == 0
+    assert det.total_size > 8192, det.total_size
+    check_vs_oracle(sift, oracle, cfg, det, img)
