@@ -74,6 +74,10 @@ static_assert(SIFT_DESC_PERM % 2 == 1, "lane permutation multiplier must be odd"
 #define SIFT_DESC_PRECISE 0
 #endif
 
+#ifndef SIFT_DESC_SERIAL_SAMPLES
+#define SIFT_DESC_SERIAL_SAMPLES 1  // scheduling barrier between an item's samples
+#endif
+
 struct DescGeom {
     float cos_t, sin_t, exp_scale;
     int ptx, pty, rows, cols;
@@ -348,13 +352,20 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
             // = r2 * (-log2(e) / 8) with the same single rounding: one multiply.
             const float wgt = __builtin_amdgcn_exp2f((sq[0] + sq[1]) * (-1.44269504088896341f / (kD * kD * 0.5f)));
 #endif
+#if SIFT_DESC_VARIANT == 4  // timing variant: no atan2 / magnitude / exp
+            const float gori = dx * 3.f + dy, gmag = dx + dy * 0.5f;
+            (void)wgt;
+#define SIFT_DESC_WGT 1.f
+#else
             const float gori = desc_atan2(dy, dx);
             const float gmag = desc_magnitude(dx, dy);
+#define SIFT_DESC_WGT wgt
+#endif
             float obin = (gori - jb.angle) * bins_per_rad;
             // x 2^S (exact): the trilinear parts come out in fixed-point units.
             // A select, not a branch around the product (every operand is
             // finite: enumerated samples are in-image).
-            const float mag = (gmag * wgt * fxs) * (valid ? 1.f : 0.f);
+            const float mag = (gmag * SIFT_DESC_WGT * fxs) * (valid ? 1.f : 0.f);
             // cvFloor in the float domain (the clamp only guards rejected
             // samples): r - floor(r) is the oracle's r - (float)cvFloor(r).
             const float r0f = fminf(fmaxf(floorf(rbin), -1.f), (float)(kD - 1));
@@ -452,6 +463,11 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
                     const unsigned o = (unsigned)((G.pty + i) * jb.pitch + G.ptx + jj) * 4u;
                     // (x-1 .. x+kItem) of the row, (x .. x+kItem-1) of the rows above and below.
                     float row6[kItem + 2], up[kItem], dn[kItem];
+#if SIFT_DESC_VARIANT == 3  // timing variant: no gradient loads (values from the offset)
+                    for (int t = 0; t < kItem + 2; t++) row6[t] = (float)((o >> (2 * t)) & 255);
+                    for (int t = 0; t < kItem; t++) up[t] = (float)((o >> (3 + t)) & 255), dn[t] = (float)((o >> (5 + t)) & 255);
+                    if (false)
+#endif
                     {
                         const f32x4d cm = __builtin_bit_cast(f32x4d, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o - 4u, 0, 0));
                         if constexpr (kItem == 2) {
@@ -480,7 +496,9 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
                         accum_rot(rot[0], rot[1], t < cnt, row6[t], row6[t + 2], up[t], dn[t]);
                         // One sample at a time: interleaving the four keeps
                         // ~90 VGPRs live (occupancy 5 instead of 8 waves/SIMD).
+#if SIFT_DESC_SERIAL_SAMPLES
                         __builtin_amdgcn_sched_barrier(0);
+#endif
                     }
                     jj += kItem;
                     if (k + 1 < k1 && jj >= jend) {  // next non-empty row

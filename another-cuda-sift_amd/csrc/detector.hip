@@ -109,6 +109,9 @@ const char* build_flags() {
 #ifdef SIFT_EX_TALL_MIN
            " SIFT_EX_TALL_MIN=" SIFT_STR(SIFT_EX_TALL_MIN)
 #endif
+#ifdef SIFT_DESC_SERIAL_SAMPLES
+           " SIFT_DESC_SERIAL_SAMPLES=" SIFT_STR(SIFT_DESC_SERIAL_SAMPLES)
+#endif
 #ifdef SIFT_BLUR_CHAIN
            " SIFT_BLUR_CHAIN=" SIFT_STR(SIFT_BLUR_CHAIN)
 #endif

@@ -1335,7 +1335,7 @@ __device__ __forceinline__ void extrema_block(const OctGeom& g, int o, float thr
 // latency-bound and want waves; tools/kernel_bench: 1920x1200 16.7 us at 6
 // rows vs 19.8 at 2; 960x600 9.2 us at 2 rows vs 10.8 at 6).
 #ifndef SIFT_EX_TALL_MIN
-#define SIFT_EX_TALL_MIN 2048  // 6-row wave strips from this many strips per launch, else 2-row (one 1920x1200 frame: 1600 -> 2-row, 26.4 -> 25.5 us)
+#define SIFT_EX_TALL_MIN 2048  // single frames: 6-row wave strips from this many strips per launch, else 2-row (1920x1200: 1600 -> 2-row, 26.4 -> 25.5 us); batches: 1024
 #endif
 struct ExtremaPlan {
     int start[kMaxOctaves + 1];  // start[nOct] = blocks per frame
@@ -1387,7 +1387,7 @@ bool launch_extrema_all(const PyrDesc& pyr, float threshold, uint2* cand, Counte
         const int strips = (g.W + EX4_COLS - 1) / EX4_COLS;
         // Frames of a batch count too: each brings its own strips.
         // (8, 12 or 20 rows per wave for batches: 147, 149, 582 us vs 131 at 6.)
-        const bool tall = strips * ((g.H + 5) / 6) * fr.nf >= SIFT_EX_TALL_MIN;
+        const bool tall = strips * ((g.H + 5) / 6) * fr.nf >= (fr.nf > 1 ? 1024 : SIFT_EX_TALL_MIN);
         const int tr = tall ? 6 : 2;
         plan.start[o] = total;
         plan.strips[o] = strips;
