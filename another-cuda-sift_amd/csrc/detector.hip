@@ -112,6 +112,9 @@ const char* build_flags() {
 #ifdef SIFT_DESC_SERIAL_SAMPLES
            " SIFT_DESC_SERIAL_SAMPLES=" SIFT_STR(SIFT_DESC_SERIAL_SAMPLES)
 #endif
+#if defined(SIFT_MATCH_VARIANT) && SIFT_MATCH_VARIANT
+           " SIFT_MATCH_VARIANT=" SIFT_STR(SIFT_MATCH_VARIANT)
+#endif
 #ifdef SIFT_BLUR_CHAIN
            " SIFT_BLUR_CHAIN=" SIFT_STR(SIFT_BLUR_CHAIN)
 #endif

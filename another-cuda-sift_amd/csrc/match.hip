@@ -46,6 +46,9 @@
 #include "sift_match.h"
 #include "sift_math.h"
 
+#ifndef SIFT_MATCH_VARIANT
+#define SIFT_MATCH_VARIANT 0  // timing variants (tools A/B builds only): 1 no epilogue, 2 no MFMA
+#endif
 #ifndef SIFT_MATCH_WG_TARGET
 #define SIFT_MATCH_WG_TARGET 512  // workgroups a launch aims for (2 per CU) when choosing train splits
 #endif
@@ -365,11 +368,28 @@ __global__ __launch_bounds__(256, 2) void k_match(MatchBatch batch, int S, int n
                 if (tile + 3 < tend) fetch(tile + 3, std::integral_constant<int, PB ^ 1>{});
             }
             i32x16 acc[2] = {{}, {}};
+#if SIFT_MATCH_VARIANT == 2  // timing variant: no MFMA (wrong results)
+#pragma unroll
+            for (int qb = 0; qb < 2; qb++)
+#pragma unroll
+                for (int i = 0; i < 16; i++) acc[qb][i] = a[i & 3][i >> 2] ^ bq[qb][i & 3][(i >> 2) & 3];
+#else
 #pragma unroll
             for (int qb = 0; qb < 2; qb++)
 #pragma unroll
                 for (int kb = 0; kb < 4; kb++)
                     acc[qb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[kb], bq[qb][kb], acc[qb], 0, 0, 0);
+#endif
+#if SIFT_MATCH_VARIANT == 1  // timing variant: no top-2 epilogue (wrong results)
+#pragma unroll
+            for (int qb = 0; qb < 2; qb++) {
+                int x = 0;
+#pragma unroll
+                for (int i = 0; i < 16; i++) x ^= acc[qb][i];
+                m1e[qb] ^= x;
+            }
+            if (false)
+#endif
 #pragma unroll
             for (int qb = 0; qb < 2; qb++)
 #pragma unroll
