@@ -120,23 +120,25 @@ __device__ __forceinline__ void trilinear(float mag, float rbf, float cbf, float
 // Shrink [lo, hi] to a superset of the integers j with -1 < j*s + b < kD
 // (margin 1e-4 in bin units and one sample each side, so float rounding of the
 // exact per-sample test can never fall outside the enumerated range).
-// inv_s = 1 / s (computed once per keypoint; an ulp of it is far inside the margins).
-__device__ __forceinline__ void clip_interval(int& lo, int& hi, double s, double inv_s, double b, int R) {
-    constexpr double lb = -1.0 - 1e-4, ub = kD + 1e-4;
-    if (fabs(s) < 1e-12) {
+// inv_s = 1 / s (computed once per keypoint).  Float: the bounds before
+// clamping to +-(R+2) carry a relative error of a few 1e-7, i.e. < 1e-4
+// samples for R <= 50, far inside the one-sample margin each side.
+__device__ __forceinline__ void clip_interval(int& lo, int& hi, float s, float inv_s, float b, int R) {
+    constexpr float lb = -1.f - 1e-4f, ub = kD + 1e-4f;
+    if (fabsf(s) < 1e-12f) {
         if (b <= lb || b >= ub) hi = lo - 1;
         return;
     }
-    double x1 = (lb - b) * inv_s, x2 = (ub - b) * inv_s;
+    float x1 = (lb - b) * inv_s, x2 = (ub - b) * inv_s;
     if (x1 > x2) {
-        const double t = x1;
+        const float t = x1;
         x1 = x2;
         x2 = t;
     }
-    x1 = fmax(x1, (double)(-R - 2));
-    x2 = fmin(x2, (double)(R + 2));
-    lo = max(lo, (int)floor(x1) - 1);
-    hi = min(hi, (int)ceil(x2) + 1);
+    x1 = fmaxf(x1, (float)(-R - 2));
+    x2 = fminf(x2, (float)(R + 2));
+    lo = max(lo, (int)floorf(x1) - 1);
+    hi = min(hi, (int)ceilf(x2) + 1);
 }
 
 // Sample math with native gfx950 instructions (v_rcp_f32, v_sqrt_f32,
@@ -297,15 +299,16 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
         const __amdgpu_buffer_rsrc_t rsrc =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(jb.img), 0, jb.rows * jb.pitch * 4, 0x00020000);
 
-        for (int i = tid; i < kCopies * kHistWords; i += kDT) histE[i] = 0u;
+        static_assert((kCopies * kHistWords) % 4 == 0, "histograms zeroed as uint4");
+        for (int i = tid; i < kCopies * kHistWords / 4; i += kDT) reinterpret_cast<uint4*>(histE)[i] = make_uint4(0u, 0u, 0u, 0u);
         if (enumerated) {
-            const double inv_sin = 1.0 / (double)G.sin_t, inv_cos = 1.0 / (double)G.cos_t;
+            const float inv_sin = __builtin_amdgcn_rcpf(G.sin_t), inv_cos = __builtin_amdgcn_rcpf(G.cos_t);
             for (int t = tid; t < side; t += kDT) {
                 const int i = t - radius, r = G.pty + i;
                 int lo = max(-radius, 1 - G.ptx), hi = min(radius, G.cols - 2 - G.ptx);
                 if (r <= 0 || r >= G.rows - 1) hi = lo - 1;
-                clip_interval(lo, hi, (double)G.sin_t, inv_sin, (double)i * G.cos_t + (kD / 2 - 0.5), radius);
-                clip_interval(lo, hi, (double)G.cos_t, inv_cos, -(double)i * G.sin_t + (kD / 2 - 0.5), radius);
+                clip_interval(lo, hi, G.sin_t, inv_sin, (float)i * G.cos_t + (kD / 2 - 0.5f), radius);
+                clip_interval(lo, hi, G.cos_t, inv_cos, -(float)i * G.sin_t + (kD / 2 - 0.5f), radius);
                 const int len = max(hi - lo + 1, 0);
                 rowlo[t] = lo;
                 rowln[t] = len;
