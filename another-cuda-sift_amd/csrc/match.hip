@@ -47,7 +47,7 @@
 #include "sift_math.h"
 
 #ifndef SIFT_MATCH_VARIANT
-#define SIFT_MATCH_VARIANT 0  // timing variants (tools A/B builds only): 1 no epilogue, 2 no MFMA
+#define SIFT_MATCH_VARIANT 0  // timing variants (tools A/B builds only): 1 no epilogue, 2 no MFMA, 3 no barrier, 4 no staging
 #endif
 #ifndef SIFT_MATCH_WG_TARGET
 #define SIFT_MATCH_WG_TARGET 512  // workgroups a launch aims for (2 per CU) when choosing train splits
@@ -322,25 +322,32 @@ __global__ __launch_bounds__(256, 2) void k_match(MatchBatch batch, int S, int n
         // tiles ahead through a ring of two register slots (tile k in slot
         // k & 1), so a tile's global load has two iterations to land before
         // it is stored to its LDS buffer (k & 1) for iteration k.
+        // The ring holds the RAW loaded words: the padding select and the key
+        // are applied at stash time, so no instruction consumes a load right
+        // after it is issued (a select on the loaded value made the compiler
+        // wait for every prefetch at once -- vmcnt(0) before each tile's
+        // MFMAs -- and the two-deep ring hid nothing).
         const int lrow = tid >> 3, lpart = tid & 7;
         i32x4 nv[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-        int nk[2] = {0, 0};
+        int nn[2] = {0, 0};
         using I0 = std::integral_constant<int, 0>;
         using I1 = std::integral_constant<int, 1>;
         auto fetch = [&](int tile, auto slot) {
             constexpr int SL = decltype(slot)::value;
             const int r = tile * kMatchTileRows + lrow;
-            const i32x4 v = *reinterpret_cast<const i32x4*>(tc + (size_t)min(r, pr.nt - 1) * 128 + 16 * lpart);
-            nv[SL] = r < pr.nt ? v : (i32x4){0, 0, 0, 0};
-            const int rr = tile * kMatchTileRows + (tid & 31);
-            const int n2 = tn[min(rr, pr.nt - 1)];
-            const int lr = ((tile - tbeg) & (kGroupTiles - 1)) * kMatchTileRows + (tid & 31);  // row in the key group
-            nk[SL] = rr < pr.nt ? -(128 * n2 + lr) : kPadBias;
+            nv[SL] = *reinterpret_cast<const i32x4*>(tc + (size_t)min(r, pr.nt - 1) * 128 + 16 * lpart);
+            nn[SL] = tn[min(tile * kMatchTileRows + (tid & 31), pr.nt - 1)];
         };
-        auto stash = [&](auto slot) {  // slot k & 1 -> LDS buffer k & 1
+        auto stash = [&](int tile, auto slot) {  // tile k, slot k & 1 -> LDS buffer k & 1
             constexpr int SL = decltype(slot)::value;
-            *reinterpret_cast<i32x4*>(s_tile[SL] + lrow * kRowPad + 16 * lpart) = nv[SL];
-            if (tid < kMatchTileRows) s_ntk[SL][tid] = nk[SL];
+            const int r = tile * kMatchTileRows + lrow;
+            *reinterpret_cast<i32x4*>(s_tile[SL] + lrow * kRowPad + 16 * lpart) =
+                r < pr.nt ? nv[SL] : (i32x4){0, 0, 0, 0};
+            if (tid < kMatchTileRows) {
+                const int rr = tile * kMatchTileRows + tid;
+                const int lr = ((tile - tbeg) & (kGroupTiles - 1)) * kMatchTileRows + tid;  // row in the key group
+                s_ntk[SL][tid] = rr < pr.nt ? -(128 * nn[SL] + lr) : kPadBias;
+            }
         };
         Best best[2] = {{kNone, kNone, kNone, kNone}, {kNone, kNone, kNone, kNone}};
         // Running key top-2 per query block in two chains (even / odd
@@ -349,13 +356,15 @@ __global__ __launch_bounds__(256, 2) void k_match(MatchBatch batch, int S, int n
         int m1o[2] = {INT_MIN, INT_MIN}, m2o[2] = {INT_MIN, INT_MIN};  // odd registers
         if (tbeg < tend) {
             fetch(tbeg, I0{});
-            stash(I0{});
+            stash(tbeg, I0{});
             if (tbeg + 1 < tend) fetch(tbeg + 1, I1{});
             if (tbeg + 2 < tend) fetch(tbeg + 2, I0{});
         }
         auto step = [&](int tile, auto par) {  // par = (tile - tbeg) & 1
             constexpr int PB = decltype(par)::value;
+#if SIFT_MATCH_VARIANT != 3  // timing variant 3: no per-tile barrier (wrong results)
             lds_barrier();  // tile `tile` is in s_tile[PB]; every wave is done with s_tile[PB ^ 1]
+#endif
             i32x4 a[4], tk[4];
             const int8_t* ta = s_tile[PB] + col * kRowPad + 64 * h;
 #pragma unroll
@@ -363,10 +372,12 @@ __global__ __launch_bounds__(256, 2) void k_match(MatchBatch batch, int S, int n
             // accumulator register i holds train row (i & 3) + 8 (i >> 2) + 4 h
 #pragma unroll
             for (int g = 0; g < 4; g++) tk[g] = *reinterpret_cast<const i32x4*>(s_ntk[PB] + 8 * g + 4 * h);
+#if SIFT_MATCH_VARIANT != 4  // timing variant 4: no tile staging after the first (wrong results)
             if (tile + 1 < tend) {
-                stash(std::integral_constant<int, PB ^ 1>{});
+                stash(tile + 1, std::integral_constant<int, PB ^ 1>{});
                 if (tile + 3 < tend) fetch(tile + 3, std::integral_constant<int, PB ^ 1>{});
             }
+#endif
             i32x16 acc[2] = {{}, {}};
 #if SIFT_MATCH_VARIANT == 2  // timing variant: no MFMA (wrong results)
 #pragma unroll
