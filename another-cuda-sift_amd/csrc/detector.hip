@@ -115,6 +115,9 @@ const char* build_flags() {
 #if defined(SIFT_MATCH_VARIANT) && SIFT_MATCH_VARIANT
            " SIFT_MATCH_VARIANT=" SIFT_STR(SIFT_MATCH_VARIANT)
 #endif
+#ifdef SIFT_BLUR_IW112
+           " SIFT_BLUR_IW112=" SIFT_STR(SIFT_BLUR_IW112)
+#endif
 #ifdef SIFT_BLUR_CHAIN
            " SIFT_BLUR_CHAIN=" SIFT_STR(SIFT_BLUR_CHAIN)
 #endif

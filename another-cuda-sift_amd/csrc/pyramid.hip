@@ -147,10 +147,14 @@ template <int R>
 constexpr int blur_org() {  // tile column 0 = image column x0 - ORG
     return SIFT_BLUR_X4LD && R <= 8 ? 8 : R;
 }
+#ifndef SIFT_BLUR_IW112
+#define SIFT_BLUR_IW112 1  // radius 11..24: pitch 112 (16 mod 32) -- 4 workgroups per CU either way at R = 13
+#endif
 template <int R>
-constexpr int blur_iw() {  // radius > 8: the next 16-mod-32 pitch (112) costs a workgroup per CU -- kept at 64 + 2R
+constexpr int blur_iw() {  // radius 9, 10: the next 16-mod-32 pitch (112) costs a workgroup per CU -- kept at 64 + 2R
     return SIFT_BLUR_IW16 && R <= 8 ? ((BLUR_TW + 2 * blur_org<R>() + 15) / 32) * 32 + 16
-                                    : (BLUR_TW + 2 * blur_org<R>() + 3) & ~3;
+           : SIFT_BLUR_IW112 && R >= 11 && R <= 24 ? 112
+                                                   : (BLUR_TW + 2 * blur_org<R>() + 3) & ~3;
 }
 template <int R>
 constexpr int blur_lds_floats() {
