@@ -547,6 +547,12 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
             val[h] = (float)((double)hv * (double)inv);
             if (tid + kDT * h < 128) sq[t] = val[h];
         }
+#if SIFT_DESC_VARIANT == 5  // timing variant: no normalisation epilogue (wrong results)
+        for (int h = 0; h < kPer; h++)
+            if (tid + kDT * h < 128) desc[(size_t)p * 128 + tid + kDT * h] = (uint16_t)val[h];
+        lds_barrier();
+        continue;
+#endif
         lds_barrier();
         if (tid < 8) {
             float a = 0.f;
