@@ -171,9 +171,17 @@ __device__ __forceinline__ int ori_sort_chunk(const OriWin& wn, const OriFetch& 
     // Lane b's bin mask eq(b) from the ballots (bit k of b selects m[k]
     // or its complement), its count cb and, since bins are lane
     // indices, start = the exclusive prefix of cb over lanes (DPP scan).
-    unsigned long long eq_l = vmask;
+    // (32-bit halves: eq & (m ^ nb) is one v_bitop3_b32 per half and bit;
+    // nb is 0 or all ones, the same in both halves.)
+    unsigned eq_lo = (unsigned)vmask, eq_hi = (unsigned)(vmask >> 32);
 #pragma unroll
-    for (int bit = 0; bit < 6; bit++) eq_l &= m[bit] ^ lane_nb[bit];
+    for (int bit = 0; bit < 6; bit++) {
+        const unsigned nb = (unsigned)lane_nb[bit];
+        // LUT 0x60 = S0 & (S1 ^ S2) (truth-table index S0 << 2 | S1 << 1 | S2)
+        eq_lo = __builtin_amdgcn_bitop3_b32(eq_lo, (unsigned)m[bit], nb, 0x60);
+        eq_hi = __builtin_amdgcn_bitop3_b32(eq_hi, (unsigned)(m[bit] >> 32), nb, 0x60);
+    }
+    const unsigned long long eq_l = ((unsigned long long)eq_hi << 32) | eq_lo;
     const int cb = __popcll(eq_l);  // lanes >= 36: no sample has that bin
     // Bins start on 16-byte boundaries (runs padded to a multiple of 4
     // with +0.0, which leaves a non-negative sum unchanged), so lane b
