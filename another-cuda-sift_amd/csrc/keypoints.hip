@@ -131,10 +131,11 @@ __device__ __forceinline__ OriFetch ori_fetch(const OriWin& wn, int base, int la
     OriFetch f;
     const int idx = base + lane;
     f.i = (int)__umulhi((unsigned)idx, wn.mside);
-    f.j = idx - f.i * wn.side;
+    f.j = idx - (int)__umul24((unsigned)f.i, (unsigned)wn.side);
     const int y = wn.r + f.i - wn.radius, x = wn.c + f.j - wn.radius;
     f.valid = idx < wn.total && y > 0 && y < wn.H - 1 && x > 0 && x < wn.W - 1;
-    const unsigned o0 = f.valid ? (unsigned)(y * wn.pitch + x) * 4u : 0x80000000u;
+    // (24-bit products: rows, pitches and window sides are < 2^24.)
+    const unsigned o0 = f.valid ? (__umul24((unsigned)y, (unsigned)wn.pitch) + (unsigned)x) * 4u : 0x80000000u;
     f.xl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wn.rsrc, o0 - 4u, 0, 0));
     f.xr = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wn.rsrc, o0 + 4u, 0, 0));
     f.yu = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wn.rsrc, o0 - 4u * wn.pitch, 0, 0));
@@ -152,12 +153,16 @@ __device__ __forceinline__ int ori_sort_chunk(const OriWin& wn, const OriFetch& 
     const bool valid = cur.valid;
     const int ii = i - wn.radius, jj = j - wn.radius;
     const float dx = cur.xr - cur.xl, dy = cur.yu - cur.yd;
-    const float w = cv_exp32f((float)(ii * ii + jj * jj) * wn.expf_scale, s_exptab);
+    // ii^2 + jj^2 in float: small integers (< 2^24), so exactly the integer
+    // sum the oracle converts (no quarter-rate / 64-bit integer multiplies).
+    const float fii = (float)ii, fjj = (float)jj;
+    const float w = cv_exp32f(__fmaf_rn(fii, fii, fjj * fjj) * wn.expf_scale, s_exptab);
     const float ori = cv_fast_atan2(dy, dx);
     const float mag = cv_magnitude(dx, dy);
     int bin = cv_round((kOriBins / 360.f) * ori);
-    if (bin >= kOriBins) bin -= kOriBins;
-    if (bin < 0) bin += kOriBins;
+    // ori is in [0, 360] (cv_fast_atan2), so bin is in [0, 36]: OpenCV's
+    // "if (bin >= n) bin -= n; if (bin < 0) bin += n" reduces to bin 36 -> 0.
+    bin = bin >= kOriBins ? 0 : bin;
     // Radix ranks from six ballots on the bin bits (MSB first): for each
     // key k, `less(k)` = valid samples with a smaller bin and `eq(k)` =
     // those with bin k.  A sample's slot is less(bin) + its lane rank
