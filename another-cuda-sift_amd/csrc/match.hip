@@ -3,7 +3,8 @@
 // Replaces /root/reference/sift_cuda/sift_func/Match.cu:8-177 (32 lanes per
 // query, half2 diff^2, an N x M fp32 score matrix written to and re-read from
 // HBM and allocated per call).  Here the distance matrix never leaves the
-// register file.  Two launches per call:
+// register file.  Two launches per call (one for a single pair: k_match<true>
+// converts its own rows, see there):
 //
 //  k_match_prep  every distinct descriptor set of the call (fp16 rows) becomes
 //                int8 codes c = v - 128 (128 B per row) and |c|^2 per row, once
@@ -178,6 +179,32 @@ __device__ __forceinline__ Best merge_best(const Best a, const Best b) {
     return Best{we, wi, ls ? le : ne, ls ? li : ni};
 }
 
+// 16 fp16 descriptor values -> int8 codes c = v - 128 (4 dwords), adding
+// sum c^2 to nrm; bad is set by a value that is not an integer 0..255 (NaN,
+// infinities and -0 included), whose code is then meaningless (the caller
+// falls back to the fp16 path).  Packed: v + 1024 puts an integer 0..1023 in
+// the mantissa bits exactly (0x6400 | v for v < 256), one v_perm gathers four
+// such low bytes, and v ^ 0x80 is v - 128 as int8; v_dot4 adds the squares.
+__device__ __forceinline__ i32x4 codes16(const uint4 a, const uint4 b, int& nrm, bool& bad) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const unsigned w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    unsigned y[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+        const h2 yv = __builtin_bit_cast(h2, w[e]) + (h2){(_Float16)1024.f, (_Float16)1024.f};
+        const h2 back = yv - (h2){(_Float16)1024.f, (_Float16)1024.f};
+        y[e] = __builtin_bit_cast(unsigned, yv);
+        bad |= (y[e] & 0xff00ff00u) != 0x64006400u || __builtin_bit_cast(unsigned, back) != w[e];
+    }
+    i32x4 pk;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        pk[k] = (int)(__builtin_amdgcn_perm(y[2 * k + 1], y[2 * k], 0x06040200u) ^ 0x80808080u);
+        nrm = __builtin_amdgcn_sdot4(pk[k], pk[k], nrm, false);
+    }
+    return pk;
+}
+
 // ---------------------------------------------------------------------------
 // General (fp16) path helpers.
 // ---------------------------------------------------------------------------
@@ -279,6 +306,13 @@ __device__ __forceinline__ void write_match(int i1, float e1, int i2, float e2, 
 }
 
 // grid = (256-query blocks, train splits, pairs), 256 threads.
+// kFused (single pairs): no k_match_prep launch -- the workgroup converts its
+// own query rows and train tiles from fp16 as it loads them and takes the
+// fp16 path itself if any of them holds a non-integer value.  Mixing paths
+// across workgroups is exact: on integer values 0..255 the fp16 path's dot
+// products and norms are exact integers below 2^24, so both paths return
+// the same (d^2, index) pairs with the same tie order.
+template <bool kFused>
 __global__ __launch_bounds__(256, 2) void k_match(MatchBatch batch, int S, int nq_stride,
                                                   const int8_t* __restrict__ codes, const int* __restrict__ norms,
                                                   const unsigned* __restrict__ flags, unsigned epoch,
@@ -298,7 +332,9 @@ __global__ __launch_bounds__(256, 2) void k_match(MatchBatch batch, int S, int n
     const int tbeg = min(ntiles, (int)blockIdx.y * tps), tend = min(ntiles, tbeg + tps);
     const int q0w = q0 + 64 * w;
     Top2 res[2];
-    if (flags[pr.qset] != epoch && flags[pr.tset] != epoch) {
+    bool bad = false;  // kFused: a non-integer value among this workgroup's rows
+    bool use_int = kFused || (flags[pr.qset] != epoch && flags[pr.tset] != epoch);
+    if (use_int) {
         // ---- integer path ----
         const int8_t* __restrict__ qc = codes + (size_t)pr.qrow0 * 128;
         const int8_t* __restrict__ tc = codes + (size_t)pr.trow0 * 128;
@@ -312,10 +348,18 @@ __global__ __launch_bounds__(256, 2) void k_match(MatchBatch batch, int S, int n
 #pragma unroll
         for (int qb = 0; qb < 2; qb++) {
             const int row = min(q0w + 32 * qb + col, pr.nq - 1);
-            const i32x4* src = reinterpret_cast<const i32x4*>(qc + (size_t)row * 128 + 64 * h);
+            if constexpr (kFused) {
+                const uint4* src = reinterpret_cast<const uint4*>(pr.q + (size_t)row * 128 + 64 * h);
+                int nrm = 0;
 #pragma unroll
-            for (int kb = 0; kb < 4; kb++) bq[qb][kb] = src[kb];
-            qn[qb] = norms[pr.qrow0 + row];
+                for (int kb = 0; kb < 4; kb++) bq[qb][kb] = codes16(src[2 * kb], src[2 * kb + 1], nrm, bad);
+                qn[qb] = nrm + __shfl_xor(nrm, 32);
+            } else {
+                const i32x4* src = reinterpret_cast<const i32x4*>(qc + (size_t)row * 128 + 64 * h);
+#pragma unroll
+                for (int kb = 0; kb < 4; kb++) bq[qb][kb] = src[kb];
+                qn[qb] = norms[pr.qrow0 + row];
+            }
         }
         // Tile loader: thread -> 16 bytes (row tid >> 3, part tid & 7) of a
         // 4 KiB tile; thread r < 32 -> row r's negated key bias.  Loads run two
@@ -330,17 +374,37 @@ __global__ __launch_bounds__(256, 2) void k_match(MatchBatch batch, int S, int n
         const int lrow = tid >> 3, lpart = tid & 7;
         i32x4 nv[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
         int nn[2] = {0, 0};
+        uint4 hv[2][2] = {};  // kFused: the raw fp16 words (32 bytes per thread per tile)
         using I0 = std::integral_constant<int, 0>;
         using I1 = std::integral_constant<int, 1>;
         auto fetch = [&](int tile, auto slot) {
             constexpr int SL = decltype(slot)::value;
             const int r = tile * kMatchTileRows + lrow;
-            nv[SL] = *reinterpret_cast<const i32x4*>(tc + (size_t)min(r, pr.nt - 1) * 128 + 16 * lpart);
-            nn[SL] = tn[min(tile * kMatchTileRows + (tid & 31), pr.nt - 1)];
+            if constexpr (kFused) {
+                const uint4* src = reinterpret_cast<const uint4*>(pr.t + (size_t)min(r, pr.nt - 1) * 128 + 16 * lpart);
+                hv[SL][0] = src[0];
+                hv[SL][1] = src[1];
+            } else {
+                nv[SL] = *reinterpret_cast<const i32x4*>(tc + (size_t)min(r, pr.nt - 1) * 128 + 16 * lpart);
+                nn[SL] = tn[min(tile * kMatchTileRows + (tid & 31), pr.nt - 1)];
+            }
         };
         auto stash = [&](int tile, auto slot) {  // tile k, slot k & 1 -> LDS buffer k & 1
             constexpr int SL = decltype(slot)::value;
             const int r = tile * kMatchTileRows + lrow;
+            if constexpr (kFused) {  // codes and the row's norm (8 threads per row, lanes 8k..8k+7)
+                int nrm = 0;
+                const i32x4 pk = codes16(hv[SL][0], hv[SL][1], nrm, bad);
+                nrm += __shfl_xor(nrm, 1);
+                nrm += __shfl_xor(nrm, 2);
+                nrm += __shfl_xor(nrm, 4);
+                *reinterpret_cast<i32x4*>(s_tile[SL] + lrow * kRowPad + 16 * lpart) = r < pr.nt ? pk : (i32x4){0, 0, 0, 0};
+                if (lpart == 0) {
+                    const int lr = ((tile - tbeg) & (kGroupTiles - 1)) * kMatchTileRows + lrow;
+                    s_ntk[SL][lrow] = r < pr.nt ? -(128 * nrm + lr) : kPadBias;
+                }
+                return;
+            }
             *reinterpret_cast<i32x4*>(s_tile[SL] + lrow * kRowPad + 16 * lpart) =
                 r < pr.nt ? nv[SL] : (i32x4){0, 0, 0, 0};
             if (tid < kMatchTileRows) {
@@ -440,7 +504,10 @@ __global__ __launch_bounds__(256, 2) void k_match(MatchBatch batch, int S, int n
             res[qb].d2 = r.e2 == kNone ? INFINITY : (float)(r.e2 + qn[qb]);
             res[qb].i2 = r.e2 == kNone ? kNone : r.i2;
         }
-    } else {
+    }
+    if constexpr (kFused)
+        if (__syncthreads_or(bad)) use_int = false;  // this workgroup's rows need the fp16 path
+    if (!use_int) {
         // ---- general path: fp16 values that are not integers 0..255 ----
         res[0] = match_f16_block(pr, q0w, tbeg, tend, col, h);
         res[1] = match_f16_block(pr, q0w + 32, tbeg, tend, col, h);
@@ -495,22 +562,35 @@ __global__ __launch_bounds__(256, 2) void k_match(MatchBatch batch, int S, int n
 int match_splits(int max_nq, int max_nt, int P) {
     const int qblocks = (max_nq + kMatchQB - 1) / kMatchQB;
     const int ntiles = (max_nt + kMatchTileRows - 1) / kMatchTileRows;
-    int S = (SIFT_MATCH_WG_TARGET + qblocks * P - 1) / (qblocks * P);
+#ifndef SIFT_MATCH_WG_TARGET_SINGLE
+#define SIFT_MATCH_WG_TARGET_SINGLE SIFT_MATCH_WG_TARGET  // single pairs (fused conversion: fewer, longer splits)
+#endif
+    const int target = P == 1 ? SIFT_MATCH_WG_TARGET_SINGLE : SIFT_MATCH_WG_TARGET;
+    int S = (target + qblocks * P - 1) / (qblocks * P);
     const int maxS = ntiles / 2 > 1 ? ntiles / 2 : 1;  // >= 2 tiles per split
     S = S < maxS ? S : maxS;
     return S < 1 ? 1 : S;
 }
 
+#ifndef SIFT_MATCH_FUSED_SINGLE
+#define SIFT_MATCH_FUSED_SINGLE 1  // single pairs: no prep launch (tools A/B builds set 0)
+#endif
 void launch_match(const MatchSets& sets, const MatchBatch& batch, int S, int nq_stride, int8_t* codes, int* norms,
                   unsigned* flags, unsigned epoch, unsigned long long* keys, unsigned* done, float ratio,
                   int ratio_on_squared, int* idx2, float* d2, int* match, hipStream_t s) {
+    if (batch.P == 1 && SIFT_MATCH_FUSED_SINGLE) {
+        dim3 g((max(batch.pair[0].nq, 1) + kMatchQB - 1) / kMatchQB, S, 1);
+        hipLaunchKernelGGL(k_match<true>, g, dim3(256), 0, s, batch, S, nq_stride, codes, norms, flags, epoch, keys,
+                           done, ratio, ratio_on_squared, idx2, d2, match);
+        return;
+    }
     if (sets.maxn > 0)
         hipLaunchKernelGGL(k_match_prep, dim3((sets.maxn + 31) / 32, sets.nsets), dim3(256), 0, s, sets, codes, norms,
                            flags, epoch);
     int max_nq = 1;
     for (int p = 0; p < batch.P; p++) max_nq = max(max_nq, batch.pair[p].nq);
     dim3 g((max_nq + kMatchQB - 1) / kMatchQB, S, batch.P);
-    hipLaunchKernelGGL(k_match, g, dim3(256), 0, s, batch, S, nq_stride, codes, norms, flags, epoch, keys, done, ratio,
+    hipLaunchKernelGGL(k_match<false>, g, dim3(256), 0, s, batch, S, nq_stride, codes, norms, flags, epoch, keys, done, ratio,
                        ratio_on_squared, idx2, d2, match);
 }
 

@@ -308,6 +308,33 @@ def test_matcher_general_values(sift, oracle):
         off += k
 
 
+def test_matcher_single_pair_fallback(sift, oracle):
+    """Single pairs skip the prep launch: each workgroup converts its own rows
+    and takes the f16 path when any of them is not an integer 0..255.  One
+    half-integer query row (one 256-query block) and one out-of-range train
+    row (one split) make workgroups of the same pair take different paths;
+    whole non-integer sets take the f16 path everywhere."""
+    rng = np.random.default_rng(9)
+    ints = rng.integers(0, 21, (1100, 128)).astype(np.float32)
+    q_one = rng.integers(0, 21, (900, 128)).astype(np.float32)
+    q_one[700, 5] += 0.5  # query block 2 only
+    t_one = rng.integers(0, 21, (1100, 128)).astype(np.float32)
+    t_one[1000, 17] = 300.0  # one train split only
+    t_one[40] = t_one[41]  # tie across the integer path
+    halves = rng.integers(0, 21, (600, 128)).astype(np.float32) + 0.5
+    cases = [(q_one, ints), (ints[:800], t_one), (q_one, t_one), (halves, ints), (ints[:300], halves)]
+    m = sift.Matcher(1100, 1100, max_pairs=1)
+    for ci, (q, t) in enumerate(cases):
+        dq, dt = sift.DeviceArray.from_numpy(_half_rows(q)), sift.DeviceArray.from_numpy(_half_rows(t))
+        idx2, d2 = sift.DeviceArray(len(q) * 8), sift.DeviceArray(len(q) * 8)
+        m.match_batched([dq.value], [len(q)], [dt.value], [len(t)], idx2_ptr=idx2.value, d2_ptr=d2.value)
+        gi = idx2.to_numpy(np.int32, (len(q), 2))
+        gd = d2.to_numpy(np.float32, (len(q), 2))
+        oi, od = oracle.knn2(q, t)
+        assert np.array_equal(gi, oi), ci
+        assert np.array_equal(np.sqrt(gd).astype(np.float32), od), ci
+
+
 def test_results_before_sync(sift):
     """Accessors called straight after an unsynchronised device-input detect
     wait for that frame's counts: batch_copy_to_host after
