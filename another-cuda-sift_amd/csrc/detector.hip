@@ -112,6 +112,9 @@ const char* build_flags() {
 #ifdef SIFT_DESC_SERIAL_SAMPLES
            " SIFT_DESC_SERIAL_SAMPLES=" SIFT_STR(SIFT_DESC_SERIAL_SAMPLES)
 #endif
+#ifdef SIFT_MATCH_WG_TARGET_SINGLE
+           " SIFT_MATCH_WG_TARGET_SINGLE=" SIFT_STR(SIFT_MATCH_WG_TARGET_SINGLE)
+#endif
 #ifdef SIFT_MATCH_FUSED_SINGLE
            " SIFT_MATCH_FUSED_SINGLE=" SIFT_STR(SIFT_MATCH_FUSED_SINGLE)
 #endif
