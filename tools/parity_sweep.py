@@ -2,7 +2,7 @@
 tests do not use) through the HIP path and the CPU oracle, keypoints compared
 bit for bit and descriptor flips counted.
 
-    python3 tools/parity_sweep.py > gpurun_out/parity_sweep.json   (GPU box)
+    python3 tools/parity_sweep.py [FRAMES_PER_CONFIG] > gpurun_out/parity_sweep.json   (GPU box)
 
 Configurations: BASELINE C2 (1920x1200, 3 octaves, numFeatures 5000) and
 OpenCV defaults (doubled base, keep all) at 752x480 (C1's frame).
@@ -19,8 +19,9 @@ import oracle_binding as oracle  # noqa: E402
 import sift_amd as sift  # noqa: E402
 from test_gpu_parity import gpu_keypoints, sort_keys  # noqa: E402
 
-CONFIGS = [("C2", 1920, 1200, dict(upscale=False, numOctaves=3, numFeatures=5000), range(100, 110)),
-           ("C1 OpenCV defaults", 752, 480, dict(upscale=True, numOctaves=0, numFeatures=0), range(200, 210))]
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 10  # frames per configuration (seeds unused by the tests)
+CONFIGS = [("C2", 1920, 1200, dict(upscale=False, numOctaves=3, numFeatures=5000), range(1000, 1000 + N)),
+           ("C1 OpenCV defaults", 752, 480, dict(upscale=True, numOctaves=0, numFeatures=0), range(5000, 5000 + N))]
 
 
 def main():
@@ -56,7 +57,7 @@ def main():
             rows.append(row)
             print(json.dumps(row), file=sys.stderr, flush=True)
     tot["exact_fraction"] = 1.0 - tot["flips"] / max(1, tot["entries"])
-    json.dump({"command": "python3 tools/parity_sweep.py", "total": tot, "frames": rows}, sys.stdout, indent=1)
+    json.dump({"command": f"python3 tools/parity_sweep.py {N}", "total": tot, "frames": rows}, sys.stdout, indent=1)
     print()
 
 
