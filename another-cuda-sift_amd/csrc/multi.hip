@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -31,17 +32,17 @@ struct Rccl {
     const char* (*errorString)(ncclResult_t) = nullptr;
 };
 
-// dlopen once per process (the library stays loaded).
+// dlopen once per process (the library stays loaded); std::call_once makes
+// the lazy load safe from several host threads.
 Rccl* rccl() {
     static Rccl r;
-    static bool tried = false;
-    if (tried) return r.so ? &r : nullptr;
-    tried = true;
+    static std::once_flag once;
+    std::call_once(once, [] {
     for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
         r.so = dlopen(name, RTLD_NOW | RTLD_LOCAL);
         if (r.so) break;
     }
-    if (!r.so) return nullptr;
+    if (!r.so) return;
     r.commInitAll = (decltype(r.commInitAll))dlsym(r.so, "ncclCommInitAll");
     r.commDestroy = (decltype(r.commDestroy))dlsym(r.so, "ncclCommDestroy");
     r.allGather = (decltype(r.allGather))dlsym(r.so, "ncclAllGather");
@@ -52,6 +53,7 @@ Rccl* rccl() {
         dlclose(r.so);
         r.so = nullptr;
     }
+    });
     return r.so ? &r : nullptr;
 }
 
@@ -148,7 +150,11 @@ int sift_hip_comm_allgather(sift_hip_comm_t c, const void* const* send, void* co
     const int n = (int)c->devices.size();
     if (r->groupStart() != ncclSuccess) return mfail(SIFT_HIP_ERR_RUNTIME, "ncclGroupStart failed");
     for (int k = 0; k < n; k++) {
-        MHIPCHK(hipSetDevice(c->devices[k]));
+        const hipError_t e = hipSetDevice(c->devices[k]);
+        if (e != hipSuccess) {
+            (void)r->groupEnd();  // never leave the thread's RCCL group open
+            return mfail(SIFT_HIP_ERR_RUNTIME, std::string("hipSetDevice: ") + hipGetErrorString(e));
+        }
         hipStream_t s = streams && streams[k] ? (hipStream_t)streams[k] : c->streams[k];
         const ncclResult_t rc = r->allGather(send[k], recv[k], bytes, ncclChar, c->comms[k], s);
         if (rc != ncclSuccess) {

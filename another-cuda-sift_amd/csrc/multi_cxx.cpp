@@ -3,6 +3,7 @@
 // (include/sift_hip.h).  Plain C++ (g++): no HIP headers, no device code.
 #include "sift_cuda/MultiDetector.hh"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <exception>
@@ -175,10 +176,17 @@ BatchMatchFn hipBatchMatch(const std::vector<int>& devices, int max_rows, float 
         const int dev = st->devices[(size_t)rank];
         check(sift_hip_set_device(dev), "sift_hip_set_device");
         if (!st->matchers[(size_t)rank]) {
-            check(sift_hip_matcher_create(dev, st->max_rows, st->max_rows, 64, &st->matchers[(size_t)rank]),
+            // One rank matches its set against the other ranks' sets: at most
+            // devices - 1 pairs per launch (scratch sized for that, not for the
+            // matcher's 64-pair maximum).
+            const int maxPairs = std::max(1, std::min((int)st->devices.size() - 1, 64));
+            check(sift_hip_matcher_create(dev, st->max_rows, st->max_rows, maxPairs, &st->matchers[(size_t)rank]),
                   "sift_hip_matcher_create");
-            check(sift_hip_malloc(&st->out[(size_t)rank], sizeof(int) * 64 * (size_t)st->max_rows), "sift_hip_malloc");
+            check(sift_hip_malloc(&st->out[(size_t)rank], sizeof(int) * (size_t)maxPairs * (size_t)st->max_rows),
+                  "sift_hip_malloc");
         }
+        if (P > std::max(1, (int)st->devices.size() - 1))
+            throw std::invalid_argument("hipBatchMatch: more train sets than peer ranks");
         std::vector<const uint16_t*> q((size_t)P, (const uint16_t*)query), t((size_t)P);
         std::vector<int> nqs((size_t)P, nq);
         for (int p = 0; p < P; p++) t[(size_t)p] = (const uint16_t*)trains[(size_t)p];

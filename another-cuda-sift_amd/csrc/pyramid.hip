@@ -276,6 +276,10 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
                         (__attribute__((address_space(3))) void*)(in + 4 * (NT * u + 64 * (tid >> 6))), 16, 0, 0);
                 }
             }
+            // LDS-DMA writes are counted by vmcnt, not lgkmcnt: wait for this
+            // wave's copies explicitly so the staging barrier below publishes
+            // them whatever fence the compiler gives __syncthreads().
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #else
             typedef unsigned u32x4s __attribute__((ext_vector_type(4)));
             u32x4s q4[QPT];

@@ -9,9 +9,11 @@ The compute path is the HIP library only: if libsift_hip.so is missing this
 module raises ImportError-like errors on first use; there is no CPU fallback.
 
 HIP runtime note: PyTorch wheels bundle their own libamdhip64.so.  A process that
-uses both torch and this library must `import torch` BEFORE the first call here,
-so that libsift_hip.so binds to the already-loaded runtime (one HIP runtime per
-process).  bench.py does this.
+uses both torch and this library must load torch's runtime BEFORE
+libsift_hip.so, so that the library binds to the already-loaded runtime (one HIP
+runtime per process; the other order leaves torch with "No HIP GPUs are
+available").  `lib()` therefore imports torch first whenever torch is
+installed, so the load order no longer depends on the caller's imports.
 """
 from __future__ import annotations
 
@@ -58,6 +60,10 @@ def lib() -> ctypes.CDLL:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise SiftHipError(f"{LIB_PATH} not found: build it with `make` (or __graft_entry__.build())")
+    try:  # torch's bundled HIP runtime first (module docstring); importing torch does not touch the GPU
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp, ip, i, f, d, sz = ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_float, ctypes.c_double, ctypes.c_size_t
     sigs = {
@@ -101,6 +107,12 @@ def lib() -> ctypes.CDLL:
         "sift_hip_match_host": (i, [vp, vp, i, vp, i, f, i, vp]),
         "sift_synth_frame": (i, [ctypes.c_uint, i, i, vp]),
         "sift_hip_device_count": (i, [ip]),
+        "sift_hip_set_device": (i, [i]),
+        "sift_hip_memcpy_d2d": (i, [vp, vp, sz, vp]),
+        "sift_hip_comm_create": (i, [i, ip, ctypes.POINTER(vp)]),
+        "sift_hip_comm_destroy": (i, [vp]),
+        "sift_hip_comm_size": (i, [vp, ip]),
+        "sift_hip_comm_allgather": (i, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), sz, ctypes.POINTER(vp)]),
         "sift_hip_malloc": (i, [ctypes.POINTER(vp), sz]),
         "sift_hip_free": (i, [vp]),
         "sift_hip_memcpy_h2d": (i, [vp, vp, sz]),

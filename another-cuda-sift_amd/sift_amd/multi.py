@@ -35,7 +35,7 @@ def all_gather_rows(local: torch.Tensor, world: int, group=None) -> torch.Tensor
     """All-gather every rank's (n, 128) descriptor rows (same n on all ranks):
     (world, n, 128).  16-bit descriptor bits travel as int32 (RCCL and gloo
     have no int16); on "nccl" (= RCCL over xGMI) one all_gather_into_tensor."""
-    if world == 1:
+    if world == 1 and not dist.is_initialized():
         return local.unsqueeze(0)
     local = local.contiguous()
     wide = local.view(torch.int32) if local.dtype in (torch.int16, torch.float16) else local

@@ -333,6 +333,42 @@ def run_c1_gpu(local):
 
 
 
+def run_ref_configs(local, dev, reps=40):
+    """The reference's published configuration beside C2 (readme.md:11-16): one
+    synchronous detectAndCompute per frame at the tool default -- auto octaves
+    (Detector.hh:27), upscale=false, numFeatures=5000 -- on 752x480, 1920x1200
+    and 1600x900 frames resident in HBM (the readme excludes transfers), median
+    of `reps`; and the device memory one Detector holds (hipMemGetInfo free
+    bytes before creation minus after warm-up), the readme's 84/298/214 MiB
+    column.  Single-frame handles, as the reference's Detector."""
+    out = {}
+    for (w, h, ref_ms, ref_mib) in ((752, 480, 0.95, 84), (1920, 1200, 3.1, 298), (1600, 900, 2.5, 214)):
+        torch.cuda.synchronize()
+        free0 = torch.cuda.mem_get_info(local)[0]
+        d = sift.Detector(sift.CudaSiftConfig(col_width=w, row_width=h, numFeatures=5000, upscale=False, numOctaves=0),
+                          device=local)
+        d.gpuWarmUpAndAllocate()
+        torch.cuda.synchronize()
+        used = free0 - torch.cuda.mem_get_info(local)[0]
+        img = torch.from_numpy(sift.synth_frame(0, w, h)).to(dev)
+        torch.cuda.synchronize()
+        for _ in range(5):
+            d.detectAndComputeDevice(img.data_ptr(), w * 4, sync=True)
+        lat = []
+        for _ in range(reps):
+            t = time.perf_counter()
+            d.detectAndComputeDevice(img.data_ptr(), w * 4, sync=True)
+            lat.append(time.perf_counter() - t)
+        ms = float(np.median(lat) * 1e3)
+        out[f"{w}x{h}"] = {"octaves": d.nOctaves, "sync_ms_per_frame": round(ms, 4),
+                           "mpix_s": round(w * h / 1e3 / ms, 1), "keypoints": d.total_size,
+                           "device_mib": round(used / 2**20, 1), "ref_ms_rtx4070s": ref_ms, "ref_mib": ref_mib}
+        del d, img
+    out["note"] = ("reference tool default (auto octaves, upscale=false, numFeatures=5000), synchronous single frame "
+                   "from HBM, median of %d; device_mib = hipMemGetInfo delta of one Detector (create + warm-up)" % reps)
+    return out
+
+
 def pmc_kernel(summary_path, kernel_names):
     """Per-dispatch means of a kernel family's counters in a committed PMC
     summary (the timed-launch groups only, as pmc_traffic): corrected HBM
@@ -775,6 +811,10 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(a, cfg, [s.cpu().view(torch.float16).float().numpy() for s in sets[:2]])
     c1_gpu = run_c1_gpu(local) if rank == 0 else None
+    try:
+        ref_cfg = run_ref_configs(local, dev) if rank == 0 else None
+    except Exception as e:  # side measurement: keep the line
+        ref_cfg = {"error": repr(e)[:300]}
 
     if rank == 0:
         line = {
@@ -819,6 +859,7 @@ def main():
             "c4_256_frames_1600x900": c4,
             "c5_allgather_match": c5,
             "c1_gpu": c1_gpu,
+            "ref_config_sync": ref_cfg,
             "ref_published": {"detect_1920x1200_ms": 3.1, "match_2k_ms": "just under 1", "hardware": "RTX 4070 Super",
                               "note": "reference readme.md:11-15; config not stated (tool default upscale=false, auto octaves)"},
         }

@@ -147,7 +147,9 @@ int sift_hip_overflow_flags(sift_hip_t h, int* flags);
 /* Device result arrays (Detector.hh:54-57): kpts = float3 {x, y, layer}
  * per keypoint, features = float4 {octave packed as float, size, response,
  * angle}, descriptors = 128 x IEEE half (values 0..255) per keypoint.
- * prev_desc = the previous frame's descriptors (Detector.cu:136-141). */
+ * prev_desc = the previous frame's descriptors (Detector.cu:136-141).  Blocks
+ * the host until the current frame's counts are final (they come from the
+ * device), as the reference's own count read-back does (Detector.cu:542-548). */
 int sift_hip_results_device(sift_hip_t h, const float** kpts3, const float** feats4,
                             const uint16_t** desc, const uint16_t** prev_desc,
                             int* prev_count, int* capacity);
@@ -157,7 +159,11 @@ int sift_hip_results_device(sift_hip_t h, const float** kpts3, const float** fea
 int sift_hip_copy_to_host(sift_hip_t h, float* kpts3, float* feats4, uint16_t* desc, int cap);
 
 /* Device-to-device copy of this frame's descriptors (e.g. into a torch tensor
- * for an RCCL all-gather).  Copies min(count, cap) rows, pads nothing. */
+ * for an RCCL all-gather).  Copies min(count, cap) rows, pads nothing.  The
+ * row count is needed on the host, so this call (like sift_hip_results_device
+ * and sift_hip_num_keypoints after an unsynchronised detect) first blocks the
+ * host until the frame's counts are final; the copy itself is then enqueued on
+ * `stream`. */
 int sift_hip_copy_descriptors_device(sift_hip_t h, uint16_t* dst, int cap, void* stream);
 
 /* Detector::setDataGen(path) (Detector.hh:48-51; the reference dumps each
@@ -243,7 +249,10 @@ int sift_hip_comm_size(sift_hip_comm_t c, int* n);
  * offset r * bytes (the C5 exchange of descriptor sets).  One ncclAllGather per
  * rank inside an ncclGroupStart/End; streams[k] may be NULL for the
  * communicator's own stream, and with streams == NULL the call returns after
- * every rank's copy has completed. */
+ * every rank's copy has completed.  Ordering: the gather runs on streams[k]
+ * (or the communicator's non-blocking stream), which is NOT ordered after the
+ * stream that produced send[k] -- pass the producer's stream in streams[k], or
+ * make send[k] complete (stream/device synchronise) before the call. */
 int sift_hip_comm_allgather(sift_hip_comm_t c, const void* const* send, void* const* recv, size_t bytes,
                             void* const* streams);
 

@@ -59,6 +59,8 @@ CONFIGS = [
     (1920, 1200, False, 3, 5000, 0),  # BASELINE C2 (the bench workload), full size
     (1600, 900, False, 0, 5000, 4),   # BASELINE C4 frame shape, auto octaves
     (1920, 1200, True, 0, 0, 7),      # OpenCV defaults (doubled base, keep all) at full HD
+    (752, 480, True, 0, 0, 0),        # BASELINE C1: cv::SIFT defaults on the 752x480 frame pair
+    (752, 480, True, 0, 0, 1),        # (seeds 0 and 1)
 ]
 
 
@@ -221,6 +223,47 @@ def test_match_batched_equals_pairs(sift, oracle):
         oi, _ = oracle.knn2(sets[i], sets[j])
         assert np.array_equal(gi[off:off + n], oi), (i, j)
         off += n
+
+
+def test_c1_frame_pair_match(sift, oracle):
+    """BASELINE C1 end to end: cv::SIFT defaults (upscale, keep all) on frames 0
+    and 1 at 752x480, then BFMatcher(NORM_L2).knnMatch(k=2) + ratio 0.8 on
+    distances.  The HIP matcher on the HIP descriptors equals the oracle's
+    knn-2 on the same descriptors (indices and distances exact), and the
+    ratio-test match count is within 2 % of the all-oracle pipeline's (the
+    descriptor bar allows +-1 flips).  Reference caller:
+    /root/reference/tool/extract_and_match_example.cc:62-100."""
+    w, h = 752, 480
+    cfg = sift.CudaSiftConfig(col_width=w, row_width=h, upscale=True, numFeatures=0)
+    det = sift.Detector(cfg)
+    det.gpuWarmUpAndAllocate()
+    gdesc, odesc = [], []
+    for f in (0, 1):
+        img = sift.synth_frame(f, w, h)
+        det.detectAndCompute(img)
+        gk, gd, _ = gpu_keypoints(det)
+        ok, od = oracle.detect_and_compute(img, oracle.from_config(cfg))
+        assert_same_keypoints(gk, ok)
+        gdesc.append(gd)
+        odesc.append(od)
+    # Frame 1 is current; prev_descriptor holds frame 0 (the reference's pairing).
+    n0, n1 = len(gdesc[0]), len(gdesc[1])
+    assert det.prev_size == n0
+    idx2, d2 = sift.DeviceArray(n0 * 8), sift.DeviceArray(n0 * 8)
+    sift.Matcher(n0, n1).match_device(det.prev_descriptor.data(), n0, det.device_descriptor.data(), n1, 0.8, False,
+                                      idx2.value, d2.value)
+    gi, gdd = idx2.to_numpy(np.int32, (n0, 2)), d2.to_numpy(np.float32, (n0, 2))
+    oi, od = oracle.knn2(gdesc[0], gdesc[1])
+    assert np.array_equal(gi, oi)
+    assert np.array_equal(np.sqrt(gdd).astype(np.float32), od)
+    n_gpu = int((od[:, 0] < 0.8 * od[:, 1]).sum())
+    _, rd = oracle.knn2(odesc[0], odesc[1])
+    n_ref = int((rd[:, 0] < 0.8 * rd[:, 1]).sum())
+    assert n_ref > 20 and abs(n_gpu - n_ref) <= max(1, 0.02 * n_ref), (n_gpu, n_ref)
+    m = sift.matchBruteForce(det.prev_descriptor, n0, det.device_descriptor, n1)
+    # matchBruteForce keeps the reference's squared ratio (Match.cu:125-175).
+    exp = np.where(oi[:, 1] < 0, oi[:, 0], np.where(gdd[:, 0] < np.float32(0.8) * gdd[:, 1], oi[:, 0], -1))
+    assert np.array_equal(m, exp)
 
 
 def test_match_brute_force_dropin(sift):

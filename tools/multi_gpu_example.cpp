@@ -6,8 +6,10 @@
 // match per GPU).
 //
 //   multi_gpu_example [--frames 256] [--width 1600] [--height 900]
-//                     [--devices N | --virtual N] [--rows 2000] [--gather rccl|copy]
+//                     [--devices N | --virtual N] [--rows 2000] [--gather rccl|copy] [--rccl]
 //
+// --rccl (= --gather rccl) forces the RCCL communicator even for one device,
+// so a one-GPU box runs ncclCommInitAll + ncclAllGather once.
 // --virtual N runs N workers on GPU 0 (several detectors/streams on one GPU;
 // the exchange then uses device copies, RCCL needs distinct GPUs).  Prints one
 // JSON line: per-frame keypoint counts, C4 throughput, per-pair match counts.
@@ -35,6 +37,7 @@ int main(int argc, char** argv) {
         else if (a == "--virtual") virt = next();
         else if (a == "--rows") rows = next();
         else if (a == "--gather" && i + 1 < argc) gatherKind = argv[++i];
+        else if (a == "--rccl") gatherKind = "rccl";
     }
     int count = 0;
     sift_hip_device_count(&count);
