@@ -149,6 +149,12 @@ void Detector::setDataGen(const std::string& path) {
     if (m_handle) check(sift_hip_set_datagen(m_handle, path.c_str()), "setDataGen");
 }
 
+void Detector::replayStage(const std::string& dump_dir, const std::string& stage, const std::string& out_dir) {
+    if (!m_initialized && !gpuWarmUpAndAllocate()) return;
+    check(sift_hip_replay_stage(m_handle, dump_dir.c_str(), stage.c_str(), out_dir.c_str()), "replayStage");
+    refreshViews();
+}
+
 void Detector::copyToHost(bool descriptor) {
     if (!m_initialized) return;
     final_kpts.resize((size_t)total_size);

@@ -94,6 +94,7 @@ def lib() -> ctypes.CDLL:
         "sift_hip_copy_to_host": (i, [vp, vp, vp, vp, i]),
         "sift_hip_copy_descriptors_device": (i, [vp, vp, i, vp]),
         "sift_hip_set_datagen": (i, [vp, ctypes.c_char_p]),
+        "sift_hip_replay_stage": (i, [vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]),
         "sift_hip_set_timing": (i, [vp, i]),
         "sift_hip_timing_count": (i, [vp, ip]),
         "sift_hip_timing_entry": (i, [vp, i, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(d), ip, ctypes.POINTER(d)]),
@@ -368,6 +369,17 @@ class Detector:
         """Detector.hh:48-51: from now on every single-frame detect writes its stage
         dumps into `path` (sift_hip_set_datagen; "" switches them off)."""
         _check(lib().sift_hip_set_datagen(self._h, (path or "").encode()), "setDataGen")
+
+    STAGES = ("pyramid", "extrema", "refine", "orientation", "order", "descriptor")
+
+    def replayStage(self, dump_dir: str, stage: str, out_dir: str) -> None:
+        """tool/perf.cu:43-100: run ONE pipeline stage on a setDataGen dump's
+        recorded input (sift_hip_replay_stage); outputs go to out_dir in the
+        dump's file formats.  The handle's current results are discarded."""
+        self.gpuWarmUpAndAllocate()
+        _check(lib().sift_hip_replay_stage(self._h, dump_dir.encode(), stage.encode(), out_dir.encode()),
+               f"replayStage({stage})")
+        self._refresh()
 
     # --- stage timing (roofline) ---------------------------------------------
     def set_timing(self, enable, blur_reps: int = 1) -> None:

@@ -53,6 +53,11 @@ public:
     // input, every Gaussian plane, candidates, keypoints, descriptors);
     // tests/stage_check.py replays them.  An empty path switches it off.
     void setDataGen(const std::string& path);
+    // tool/perf.cu:43-100 (HostInterface.hh:11-69 run<Stage>): one stage --
+    // "pyramid", "extrema", "refine", "orientation", "order", "descriptor" --
+    // alone on a setDataGen dump's recorded input; its outputs go to out_dir
+    // in the dump's formats (sift_hip_replay_stage).  Discards the current results.
+    void replayStage(const std::string& dump_dir, const std::string& stage, const std::string& out_dir);
 
     int numOctaves() const { return m_nOctaves; }
     sift_hip_detector* handle() const { return m_handle; }

@@ -172,10 +172,26 @@ int sift_hip_copy_descriptors_device(sift_hip_t h, uint16_t* dst, int cap, void*
  * detect completes synchronously and writes this build's stage dumps of the
  * frame into dir (overwritten per frame; dir is created): meta.json (config,
  * octave geometry, counts, file layouts), input.f32, gauss_o<o>_l<l>.f32 (every
- * Gaussian plane), candidates.i32, kpts3.f32, feats4.f32, desc.f16 -- raw
- * little-endian row-major arrays.  tests/stage_check.py replays a dump against
+ * Gaussian plane), candidates.i32, kpts3.f32, feats4.f32, desc.f16, and the
+ * keypoint stages' device records refined.rec, oriented.rec, jobs.rec,
+ * range.u32, counters.u32 -- raw little-endian arrays.  tests/stage_check.py replays a dump against
  * the CPU oracle and this library.  NULL or "" switches the dumps off. */
 int sift_hip_set_datagen(sift_hip_t h, const char* dir);
+
+/* Per-stage replay (the reference's tool/perf.cu:43-100, which runs each
+ * HostInterface.hh:11-69 stage -- runFilter ... runDescriptor -- alone on a
+ * setDataGen snapshot): runs ONE stage of the pipeline on the inputs recorded
+ * in a sift_hip_set_datagen dump directory and writes that stage's outputs,
+ * with the dump's file names and formats, into out_dir.  Stages and files:
+ *   "pyramid"     input.f32                          -> gauss_o<o>_l<l>.f32
+ *   "extrema"     gauss planes                       -> candidates.i32
+ *   "refine"      planes, candidates.i32             -> refined.rec
+ *   "orientation" planes, refined.rec                -> oriented.rec
+ *   "order"       planes, oriented.rec, counters.u32 -> kpts3.f32, feats4.f32, jobs.rec
+ *   "descriptor"  planes, jobs.rec, range.u32        -> desc.f16
+ * The dump must come from a handle of the same configuration.  Synchronous;
+ * the handle's current results are discarded (it is left as after warm-up). */
+int sift_hip_replay_stage(sift_hip_t h, const char* dump_dir, const char* stage, const char* out_dir);
 
 /* Stage timing for roofline reporting: when enabled, the next detect calls run
  * un-graphed with HIP events around every kernel; names are stable strings.

@@ -16,6 +16,27 @@
  *     restated here; cos/sin/pow go through double and round once to float.
  * Known, documented differences from a real OpenCV build are listed in DESIGN.md
  * ("Oracle: what is pinned and what is not").
+ *
+ * Build variants (the OpenCV-tolerance ensemble; built by
+ * oracle/Makefile into separate libraries, selected in tests/oracle_binding.py):
+ *   SIFT_ORACLE_VEC = 0   the pinned restatement above: every stage in the
+ *                         formulas of OpenCV's SIMD bodies (the HIP path
+ *                         reproduces this build bit for bit);
+ *                   = 8   the AVX2 dispatch of sift.simd.hpp / core: SIMD loops
+ *                         of 8 lanes with their scalar tails (orientation
+ *                         histogram tail, smoothing of bins 32..35, in-place
+ *                         tails of the hal calls), v_reduce_sum of v_float32x8
+ *                         by two hadds, the descriptor's scalar clipped norm;
+ *                   = 16  the AVX-512 (AVX512_SKX) dispatch: 16 lanes, the
+ *                         512-bit v_reduce_sum;
+ *   SIFT_ORACLE_CONTRACT = 1  GCC's default -ffp-contract=fast applied to
+ *                         exactly the functions OpenCV compiles in the
+ *                         FMA-enabled dispatch TU sift.simd.hpp
+ *                         (adjustLocalExtrema with the inlined Matx33f Cramer
+ *                         solve, calcOrientationHist, the peak interpolation of
+ *                         findScaleSpaceExtremaT, calcSIFTDescriptor), and to
+ *                         the scalar tails of the core hal calls; everything in
+ *                         sift.dispatch.cpp / imgproc keeps its unfused form.
  */
 #include "sift_oracle.h"
 
@@ -27,6 +48,23 @@
 #include <vector>
 #ifdef _OPENMP
 #include <omp.h>
+#endif
+
+#ifndef SIFT_ORACLE_VEC
+#define SIFT_ORACLE_VEC 0
+#endif
+#ifndef SIFT_ORACLE_CONTRACT
+#define SIFT_ORACLE_CONTRACT 0
+#endif
+#if SIFT_ORACLE_VEC != 0 && SIFT_ORACLE_VEC != 8 && SIFT_ORACLE_VEC != 16
+#error "SIFT_ORACLE_VEC must be 0, 8 or 16"
+#endif
+// Contracted builds keep the hal helpers out of line so the caller's
+// contraction setting never reaches their bodies (core's own SIMD formulas).
+#if SIFT_ORACLE_CONTRACT
+#define ORACLE_HAL __attribute__((noinline))
+#else
+#define ORACLE_HAL inline
 #endif
 
 namespace {
@@ -218,7 +256,9 @@ const ExpTables& expTables() {
 }
 
 // [OpenCV 4.x hal::exp32f] SIMD body (v_round, v_fma) applied to every element.
-float cvExp32f(float x) {
+// (Its scalar tail, ((x0 + A1)*x0 + A2)*x0 ..., contracted by an FMA build,
+// gives the same bits, so every variant uses this form.)
+ORACLE_HAL float cvExp32f(float x) {
     const ExpTables& T = expTables();
     x = std::min(std::max(x, T.minval), T.maxval);
     x = x * T.prescale;
@@ -239,7 +279,7 @@ float cvExp32f(float x) {
 }
 
 // [OpenCV 4.x hal::fastAtan2 / v_atan_f32::compute], degrees.
-float cvFastAtan2(float y, float x) {
+ORACLE_HAL float cvFastAtan2(float y, float x) {
     static const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
     static const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
     static const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
@@ -255,7 +295,62 @@ float cvFastAtan2(float y, float x) {
 }
 
 // [OpenCV 4.x hal::magnitude32f] SIMD body: sqrt(fma(x, x, y*y)).
-inline float cvMagnitude(float x, float y) { return std::sqrt(fmaf(x, x, y * y)); }
+ORACLE_HAL float cvMagnitude(float x, float y) { return std::sqrt(fmaf(x, x, y * y)); }
+
+#if SIFT_ORACLE_VEC
+#if SIFT_ORACLE_CONTRACT
+#pragma GCC push_options
+#pragma GCC optimize("fp-contract=fast")
+#endif
+// [OpenCV 4.x core mathfuncs_core.simd.hpp: atan_f32] -- the scalar loop
+// fastAtan32f runs when a call has fewer than 2 vectors of elements (the SIMD
+// loop re-processes an overlapped last block otherwise).  Written as OpenCV
+// writes it: a contracting build fuses `90.f - poly*c` into one fma, which the
+// SIMD body (a = poly*c; 90 - a) does not.
+__attribute__((noinline)) float cvFastAtan2Scalar(float y, float x) {
+    static const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
+    static const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
+    static const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
+    static const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
+    float ax = std::fabs(x), ay = std::fabs(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+#if SIFT_ORACLE_CONTRACT
+#pragma GCC pop_options
+#endif
+
+// hal::fastAtan2 over an array of n elements: SIMD body for n >= 2 vectors.
+void cvFastAtan2Array(const float* Y, const float* X, float* ori, int n) {
+    const bool simd = n >= 2 * SIFT_ORACLE_VEC;
+    for (int k = 0; k < n; k++) ori[k] = simd ? cvFastAtan2(Y[k], X[k]) : cvFastAtan2Scalar(Y[k], X[k]);
+}
+
+// v_reduce_sum(v_float32) of the dispatch width.
+float reduceSum(const float* a) {
+#if SIFT_ORACLE_VEC == 8
+    // intrin_avx.hpp: two _mm256_hadd_ps, then low + high 128-bit halves.
+    return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+#else
+    // intrin_avx512.hpp: 256-bit halves added, 128-bit halves added, two hadds.
+    float h[8], q[4];
+    for (int i = 0; i < 8; i++) h[i] = a[i] + a[i + 8];
+    for (int i = 0; i < 4; i++) q[i] = h[i] + h[i + 4];
+    return (q[0] + q[1]) + (q[2] + q[3]);
+#endif
+}
+#endif  // SIFT_ORACLE_VEC
 
 inline float pow2f(float t) { return (float)std::exp2((double)t); }
 
@@ -388,6 +483,12 @@ public:
         return (int)std::floor(0.5 * P_.contrastThreshold / P_.L * 255 * SIFT_FIXPT_SCALE);
     }
 
+    // ---- sift.simd.hpp: compiled in OpenCV's FMA-enabled dispatch TU (variants:
+    // contracted like GCC's default -ffp-contract=fast, see the header) ----
+#if SIFT_ORACLE_CONTRACT
+#pragma GCC push_options
+#pragma GCC optimize("fp-contract=fast")
+#endif
     // [OpenCV 4.x sift.simd.hpp: adjustLocalExtrema] with Matx33f::solve(DECOMP_LU)
     // = Matx_FastSolveOp<float,3,1> (Cramer's rule, det via Matx_DetOp<float,3>).
     // Reference: SiftOps.cu:6-208 (Gaussian elimination, no sub-pixel offset in the
@@ -491,6 +592,62 @@ public:
         float expf_scale = -1.f / (2.f * sigma * sigma);
         float temp[SIFT_ORI_HIST_BINS + 4] = {0};
         float* temphist = temp + 2;
+#if SIFT_ORACLE_VEC
+        // OpenCV's structure: gather X, Y, W over the window, hal::exp32f (in
+        // place), hal::fastAtan2, hal::magnitude32f (Mag = X, in place), then
+        // the histogram: SIMD blocks add the rounded w*mag, the scalar tail
+        // (len % VEC samples) does temphist[bin] += W[k]*Mag[k] (one fma in a
+        // contracting build).
+        const int maxlen = (2 * radius + 1) * (2 * radius + 1);
+        std::vector<float> X(maxlen), Y(maxlen), W(maxlen), Ori(maxlen);
+        int len = 0;
+        for (int i = -radius; i <= radius; i++) {
+            int y = py + i;
+            if (y <= 0 || y >= img.h - 1) continue;
+            for (int j = -radius; j <= radius; j++) {
+                int x = px + j;
+                if (x <= 0 || x >= img.w - 1) continue;
+                X[len] = img.at(y, x + 1) - img.at(y, x - 1);
+                Y[len] = img.at(y - 1, x) - img.at(y + 1, x);
+                W[len] = (float)(i * i + j * j) * expf_scale;
+                len++;
+            }
+        }
+        for (int k = 0; k < len; k++) W[k] = cvExp32f(W[k]);
+        cvFastAtan2Array(Y.data(), X.data(), Ori.data(), len);
+        for (int k = 0; k < len; k++) X[k] = cvMagnitude(X[k], Y[k]);
+        const float* Mag = X.data();
+        const int simd_end = len - len % SIFT_ORACLE_VEC;
+        int k = 0;
+        for (; k < simd_end; k++) {
+            int bin = cvRoundF((n / 360.f) * Ori[k]);
+            if (bin >= n) bin -= n;
+            if (bin < 0) bin += n;
+            volatile float wm = W[k] * Mag[k];  // v_mul: rounded before the add
+            temphist[bin] += wm;
+        }
+        for (; k < len; k++) {
+            int bin = cvRoundF((n / 360.f) * Ori[k]);
+            if (bin >= n) bin -= n;
+            if (bin < 0) bin += n;
+            temphist[bin] += W[k] * Mag[k];
+        }
+        temphist[-1] = temphist[n - 1];
+        temphist[-2] = temphist[n - 2];
+        temphist[n] = temphist[0];
+        temphist[n + 1] = temphist[1];
+        int i = 0;
+        for (; i <= n - SIFT_ORACLE_VEC; i += SIFT_ORACLE_VEC)  // v_fma body
+            for (int v = i; v < i + SIFT_ORACLE_VEC; v++)
+                hist[v] = fmaf(temphist[v - 2] + temphist[v + 2], 1.f / 16.f,
+                               fmaf(temphist[v - 1] + temphist[v + 1], 4.f / 16.f, temphist[v] * (6.f / 16.f)));
+        for (; i < n; i++)  // scalar tail (bins 32..35), as OpenCV writes it
+            hist[i] = (temphist[i - 2] + temphist[i + 2]) * (1.f / 16.f) +
+                      (temphist[i - 1] + temphist[i + 1]) * (4.f / 16.f) + temphist[i] * (6.f / 16.f);
+        float vmax = hist[0];
+        for (int b = 1; b < n; b++) vmax = std::max(vmax, hist[b]);
+        return vmax;
+#endif
         for (int i = -radius; i <= radius; i++) {
             int y = py + i;
             if (y <= 0 || y >= img.h - 1) continue;
@@ -581,6 +738,64 @@ public:
         sin_t /= hist_width;
         const int rows = img.h, cols = img.w;
         float hist[(SIFT_DESCR_WIDTH + 2) * (SIFT_DESCR_WIDTH + 2) * (SIFT_DESCR_HIST_BINS + 2)] = {0};
+#if SIFT_ORACLE_VEC
+        // OpenCV's structure: gather the window's samples (rotated bins, X, Y and
+        // the Gaussian weight argument) in scalar code, then hal::exp32f (in
+        // place), hal::fastAtan2, hal::magnitude32f (Mag = Y, in place), then the
+        // trilinear accumulation (its SIMD body and scalar tail give the same
+        // bits: every product there has a second use, so nothing contracts).
+        const int maxlen = (2 * radius + 1) * (2 * radius + 1);
+        std::vector<float> X(maxlen), Y(maxlen), W(maxlen), RB(maxlen), CB(maxlen), Ori(maxlen);
+        int len = 0;
+        for (int i = -radius; i <= radius; i++)
+            for (int j = -radius; j <= radius; j++) {
+                float c_rot = j * cos_t - i * sin_t;
+                float r_rot = j * sin_t + i * cos_t;
+                float rbin = r_rot + d / 2 - 0.5f;
+                float cbin = c_rot + d / 2 - 0.5f;
+                int r = pty + i, c = ptx + j;
+                if (rbin > -1 && rbin < d && cbin > -1 && cbin < d && r > 0 && r < rows - 1 && c > 0 &&
+                    c < cols - 1) {
+                    X[len] = img.at(r, c + 1) - img.at(r, c - 1);
+                    Y[len] = img.at(r - 1, c) - img.at(r + 1, c);
+                    RB[len] = rbin;
+                    CB[len] = cbin;
+                    W[len] = (c_rot * c_rot + r_rot * r_rot) * exp_scale;
+                    len++;
+                }
+            }
+        for (int k = 0; k < len; k++) W[k] = cvExp32f(W[k]);
+        cvFastAtan2Array(Y.data(), X.data(), Ori.data(), len);
+        for (int k = 0; k < len; k++) Y[k] = cvMagnitude(X[k], Y[k]);
+        for (int k = 0; k < len; k++) {
+            float rbin = RB[k], cbin = CB[k];
+            float obin = (Ori[k] - ori) * bins_per_rad;
+            float mag = Y[k] * W[k];
+            int r0 = cvFloorF(rbin), c0 = cvFloorF(cbin), o0 = cvFloorF(obin);
+            rbin -= (float)r0;
+            cbin -= (float)c0;
+            obin -= (float)o0;
+            if (o0 < 0) o0 += n;
+            if (o0 >= n) o0 -= n;
+            float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+            float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
+            float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+            float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
+            float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
+            float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
+            float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
+            int idx = ((r0 + 1) * (d + 2) + c0 + 1) * (n + 2) + o0;
+            hist[idx] += v_rco000;
+            hist[idx + 1] += v_rco001;
+            hist[idx + (n + 2)] += v_rco010;
+            hist[idx + (n + 3)] += v_rco011;
+            hist[idx + (d + 2) * (n + 2)] += v_rco100;
+            hist[idx + (d + 2) * (n + 2) + 1] += v_rco101;
+            hist[idx + (d + 3) * (n + 2)] += v_rco110;
+            hist[idx + (d + 3) * (n + 2) + 1] += v_rco111;
+        }
+        if (false)
+#endif
         for (int i = -radius; i <= radius; i++)
             for (int j = -radius; j <= radius; j++) {
                 float c_rot = (float)j * cos_t - (float)i * sin_t;
@@ -629,11 +844,18 @@ public:
                 hist[idx + 1] += hist[idx + n + 1];
                 for (int k = 0; k < n; k++) raw[(i * d + j) * n + k] = hist[idx + k];
             }
+#if SIFT_ORACLE_VEC
+        // Norm: VEC fma lanes, v_reduce_sum of the dispatch width.
+        float acc[SIFT_ORACLE_VEC] = {0};
+        for (int k = 0; k < 128; k++) acc[k % SIFT_ORACLE_VEC] = fmaf(raw[k], raw[k], acc[k % SIFT_ORACLE_VEC]);
+        float nrm2 = reduceSum(acc);
+#else
         // Norm: 8 fma lanes (AVX2 v_float32), reduced as v_reduce_sum.
         float acc[8] = {0};
         for (int k = 0; k < 128; k++) acc[k & 7] = fmaf(raw[k], raw[k], acc[k & 7]);
         float t0 = acc[0] + acc[4], t1 = acc[1] + acc[5], t2 = acc[2] + acc[6], t3 = acc[3] + acc[7];
         float nrm2 = (t0 + t2) + (t1 + t3);
+#endif
         float thr = std::sqrt(nrm2) * SIFT_DESCR_MAG_THR;
         nrm2 = 0;
         for (int k = 0; k < 128; k++) {
@@ -647,6 +869,11 @@ public:
             dst[k] = (float)std::min(std::max(v, 0), 255);
         }
     }
+
+#if SIFT_ORACLE_CONTRACT
+#pragma GCC pop_options
+#endif
+    // ---- end of sift.simd.hpp ----
 
     // [OpenCV 4.x sift.dispatch.cpp: calcDescriptorsComputer]
     void descriptors(const std::vector<Plane>& gpyr, const std::vector<Keypoint>& kpts, float* desc) const {
@@ -739,6 +966,16 @@ Plane toPlane(const float* img, int w, int h) {
 }  // namespace
 
 extern "C" {
+
+const char* sift_oracle_variant(void) {
+#if SIFT_ORACLE_VEC == 0
+    return SIFT_ORACLE_CONTRACT ? "simd-formulas+contract" : "pinned";
+#elif SIFT_ORACLE_VEC == 8
+    return SIFT_ORACLE_CONTRACT ? "avx2-fma" : "avx2";
+#else
+    return SIFT_ORACLE_CONTRACT ? "avx512-fma" : "avx512";
+#endif
+}
 
 void sift_oracle_default_params(sift_oracle_params* p) {
     p->nfeatures = 0;

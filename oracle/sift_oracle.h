@@ -44,6 +44,11 @@ typedef struct {
 
 void sift_oracle_default_params(sift_oracle_params* p);
 
+/* Which build of the restatement this library is (oracle/Makefile):
+ * "pinned" (the parity pin of the HIP path), "avx2-fma", "avx512-fma" (the
+ * OpenCV-tolerance ensemble). */
+const char* sift_oracle_variant(void);
+
 /* Gaussian taps exactly as cv::getGaussianKernel(cvRound(8*sigma+1)|1, sigma, CV_32F).
  * Returns the tap count (odd) or -1 if cap is too small. */
 int sift_oracle_gaussian_taps(double sigma, float* taps, int cap);

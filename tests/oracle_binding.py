@@ -15,6 +15,14 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
 ORACLE_LIB = os.path.join(ORACLE_DIR, "_build", "libsift_oracle.so")
+# Builds of the same restatement (oracle/Makefile): "pinned" is the parity pin
+# of the HIP path; the others model OpenCV's AVX2 / AVX-512 dispatch as GCC
+# compiles it (the ensemble the stated OpenCV tolerance comes from).
+VARIANTS = {
+    "pinned": ORACLE_LIB,
+    "avx2-fma": os.path.join(ORACLE_DIR, "_build", "libsift_oracle_avx2fma.so"),
+    "avx512-fma": os.path.join(ORACLE_DIR, "_build", "libsift_oracle_avx512fma.so"),
+}
 
 
 class Params(ctypes.Structure):
@@ -42,15 +50,15 @@ class Kpt(ctypes.Structure):
 
 KPT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"), ("octave", "<i4")])
 
-_lib = None
+_libs = {}
 
 
-def lib() -> ctypes.CDLL:
-    global _lib
-    if _lib is None:
-        if not os.path.exists(ORACLE_LIB):
+def lib(variant: str = "pinned") -> ctypes.CDLL:
+    if variant not in _libs:
+        path = VARIANTS[variant]
+        if not os.path.exists(path):
             subprocess.run(["make", "-C", ORACLE_DIR], check=True, capture_output=True)
-        L = ctypes.CDLL(ORACLE_LIB)
+        L = ctypes.CDLL(path)
         vp, i, l, d = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_double
         P = ctypes.POINTER(Params)
         L.sift_oracle_default_params.argtypes = [P]
@@ -67,8 +75,12 @@ def lib() -> ctypes.CDLL:
         L.sift_oracle_detect_and_compute.restype = l
         L.sift_oracle_compute_descriptors.argtypes = [vp, i, i, P, vp, l, vp]
         L.sift_oracle_knn2.argtypes = [vp, l, vp, l, i, vp, vp]
-        _lib = L
-    return _lib
+        L.sift_oracle_variant.restype = ctypes.c_char_p
+        got = L.sift_oracle_variant().decode()
+        if got != variant:
+            raise RuntimeError(f"{path} is the {got!r} build, expected {variant!r}")
+        _libs[variant] = L
+    return _libs[variant]
 
 
 def params(nfeatures=0, nOctaveLayers=3, contrastThreshold=0.04, edgeThreshold=10.0, sigma=1.6, firstOctave=-1, nOctaves=0) -> Params:
@@ -118,22 +130,23 @@ def gaussian_pyramid(img: np.ndarray, p: Params):
     return out
 
 
-def extrema(img: np.ndarray, p: Params) -> np.ndarray:
+def extrema(img: np.ndarray, p: Params, variant: str = "pinned") -> np.ndarray:
     img = np.ascontiguousarray(img, np.float32)
     h, w = img.shape
-    n = lib().sift_oracle_extrema(img.ctypes.data, w, h, ctypes.byref(p), None, 0)
+    n = lib(variant).sift_oracle_extrema(img.ctypes.data, w, h, ctypes.byref(p), None, 0)
     q = np.zeros((max(n, 1), 4), np.int32)
-    lib().sift_oracle_extrema(img.ctypes.data, w, h, ctypes.byref(p), q.ctypes.data, n)
+    lib(variant).sift_oracle_extrema(img.ctypes.data, w, h, ctypes.byref(p), q.ctypes.data, n)
     return q[:n]
 
 
-def detect_and_compute(img: np.ndarray, p: Params, threads: int = 0, cap: int = 1 << 20):
+def detect_and_compute(img: np.ndarray, p: Params, threads: int = 0, cap: int = 1 << 20, variant: str = "pinned"):
     """(keypoints structured array, descriptors float32 (n,128) of 0..255 integers)."""
     img = np.ascontiguousarray(img, np.float32)
     h, w = img.shape
     kp = np.zeros(cap, KPT_DTYPE)
     desc = np.zeros((cap, 128), np.float32)
-    n = lib().sift_oracle_detect_and_compute(img.ctypes.data, w, h, ctypes.byref(p), threads, kp.ctypes.data, desc.ctypes.data, cap)
+    n = lib(variant).sift_oracle_detect_and_compute(img.ctypes.data, w, h, ctypes.byref(p), threads, kp.ctypes.data,
+                                                    desc.ctypes.data, cap)
     n = min(n, cap)
     return kp[:n].copy(), desc[:n].copy()
 

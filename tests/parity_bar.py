@@ -1,14 +1,24 @@
-"""The descriptor parity bar shared by every GPU test that compares descriptors
-with the CPU oracle.
+"""The parity bars shared by the GPU tests.
 
-Keypoints (position, size, angle, response, packed octave) are bit-exact; a
-descriptor entry may differ from the oracle's by at most 1.  The 4x4x8
-histogram is summed here in exact fixed point (order independent) while
-OpenCV sums the same float contributions sequentially, so an entry whose
-value x 512 / |v| lands within the float summation error of a .5 boundary
-rounds the other way.  Measured on the GPU: up to 0.15 % of the entries of a
-configuration (gpurun_out/descriptor_exact.txt on the box), so the bar is
-99.8 % exact: a regression that doubles the flip rate fails it.
+1. Against the pinned oracle (the regression pin).  Keypoints (position, size,
+   angle, response, packed octave) are bit-exact; a descriptor entry may
+   differ from the oracle's by at most 1.  The 4x4x8 histogram is summed here
+   in exact fixed point (order independent) while OpenCV sums the same float
+   contributions sequentially, so an entry whose value x 512 / |v| lands
+   within the float summation error of a .5 boundary rounds the other way.
+   Measured: 0.12 % of the entries over the 200-frame sweep, worst frame
+   0.193 % (99.807 % exact, profiles/round2/parity_sweep.json), fixtures
+   0.03-0.17 % (profiles/round3/descriptor_exact_a1.txt).  The bar, 99.8 %,
+   sits 0.007 points under that worst frame: deterministic (same inputs, same
+   flips), but a new resolution can land on it, so a failure here means "look
+   at the flip log", not "loosen the bar".
+
+2. Against OpenCV (the stated fp32 tolerance).  OpenCV
+   itself is not in this image; its build-to-build spread is modelled by the
+   oracle ensemble (oracle/Makefile: pinned, avx2-fma, avx512-fma) and
+   measured over 200 frames by tools/oracle_ensemble.py
+   (profiles/round3/oracle_ensemble.json).  OPENCV_TOL is that envelope with
+   headroom; the HIP path must sit inside it against EVERY ensemble member.
 """
 import os
 
@@ -16,6 +26,33 @@ import numpy as np
 
 DESC_MAX_ABS_DIFF = 1.0
 DESC_EXACT_MIN = 0.998
+
+# Stated tolerance of "equal to OpenCV SIFT" (per frame).  Integer outputs --
+# the 3x3x3 candidate set and the refined grid index (octave, layer, r, c) of
+# every paired keypoint -- are exact; unpaired keypoints (a peak or a
+# threshold decision flipping between builds) are counted.
+OPENCV_TOL = {
+    "max_dx": 2e-3,              # px, original image
+    "max_dy": 2e-3,
+    "max_dsize_rel": 1e-4,
+    "max_dangle": 1e-2,          # degrees
+    "max_dresponse_rel": 1e-4,
+    "max_unpaired_frac": 2e-3,   # keypoints without a partner, per frame
+    "grid_index_mismatch": 0,
+    "desc_max_abs": 1.0,
+}
+OPENCV_DESC_EXACT_MIN = DESC_EXACT_MIN
+
+
+def assert_opencv_tolerance(row, tag=""):
+    """row: tests/ensemble.py compare() (or merge()) output of one frame."""
+    assert max(row["unpaired_a"], row["unpaired_b"]) <= OPENCV_TOL["max_unpaired_frac"] * max(1, min(row["n_a"], row["n_b"])) + 1, (tag, row)
+    for k in ("max_dx", "max_dy", "max_dsize_rel", "max_dangle", "max_dresponse_rel", "desc_max_abs"):
+        assert row.get(k, 0.0) <= OPENCV_TOL[k], (tag, k, row.get(k), OPENCV_TOL[k])
+    assert row.get("grid_index_mismatch", 0) <= OPENCV_TOL["grid_index_mismatch"], (tag, row)
+    if row.get("desc_entries"):
+        exact = 1.0 - row["desc_flips"] / row["desc_entries"]
+        assert exact >= OPENCV_DESC_EXACT_MIN, (tag, exact)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 

@@ -6,16 +6,24 @@ sift_cuda/perf/PerfData.cuh:12-155) and tool/perf.cu:16-113 re-runs each
 stage on them, comparing with HostInterface.cu's rules (exact floats for
 blur / resize / DoG / peaks / refine / orientation, |diff| <= 1 for
 descriptors).  This build's dump is the whole frame (meta.json + raw arrays,
-layouts in meta.json); this checker replays it two ways:
+layouts in meta.json) plus the keypoint stages' device records; this checker
+replays it three ways:
 
   * against the CPU oracle (test infrastructure): every Gaussian plane
     bit-exact, the 3x3x3 candidate set exact, keypoints bit-exact, descriptors
     within the parity bar (parity_bar.py);
-  * against this library (--gpu): the dumped input through a fresh detector
-    gives the dumped planes, keypoints and descriptors bit for bit (a kernel
-    regression check across builds or boxes).
+  * against this library, whole frame (--gpu): the dumped input through a
+    fresh detector gives the dumped planes, keypoints and descriptors bit for
+    bit (a kernel regression check across builds or boxes);
+  * against this library, ONE stage at a time (--stage S|all; S in
+    pyramid, extrema, refine, orientation, order, descriptor): the stage's
+    kernels alone on the dump's recorded input of that stage
+    (sift_hip_replay_stage, as tool/perf.cu:43-100 runs HostInterface's
+    run<Stage>), their output equal to the dump's -- bit for bit, as sets
+    where the device appends with atomics (candidates, refined and oriented
+    records).
 
-    python tests/stage_check.py DIR [--gpu]      (exit status 1 on a mismatch)
+    python tests/stage_check.py DIR [--gpu] [--stage S|all]   (exit status 1 on a mismatch)
 """
 import json
 import os
@@ -39,6 +47,59 @@ def load(dirname):
     d["feats4"] = rd("feats4.f32", np.float32).reshape(-1, 4)
     d["desc"] = rd("desc.f16", np.float16).reshape(-1, 128)
     return d
+
+
+STAGES = ("pyramid", "extrema", "refine", "orientation", "order", "descriptor")
+# Outputs of each stage (the dump's file names) and how they compare:
+# "exact" byte for byte, "rows" as sets of fixed-size records (appended by
+# device atomics in any order).
+STAGE_OUTPUTS = {
+    "pyramid": None,  # every gauss_o<o>_l<l>.f32
+    "extrema": [("candidates.i32", "rows", 16)],
+    "refine": [("refined.rec", "rows", 32)],
+    "orientation": [("oriented.rec", "rows", 32)],
+    "order": [("kpts3.f32", "exact", 0), ("feats4.f32", "exact", 0), ("jobs.rec", "exact", 0)],
+    "descriptor": [("desc.f16", "exact", 0)],
+}
+
+
+def _same_file(a, b, how, rec):
+    x, y = np.fromfile(a, np.uint8), np.fromfile(b, np.uint8)
+    if how == "exact" or x.size != y.size:
+        return x.size == y.size and bool(np.array_equal(x, y))
+    xr, yr = x.view(np.uint32).reshape(-1, rec // 4), y.view(np.uint32).reshape(-1, rec // 4)
+    return bool(np.array_equal(xr[np.lexsort(xr.T[::-1])], yr[np.lexsort(yr.T[::-1])]))
+
+
+def check_stages(dirname, stages=STAGES, det=None, out_root=None):
+    """Each stage's kernels alone on the dump's recorded input
+    (Detector.replayStage); {stage: True} where the outputs equal the dump's."""
+    import tempfile
+
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "another-cuda-sift_amd"))
+    import sift_amd as sift
+
+    d = load(dirname)
+    m, c = d["meta"], d["meta"]["config"]
+    if det is None:
+        cfg = sift.CudaSiftConfig(col_width=m["width"], row_width=m["height"], numFeatures=c["numFeatures"],
+                                  numOctaveLayers=c["numOctaveLayers"], contrastThreshould=c["contrastThreshould"],
+                                  edgeThreshould=c["edgeThreshould"], sigma=c["sigma"], upscale=bool(c["upscale"]),
+                                  numOctaves=c["numOctaves"])
+        det = sift.Detector(cfg)
+        det.gpuWarmUpAndAllocate()
+    out_root = out_root or tempfile.mkdtemp(prefix="sift_replay_")
+    res = {}
+    for st in stages:
+        out = os.path.join(out_root, st)
+        det.replayStage(dirname, st, out)
+        if STAGE_OUTPUTS[st] is None:
+            names = [f"gauss_o{o}_l{l}.f32" for o in range(len(m["octaves"])) for l in range(m["planes_per_octave"])]
+            res[st] = all(_same_file(os.path.join(dirname, n), os.path.join(out, n), "exact", 0) for n in names)
+        else:
+            res[st] = all(_same_file(os.path.join(dirname, n), os.path.join(out, n), how, rec)
+                          for n, how, rec in STAGE_OUTPUTS[st])
+    return res
 
 
 def _keys(k3, f4):
@@ -115,9 +176,10 @@ def main(argv):
     d = load(argv[1])
     res = {"oracle": check_oracle(d)}
     if "--gpu" in argv:
-        import torch  # noqa: F401  (one HIP runtime per process: torch's, loaded first)
-
         res["gpu_replay"] = check_gpu(d)
+    if "--stage" in argv:
+        st = argv[argv.index("--stage") + 1]
+        res["stage_replay"] = check_stages(argv[1], STAGES if st == "all" else (st,))
     print(json.dumps(res, indent=1))
     ok = all(v for part in res.values() for k, v in part.items() if isinstance(v, bool))
     return 0 if ok else 1

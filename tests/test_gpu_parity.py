@@ -108,6 +108,42 @@ def test_keypoints_and_descriptors(sift, oracle, w, h, upscale, nOct, nfeat, fra
     assert gd.min() >= 0 and gd.max() <= 255 and np.all(gd == np.round(gd))
 
 
+ENSEMBLE = ["avx2-fma", "avx512-fma"]
+
+
+@pytest.mark.parametrize("w,h,upscale,nOct,nfeat,frame", [c for c in CONFIGS if c[0] * c[1] <= 1920 * 1200])
+def test_opencv_tolerance_vs_ensemble(sift, oracle, w, h, upscale, nOct, nfeat, frame):
+    """The stated OpenCV tolerance (parity_bar.OPENCV_TOL): the
+    HIP result against every build of the oracle ensemble that models
+    OpenCV's AVX2 / AVX-512 dispatch as GCC compiles it (the pinned build is
+    checked bit for bit above)."""
+    import ensemble
+    from parity_bar import assert_opencv_tolerance
+
+    img = sift.synth_frame(frame, w, h)
+    cfg, det = make_detector(sift, w, h, upscale=upscale, numOctaves=nOct, numFeatures=nfeat)
+    det.detectAndCompute(img)
+    gk, gd, _ = gpu_keypoints(det)
+    p = oracle.from_config(cfg)
+    cand = det.debug_candidates()
+    for v in ENSEMBLE:
+        oc = oracle.extrema(img, p, variant=v)
+        assert np.array_equal(cand[np.lexsort(cand.T[::-1])], oc[np.lexsort(oc.T[::-1])]), v
+        vk, vd = oracle.detect_and_compute(img, p, variant=v)
+        row = ensemble.compare(gk, gd, vk, vd)
+        record_tolerance(f"{w}x{h} up={upscale} nOct={nOct} nfeat={nfeat} vs {v}", row)
+        assert_opencv_tolerance(row, (w, h, upscale, v))
+
+
+def record_tolerance(tag, row):
+    out = os.path.join(ROOT, "gpurun_out")
+    if os.path.isdir(out):
+        import json
+
+        with open(os.path.join(out, "opencv_tolerance.jsonl"), "a") as f:
+            f.write(json.dumps({"case": tag, **row}) + "\n")
+
+
 def test_output_order_deterministic(sift):
     w, h = 640, 480
     img = sift.synth_frame(11, w, h)
