@@ -946,6 +946,16 @@ int wait_frame(sift_hip_detector* d, long long f) {
 // Detector.cu:145-229 / PerfData.cuh): raw little-endian row-major files plus a
 // meta.json describing them; tests/stage_check.py replays them against the CPU
 // oracle (and against this library).
+// mkdir -p
+bool make_dirs(const std::string& path) {
+    for (size_t i = 1; i <= path.size(); i++)
+        if (i == path.size() || path[i] == '/') {
+            const std::string p = path.substr(0, i);
+            if (mkdir(p.c_str(), 0755) != 0 && errno != EEXIST) return false;
+        }
+    return true;
+}
+
 int write_file(const std::string& path, const void* data, size_t bytes) {
     FILE* fp = fopen(path.c_str(), "wb");
     if (!fp) return fail(SIFT_HIP_ERR_INVALID, "cannot write " + path);
@@ -996,7 +1006,7 @@ int dump_records(sift_hip_detector* d, const std::string& dir) {
 
 int dump_stage_files(sift_hip_detector* d) {
     const std::string& dir = d->dgDir;
-    if (mkdir(dir.c_str(), 0755) != 0 && errno != EEXIST) return fail(SIFT_HIP_ERR_INVALID, "cannot create " + dir);
+    if (!make_dirs(dir)) return fail(SIFT_HIP_ERR_INVALID, "cannot create " + dir);
     const int W = d->cfg.col_width, H = d->cfg.row_width;
     std::vector<float> buf((size_t)W * H);
     HIPCHK(hipMemcpy(buf.data(), d->dDg, sizeof(float) * buf.size(), hipMemcpyDeviceToHost));
@@ -1143,7 +1153,7 @@ int replay_stage(sift_hip_detector* d, const std::string& in, const std::string&
     bool known = false;
     for (const char* k : kStages) known |= stage == k;
     if (!known) return fail(SIFT_HIP_ERR_INVALID, "unknown stage '" + stage + "'");
-    if (mkdir(out.c_str(), 0755) != 0 && errno != EEXIST) return fail(SIFT_HIP_ERR_INVALID, "cannot create " + out);
+    if (!make_dirs(out)) return fail(SIFT_HIP_ERR_INVALID, "cannot create " + out);
     HIPCHK(hipStreamSynchronize(d->stream));
     const bool timing = d->timing;
     d->timing = false;
