@@ -191,10 +191,6 @@ struct JobWords {
     u32x4 w[4];
 };
 
-#ifdef SIFT_DESC_STAMPS
-__device__ unsigned long long g_desc_stamps[8];
-#endif
-
 // kDT threads per keypoint: 4 waves for a single frame (few keypoints, the
 // chip needs the parallelism inside each), 2 waves for frame batches (more
 // keypoints in flight per CU: 296 vs 311 us per 8-frame launch, tools/ab_*).
@@ -257,29 +253,13 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
     // (octave, layer, row) order and their cost grows with scale, so handing
     // each XCD a contiguous run (L2 locality) unbalances the XCDs -- measured
     // 10-30 % slower frames.
-#ifndef SIFT_DESC_VARIANT
-#define SIFT_DESC_VARIANT 0
-#endif
-    unsigned sink = 0;  // timing variant 2 only
     // Jobs are prefetched one keypoint ahead as vector loads (lanes 0-15, one
     // dword each) and moved to SGPRs with v_readlane: a scalar load at the
     // top of each keypoint would expose a memory latency per keypoint, and a
     // scalar prefetch would be waited for by the body's first lgkmcnt(0).
     const unsigned* __restrict__ jw = reinterpret_cast<const unsigned*>(jobs);
     unsigned jnext = n ? jw[min(wg, n - 1) * 16u + (lane & 15)] : 0u;
-#ifdef SIFT_DESC_STAMPS  // in-kernel phase timing (tools only): s_memtime deltas per phase, summed
-    unsigned long long st_acc[4] = {0, 0, 0, 0}, st_prev = __builtin_amdgcn_s_memtime();
-#define SIFT_STAMP(ph)                                              \
-    do {                                                            \
-        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-        st_acc[ph] += t_ - st_prev;                                 \
-        st_prev = t_;                                               \
-    } while (0)
-#else
-#define SIFT_STAMP(ph) (void)0
-#endif
     for (unsigned p = wg; p < n; p += nwg) {
-        SIFT_STAMP(0);
         const unsigned jcur = jnext;
         jnext = jw[min(p + nwg, n - 1) * 16u + (lane & 15)];
         JobWords jwd;
@@ -334,9 +314,7 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
         const int S = min(31 - e, 40);
         const float fxs = ldexpf(1.f, S);
         lds_barrier();
-        SIFT_STAMP(1);
 
-        // One sample from its four neighbours (l, r, u, d).
         // One sample from its four neighbours (l, r, u, d).  Branch-free so
         // that the kGroup samples of a group interleave (ILP): a rejected
         // sample keeps in-range bin indices and adds zeros.
@@ -355,20 +333,13 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
             // = r2 * (-log2(e) / 8) with the same single rounding: one multiply.
             const float wgt = __builtin_amdgcn_exp2f((sq[0] + sq[1]) * (-1.44269504088896341f / (kD * kD * 0.5f)));
 #endif
-#if SIFT_DESC_VARIANT == 4  // timing variant: no atan2 / magnitude / exp
-            const float gori = dx * 3.f + dy, gmag = dx + dy * 0.5f;
-            (void)wgt;
-#define SIFT_DESC_WGT 1.f
-#else
             const float gori = desc_atan2(dy, dx);
             const float gmag = desc_magnitude(dx, dy);
-#define SIFT_DESC_WGT wgt
-#endif
             float obin = (gori - jb.angle) * bins_per_rad;
             // x 2^S (exact): the trilinear parts come out in fixed-point units.
             // A select, not a branch around the product (every operand is
             // finite: enumerated samples are in-image).
-            const float mag = (gmag * SIFT_DESC_WGT * fxs) * (valid ? 1.f : 0.f);
+            const float mag = (gmag * wgt * fxs) * (valid ? 1.f : 0.f);
             // cvFloor in the float domain (the clamp only guards rejected
             // samples): r - floor(r) is the oracle's r - (float)cvFloor(r).
             const float r0f = fminf(fmaxf(floorf(rbin), -1.f), (float)(kD - 1));
@@ -396,12 +367,8 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
                 const int off = (q & 4 ? (kD + 2) * kCellW : 0) + (q & 2 ? kCellW : 0);
                 const unsigned lo = (unsigned)v[q];  // truncation: < 2^-S per contribution
                 const unsigned hi = (unsigned)v[q + 1];
-#if SIFT_DESC_VARIANT == 2  // timing variant: no LDS atomics
-                sink += lo ^ hi ^ (unsigned)(uintptr_t)(hb + off);
-#else
                 atomicAdd(reinterpret_cast<unsigned long long*>(hb + off),
                           ((unsigned long long)hi << 32) | (unsigned long long)lo);
-#endif
             }
         };
         auto accumulate = [&](int i, int j, bool in, float l, float r, float u, float d) {
@@ -417,10 +384,6 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
 #pragma unroll
             for (int t = 0; t < kGroup; t++) {
                 const unsigned o = (unsigned)((G.pty + gi[t]) * jb.pitch + G.ptx + gj[t]) * 4u;
-#if SIFT_DESC_VARIANT == 3  // timing variant: no gradient loads
-                l[t] = (float)(o & 255); r[t] = (float)((o >> 3) & 255); u[t] = (float)((o >> 5) & 255); d[t] = (float)((o >> 7) & 255);
-                continue;
-#endif
                 l[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o - 4u, 0, 0));
                 r[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o + 4u, 0, 0));
                 u[t] = __builtin_bit_cast(float,
@@ -439,11 +402,7 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
             // of items.  Rows hold only in-image samples (the intervals are
             // clipped to 1 .. cols-2 / rows 1 .. rows-2), so validity is the
             // oracle's bin-range test alone.
-#if SIFT_DESC_VARIANT == 1
-            const int N = 0;
-#else
             const int N = rowpre[side];
-#endif
             const int run = (N + kDT - 1) / kDT;
             const int tq = (tid & ~63) | ((lane * SIFT_DESC_PERM) & 63);  // this thread's run
             const int k0 = min(N, tq * run), k1 = min(N, k0 + run);
@@ -466,11 +425,6 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
                     const unsigned o = (unsigned)((G.pty + i) * jb.pitch + G.ptx + jj) * 4u;
                     // (x-1 .. x+kItem) of the row, (x .. x+kItem-1) of the rows above and below.
                     float row6[kItem + 2], up[kItem], dn[kItem];
-#if SIFT_DESC_VARIANT == 3  // timing variant: no gradient loads (values from the offset)
-                    for (int t = 0; t < kItem + 2; t++) row6[t] = (float)((o >> (2 * t)) & 255);
-                    for (int t = 0; t < kItem; t++) up[t] = (float)((o >> (3 + t)) & 255), dn[t] = (float)((o >> (5 + t)) & 255);
-                    if (false)
-#endif
                     {
                         const f32x4d cm = __builtin_bit_cast(f32x4d, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o - 4u, 0, 0));
                         if constexpr (kItem == 2) {
@@ -526,7 +480,6 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
             }
         }
         lds_barrier();
-        SIFT_STAMP(2);
 
         // Wrap, L2 norm (8 fma lanes, then v_reduce_sum's pairing), 0.2 clip.
         const float inv = ldexpf(1.f, -S);
@@ -547,12 +500,6 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
             val[h] = (float)((double)hv * (double)inv);
             if (tid + kDT * h < 128) sq[t] = val[h];
         }
-#if SIFT_DESC_VARIANT == 5  // timing variant: no normalisation epilogue (wrong results)
-        for (int h = 0; h < kPer; h++)
-            if (tid + kDT * h < 128) desc[(size_t)p * 128 + tid + kDT * h] = (uint16_t)val[h];
-        lds_barrier();
-        continue;
-#endif
         lds_barrier();
         if (tid < 8) {
             float a = 0.f;
@@ -589,25 +536,11 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
             int v = cv_round(val[h] * scale);
             v = v < 0 ? 0 : (v > 255 ? 255 : v);
             const _Float16 hv = (_Float16)(float)v;
-            if (tid + kDT * h < 128) desc[(size_t)p * 128 + tid + kDT * h] = __builtin_bit_cast(uint16_t, hv) + (uint16_t)(sink == 0x12345u);
+            if (tid + kDT * h < 128) desc[(size_t)p * 128 + tid + kDT * h] = __builtin_bit_cast(uint16_t, hv);
         }
         lds_barrier();  // sq / histograms are rewritten by the next keypoint
-        SIFT_STAMP(3);
     }
-#ifdef SIFT_DESC_STAMPS
-    if (tid == 0) {
-        for (int q = 0; q < 4; q++) atomicAdd(&g_desc_stamps[q], st_acc[q]);
-        atomicAdd(&g_desc_stamps[4], (unsigned long long)((n > wg) ? (n - wg + nwg - 1) / nwg : 0));
-        atomicAdd(&g_desc_stamps[5], 1ull);
-    }
-#endif
 }
-
-#ifdef SIFT_DESC_STAMPS
-extern "C" int sift_hip_debug_desc_stamps(unsigned long long* out) {
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_desc_stamps), sizeof(g_desc_stamps));
-}
-#endif
 
 void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned* range_keys, uint16_t* desc,
                        Counters* host_ctr, const KeypointParams& kp, const Frames& fr, hipStream_t s) {

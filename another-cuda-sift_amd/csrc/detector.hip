@@ -76,21 +76,6 @@ Taps gaussian_taps(double sigma) {
 #define SIFT_STR(x) SIFT_XSTR(x)
 const char* build_flags() {
     return ""
-#ifdef SIFT_SKIP_STAGES
-           " SIFT_SKIP_STAGES=" SIFT_SKIP_STAGES
-#endif
-#ifdef SIFT_DESC_VARIANT
-           " SIFT_DESC_VARIANT=" SIFT_STR(SIFT_DESC_VARIANT)
-#endif
-#ifdef SIFT_DESC_STAMPS
-           " SIFT_DESC_STAMPS"
-#endif
-#ifdef SIFT_BLUR_STAMPS
-           " SIFT_BLUR_STAMPS"
-#endif
-#ifdef SIFT_BLUR_COL_UNIQUE
-           " SIFT_BLUR_COL_UNIQUE=" SIFT_STR(SIFT_BLUR_COL_UNIQUE)
-#endif
 #ifdef SIFT_BLUR_TH
            " SIFT_BLUR_TH=" SIFT_STR(SIFT_BLUR_TH)
 #endif
@@ -117,9 +102,6 @@ const char* build_flags() {
 #endif
 #ifdef SIFT_MATCH_FUSED_SINGLE
            " SIFT_MATCH_FUSED_SINGLE=" SIFT_STR(SIFT_MATCH_FUSED_SINGLE)
-#endif
-#if defined(SIFT_MATCH_VARIANT) && SIFT_MATCH_VARIANT
-           " SIFT_MATCH_VARIANT=" SIFT_STR(SIFT_MATCH_VARIANT)
 #endif
 #ifdef SIFT_BLUR_IW112
            " SIFT_BLUR_IW112=" SIFT_STR(SIFT_BLUR_IW112)
@@ -292,9 +274,6 @@ struct sift_hip_detector {
     }
     template <class F>
     void timed(const char* name, double bytes, F&& fn) {
-#ifdef SIFT_SKIP_STAGES  // cost A/B builds only (tools/stage_ab.sh): results are wrong
-        if (strstr(SIFT_SKIP_STAGES, name)) return;
-#endif
         if (!timing) {
             fn();
             return;

@@ -47,9 +47,6 @@
 #include "sift_match.h"
 #include "sift_math.h"
 
-#ifndef SIFT_MATCH_VARIANT
-#define SIFT_MATCH_VARIANT 0  // timing variants (tools A/B builds only): 1 no epilogue, 2 no MFMA, 3 no barrier, 4 no staging
-#endif
 #ifndef SIFT_MATCH_WG_TARGET
 #define SIFT_MATCH_WG_TARGET 512  // workgroups a launch aims for (2 per CU) when choosing train splits
 #endif
@@ -426,9 +423,7 @@ __global__ __launch_bounds__(256, 2) void k_match(MatchBatch batch, int S, int n
         }
         auto step = [&](int tile, auto par) {  // par = (tile - tbeg) & 1
             constexpr int PB = decltype(par)::value;
-#if SIFT_MATCH_VARIANT != 3  // timing variant 3: no per-tile barrier (wrong results)
             lds_barrier();  // tile `tile` is in s_tile[PB]; every wave is done with s_tile[PB ^ 1]
-#endif
             i32x4 a[4], tk[4];
             const int8_t* ta = s_tile[PB] + col * kRowPad + 64 * h;
 #pragma unroll
@@ -436,35 +431,16 @@ __global__ __launch_bounds__(256, 2) void k_match(MatchBatch batch, int S, int n
             // accumulator register i holds train row (i & 3) + 8 (i >> 2) + 4 h
 #pragma unroll
             for (int g = 0; g < 4; g++) tk[g] = *reinterpret_cast<const i32x4*>(s_ntk[PB] + 8 * g + 4 * h);
-#if SIFT_MATCH_VARIANT != 4  // timing variant 4: no tile staging after the first (wrong results)
             if (tile + 1 < tend) {
                 stash(tile + 1, std::integral_constant<int, PB ^ 1>{});
                 if (tile + 3 < tend) fetch(tile + 3, std::integral_constant<int, PB ^ 1>{});
             }
-#endif
             i32x16 acc[2] = {{}, {}};
-#if SIFT_MATCH_VARIANT == 2  // timing variant: no MFMA (wrong results)
-#pragma unroll
-            for (int qb = 0; qb < 2; qb++)
-#pragma unroll
-                for (int i = 0; i < 16; i++) acc[qb][i] = a[i & 3][i >> 2] ^ bq[qb][i & 3][(i >> 2) & 3];
-#else
 #pragma unroll
             for (int qb = 0; qb < 2; qb++)
 #pragma unroll
                 for (int kb = 0; kb < 4; kb++)
                     acc[qb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[kb], bq[qb][kb], acc[qb], 0, 0, 0);
-#endif
-#if SIFT_MATCH_VARIANT == 1  // timing variant: no top-2 epilogue (wrong results)
-#pragma unroll
-            for (int qb = 0; qb < 2; qb++) {
-                int x = 0;
-#pragma unroll
-                for (int i = 0; i < 16; i++) x ^= acc[qb][i];
-                m1e[qb] ^= x;
-            }
-            if (false)
-#endif
 #pragma unroll
             for (int qb = 0; qb < 2; qb++)
 #pragma unroll

@@ -82,9 +82,6 @@ __device__ __forceinline__ f32x2 pk_mov_hi_lo(f32x2 a, f32x2 b) {
     __asm__("v_pk_mov_b32 %0, %1, %2 op_sel:[1,0]" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
-#ifndef SIFT_BLUR_COL_UNIQUE
-#define SIFT_BLUR_COL_UNIQUE 0
-#endif
 constexpr int BLUR_TW = 64;
 #ifndef SIFT_BLUR_TH  // tile height: 64 (8 waves) beat 32 by 3-5 % of frame time (A/B builds: -DSIFT_BLUR_TH=32)
 #define SIFT_BLUR_TH 64
@@ -166,29 +163,11 @@ constexpr int blur_lds_floats() {
 // for a caller's 8-bit frame read by the frame's first blur (OpenCV converts
 // CV_8U to float exactly, so the planes are those of the float frame with the
 // same values).
-#ifdef SIFT_BLUR_STAMPS  // in-kernel phase timing (tools only), per radius: s_memtime deltas summed over tiles
-__device__ unsigned long long g_blur_stamps[32][6];
-extern "C" int sift_hip_debug_blur_stamps(unsigned long long* out) {
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_blur_stamps), sizeof(g_blur_stamps));
-}
-#define BLUR_STAMP(ph)                                                                  \
-    do {                                                                                \
-        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                     \
-        if (threadIdx.x == 0) atomicAdd(&g_blur_stamps[R][ph], t_ - bst_prev);          \
-        bst_prev = t_;                                                                  \
-    } while (0)
-#else
-#define BLUR_STAMP(ph) (void)0
-#endif
 
 template <int R, typename T, int NWAVES>
 __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __restrict__ in) {
     constexpr int BLUR_NW = NWAVES;                   // waves per workgroup
     constexpr int BLUR_CB = BLUR_TH / (8 * BLUR_NW);  // 8-row column-pass blocks per wave
-#ifdef SIFT_BLUR_STAMPS
-    unsigned long long bst_prev = __builtin_amdgcn_s_memtime();
-    if (threadIdx.x == 0) atomicAdd(&g_blur_stamps[R][5], 1ull);
-#endif
     constexpr int IW = blur_iw<R>();                 // LDS row stride (floats)
     constexpr int IH = BLUR_TH + 2 * R;
     constexpr int ORG = blur_org<R>();               // LDS column 0 = image column x0 - ORG
@@ -319,7 +298,6 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
                     if (i < RPW - 1 || wv + BLUR_NW * i < IH) irow[BLUR_NW * i * IW + 64] = v1[i];
             }
         }
-        BLUR_STAMP(0);  // loads landed, LDS written
         if (ES == 4 && copy_out) {  // decimated base plane of this octave = the tile's interior inputs
 #pragma unroll
             for (int i = 0; i < RPW; i++) {
@@ -333,7 +311,6 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
         }
     }
     __syncthreads();
-    BLUR_STAMP(1);  // staging barrier
 
     {
         // ds_read_b128 serves a wave in four 16-lane groups {0-3,12-15,20-27},
@@ -395,7 +372,6 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
         }
     }
     __syncthreads();
-    BLUR_STAMP(2);  // row pass + barrier
 
     float mx = -FLT_MAX, nmn = -FLT_MAX;  // pixel range (range_keys only)
     const int gx = x0 + lane;
@@ -409,21 +385,11 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
         // from two loads.
         // (volatile: every element is loaded twice, into both pairs it belongs
         // to, instead of being loaded once and copied with v_mov.)
-#if SIFT_BLUR_COL_UNIQUE  // each mid value read once, pairs assembled with v_mov
-        const float* cmid = mid + yb * IW + lx;
-        float cv[8 + 2 * R];
-#pragma unroll
-        for (int j = 0; j < 8 + 2 * R; j++) cv[j] = cmid[j * IW];
-        f32x2 cp[4 + 2 * R];
-#pragma unroll
-        for (int j = 0; j < 4 + 2 * R; j++) cp[j] = (f32x2){cv[j], cv[j + 4]};
-#else
         const volatile __attribute__((address_space(3))) float* vmid =
             (const volatile __attribute__((address_space(3))) float*)(mid + yb * IW + lx);
         f32x2 cp[4 + 2 * R];
 #pragma unroll
         for (int j = 0; j < 4 + 2 * R; j++) cp[j] = (f32x2){vmid[j * IW], vmid[(j + 4) * IW]};
-#endif
         float out[8];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
@@ -489,11 +455,6 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
             }
         }
     }
-    BLUR_STAMP(3);  // column pass, stores issued
-#ifdef SIFT_BLUR_STAMPS
-    __builtin_amdgcn_s_waitcnt(0);
-    BLUR_STAMP(4);  // stores done
-#endif
     {
         // Pixel range of the plane (requested for octave 0 / plane 0 only: every
         // later plane is a convex combination of it).  The descriptor sizes its

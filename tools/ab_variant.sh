@@ -1,6 +1,6 @@
 #!/bin/bash
-# Build the working tree's libsift_hip.so with extra compiler flags (timing
-# variants, e.g. -DSIFT_DESC_VARIANT=1) into ab/NAME.so.
+# Build the working tree's libsift_hip.so with extra compiler flags (tuning
+# knobs, e.g. -DSIFT_BLUR_TH=32 or -DSIFT_DESC_PRECISE=1) into ab/NAME.so.
 # Usage: tools/ab_variant.sh NAME "FLAGS"
 set -e
 NAME=$1; FLAGS=$2
