@@ -1660,13 +1660,13 @@ struct sift_hip_matcher {
     unsigned* dDone = nullptr;            // finished splits per (pair, 256-query block), zero between calls
     int* dMatch = nullptr;
     int8_t* dCodes = nullptr;             // int8 codes of a call's distinct sets (k_match_prep)
-    int* dNorms = nullptr;                // |code|^2 per code row
+    int* dRowKeys = nullptr;              // key bias per code row; row codeRows: the zero/padding sentinel
     unsigned* dFlags = nullptr;           // per set slot: == epoch if the set is not all integers 0..255
     long codeRows = 0;
     unsigned epoch = 0;
     ~sift_hip_matcher() {
         (void)hipSetDevice(device);
-        for (void* p : {(void*)dKeys, (void*)dDone, (void*)dMatch, (void*)dCodes, (void*)dNorms, (void*)dFlags})
+        for (void* p : {(void*)dKeys, (void*)dDone, (void*)dMatch, (void*)dCodes, (void*)dRowKeys, (void*)dFlags})
             if (p) (void)hipFree(p);
     }
 };
@@ -1694,8 +1694,10 @@ int sift_hip_matcher_create(int device, int max_query, int max_train, int max_pa
         hipMalloc((void**)&m->dKeys, sizeof(unsigned long long) * nkeys) != hipSuccess ||
         hipMalloc((void**)&m->dDone, sizeof(unsigned) * nblk) != hipSuccess ||
         hipMalloc((void**)&m->dMatch, sizeof(int) * (size_t)max_pairs * max_query) != hipSuccess ||
-        hipMalloc((void**)&m->dCodes, (size_t)m->codeRows * 128) != hipSuccess ||
-        hipMalloc((void**)&m->dNorms, sizeof(int) * (size_t)m->codeRows) != hipSuccess ||
+        hipMalloc((void**)&m->dCodes, (size_t)(m->codeRows + 1) * 128) != hipSuccess ||
+        hipMalloc((void**)&m->dRowKeys, sizeof(int) * (size_t)(m->codeRows + 1)) != hipSuccess ||
+        hipMemset(m->dCodes + (size_t)m->codeRows * 128, 0, 128) != hipSuccess ||
+        hipMemcpy(m->dRowKeys + m->codeRows, &kMatchPadKey, sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
         hipMalloc((void**)&m->dFlags, sizeof(unsigned) * 2 * kMaxMatchPairs) != hipSuccess ||
         hipMemset(m->dKeys, 0xff, sizeof(unsigned long long) * nkeys) != hipSuccess ||
         hipMemset(m->dDone, 0, sizeof(unsigned) * nblk) != hipSuccess ||
@@ -1754,8 +1756,8 @@ int sift_hip_match_batched(sift_hip_matcher_t m, int P, const uint16_t* const* q
     }
     m->epoch = m->epoch + 1 == 0 ? 1 : m->epoch + 1;  // flags from earlier calls never equal it
     HIPCHK(hipSetDevice(m->device));
-    const int S = match_splits(maxq, maxt, P);
-    launch_match(sets, b, S, m->maxQ, m->dCodes, m->dNorms, m->dFlags, m->epoch, m->dKeys, m->dDone, ratio,
+    const MatchPlan plan = match_plan(maxq, maxt, P);
+    launch_match(sets, b, plan, m->maxQ, m->dCodes, m->dRowKeys, (int)m->codeRows, m->dFlags, m->epoch, m->dKeys, m->dDone, ratio,
                  ratio_on_squared, idx2, d2, match, (hipStream_t)stream);
     HIPCHK(hipGetLastError());
     return SIFT_HIP_OK;

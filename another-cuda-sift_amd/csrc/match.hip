@@ -3,31 +3,34 @@
 // Replaces /root/reference/sift_cuda/sift_func/Match.cu:8-177 (32 lanes per
 // query, half2 diff^2, an N x M fp32 score matrix written to and re-read from
 // HBM and allocated per call).  Here the distance matrix never leaves the
-// register file.  Two launches per call (one for a single pair: k_match<true>
-// converts its own rows, see there):
+// register file.  Two launches per batched call, one for a single pair:
 //
-//  k_match_prep  every distinct descriptor set of the call (fp16 rows) becomes
-//                int8 codes c = v - 128 (128 B per row) and |c|^2 per row, once
-//                per set (the 8-way match: 8 sets for 56 pairs).  A set holding
-//                a value that is not an integer 0..255 is flagged.
-//  k_match       the distance GEMM on v_mfma_i32_32x32x32_i8.  A workgroup owns
-//                256 queries (4 waves x 64; a wave keeps its two 32-query B
-//                operands in registers for the whole launch) and streams its
-//                split of the train rows through LDS in 32-row tiles, double
-//                buffered (one 16-byte load per thread per tile, the next
-//                tile in flight while this one computes): a tile is read from
-//                L2 once per 256 queries and feeds 8 MFMAs per wave.
+//  k_match_prep    every distinct descriptor set of the call (fp16 rows)
+//                  becomes int8 codes c = v - 128 (128 B per row) and a key
+//                  bias -(256 |c|^2 + (row mod 256)) per row, once per set (the
+//                  8-way match: 8 sets for 56 pairs).  A set holding a value
+//                  that is not an integer 0..255 is flagged.
+//  k_match_batch   the distance GEMM on v_mfma_i32_32x32x32_i8 for prepared
+//                  sets: a workgroup owns 512 queries (8 waves x 64; a wave
+//                  keeps its two 32-query B operands in registers) and one
+//                  split of the train tiles, which it streams through two LDS
+//                  chunk buffers of 8 tiles by LDS-DMA (the next chunk lands
+//                  while this one computes: one barrier per 8 tiles instead
+//                  of one per tile); per 32-row tile 8 MFMAs per wave.
+//  k_match_single  one pair without the prep launch: each workgroup (256
+//                  queries) converts its own query rows and train tiles.
 //
 // Exactness: d^2 = sum (t - q)^2 = |c_t|^2 + |c_q|^2 - 2 c_t.c_q for the
-// shifted codes (translation invariant); |c|^2 <= 2^21 and |c_t.c_q| <= 2^21, so
-// the int32 accumulator and every key below are exact.  A lane folds the 16
-// train rows of its accumulator into a running top-2 with three VALU per
-// element: key = 256 dot - (128 |c_t|^2 + r) (v_lshl_add_u32), where r is the
-// row's index inside a group of 4 tiles, orders (e = d^2 - |c_q|^2, train row)
-// in reverse, and the top-2 of the keys is v_max_i32 + v_med3_i32.  Every 4
-// tiles the group's top-2 is decoded into (e, train index) and merged into the
-// running pair.  Ties keep the lower train index -- OpenCV's batchDistance /
-// knnMatch order and the oracle's (sift_oracle_knn2).
+// shifted codes (translation invariant), so the int32 accumulator and every
+// key below are exact.  A lane folds the 16 train rows of its accumulator
+// into a running top-2 of keys key = 512 dot - (256 |c_t|^2 + r) (one
+// v_lshl_add_u32 each), where r is the row's index inside its group of 8
+// tiles; keys order (e = d^2 - |c_q|^2, train row) in reverse, and two new
+// keys at a time enter the top-2 with v_med3 + v_max3 (3 VALU per 2 keys).
+// Each staged chunk is one key group: its top-2 is decoded into (e, train
+// index) and merged into the running pair.  Ties keep the lower train index
+// -- OpenCV's batchDistance / knnMatch order and the oracle's
+// (sift_oracle_knn2).
 //
 // A pair with a flagged set (non-integer or out-of-range fp16 values, e.g. the
 // reference's own unrounded x512 descriptors) runs the general path in the
@@ -47,10 +50,6 @@
 #include "sift_match.h"
 #include "sift_math.h"
 
-#ifndef SIFT_MATCH_WG_TARGET
-#define SIFT_MATCH_WG_TARGET 512  // workgroups a launch aims for (2 per CU) when choosing train splits
-#endif
-
 namespace sift_amd {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
@@ -59,10 +58,15 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kNone = 0x7fffffff;
-constexpr int kRowPad = 144;  // LDS bytes per code row: rows 36 dwords apart -> conflict-free ds_read_b128
-constexpr int kGroupTiles = 4;  // tiles per key group: local row r < 128 in the key's low 7 bits
-constexpr int kInvalidKey = -(1 << 30);  // keys <= this are padding rows (or none)
-constexpr int kPadBias = -(3 << 29);     // key bias of a padding row (codes 0: key = bias <= kInvalidKey)
+// Row keys: key = 512 dot - (256 |c_t|^2 + r) orders (d^2, train row) in
+// reverse for one query, where r < 256 is the row's index inside its group of
+// kGroupTiles tiles: 256 (2 dot - |c_t|^2) = 256 (|c_q|^2 - d^2) lies in
+// [-2^31 + 2^24, 2^29] for any codes (d^2 <= 128 * 255^2 < 2^23), so every key
+// is an exact int32.  A padding row has zero codes and key kPadBias, below
+// every valid key.
+constexpr int kGroupTiles = 8;
+constexpr int kPadBias = kMatchPadKey;
+constexpr int kInvalidKey = kPadBias;  // keys <= this are padding rows (or none)
 
 struct Top2 {
     float d1, d2;
@@ -99,10 +103,11 @@ __device__ __forceinline__ Top2 shfl_top2(const Top2& t, int mask) {
 }
 
 // ---------------------------------------------------------------------------
-// Set preparation: 8 threads per row (16 halves each).
+// Set preparation: 8 threads per row (16 halves each); per row the int8
+// codes and the key bias -(256 |c|^2 + (row & 255)) (the norm is -bias >> 8).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_match_prep(MatchSets sets, int8_t* __restrict__ codes,
-                                                    int* __restrict__ norms, unsigned* __restrict__ flags,
+                                                    int* __restrict__ rowkeys, unsigned* __restrict__ flags,
                                                     unsigned epoch) {
     const MatchSet& st = sets.set[blockIdx.y];
     if ((int)blockIdx.x * 32 >= st.n) return;
@@ -128,7 +133,7 @@ __global__ __launch_bounds__(256) void k_match_prep(MatchSets sets, int8_t* __re
     if (in) {
         *reinterpret_cast<uint4*>(codes + ((size_t)st.row0 + row) * 128 + part * 16) =
             make_uint4(pk[0], pk[1], pk[2], pk[3]);
-        if (part == 0) norms[st.row0 + row] = nrm;
+        if (part == 0) rowkeys[st.row0 + row] = -(256 * nrm + (row & 255));  // the row's key bias (r = row mod 256)
         if (bad) flags[blockIdx.y] = epoch;  // every writer stores the same word
     }
 }
@@ -142,6 +147,12 @@ __device__ __forceinline__ int med3_i32(int a, int b, int c) {
     return r;
 }
 
+__device__ __forceinline__ int max3_i32(int a, int b, int c) {
+    int r;
+    __asm__("v_max3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 struct Best {
     int e1, i1, e2, i2;  // e = d^2 - |c_q|^2 (kNone: no entry), i = train index
 };
@@ -152,9 +163,9 @@ struct Best {
 __device__ __forceinline__ Best fold_group(const Best b, int m1, int m2, int t0) {
     const int be1 = b.e1, bi1 = b.i1, be2 = b.e2, bi2 = b.i2;  // values: no member-address selects (scratch)
     const bool v1 = m1 > kInvalidKey, v2 = m2 > kInvalidKey;
-    const int s1 = v1 ? -m1 : 0, s2 = v2 ? -m2 : 0;  // 128 e + r
-    const int te1 = v1 ? (s1 >> 7) : kNone, ti1 = t0 + (s1 & 127);
-    const int te2 = v2 ? (s2 >> 7) : kNone, ti2 = t0 + (s2 & 127);
+    const int s1 = v1 ? -m1 : 0, s2 = v2 ? -m2 : 0;  // 256 e + r
+    const int te1 = v1 ? (s1 >> 8) : kNone, ti1 = t0 + (s1 & 255);
+    const int te2 = v2 ? (s2 >> 8) : kNone, ti2 = t0 + (s2 & 255);
     const bool c1 = te1 < be1;
     const bool c2 = c1 ? te2 < be1 : te1 < be2;
     Best r;
@@ -302,139 +313,90 @@ __device__ __forceinline__ void write_match(int i1, float e1, int i2, float e2, 
     }
 }
 
-// grid = (256-query blocks, train splits, pairs), 256 threads.
-// kFused (single pairs): no k_match_prep launch -- the workgroup converts its
-// own query rows and train tiles from fp16 as it loads them and takes the
-// fp16 path itself if any of them holds a non-integer value.  Mixing paths
-// across workgroups is exact: on integer values 0..255 the fp16 path's dot
-// products and norms are exact integers below 2^24, so both paths return
-// the same (d^2, index) pairs with the same tie order.
-template <bool kFused>
-__global__ __launch_bounds__(256, 2) void k_match(MatchBatch batch, int S, int nq_stride,
-                                                  const int8_t* __restrict__ codes, const int* __restrict__ norms,
-                                                  const unsigned* __restrict__ flags, unsigned epoch,
-                                                  unsigned long long* __restrict__ keys, unsigned* __restrict__ done,
-                                                  float ratio, int ratio_on_squared, int* __restrict__ idx2,
-                                                  float* __restrict__ d2out, int* __restrict__ match) {
-    __shared__ __attribute__((aligned(16))) int8_t s_tile[2][kMatchTileRows * kRowPad];
-    __shared__ __attribute__((aligned(16))) int s_ntk[2][kMatchTileRows];
-    __shared__ Top2 s_res[kMatchQB];
-    __shared__ unsigned s_last;
-    const int p = blockIdx.z;
-    const MatchPair& pr = batch.pair[p];
-    const int q0 = blockIdx.x * kMatchQB;
-    if (q0 >= pr.nq) return;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, col = lane & 31, h = lane >> 5;
-    const int ntiles = (pr.nt + kMatchTileRows - 1) / kMatchTileRows, tps = (ntiles + S - 1) / S;
-    const int tbeg = min(ntiles, (int)blockIdx.y * tps), tend = min(ntiles, tbeg + tps);
-    const int q0w = q0 + 64 * w;
-    Top2 res[2];
-    bool bad = false;  // kFused: a non-integer value among this workgroup's rows
-    bool use_int = kFused || (flags[pr.qset] != epoch && flags[pr.tset] != epoch);
-    if (use_int) {
-        // ---- integer path ----
-        const int8_t* __restrict__ qc = codes + (size_t)pr.qrow0 * 128;
-        const int8_t* __restrict__ tc = codes + (size_t)pr.trow0 * 128;
-        const int* __restrict__ tn = norms + pr.trow0;
-        // B operands: lane (col, h) holds bytes [64h, 64h + 64) of query row
-        // q0w + 32 qb + col, one 16-byte fragment per MFMA; the A fragments
-        // take the same bytes of the train rows, so both sides pair the same
-        // descriptor dimensions in every K slot.
-        i32x4 bq[2][4];
-        int qn[2];
+
+// ---------------------------------------------------------------------------
+// Integer-path building blocks shared by both kernels.
+//
+// Train tiles are staged in LDS a chunk (<= one key group of kGroupTiles
+// tiles) at a time.  Code rows are stored unpadded (128 B) with their 16-byte
+// pieces XOR-swizzled by (row >> 1) & 7, so a wave's ds_read_b128 of 32 rows x
+// one piece covers the 64 banks once per 16-lane group; the swizzle also lets
+// prepared codes go global -> LDS by LDS-DMA (a lane's source address is free,
+// its LDS slot is lane x 16 B).
+// ---------------------------------------------------------------------------
+constexpr int kTileBytes = kMatchTileRows * 128;
+constexpr int kMatchBatchNW = 8;  // waves per k_match_batch workgroup (512 queries)
+constexpr int kChunkRows = kChunkTiles * kMatchTileRows;
+static_assert(kChunkTiles == kGroupTiles, "a staged chunk is at most one key group");
+
+__device__ __forceinline__ int piece_swz(int row, int piece) { return piece ^ ((row >> 1) & 7); }
+
+// A wave's two 32-query B operands: lane (col, h) holds bytes [64h, 64h + 64)
+// of query row q0w + 32 qb + col, one 16-byte fragment per MFMA; the A
+// fragments take the same bytes of the train rows, so both sides pair the same
+// descriptor dimensions in every K slot.  qn = |c_q|^2.
+__device__ __forceinline__ void load_queries(const int8_t* __restrict__ qc, const int* __restrict__ qkeys, int nq,
+                                             int q0w, int col, int h, i32x4 (&bq)[2][4], int (&qn)[2]) {
 #pragma unroll
-        for (int qb = 0; qb < 2; qb++) {
-            const int row = min(q0w + 32 * qb + col, pr.nq - 1);
-            if constexpr (kFused) {
-                const uint4* src = reinterpret_cast<const uint4*>(pr.q + (size_t)row * 128 + 64 * h);
-                int nrm = 0;
+    for (int qb = 0; qb < 2; qb++) {
+        const int row = min(q0w + 32 * qb + col, nq - 1);
+        const i32x4* src = reinterpret_cast<const i32x4*>(qc + (size_t)row * 128 + 64 * h);
 #pragma unroll
-                for (int kb = 0; kb < 4; kb++) bq[qb][kb] = codes16(src[2 * kb], src[2 * kb + 1], nrm, bad);
-                qn[qb] = nrm + __shfl_xor(nrm, 32);
-            } else {
-                const i32x4* src = reinterpret_cast<const i32x4*>(qc + (size_t)row * 128 + 64 * h);
+        for (int kb = 0; kb < 4; kb++) bq[qb][kb] = src[kb];
+        qn[qb] = (-qkeys[row]) >> 8;
+    }
+}
+
+// Stage prepared train rows [row0, row0 + 32 nc) of a set (codes tc, key
+// biases tk) into one LDS chunk by LDS-DMA; rows past nt read the zero
+// sentinel row (zc, zk).  Codes: wave w fills 8-row blocks w, w + NW, ...
+// (1 KiB each); lane l lands at slot (row 8b + l / 8, piece l & 7) and loads
+// the global piece the swizzle puts there.  Keys: 64 rows per 4-byte-per-lane
+// instruction.  Completion is this wave's vmcnt.
+template <int NW>
+__device__ __forceinline__ void stage_dma(const int8_t* __restrict__ tc, const int* __restrict__ tk, int nt, int row0,
+                                          int nc, const int8_t* __restrict__ zc, const int* __restrict__ zk,
+                                          int8_t* sc, int* sk, int w, int lane) {
+    const int wv = __builtin_amdgcn_readfirstlane(w);
+    for (int b = wv; b < nc * (kMatchTileRows / 8); b += NW) {
+        const int r = 8 * b + (lane >> 3), gr = row0 + r;
+        const int8_t* src = (gr < nt ? tc + (size_t)gr * 128 : zc) + 16 * piece_swz(r, lane & 7);
+        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(sc + 1024 * b), 16,
+                                         0, 0);
+    }
+    for (int b = wv; b < (nc * kMatchTileRows + 63) / 64; b += NW) {
+        const int gr = row0 + 64 * b + lane;
+        const int* src = gr < nt ? tk + gr : zk;
+        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(sk + 64 * b), 4, 0,
+                                         0);
+    }
+}
+
+// One staged chunk of nc tiles (rows t0 ...) against a wave's two query
+// blocks: per tile 8 MFMAs from LDS fragments, then each lane folds its 32
+// keys into a per-block running key top-2 -- two at a time: for a pair (x, y)
+// of new keys and the running m1 >= m2 the new second is max(med3(m1, x, y),
+// m2) and the new first max3(m1, x, y), 3 VALU per 2 keys, in two chains per
+// block (accumulator registers 0-7 / 8-15).  The chunk lies in one key group
+// (r = row - t0 < 256), so its top-2 is decoded once into (e, train index) and
+// merged into the running pair (earlier groups win ties).
+__device__ __forceinline__ void chunk_top2(const int8_t* sc, const int* sk, int nc, int t0, int col, int h,
+                                           const i32x4 (&bq)[2][4], Best (&best)[2]) {
+    int m1e[2] = {INT_MIN, INT_MIN}, m2e[2] = {INT_MIN, INT_MIN};  // registers 0-7
+    int m1o[2] = {INT_MIN, INT_MIN}, m2o[2] = {INT_MIN, INT_MIN};  // registers 8-15
+    const int sw = (col >> 1) & 7;
+    const int8_t* const ta0 = sc + col * 128;
+    const int* const tk1 = sk + 4 * h;
 #pragma unroll
-                for (int kb = 0; kb < 4; kb++) bq[qb][kb] = src[kb];
-                qn[qb] = norms[pr.qrow0 + row];
-            }
-        }
-        // Tile loader: thread -> 16 bytes (row tid >> 3, part tid & 7) of a
-        // 4 KiB tile; thread r < 32 -> row r's negated key bias.  Loads run two
-        // tiles ahead through a ring of two register slots (tile k in slot
-        // k & 1), so a tile's global load has two iterations to land before
-        // it is stored to its LDS buffer (k & 1) for iteration k.
-        // The ring holds the RAW loaded words: the padding select and the key
-        // are applied at stash time, so no instruction consumes a load right
-        // after it is issued (a select on the loaded value made the compiler
-        // wait for every prefetch at once -- vmcnt(0) before each tile's
-        // MFMAs -- and the two-deep ring hid nothing).
-        const int lrow = tid >> 3, lpart = tid & 7;
-        i32x4 nv[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-        int nn[2] = {0, 0};
-        uint4 hv[2][2] = {};  // kFused: the raw fp16 words (32 bytes per thread per tile)
-        using I0 = std::integral_constant<int, 0>;
-        using I1 = std::integral_constant<int, 1>;
-        auto fetch = [&](int tile, auto slot) {
-            constexpr int SL = decltype(slot)::value;
-            const int r = tile * kMatchTileRows + lrow;
-            if constexpr (kFused) {
-                const uint4* src = reinterpret_cast<const uint4*>(pr.t + (size_t)min(r, pr.nt - 1) * 128 + 16 * lpart);
-                hv[SL][0] = src[0];
-                hv[SL][1] = src[1];
-            } else {
-                nv[SL] = *reinterpret_cast<const i32x4*>(tc + (size_t)min(r, pr.nt - 1) * 128 + 16 * lpart);
-                nn[SL] = tn[min(tile * kMatchTileRows + (tid & 31), pr.nt - 1)];
-            }
-        };
-        auto stash = [&](int tile, auto slot) {  // tile k, slot k & 1 -> LDS buffer k & 1
-            constexpr int SL = decltype(slot)::value;
-            const int r = tile * kMatchTileRows + lrow;
-            if constexpr (kFused) {  // codes and the row's norm (8 threads per row, lanes 8k..8k+7)
-                int nrm = 0;
-                const i32x4 pk = codes16(hv[SL][0], hv[SL][1], nrm, bad);
-                nrm += __shfl_xor(nrm, 1);
-                nrm += __shfl_xor(nrm, 2);
-                nrm += __shfl_xor(nrm, 4);
-                *reinterpret_cast<i32x4*>(s_tile[SL] + lrow * kRowPad + 16 * lpart) = r < pr.nt ? pk : (i32x4){0, 0, 0, 0};
-                if (lpart == 0) {
-                    const int lr = ((tile - tbeg) & (kGroupTiles - 1)) * kMatchTileRows + lrow;
-                    s_ntk[SL][lrow] = r < pr.nt ? -(128 * nrm + lr) : kPadBias;
-                }
-                return;
-            }
-            *reinterpret_cast<i32x4*>(s_tile[SL] + lrow * kRowPad + 16 * lpart) =
-                r < pr.nt ? nv[SL] : (i32x4){0, 0, 0, 0};
-            if (tid < kMatchTileRows) {
-                const int rr = tile * kMatchTileRows + tid;
-                const int lr = ((tile - tbeg) & (kGroupTiles - 1)) * kMatchTileRows + tid;  // row in the key group
-                s_ntk[SL][tid] = rr < pr.nt ? -(128 * nn[SL] + lr) : kPadBias;
-            }
-        };
-        Best best[2] = {{kNone, kNone, kNone, kNone}, {kNone, kNone, kNone, kNone}};
-        // Running key top-2 per query block in two chains (even / odd
-        // accumulator registers): half the dependent v_max / v_med3 chain.
-        int m1e[2] = {INT_MIN, INT_MIN}, m2e[2] = {INT_MIN, INT_MIN};  // even registers
-        int m1o[2] = {INT_MIN, INT_MIN}, m2o[2] = {INT_MIN, INT_MIN};  // odd registers
-        if (tbeg < tend) {
-            fetch(tbeg, I0{});
-            stash(tbeg, I0{});
-            if (tbeg + 1 < tend) fetch(tbeg + 1, I1{});
-            if (tbeg + 2 < tend) fetch(tbeg + 2, I0{});
-        }
-        auto step = [&](int tile, auto par) {  // par = (tile - tbeg) & 1
-            constexpr int PB = decltype(par)::value;
-            lds_barrier();  // tile `tile` is in s_tile[PB]; every wave is done with s_tile[PB ^ 1]
+    for (int j = 0; j < kChunkTiles; j++) {
+        if (j < nc) {
             i32x4 a[4], tk[4];
-            const int8_t* ta = s_tile[PB] + col * kRowPad + 64 * h;
 #pragma unroll
-            for (int kb = 0; kb < 4; kb++) a[kb] = *reinterpret_cast<const i32x4*>(ta + 16 * kb);
+            for (int kb = 0; kb < 4; kb++)
+                a[kb] = *reinterpret_cast<const i32x4*>(ta0 + j * kTileBytes + 16 * ((4 * h + kb) ^ sw));
             // accumulator register i holds train row (i & 3) + 8 (i >> 2) + 4 h
 #pragma unroll
-            for (int g = 0; g < 4; g++) tk[g] = *reinterpret_cast<const i32x4*>(s_ntk[PB] + 8 * g + 4 * h);
-            if (tile + 1 < tend) {
-                stash(tile + 1, std::integral_constant<int, PB ^ 1>{});
-                if (tile + 3 < tend) fetch(tile + 3, std::integral_constant<int, PB ^ 1>{});
-            }
+            for (int g = 0; g < 4; g++) tk[g] = *reinterpret_cast<const i32x4*>(tk1 + j * kMatchTileRows + 8 * g);
             i32x16 acc[2] = {{}, {}};
 #pragma unroll
             for (int qb = 0; qb < 2; qb++)
@@ -444,74 +406,65 @@ __global__ __launch_bounds__(256, 2) void k_match(MatchBatch batch, int S, int n
 #pragma unroll
             for (int qb = 0; qb < 2; qb++)
 #pragma unroll
-                for (int i = 0; i < 16; i += 2) {
-                    const int ke = (acc[qb][i] << 8) + tk[i >> 2][i & 3];
-                    const int ko = (acc[qb][i + 1] << 8) + tk[i >> 2][(i & 3) + 1];
-                    m2e[qb] = med3_i32(m1e[qb], ke, m2e[qb]);  // second largest of {m1 >= m2, key}
-                    m1e[qb] = max(m1e[qb], ke);
-                    m2o[qb] = med3_i32(m1o[qb], ko, m2o[qb]);
-                    m1o[qb] = max(m1o[qb], ko);
+                for (int i = 0; i < 8; i += 2) {
+                    const int x0 = (acc[qb][i] << 9) + tk[i >> 2][i & 3];
+                    const int y0 = (acc[qb][i + 1] << 9) + tk[i >> 2][(i & 3) + 1];
+                    const int x1 = (acc[qb][i + 8] << 9) + tk[(i + 8) >> 2][i & 3];
+                    const int y1 = (acc[qb][i + 9] << 9) + tk[(i + 8) >> 2][(i & 3) + 1];
+                    m2e[qb] = max(med3_i32(m1e[qb], x0, y0), m2e[qb]);
+                    m1e[qb] = max3_i32(m1e[qb], x0, y0);
+                    m2o[qb] = max(med3_i32(m1o[qb], x1, y1), m2o[qb]);
+                    m1o[qb] = max3_i32(m1o[qb], x1, y1);
                 }
-            const int gi = tile - tbeg;
-            if ((gi & (kGroupTiles - 1)) == kGroupTiles - 1 || tile + 1 == tend) {
-                const int t0 = (tile - (gi & (kGroupTiles - 1))) * kMatchTileRows;
+        }
+    }
 #pragma unroll
-                for (int qb = 0; qb < 2; qb++) {
-                    const int a1 = m1e[qb], a2 = m2e[qb], b1 = m1o[qb], b2 = m2o[qb];
-                    best[qb] = fold_group(best[qb], max(a1, b1), max(min(a1, b1), max(a2, b2)), t0);
-                    m1e[qb] = m2e[qb] = m1o[qb] = m2o[qb] = INT_MIN;
-                }
-            }
-        };
-        for (int tile = tbeg; tile < tend; tile += 2) {
-            step(tile, I0{});
-            if (tile + 1 < tend) step(tile + 1, I1{});
-        }
-#pragma unroll
-        for (int qb = 0; qb < 2; qb++) {
-            Best o;  // the other half of the train rows (lane ^ 32)
-            o.e1 = __shfl_xor(best[qb].e1, 32);
-            o.i1 = __shfl_xor(best[qb].i1, 32);
-            o.e2 = __shfl_xor(best[qb].e2, 32);
-            o.i2 = __shfl_xor(best[qb].i2, 32);
-            const Best r = merge_best(best[qb], o);
-            res[qb].d1 = r.e1 == kNone ? INFINITY : (float)(r.e1 + qn[qb]);
-            res[qb].i1 = r.e1 == kNone ? kNone : r.i1;
-            res[qb].d2 = r.e2 == kNone ? INFINITY : (float)(r.e2 + qn[qb]);
-            res[qb].i2 = r.e2 == kNone ? kNone : r.i2;
-        }
+    for (int qb = 0; qb < 2; qb++) {
+        const int a1 = m1e[qb], a2 = m2e[qb], b1 = m1o[qb], b2 = m2o[qb];
+        best[qb] = fold_group(best[qb], max(a1, b1), max(min(a1, b1), max(a2, b2)), t0);
     }
-    if constexpr (kFused)
-        if (__syncthreads_or(bad)) use_int = false;  // this workgroup's rows need the fp16 path
-    if (!use_int) {
-        // ---- general path: fp16 values that are not integers 0..255 ----
-        res[0] = match_f16_block(pr, q0w, tbeg, tend, col, h);
-        res[1] = match_f16_block(pr, q0w + 32, tbeg, tend, col, h);
-    }
-    if (h == 0) {
-        s_res[64 * w + col] = res[0];
-        s_res[64 * w + 32 + col] = res[1];
-    }
-    __syncthreads();
-    const int q = q0 + tid;
-    const bool qv = q < pr.nq;
-    const size_t o = (size_t)pr.out_off + q;
-    if (S == 1) {
-        if (qv) {
-            const Top2 r = s_res[tid];
-            const int i1 = r.i1 == kNone ? -1 : r.i1, i2 = r.i2 == kNone ? -1 : r.i2;
-            write_match(i1, i1 >= 0 ? r.d1 : FLT_MAX, i2, i2 >= 0 ? r.d2 : FLT_MAX, o, ratio, ratio_on_squared, idx2,
-                        d2out, match);
-        }
-        return;
-    }
-    // Global top-2 of a query across the S splits: 64-bit atomicMin on keys.
-    // A split min's its best into K1; whatever that displaced (or its best, if
-    // it lost) and its runner-up are candidates for K2, of which the smaller is
-    // min'ed in (the larger can never be second).  Every key except the final
-    // K1 reaches K2 this way, so K2 ends as the true second.  Device-scope
-    // atomics only (coherent across XCDs, no cache write-back fences).
-    unsigned long long* K = keys + 2 * ((size_t)p * nq_stride + q);
+}
+
+// A lane's two halves of the train rows (lane, lane ^ 32) -> the query's
+// (d^2, index) top-2 (d^2 = e + |c_q|^2).
+__device__ __forceinline__ Top2 finish_best(const Best b, int qn) {
+    Best o;
+    o.e1 = __shfl_xor(b.e1, 32);
+    o.i1 = __shfl_xor(b.i1, 32);
+    o.e2 = __shfl_xor(b.e2, 32);
+    o.i2 = __shfl_xor(b.i2, 32);
+    const Best r = merge_best(b, o);
+    Top2 t;
+    t.d1 = r.e1 == kNone ? INFINITY : (float)(r.e1 + qn);
+    t.i1 = r.e1 == kNone ? kNone : r.i1;
+    t.d2 = r.e2 == kNone ? INFINITY : (float)(r.e2 + qn);
+    t.i2 = r.e2 == kNone ? kNone : r.i2;
+    return t;
+}
+
+__device__ __forceinline__ void write_top2(const Top2 r, size_t o, float ratio, int ratio_on_squared, int* idx2,
+                                           float* d2out, int* match) {
+    const int i1 = r.i1 == kNone ? -1 : r.i1, i2 = r.i2 == kNone ? -1 : r.i2;
+    write_match(i1, i1 >= 0 ? r.d1 : FLT_MAX, i2, i2 >= 0 ? r.d2 : FLT_MAX, o, ratio, ratio_on_squared, idx2, d2out,
+                match);
+}
+
+// Global top-2 of a query over several contributions (train ranges):
+// 64-bit atomicMin on keys (d^2 bits << 32 | train index).  A contribution
+// min's its best into K1; whatever that displaced (or its best, if it lost)
+// and its runner-up are candidates for K2, of which the smaller is min'ed in
+// (the larger can never be second).  Every key except the final K1 reaches K2
+// this way, so K2 ends as the true second.  Device-scope atomics only
+// (coherent across XCDs, no cache write-back fences).  The contribution that
+// completes the count (`units` of `total`, counted on *cnt) reads and
+// restores the keys and the counter and writes the outputs.  Called by every
+// thread of the workgroup, thread t for query q0 + t (s_res[t]).
+__device__ __forceinline__ void merge_contribution(const Top2* s_res, unsigned* s_last, unsigned long long* K0,
+                                                   unsigned* cnt, unsigned units, unsigned total, bool qv, size_t o,
+                                                   float ratio, int ratio_on_squared, int* idx2, float* d2out,
+                                                   int* match) {
+    const int tid = threadIdx.x;
+    unsigned long long* K = K0 + 2 * tid;
     if (qv) {
         const Top2 r = s_res[tid];
         const unsigned long long a1 = match_key(r.d1, r.i1), a2 = match_key(r.d2, r.i2);
@@ -523,51 +476,277 @@ __global__ __launch_bounds__(256, 2) void k_match(MatchBatch batch, int S, int n
         }
     }
     __syncthreads();
-    unsigned* cnt = done + (size_t)p * gridDim.x + blockIdx.x;
-    if (tid == 0) s_last = atomicAdd(cnt, 1u) == (unsigned)(S - 1);
+    if (tid == 0) *s_last = atomicAdd(cnt, units) + units == total;
     __syncthreads();
-    if (!s_last || !qv) return;
-    const unsigned long long k1 = atomicExch(&K[0], ~0ull), k2 = atomicExch(&K[1], ~0ull);
+    if (!*s_last) return;
+    if (qv) {
+        const unsigned long long k1 = atomicExch(&K[0], ~0ull), k2 = atomicExch(&K[1], ~0ull);
+        const int i1 = k1 == ~0ull ? -1 : (int)(unsigned)k1, i2 = k2 == ~0ull ? -1 : (int)(unsigned)k2;
+        const float e1 = i1 >= 0 ? __uint_as_float((unsigned)(k1 >> 32)) : FLT_MAX;
+        const float e2 = i2 >= 0 ? __uint_as_float((unsigned)(k2 >> 32)) : FLT_MAX;
+        write_match(i1, e1, i2, e2, o, ratio, ratio_on_squared, idx2, d2out, match);
+    }
     if (tid == 0) atomicExch(cnt, 0u);
-    const int i1 = k1 == ~0ull ? -1 : (int)(unsigned)k1, i2 = k2 == ~0ull ? -1 : (int)(unsigned)k2;
-    const float e1 = i1 >= 0 ? __uint_as_float((unsigned)(k1 >> 32)) : FLT_MAX;
-    const float e2 = i2 >= 0 ? __uint_as_float((unsigned)(k2 >> 32)) : FLT_MAX;
-    write_match(i1, e1, i2, e2, o, ratio, ratio_on_squared, idx2, d2out, match);
 }
 
-int match_splits(int max_nq, int max_nt, int P) {
-    const int qblocks = (max_nq + kMatchQB - 1) / kMatchQB;
-    const int ntiles = (max_nt + kMatchTileRows - 1) / kMatchTileRows;
+// ---------------------------------------------------------------------------
+// k_match_single: one pair, fp16 rows converted in the kernel (no prep
+// launch).  grid = (query blocks of 64 NW, train splits S), 64 NW threads; a
+// workgroup converts its query rows and its split's train rows as it stages
+// them (8 threads per row: two 16-byte fp16 loads -> one swizzled 16-byte code
+// piece; the row norm by three shuffles) and takes the fp16 path itself if
+// any of them holds a non-integer value.  Mixing paths across workgroups is
+// exact: on integer values 0..255 the fp16 path's dot products and norms are
+// exact integers below 2^24, so both paths return the same (d^2, index) pairs
+// with the same tie order.  Key groups start at the split's first tile.
+// ---------------------------------------------------------------------------
+template <int NW>
+__global__ __launch_bounds__(64 * NW, (kMatchWgPerCu * NW) / 4) void k_match_single(
+    MatchPair pr, int S, unsigned long long* __restrict__ keys, unsigned* __restrict__ done, float ratio,
+    int ratio_on_squared, int* __restrict__ idx2, float* __restrict__ d2out, int* __restrict__ match) {
+    constexpr int NT = 64 * NW, QB = 64 * NW;
+    __shared__ __attribute__((aligned(16))) int8_t s_codes[2][kChunkTiles * kTileBytes];
+    __shared__ __attribute__((aligned(16))) int s_key[2][kChunkRows];
+    __shared__ unsigned s_last;
+    static_assert(sizeof(Top2) * QB <= sizeof(s_codes), "results alias the code tiles");
+    Top2* const s_res = reinterpret_cast<Top2*>(&s_codes[0][0]);
+    const int q0 = blockIdx.x * QB;
+    if (q0 >= pr.nq) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, col = lane & 31, h = lane >> 5;
+    const int ntiles = (pr.nt + kMatchTileRows - 1) / kMatchTileRows, tps = (ntiles + S - 1) / S;
+    const int tbeg = min(ntiles, (int)blockIdx.y * tps), tend = min(ntiles, tbeg + tps);
+    const int q0w = q0 + 64 * w;
+    Top2 res[2];
+    bool bad = false;  // a non-integer value among this workgroup's rows
+    {
+        i32x4 bq[2][4];
+        int qn[2];
+#pragma unroll
+        for (int qb = 0; qb < 2; qb++) {
+            const int row = min(q0w + 32 * qb + col, pr.nq - 1);
+            const uint4* src = reinterpret_cast<const uint4*>(pr.q + (size_t)row * 128 + 64 * h);
+            int nrm = 0;
+#pragma unroll
+            for (int kb = 0; kb < 4; kb++) bq[qb][kb] = codes16(src[2 * kb], src[2 * kb + 1], nrm, bad);
+            qn[qb] = nrm + __shfl_xor(nrm, 32);
+        }
+        auto stage = [&](int c0, int buf) {
+            const int nc = min(kChunkTiles, tend - c0);
+            int8_t* const sc = s_codes[buf];
+            int* const sk = s_key[buf];
+            constexpr int U = 2;  // loads go out U pieces at a time
+            const int npieces = nc * kMatchTileRows * 8;
+            for (int base = 0; base < npieces; base += NT * U) {
+                uint4 hv[U][2];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int idx = min(base + tid + NT * u, npieces - 1), r = idx >> 3;
+                    const uint4* src = reinterpret_cast<const uint4*>(
+                        pr.t + (size_t)min(c0 * kMatchTileRows + r, pr.nt - 1) * 128 + 16 * (idx & 7));
+                    hv[u][0] = src[0];
+                    hv[u][1] = src[1];
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int idx = base + tid + NT * u, r = idx >> 3, part = idx & 7;
+                    const int gr = c0 * kMatchTileRows + r;
+                    int nrm = 0;
+                    const i32x4 pk = codes16(hv[u][0], hv[u][1], nrm, bad);
+                    nrm += __shfl_xor(nrm, 1);
+                    nrm += __shfl_xor(nrm, 2);
+                    nrm += __shfl_xor(nrm, 4);
+                    if (idx < npieces) {  // whole rows of 8 lanes: the shuffles above stay inside a row
+                        *reinterpret_cast<i32x4*>(sc + r * 128 + 16 * piece_swz(r, part)) =
+                            gr < pr.nt ? pk : (i32x4){0, 0, 0, 0};
+                        if (part == 0)
+                            sk[r] = gr < pr.nt ? -(256 * nrm + ((gr - tbeg * kMatchTileRows) & 255)) : kPadBias;
+                    }
+                }
+            }
+        };
+        Best best[2] = {{kNone, kNone, kNone, kNone}, {kNone, kNone, kNone, kNone}};
+        if (tbeg < tend) stage(tbeg, 0);
+        int buf = 0;
+        for (int c0 = tbeg; c0 < tend; c0 += kChunkTiles, buf ^= 1) {
+            __syncthreads();  // chunk c0 is staged; every wave is done with the other buffer
+            if (c0 + kChunkTiles < tend) stage(c0 + kChunkTiles, buf ^ 1);
+            chunk_top2(s_codes[buf], s_key[buf], min(kChunkTiles, tend - c0), c0 * kMatchTileRows, col, h, bq, best);
+        }
+        res[0] = finish_best(best[0], qn[0]);
+        res[1] = finish_best(best[1], qn[1]);
+    }
+    if (__syncthreads_or(bad)) {
+        // ---- general path: fp16 values that are not integers 0..255 ----
+        res[0] = match_f16_block(pr, q0w, tbeg, tend, col, h);
+        res[1] = match_f16_block(pr, q0w + 32, tbeg, tend, col, h);
+    }
+    __syncthreads();  // s_res aliases the code tiles
+    if (h == 0) {
+        s_res[64 * w + col] = res[0];
+        s_res[64 * w + 32 + col] = res[1];
+    }
+    __syncthreads();
+    const int q = q0 + tid;
+    const bool qv = q < pr.nq;
+    const size_t o = (size_t)pr.out_off + q;
+    if (S == 1) {
+        if (qv) write_top2(s_res[tid], o, ratio, ratio_on_squared, idx2, d2out, match);
+        return;
+    }
+    merge_contribution(s_res, &s_last, keys + 2 * (size_t)q0, done + blockIdx.x, 1u, (unsigned)S, qv, o, ratio,
+                       ratio_on_squared, idx2, d2out, match);
+}
+
+// ---------------------------------------------------------------------------
+// k_match_batch: prepared sets (k_match_prep), any number of pairs.
+// grid = (query blocks of 64 NW, train splits S, pairs), 64 NW threads.  A
+// split is whole key groups of the pair's train tiles; the workgroup loads
+// each wave's query operands once and streams its split through two LDS chunk
+// buffers (the next group by LDS-DMA while this one computes: one barrier per
+// 8 tiles).  With S > 1 the splits merge through the keys scratch and the one
+// that completes the query block's count writes the outputs.
+// ---------------------------------------------------------------------------
+template <int NW>
+__global__ __launch_bounds__(64 * NW, (kMatchWgPerCu * NW) / 4) void k_match_batch(
+    MatchBatch batch, int S, int nq_stride, const int8_t* __restrict__ codes, const int* __restrict__ rowkeys,
+    int sentinel, const unsigned* __restrict__ flags, unsigned epoch, unsigned long long* __restrict__ keys,
+    unsigned* __restrict__ done, float ratio, int ratio_on_squared, int* __restrict__ idx2, float* __restrict__ d2out,
+    int* __restrict__ match) {
+    constexpr int QB = 64 * NW;
+    __shared__ __attribute__((aligned(16))) int8_t s_codes[2][kChunkTiles * kTileBytes];
+    __shared__ __attribute__((aligned(16))) int s_key[2][kChunkRows];
+    __shared__ unsigned s_last;
+    static_assert(sizeof(Top2) * QB <= sizeof(s_codes), "results alias the code tiles");
+    Top2* const s_res = reinterpret_cast<Top2*>(&s_codes[0][0]);
+    const int p = blockIdx.z;
+    const MatchPair& pr = batch.pair[p];
+    const int q0 = blockIdx.x * QB;
+    if (q0 >= pr.nq) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, col = lane & 31, h = lane >> 5;
+    const int ntiles = (pr.nt + kMatchTileRows - 1) / kMatchTileRows;
+    const int tps = ((ntiles + S - 1) / S + kGroupTiles - 1) / kGroupTiles * kGroupTiles;  // whole key groups
+    const int tb = min(ntiles, (int)blockIdx.y * tps), te = min(ntiles, tb + tps);
+    const int q0w = q0 + 64 * w;
+    Top2 res[2];
+    if (flags[pr.qset] != epoch && flags[pr.tset] != epoch) {
+        // ---- integer path ----
+        const int8_t* __restrict__ tc = codes + (size_t)pr.trow0 * 128;
+        const int* __restrict__ tk = rowkeys + pr.trow0;
+        const int8_t* __restrict__ zc = codes + (size_t)sentinel * 128;  // zero code row (padding)
+        const int* __restrict__ zk = rowkeys + sentinel;
+        i32x4 bq[2][4];
+        int qn[2];
+        load_queries(codes + (size_t)pr.qrow0 * 128, rowkeys + pr.qrow0, pr.nq, q0w, col, h, bq, qn);
+        Best best[2] = {{kNone, kNone, kNone, kNone}, {kNone, kNone, kNone, kNone}};
+        if (tb < te)
+            stage_dma<NW>(tc, tk, pr.nt, tb * kMatchTileRows, min(kChunkTiles, te - tb), zc, zk, s_codes[0], s_key[0],
+                          w, lane);
+        int buf = 0;
+        for (int c0 = tb; c0 < te; c0 += kChunkTiles, buf ^= 1) {
+            // LDS-DMA writes are counted by vmcnt: this wave's copies of the
+            // chunk have landed; the barrier publishes every wave's, and every
+            // wave is done with the other buffer.
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            const int c1 = c0 + kChunkTiles;
+            if (c1 < te)
+                stage_dma<NW>(tc, tk, pr.nt, c1 * kMatchTileRows, min(kChunkTiles, te - c1), zc, zk, s_codes[buf ^ 1],
+                              s_key[buf ^ 1], w, lane);
+            chunk_top2(s_codes[buf], s_key[buf], min(kChunkTiles, te - c0), c0 * kMatchTileRows, col, h, bq, best);
+        }
+        res[0] = finish_best(best[0], qn[0]);
+        res[1] = finish_best(best[1], qn[1]);
+    } else {
+        // ---- general path: fp16 values that are not integers 0..255 ----
+        res[0] = match_f16_block(pr, q0w, tb, te, col, h);
+        res[1] = match_f16_block(pr, q0w + 32, tb, te, col, h);
+    }
+    __syncthreads();  // s_res aliases the code tiles
+    if (h == 0) {
+        s_res[64 * w + col] = res[0];
+        s_res[64 * w + 32 + col] = res[1];
+    }
+    __syncthreads();
+    const int q = q0 + tid;
+    const bool qv = q < pr.nq;
+    const size_t o = (size_t)pr.out_off + q;
+    if (S == 1) {
+        if (qv) write_top2(s_res[tid], o, ratio, ratio_on_squared, idx2, d2out, match);
+        return;
+    }
+    merge_contribution(s_res, &s_last, keys + 2 * ((size_t)p * nq_stride + q0), done + (size_t)p * gridDim.x + blockIdx.x,
+                       1u, (unsigned)S, qv, o, ratio, ratio_on_squared, idx2, d2out, match);
+}
+
 #ifndef SIFT_MATCH_WG_TARGET_SINGLE
-#define SIFT_MATCH_WG_TARGET_SINGLE SIFT_MATCH_WG_TARGET  // single pairs (fused conversion: fewer, longer splits)
+#define SIFT_MATCH_WG_TARGET_SINGLE 256  // single pairs: workgroups a launch aims for when choosing train splits
 #endif
-    const int target = P == 1 ? SIFT_MATCH_WG_TARGET_SINGLE : SIFT_MATCH_WG_TARGET;
-    int S = (target + qblocks * P - 1) / (qblocks * P);
-    const int maxS = ntiles / 2 > 1 ? ntiles / 2 : 1;  // >= 2 tiles per split
-    S = S < maxS ? S : maxS;
-    return S < 1 ? 1 : S;
-}
-
+#ifndef SIFT_MATCH_NW_SINGLE
+#define SIFT_MATCH_NW_SINGLE 4  // single pairs: waves per workgroup (256 queries)
+#endif
 #ifndef SIFT_MATCH_FUSED_SINGLE
 #define SIFT_MATCH_FUSED_SINGLE 1  // single pairs: no prep launch (tools A/B builds set 0)
 #endif
-void launch_match(const MatchSets& sets, const MatchBatch& batch, int S, int nq_stride, int8_t* codes, int* norms,
-                  unsigned* flags, unsigned epoch, unsigned long long* keys, unsigned* done, float ratio,
-                  int ratio_on_squared, int* idx2, float* d2, int* match, hipStream_t s) {
+
+static int device_cus() {
+    static int cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        return n;
+    }();
+    return cus;
+}
+
+#ifndef SIFT_MATCH_BATCH_SLOTS
+#define SIFT_MATCH_BATCH_SLOTS 2  // batched: workgroups per CU the splits aim for (one round)
+#endif
+
+MatchPlan match_plan(int max_nq, int max_nt, int P) {
+    MatchPlan pl;
+    const int ntiles = (max_nt + kMatchTileRows - 1) / kMatchTileRows;
+    if (P == 1 && SIFT_MATCH_FUSED_SINGLE) {
+        pl.nw = SIFT_MATCH_NW_SINGLE;
+        const int qblocks = (max_nq + 64 * pl.nw - 1) / (64 * pl.nw);
+        int S = (SIFT_MATCH_WG_TARGET_SINGLE + qblocks - 1) / qblocks;
+        const int maxS = ntiles / 2 > 1 ? ntiles / 2 : 1;  // >= 2 tiles per split
+        S = S < maxS ? S : maxS;
+        pl.S = S < 1 ? 1 : S;
+    } else {
+        // As many splits as fit the chip in one round (a second, partial
+        // round costs a whole split's time), each whole key groups.
+        pl.nw = kMatchBatchNW;
+        const int qblocks = (max_nq + 64 * pl.nw - 1) / (64 * pl.nw);
+        const int groups = (ntiles + kGroupTiles - 1) / kGroupTiles;
+        int S = SIFT_MATCH_BATCH_SLOTS * device_cus() / (qblocks * P);
+        S = S < groups ? S : groups;
+        S = S < 1 ? 1 : S;
+        const int tps = ((ntiles + S - 1) / S + kGroupTiles - 1) / kGroupTiles * kGroupTiles;
+        S = tps > 0 ? (ntiles + tps - 1) / tps : 1;
+        pl.S = S < 1 ? 1 : S;
+    }
+    return pl;
+}
+
+void launch_match(const MatchSets& sets, MatchBatch& batch, const MatchPlan& plan, int nq_stride, int8_t* codes,
+                  int* rowkeys, int sentinel, unsigned* flags, unsigned epoch, unsigned long long* keys,
+                  unsigned* done, float ratio, int ratio_on_squared, int* idx2, float* d2, int* match, hipStream_t s) {
     if (batch.P == 1 && SIFT_MATCH_FUSED_SINGLE) {
-        dim3 g((max(batch.pair[0].nq, 1) + kMatchQB - 1) / kMatchQB, S, 1);
-        hipLaunchKernelGGL(k_match<true>, g, dim3(256), 0, s, batch, S, nq_stride, codes, norms, flags, epoch, keys,
-                           done, ratio, ratio_on_squared, idx2, d2, match);
+        const MatchPair& pr = batch.pair[0];
+        dim3 g((max(pr.nq, 1) + 64 * SIFT_MATCH_NW_SINGLE - 1) / (64 * SIFT_MATCH_NW_SINGLE), plan.S, 1);
+        hipLaunchKernelGGL(k_match_single<SIFT_MATCH_NW_SINGLE>, g, dim3(64 * SIFT_MATCH_NW_SINGLE), 0, s, pr, plan.S,
+                           keys, done, ratio, ratio_on_squared, idx2, d2, match);
         return;
     }
     if (sets.maxn > 0)
-        hipLaunchKernelGGL(k_match_prep, dim3((sets.maxn + 31) / 32, sets.nsets), dim3(256), 0, s, sets, codes, norms,
+        hipLaunchKernelGGL(k_match_prep, dim3((sets.maxn + 31) / 32, sets.nsets), dim3(256), 0, s, sets, codes, rowkeys,
                            flags, epoch);
     int max_nq = 1;
     for (int p = 0; p < batch.P; p++) max_nq = max(max_nq, batch.pair[p].nq);
-    dim3 g((max_nq + kMatchQB - 1) / kMatchQB, S, batch.P);
-    hipLaunchKernelGGL(k_match<false>, g, dim3(256), 0, s, batch, S, nq_stride, codes, norms, flags, epoch, keys, done, ratio,
-                       ratio_on_squared, idx2, d2, match);
+    dim3 g((max_nq + 64 * kMatchBatchNW - 1) / (64 * kMatchBatchNW), plan.S, batch.P);
+    hipLaunchKernelGGL(k_match_batch<kMatchBatchNW>, g, dim3(64 * kMatchBatchNW), 0, s, batch, plan.S, nq_stride, codes,
+                       rowkeys, sentinel, flags, epoch, keys, done, ratio, ratio_on_squared, idx2, d2, match);
 }
 
 }  // namespace sift_amd

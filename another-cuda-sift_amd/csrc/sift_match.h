@@ -6,8 +6,11 @@
 namespace sift_amd {
 
 constexpr int kMaxMatchPairs = 64;
-constexpr int kMatchQB = 256;       // queries per workgroup: 4 waves x 64
-constexpr int kMatchTileRows = 32;  // train rows per LDS tile
+constexpr int kMatchQB = 256;       // queries per workgroup, smallest plan (4 waves x 64; 8 waves: 512)
+constexpr int kMatchTileRows = 32;  // train rows per MFMA tile
+constexpr int kChunkTiles = 8;      // train tiles per LDS chunk (32 KiB of codes + 1 KiB of keys, double buffered)
+constexpr int kMatchWgPerCu = 2;    // workgroups per CU the kernel is register-budgeted for
+constexpr int kMatchPadKey = -2140000000;  // key bias of a padding row (below every valid key)
 
 struct MatchPair {
     const uint16_t* q;  // nq x 128 half, row-major
@@ -36,13 +39,23 @@ struct MatchSets {
     int nsets, maxn;
 };
 
-int match_splits(int max_nq, int max_nt, int P);
-// codes / norms: int8 code rows (128 B) and |code|^2 per row, capacity for the
+// Launch plan: waves per workgroup (64 queries per wave) and, for the fused
+// single-pair kernel, train splits S (the train tiles are cut into S
+// contiguous ranges, one workgroup per (query block, range), merged through
+// the keys scratch); batched splits are whole key groups.
+struct MatchPlan {
+    int nw, S;
+};
+MatchPlan match_plan(int max_nq, int max_nt, int P);
+// codes / rowkeys: int8 code rows (128 B) and per row the key bias
+// -(256 |code|^2 + (row mod 256)); row `sentinel` of both is a zero code row with
+// the padding key (written once at allocation, never by a call); capacity for the
 // call's sets; flags: one word per set slot, == epoch when that set holds a
 // value that is not an integer 0..255 (matched by the general f16 path).
 // keys: 2 x u64 per (pair, query), all ones between calls; done: a counter per
-// (pair, 256-query block), zero between calls (the merging workgroup resets both).
-void launch_match(const MatchSets& sets, const MatchBatch& batch, int S, int nq_stride, int8_t* codes, int* norms,
+// (pair, kMatchQB-query block), zero between calls (the merging workgroup resets both).
+void launch_match(const MatchSets& sets, MatchBatch& batch, const MatchPlan& plan, int nq_stride, int8_t* codes,
+                  int* rowkeys, int sentinel,
                   unsigned* flags, unsigned epoch, unsigned long long* keys, unsigned* done, float ratio,
                   int ratio_on_squared, int* idx2, float* d2, int* match, hipStream_t s);
 

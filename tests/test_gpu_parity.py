@@ -261,6 +261,51 @@ def test_match_batched_equals_pairs(sift, oracle):
         off += n
 
 
+def test_match_batched_ragged_ranges(sift, oracle):
+    """The persistent batched matcher cuts the (pair, query block, train tile)
+    sequence into equal ranges per workgroup: ragged pairs put range edges in
+    the middle of key groups and query blocks, so the same query block merges
+    contributions of several workgroups.  Ties between far-apart train rows,
+    a pair without train rows and a pair without queries, three calls on one
+    matcher (the merge restores keys and counters)."""
+    rng = np.random.default_rng(23)
+    shapes = [(700, 1999), (513, 33), (1, 2500), (64, 0), (0, 100), (1200, 257), (37, 5), (2000, 2000)]
+    qs, ts = [], []
+    for nq, nt in shapes:
+        q = rng.integers(0, 256, (nq, 128)).astype(np.float32)
+        t = rng.integers(0, 256, (nt, 128)).astype(np.float32)
+        if nt > 1900:
+            t[1800] = t[5]  # same row in different key groups / ranges
+            t[300] = t[5]
+            if nq > 2:
+                q[2] = t[5]
+        qs.append(q)
+        ts.append(t)
+    dq = [sift.DeviceArray.from_numpy(_half_rows(q)) if len(q) else None for q in qs]
+    dt = [sift.DeviceArray.from_numpy(_half_rows(t)) if len(t) else None for t in ts]
+    tot = sum(n for n, _ in shapes)
+    m = sift.Matcher(2000, 2500, max_pairs=len(shapes))
+    for rep in range(3):
+        idx2, d2 = sift.DeviceArray(tot * 8), sift.DeviceArray(tot * 8)
+        m.match_batched([d.value if d else 0 for d in dq], [n for n, _ in shapes],
+                        [d.value if d else 0 for d in dt], [n for _, n in shapes],
+                        idx2_ptr=idx2.value, d2_ptr=d2.value)
+        gi = idx2.to_numpy(np.int32, (tot, 2))
+        gd = d2.to_numpy(np.float32, (tot, 2))
+        off = 0
+        for (nq, nt), q, t in zip(shapes, qs, ts):
+            if nq:
+                if nt:
+                    oi, od = oracle.knn2(q, t)
+                else:
+                    oi, od = np.full((nq, 2), -1, np.int32), None
+                assert np.array_equal(gi[off:off + nq], oi), (rep, nq, nt)
+                if od is not None:
+                    valid = oi >= 0
+                    assert np.array_equal(np.sqrt(gd[off:off + nq][valid]).astype(np.float32), od[valid])
+            off += nq
+
+
 def test_c1_frame_pair_match(sift, oracle):
     """BASELINE C1 end to end: cv::SIFT defaults (upscale, keep all) on frames 0
     and 1 at 752x480, then BFMatcher(NORM_L2).knnMatch(k=2) + ratio 0.8 on
