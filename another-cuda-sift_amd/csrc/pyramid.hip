@@ -144,9 +144,6 @@ template <int R>
 constexpr int blur_org() {  // tile column 0 = image column x0 - ORG
     return SIFT_BLUR_X4LD && R <= 8 ? 8 : R;
 }
-#ifndef SIFT_BLUR_STRIP
-#define SIFT_BLUR_STRIP 0  // large float jobs: row-streaming kernel (k_blur_strip; measured slower than the tile kernel so far)
-#endif
 #ifndef SIFT_BLUR_IW112
 #define SIFT_BLUR_IW112 1  // radius 11..24: pitch 112 (16 mod 32) -- 4 workgroups per CU either way at R = 13
 #endif
@@ -509,385 +506,6 @@ __global__ __launch_bounds__(64 * NW) void k_blur2(BlurJob A, BlurJob B) {
         blur_tile<RB, float, NW>(B, blockIdx.x - na, in);
 }
 
-
-// ---------------------------------------------------------------------------
-// Row-streaming separable blur for large launches (the octave-0 / octave-1
-// planes of frame batches).  A 2-D tile re-reads a halo on all four sides and
-// lives through a load -> passes -> store chain: the 64x64 tile pattern moves
-// bytes at 4.4 TB/s even without arithmetic, a row-streaming copy of the same
-// frames at 6.0-6.3 TB/s (tools/blur_pattern_bench.hip).  Here a 4-wave
-// workgroup owns a strip of ST_SW = 128 output columns over a segment of rows
-// and walks down it ST_CH = 16 rows per iteration:
-//   row pass     the iteration's 16 input rows (staged in LDS, columns
-//                x0 - 16 .. x0 + 143) -> 16 rows of horizontal results in a
-//                64-row LDS ring (OpenCV's row-filter order, as blur_tile);
-//   staging      the next iteration's input rows (loaded into registers one
-//                iteration earlier still) -> the other staging buffer;
-//   loads        the rows of the iteration after next;
-//   one barrier;
-//   column pass  16 output rows, lagging the row pass by LC = ceil(2R/16)
-//                iterations: column c, 8 rows per thread from 8 + 2R ring
-//                rows (pairs (y, y+4), symmetric taps, as blur_tile).
-// Only the horizontal halo (32 columns) and the segment's 2R boundary rows are
-// read twice; loads of two iterations are in flight behind the passes.  Output
-// floats are bit-identical to blur_tile's (same operations per output).
-// ---------------------------------------------------------------------------
-constexpr int ST_SW = 128;                  // output columns per strip
-constexpr int ST_CH = 16;                   // rows per iteration
-constexpr int ST_ORG = 16;                  // staged row = image columns x0 - ST_ORG ..
-constexpr int ST_IW = ST_SW + 2 * ST_ORG;   // 160 floats per staged row
-constexpr int ST_RING = 64;                 // ring rows of row-pass results
-constexpr int ST_SLOTS = ST_CH * ST_IW / 4;  // float4 slots per staged chunk (640)
-constexpr int ST_LPT = (ST_SLOTS + 255) / 256;  // staging loads per thread (3)
-
-// Row pass of one staged row: 4 outputs from the window starting at the
-// staged column xq - R + ST_ORG (OpenCV's row-filter operation order, packed
-// in pairs exactly as blur_tile's row pass).
-template <int R>
-__device__ __forceinline__ void strip_row4(const float* __restrict__ srow, float* __restrict__ dst4,
-                                           const Taps& taps) {
-    typedef float f4 __attribute__((ext_vector_type(4)));
-    constexpr int SA = (ST_ORG - R) & ~3, SS = (ST_ORG - R) & 3;  // aligned window start, shift
-    constexpr int NWV = (SS + 2 * R + 4 + 3) / 4;                 // float4 reads per window
-    float win[4 * NWV];
-    const f4* p = reinterpret_cast<const f4*>(srow + SA);
-#pragma unroll
-    for (int v = 0; v < NWV; v++) {
-        f4 t = p[v];
-        __asm__ volatile("" : "+v"(t));
-        win[4 * v] = t[0];
-        win[4 * v + 1] = t[1];
-        win[4 * v + 2] = t[2];
-        win[4 * v + 3] = t[3];
-    }
-    f32x2 pe[2 * NWV], po[2 * NWV - 1];
-#pragma unroll
-    for (int j = 0; j < 2 * NWV; j++) pe[j] = (f32x2){win[2 * j], win[2 * j + 1]};
-#pragma unroll
-    for (int j = 0; j < 2 * NWV - 1; j++) po[j] = pk_mov_hi_lo(pe[j], pe[j + 1]);
-    f32x2 s2[2];
-#pragma unroll
-    for (int hq = 0; hq < 2; hq++) {
-        const int q = 2 * hq;
-        if constexpr (2 * R + 1 > 5) {
-            f32x2 a = {0.f, 0.f};
-#pragma unroll
-            for (int k = 0; k <= 2 * R; k++) {
-                const int i = q + k + SS;
-                a = __builtin_elementwise_fma((i & 1) ? po[i >> 1] : pe[i >> 1], (f32x2)taps.w[k], a);
-            }
-            s2[hq] = a;
-        } else {
-            const int c = q + R + SS;
-            f32x2 a = ((c & 1) ? po[c >> 1] : pe[c >> 1]) * (f32x2)taps.w[R];
-#pragma unroll
-            for (int k = 1; k <= R; k++) {
-                const int il = q + R - k + SS, ir = q + R + k + SS;
-                a = __builtin_elementwise_fma(((il & 1) ? po[il >> 1] : pe[il >> 1]) + ((ir & 1) ? po[ir >> 1] : pe[ir >> 1]),
-                                              (f32x2)taps.w[R + k], a);
-            }
-            s2[hq] = a;
-        }
-    }
-    *reinterpret_cast<f4*>(dst4) = (f4){s2[0][0], s2[0][1], s2[1][0], s2[1][1]};
-}
-
-// Column pass: 8 outputs of one column from ring rows M0 .. M0 + 7 + 2R (mod
-// ST_RING), pairs (y, y + 4) and symmetric taps exactly as blur_tile's.
-template <int R, int M0>
-__device__ __forceinline__ void strip_col8(const float* __restrict__ col, const Taps& taps, float out[8]) {
-    f32x2 cp[4 + 2 * R];
-#pragma unroll
-    for (int j = 0; j < 4 + 2 * R; j++)
-        cp[j] = (f32x2){col[((M0 + j) & (ST_RING - 1)) * ST_SW], col[((M0 + j + 4) & (ST_RING - 1)) * ST_SW]};
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        f32x2 a = __builtin_elementwise_fma(cp[q + R], (f32x2)taps.w[R], (f32x2){0.f, 0.f});
-#pragma unroll
-        for (int k = 1; k <= R; k++) a = __builtin_elementwise_fma(cp[q + R + k] + cp[q + R - k], (f32x2)taps.w[R + k], a);
-        out[q] = a[0];
-        out[q + 4] = a[1];
-    }
-}
-
-struct StripJob {
-    const void* src;  // float, or uint8_t (the frame's first blur of an 8-bit frame)
-    float* dst;
-    unsigned* range_keys;
-    Counters* zero_ctr;
-    int spitch, W, H, dpitch;
-    int strips, seg, nseg;  // strips per row band, rows per segment (multiple of ST_CH), segments per frame
-    int nf;
-    long sfs, dfs;
-    Taps taps;
-};
-
-template <int R, typename T>
-struct StripStage {
-    typedef float f4 __attribute__((ext_vector_type(4)));
-    f4 v[ST_LPT];
-};
-
-template <int R, typename T>
-__global__ __launch_bounds__(256, 3) void k_blur_strip(StripJob J) {
-    constexpr int LC = (2 * R + ST_CH - 1) / ST_CH;  // column-pass lag (iterations)
-    static_assert(R <= ST_ORG && LC <= 2, "ring and staging sized for R <= 16");
-    typedef float f4 __attribute__((ext_vector_type(4)));
-    __shared__ __attribute__((aligned(16))) float stg[2][ST_CH * ST_IW];
-    __shared__ __attribute__((aligned(16))) float mid[ST_RING * ST_SW];
-    const int per_frame = J.strips * J.nseg;
-    const int b = xcd_tile(blockIdx.x, per_frame * J.nf);
-    const int f = b / per_frame, rem = b - f * per_frame, seg = rem / J.strips, strip = rem - seg * J.strips;
-    const T* __restrict__ src = fptr(static_cast<const T*>(J.src), f * J.sfs);
-    float* __restrict__ dst = fptr(J.dst, f * J.dfs);
-    unsigned* __restrict__ range_keys = J.range_keys ? fptr(J.range_keys, f * J.dfs) : nullptr;
-    const int W = J.W, H = J.H, spitch = J.spitch, dpitch = J.dpitch;
-    const int x0 = strip * ST_SW, ys = seg * J.seg, ye = min(H, ys + J.seg);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (J.zero_ctr && b == f * per_frame && tid < (int)(sizeof(Counters) / 4))
-        reinterpret_cast<unsigned*>(fptr(J.zero_ctr, f * J.dfs))[tid] = 0u;
-    const Taps& taps = J.taps;
-    const int nout = (ye - ys + ST_CH - 1) / ST_CH;  // column-pass iterations
-    const int iters = nout + LC;                      // row-pass iterations
-
-    // ---- staging loads: chunk i = image rows ys - R + 16 i + rr, rr < 16.
-    // Buffer loads (wave-uniform resource, no flat addressing); interior strips
-    // (uniform per workgroup) load 16-byte pieces, the two border strips one
-    // reflected column per dword.  The pipeline below is instantiated for each
-    // case, so no branch joins a loaded register. ----
-    const bool interior = x0 >= ST_ORG && x0 + ST_SW + ST_ORG <= W;  // uniform
-    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<T*>(src), 0, (int)min((long)spitch * H * (long)sizeof(T), 0x7fffffffL), 0x00020000);
-    auto load_chunk = [&](int i, StripStage<R, T>& st, auto inner) __attribute__((always_inline)) {
-        constexpr bool INNER = decltype(inner)::value;
-#pragma unroll
-        for (int u = 0; u < ST_LPT; u++) {
-            const int s = min(tid + 256 * u, ST_SLOTS - 1), rr = s / (ST_IW / 4), q = s - rr * (ST_IW / 4);
-            int y = ys - R + ST_CH * i + rr;
-            y = y < 0 ? -y : (y >= H ? 2 * H - 2 - y : y);  // reflect-101 (|offset| <= R < H)
-            y = min(max(y, 0), H - 1);                       // rows past the segment's need: any row
-            const int xs = x0 - ST_ORG + 4 * q;
-            if constexpr (INNER) {
-                if constexpr (sizeof(T) == 4) {
-                    st.v[u] = __builtin_bit_cast(
-                        f4, __builtin_amdgcn_raw_buffer_load_b128(srs, (unsigned)(y * spitch + xs) * 4u, 0, 0));
-                } else {
-                    const unsigned wd = __builtin_amdgcn_raw_buffer_load_b32(srs, (unsigned)(y * spitch + xs), 0, 0);
-                    st.v[u] = (f4){(float)(wd & 255u), (float)((wd >> 8) & 255u), (float)((wd >> 16) & 255u),
-                                   (float)(wd >> 24)};
-                }
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    int x = xs + e;
-                    x = x < 0 ? -x : (x >= W ? 2 * W - 2 - x : x);
-                    x = min(max(x, 0), W - 1);
-                    if constexpr (sizeof(T) == 4)
-                        st.v[u][e] = __builtin_bit_cast(
-                            float, __builtin_amdgcn_raw_buffer_load_b32(srs, (unsigned)(y * spitch + x) * 4u, 0, 0));
-                    else
-                        st.v[u][e] = (float)__builtin_amdgcn_raw_buffer_load_b8(srs, (unsigned)(y * spitch + x), 0, 0);
-                }
-            }
-        }
-    };
-    auto store_chunk = [&](const StripStage<R, T>& st, int buf) __attribute__((always_inline)) {
-#pragma unroll
-        for (int u = 0; u < ST_LPT; u++)
-            if (u < ST_LPT - 1 || tid + 256 * u < ST_SLOTS)
-                *reinterpret_cast<f4*>(&stg[buf][4 * (tid + 256 * u)]) = st.v[u];
-    };
-
-    // ---- row pass: lane -> (row, 4-column block); each 16-lane ds_read_b128
-    // group {0-3,12-15,20-27} / {4-11,16-19,28-31} (+32) reads 16 consecutive
-    // blocks of one row (conflict-free) ----
-    const int l = lane & 31;
-    const bool grpB = (l >= 4 && l < 12) || (l >= 16 && l < 20) || l >= 28;
-    const int blk = (grpB ? 16 : 0) + (grpB ? (l < 12 ? l - 4 : (l < 20 ? l - 8 : l - 16))
-                                            : (l < 4 ? l : (l < 16 ? l - 8 : l - 12)));
-    const int xq = 4 * blk;
-    const int rrow = 2 * wave + (lane >> 5);  // rows rrow and rrow + 8 of the chunk
-    auto row_pass = [&](int buf, int ring0) __attribute__((always_inline)) {
-#pragma unroll
-        for (int hh = 0; hh < 2; hh++) {
-            const int rr = rrow + 8 * hh;
-            strip_row4<R>(&stg[buf][rr * ST_IW + xq], &mid[((ring0 + rr) & (ST_RING - 1)) * ST_SW + xq], taps);
-        }
-    };
-
-    // ---- column pass: wave w -> columns 64 (w & 1) + lane, rows 8 (w >> 1) ..
-    // + 7 of the output chunk; M0 = first ring row of the window (compile
-    // time, so the ring wrap is resolved at compile time) ----
-    const int cc = 64 * (wave & 1) + lane, gx = x0 + cc;
-    const bool colv = gx < W;
-    float mx = -FLT_MAX, nmn = -FLT_MAX;
-    auto col_pass = [&](auto m0c, int y0) __attribute__((always_inline)) {
-        constexpr int M0 = decltype(m0c)::value;
-        float out[8];
-        strip_col8<R, M0>(mid + cc, taps, out);
-        // Stores without branches (a store under exec masking makes the
-        // compiler wait for every outstanding load at the next use of the
-        // register ring): rows past the segment or columns past W get an
-        // offset past the buffer's records, which the hardware drops.
-        const __amdgpu_buffer_rsrc_t drs =
-            __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)min((long)dpitch * H * 4, 0x7fffffffL), 0x00020000);
-        const unsigned voff = (unsigned)(y0 * dpitch + gx) * 4u;
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const bool ok = colv && y0 + q < ye;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, out[q]), drs,
-                                                  ok ? voff + (unsigned)(q * dpitch * 4) : 0x80000000u, 0, 0);
-            if (range_keys) {
-                mx = ok ? fmaxf(mx, out[q]) : mx;
-                nmn = ok ? fmaxf(nmn, -out[q]) : nmn;
-            }
-        }
-    };
-    // Ring row of image row ys - R + m is m mod 64; output row ys + 16 j + 8 h
-    // needs ring rows from 16 j + 8 h on.
-    const int half = wave >> 1;
-    auto col_iter = [&](auto jm, int j) __attribute__((always_inline)) {  // jm = j mod 4 (compile time)
-        constexpr int JM = decltype(jm)::value;
-        const int y0 = ys + ST_CH * j + 8 * half;
-        if (half)
-            col_pass(std::integral_constant<int, (16 * JM + 8) & (ST_RING - 1)>{}, y0);
-        else
-            col_pass(std::integral_constant<int, (16 * JM) & (ST_RING - 1)>{}, y0);
-    };
-
-    auto run = [&](auto inner) __attribute__((always_inline)) {
-        StripStage<R, T> ra, rb;  // register ring: chunk i + 1 in ra / rb by parity
-        load_chunk(0, ra, inner);
-        load_chunk(1, rb, inner);
-        store_chunk(ra, 0);
-        load_chunk(2, ra, inner);
-        lds_barrier();
-        // One step of the pipeline for iteration i (IM = i mod 4, compile time).
-        // Every step runs unconditionally (the iteration count is padded to a
-        // multiple of 4; loads past the segment read clamped rows, column
-        // passes past it store nothing): a load under a branch would make the
-        // compiler copy -- and so wait for -- the register ring at the join.
-        auto step = [&](auto im, int i) __attribute__((always_inline)) {
-            constexpr int IM = decltype(im)::value;
-            row_pass(IM & 1, 16 * IM);
-            // chunk i + 1 (loaded at iteration i - 1) -> staging buffer (i + 1) & 1
-            if constexpr ((IM & 1) == 0) {
-                store_chunk(rb, 1);
-                load_chunk(i + 3, rb, inner);
-            } else {
-                store_chunk(ra, 0);
-                load_chunk(i + 3, ra, inner);
-            }
-            lds_barrier();
-            const int j = i - LC;
-            if (j >= 0) col_iter(std::integral_constant<int, (IM - LC + 4) & 3>{}, j);
-        };
-        for (int i = 0; i < iters; i += 4) {
-            step(std::integral_constant<int, 0>{}, i);
-            step(std::integral_constant<int, 1>{}, i + 1);
-            step(std::integral_constant<int, 2>{}, i + 2);
-            step(std::integral_constant<int, 3>{}, i + 3);
-        }
-    };
-    if (interior)
-        run(std::true_type{});
-    else
-        run(std::false_type{});
-    if (range_keys) {
-        for (int off = 32; off > 0; off >>= 1) {
-            mx = fmaxf(mx, __shfl_xor(mx, off));
-            nmn = fmaxf(nmn, __shfl_xor(nmn, off));
-        }
-        __shared__ float part[8];
-        if (lane == 0) {
-            part[wave] = mx;
-            part[4 + wave] = nmn;
-        }
-        lds_barrier();
-        if (tid == 0) {
-            unsigned* slot = range_keys + 2 * (rem % kRangeSlots);
-            atomicMax(slot, range_key(fmaxf(fmaxf(part[0], part[1]), fmaxf(part[2], part[3]))));
-            atomicMax(slot + 1, range_key(fmaxf(fmaxf(part[4], part[5]), fmaxf(part[6], part[7]))));
-        }
-    }
-}
-
-#ifndef SIFT_BLUR_STRIP_MIN_PX
-#define SIFT_BLUR_STRIP_MIN_PX (4L << 20)  // launches of at least this many output pixels stream rows
-#endif
-#ifndef SIFT_BLUR_STRIP_WG_PER_CU
-#define SIFT_BLUR_STRIP_WG_PER_CU 3  // 52 KiB of LDS per workgroup
-#endif
-#ifndef SIFT_BLUR_STRIP_ROUNDS
-#define SIFT_BLUR_STRIP_ROUNDS 1  // workgroups per resident slot the segments aim for
-#endif
-
-static int blur_device_cus() {
-    static int cus = [] {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
-        return n;
-    }();
-    return cus;
-}
-
-// A float job the row-streaming kernel takes: plain (no decimation, no base
-// copy), a radius it is instantiated for, 16-byte aligned rows, a frame wide
-// and tall enough for single reflections, and enough pixels to fill the chip.
-static bool strip_eligible(const BlurJob& j) {
-    const int r = j.taps.n >> 1;
-    if (!(r == 5 || r == 6 || r == 8 || r == 10 || r == 13)) return false;
-    if (j.sstep != 1 || j.copy_out) return false;
-    if (j.W < ST_SW || j.H <= 2 * r + 1 || j.W <= 2 * r + 1) return false;
-    if ((j.spitch & 3) || (reinterpret_cast<uintptr_t>(j.src) & 15) || (j.sfs & 15)) return false;
-    return (long)j.nf * j.W * j.H >= SIFT_BLUR_STRIP_MIN_PX;
-}
-
-template <int R>
-static void strip_launch(const BlurJob& j, hipStream_t s) {
-    StripJob sj;
-    sj.src = j.src;
-    sj.dst = j.dst;
-    sj.range_keys = j.range_keys;
-    sj.zero_ctr = j.zero_ctr;
-    sj.spitch = j.spitch;
-    sj.W = j.W;
-    sj.H = j.H;
-    sj.dpitch = j.dpitch;
-    sj.strips = (j.W + ST_SW - 1) / ST_SW;
-    sj.nf = j.nf;
-    sj.sfs = j.sfs;
-    sj.dfs = j.dfs;
-    sj.taps = j.taps;
-    // Segments: about SIFT_BLUR_STRIP_ROUNDS workgroups per resident slot.
-    const long slots = (long)SIFT_BLUR_STRIP_WG_PER_CU * blur_device_cus() * SIFT_BLUR_STRIP_ROUNDS;
-    int nseg = (int)(slots / ((long)sj.strips * j.nf));
-    nseg = max(1, min(nseg, (j.H + ST_CH - 1) / ST_CH));
-    // Column-pass iterations per segment: nout with nout + LC a multiple of 4
-    // (the kernel runs whole groups of 4 iterations).
-    constexpr int LC = (2 * R + ST_CH - 1) / ST_CH;
-    int nout = (j.H + nseg - 1) / nseg;
-    nout = (nout + ST_CH - 1) / ST_CH;
-    nout = ((nout + LC + 3) / 4) * 4 - LC;
-    sj.seg = nout * ST_CH;
-    sj.nseg = (j.H + sj.seg - 1) / sj.seg;
-    hipLaunchKernelGGL((k_blur_strip<R, float>), dim3(sj.strips * sj.nseg * j.nf), dim3(256), 0, s, sj);
-}
-
-static bool try_strip(const BlurJob& j, hipStream_t s) {
-    if (!strip_eligible(j)) return false;
-    switch (j.taps.n >> 1) {
-        case 5: strip_launch<5>(j, s); return true;
-        case 6: strip_launch<6>(j, s); return true;
-        case 8: strip_launch<8>(j, s); return true;
-        case 10: strip_launch<10>(j, s); return true;
-        case 13: strip_launch<13>(j, s); return true;
-        default: return false;
-    }
-}
-
 static BlurJob make_job(const void* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, float* copy_out,
                         const Taps& taps, unsigned* range_keys, Counters* zero_ctr, const Frames& fr, long sfs) {
     BlurJob j;
@@ -914,7 +532,6 @@ using BlurLaunch = void (*)(const BlurJob&, hipStream_t);
 
 template <int R>
 void blur_launch_r(const BlurJob& j, hipStream_t s) {
-    if (SIFT_BLUR_STRIP && try_strip(j, s)) return;
     const int tiles = j.ntiles * j.nf;
     if (blur_waves(tiles) == 4)
         hipLaunchKernelGGL((k_blur<R, float, 4>), dim3(tiles), dim3(256), 0, s, j);
@@ -939,8 +556,6 @@ void blur2_launch(const BlurJob& a, const BlurJob& b, hipStream_t s) {
         hipLaunchKernelGGL((k_blur2<RA, RB, 8>), dim3(tiles), dim3(512), 0, s, a, b);
 }
 bool launch_blur_pair_jobs(const BlurJob& a, const BlurJob& b, hipStream_t s) {
-    // A job the row-streaming kernel takes runs in its own launch.
-    if (SIFT_BLUR_STRIP && (strip_eligible(a) || strip_eligible(b))) return false;
     const int ra = a.taps.n >> 1, rb = b.taps.n >> 1;
 #define SIFT_PAIR(X, Y)                      \
     if (ra == X && rb == Y) {                \

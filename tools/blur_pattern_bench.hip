@@ -2,9 +2,9 @@
 // 1920x1200 fp32 frames copied (read once + written once, 295 MB moved) by
 //   d2d      hipMemcpyAsync
 //   flat     a grid-stride float4 copy
-//   tile     the k_blur tile pattern: one 64x64 output tile per 4-wave
-//            workgroup, the (64+16)^2 input window loaded as float4 (all
-//            loads in flight), staged in LDS, barrier, 64x64 stored as float4
+//   tile     the k_blur tile pattern: one TW x TH output tile per workgroup,
+//            the (TW+16) x (TH+16) input window loaded as float4 (all loads
+//            in flight), staged in LDS, barrier, TW x TH stored as float4
 //   strip    a row-streaming pattern: a workgroup owns SW (64, 128) columns x SEG rows
 //            (+16 halo rows read), one pass = 256/(SW/4) rows, loads kept D
 //            passes ahead in registers, each pass staged through an LDS ring
@@ -31,34 +31,49 @@ __global__ __launch_bounds__(256) void k_flat(const float4* __restrict__ a, floa
     for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) b[i] = a[i];
 }
 
-// Tile pattern: blockIdx.x -> (frame, tile); 30 x 19 tiles per frame.
-__global__ __launch_bounds__(256) void k_tile(const float* __restrict__ a, float* __restrict__ b) {
-    __shared__ __attribute__((aligned(16))) float lds[80 * 80];
-    constexpr int TX = W / 64, TY = (H + 63) / 64;
-    const int f = blockIdx.x / (TX * TY), t = blockIdx.x % (TX * TY);
-    const int x0 = (t % TX) * 64, y0 = (t / TX) * 64;
+// Tile pattern: blockIdx.x -> (frame, tile), TW x TH output tiles, the
+// (TW + 16) x (TH + 16) window loaded as float4 (all loads in flight), staged in
+// LDS, barrier, the TW x TH interior stored as float4.
+// XCD k gets a contiguous run of tiles in raster order (as the blur's
+// xcd_tile): vertically adjacent tiles share an L2 for their halo rows.
+__device__ __forceinline__ int xcd_tile(int b, int ntiles) {
+    const int q = ntiles >> 3, rem = ntiles & 7, k = b & 7, i = b >> 3;
+    return k * q + min(k, rem) + i;
+}
+
+template <int TW, int TH, int NT, bool XCD>
+__global__ __launch_bounds__(NT) void k_tile(const float* __restrict__ a, float* __restrict__ b) {
+    constexpr int IW = TW + 16, IH = TH + 16, NQ = IW / 4 * IH, LPT = (NQ + NT - 1) / NT, SPT = TW * TH / 4 / NT;
+    __shared__ __attribute__((aligned(16))) float lds[IW * IH];
+    constexpr int TX = W / TW, TY = (H + TH - 1) / TH;
+    const int bid = XCD ? xcd_tile(blockIdx.x, NF * TX * TY) : blockIdx.x;
+    const int f = bid / (TX * TY), t = bid % (TX * TY);
+    const int x0 = (t % TX) * TW, y0 = (t / TX) * TH;
     const float* src = a + (size_t)f * W * H;
     float* dst = b + (size_t)f * W * H;
     const int tid = threadIdx.x;
-    float4 v[7];
+    float4 v[LPT];
 #pragma unroll
-    for (int u = 0; u < 7; u++) {
-        const int idx = min(tid + 256 * u, 1599), row = idx / 20, q = idx % 20;
+    for (int u = 0; u < LPT; u++) {
+        const int idx = min(tid + NT * u, NQ - 1), row = idx / (IW / 4), q = idx % (IW / 4);
         const int gy = min(max(y0 - 8 + row, 0), H - 1), gx = min(max(x0 - 8 + 4 * q, 0), W - 4);
         v[u] = *reinterpret_cast<const float4*>(src + (size_t)gy * W + gx);
     }
 #pragma unroll
-    for (int u = 0; u < 7; u++)
-        if (tid + 256 * u < 1600) *reinterpret_cast<float4*>(lds + 4 * (tid + 256 * u)) = v[u];
+    for (int u = 0; u < LPT; u++)
+        if (tid + NT * u < NQ) *reinterpret_cast<float4*>(lds + 4 * (tid + NT * u)) = v[u];
     __syncthreads();
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-        const int idx = tid + 256 * u, row = idx >> 4, q = idx & 15;
+    for (int u = 0; u < SPT; u++) {
+        const int idx = tid + NT * u, row = idx / (TW / 4), q = idx % (TW / 4);
         if (y0 + row < H)
             *reinterpret_cast<float4*>(dst + (size_t)(y0 + row) * W + x0 + 4 * q) =
-                *reinterpret_cast<const float4*>(lds + (row + 8) * 80 + 8 + 4 * q);
+                *reinterpret_cast<const float4*>(lds + (row + 8) * IW + 8 + 4 * q);
     }
 }
+
+template <int TW, int TH, int NT, bool XCD>
+static void tile(const float* a, float* b, hipStream_t s, int iters);
 
 // Strip pattern: blockIdx.x -> (frame, strip, segment).
 template <int SW, int SEG, int D>
@@ -114,6 +129,16 @@ static double time_us(int iters, hipStream_t s, F&& f) {
     return ms * 1e3 / iters;
 }
 
+template <int TW, int TH, int NT, bool XCD>
+static void tile(const float* a, float* b, hipStream_t s, int iters) {
+    constexpr int TX = W / TW, TY = (H + TH - 1) / TH;
+    const double us = time_us(iters, s, [&] {
+        hipLaunchKernelGGL((k_tile<TW, TH, NT, XCD>), dim3(NF * TX * TY), dim3(NT), 0, s, a, b);
+    });
+    std::printf("{\"pattern\": \"tile\", \"TW\": %d, \"TH\": %d, \"threads\": %d, \"xcd\": %d, \"wgs\": %d, \"us\": %.2f, \"TBps\": %.3f}\n",
+                TW, TH, NT, (int)XCD, NF * TX * TY, us, 2.0 * NF * W * H * 4 / us / 1e6);
+}
+
 template <int SW, int SEG, int D>
 static void strip(const float* a, float* b, hipStream_t s, int iters) {
     constexpr int NS = W / SW, NSEG = (H + SEG - 1) / SEG;
@@ -142,15 +167,15 @@ int main(int argc, char** argv) {
         });
         std::printf("{\"pattern\": \"flat\", \"wgs\": %d, \"us\": %.2f, \"TBps\": %.3f}\n", g, us, bytes / us / 1e6);
     }
-    us = time_us(iters, s, [&] { hipLaunchKernelGGL(k_tile, dim3(NF * 30 * 19), dim3(256), 0, s, a, b); });
-    std::printf("{\"pattern\": \"tile\", \"wgs\": %d, \"us\": %.2f, \"TBps\": %.3f}\n", NF * 30 * 19, us, bytes / us / 1e6);
-    strip<128, 150, 2>(a, b, s, iters);
-    strip<128, 150, 4>(a, b, s, iters);
+    tile<64, 64, 256, false>(a, b, s, iters);
+    tile<64, 64, 256, true>(a, b, s, iters);
+    tile<64, 64, 512, true>(a, b, s, iters);
+    tile<128, 64, 512, true>(a, b, s, iters);
+    tile<192, 64, 512, true>(a, b, s, iters);
+    tile<240, 32, 512, false>(a, b, s, iters);
+    tile<240, 32, 512, true>(a, b, s, iters);
+    tile<240, 64, 512, true>(a, b, s, iters);
+    tile<128, 32, 256, true>(a, b, s, iters);
     strip<128, 300, 4>(a, b, s, iters);
-    strip<128, 75, 4>(a, b, s, iters);
-    strip<128, 600, 4>(a, b, s, iters);
-    strip<64, 150, 4>(a, b, s, iters);
-    strip<64, 300, 8>(a, b, s, iters);
-    strip<64, 600, 8>(a, b, s, iters);
     return 0;
 }
