@@ -102,6 +102,32 @@ __device__ __forceinline__ Top2 shfl_top2(const Top2& t, int mask) {
     return r;
 }
 
+// 16 fp16 descriptor values -> int8 codes c = v - 128 (4 dwords), adding
+// sum c^2 to nrm; bad is set by a value that is not an integer 0..255 (NaN,
+// infinities and -0 included), whose code is then meaningless (the caller
+// falls back to the fp16 path).  Packed: v + 1024 puts an integer 0..1023 in
+// the mantissa bits exactly (0x6400 | v for v < 256), one v_perm gathers four
+// such low bytes, and v ^ 0x80 is v - 128 as int8; v_dot4 adds the squares.
+__device__ __forceinline__ i32x4 codes16(const uint4 a, const uint4 b, int& nrm, bool& bad) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const unsigned w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    unsigned y[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+        const h2 yv = __builtin_bit_cast(h2, w[e]) + (h2){(_Float16)1024.f, (_Float16)1024.f};
+        const h2 back = yv - (h2){(_Float16)1024.f, (_Float16)1024.f};
+        y[e] = __builtin_bit_cast(unsigned, yv);
+        bad |= (y[e] & 0xff00ff00u) != 0x64006400u || __builtin_bit_cast(unsigned, back) != w[e];
+    }
+    i32x4 pk;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        pk[k] = (int)(__builtin_amdgcn_perm(y[2 * k + 1], y[2 * k], 0x06040200u) ^ 0x80808080u);
+        nrm = __builtin_amdgcn_sdot4(pk[k], pk[k], nrm, false);
+    }
+    return pk;
+}
+
 // ---------------------------------------------------------------------------
 // Set preparation: 8 threads per row (16 halves each); per row the int8
 // codes and the key bias -(256 |c|^2 + (row & 255)) (the norm is -bias >> 8).
@@ -114,25 +140,14 @@ __global__ __launch_bounds__(256) void k_match_prep(MatchSets sets, int8_t* __re
     const int row = blockIdx.x * 32 + (threadIdx.x >> 3), part = threadIdx.x & 7;
     const bool in = row < st.n;
     const uint4* src = reinterpret_cast<const uint4*>(st.src + (size_t)min(row, st.n - 1) * 128 + part * 16);
-    const uint4 a = src[0], b = src[1];
-    const unsigned w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    unsigned pk[4] = {0u, 0u, 0u, 0u};
     int nrm = 0;
     bool bad = false;
-#pragma unroll
-    for (int e = 0; e < 16; e++) {
-        const float v = (float)__builtin_bit_cast(_Float16, (unsigned short)(w[e >> 1] >> (16 * (e & 1))));
-        bad |= !(v >= 0.f && v <= 255.f && v == __builtin_rintf(v));  // NaN fails every test
-        const int c = (int)fminf(fmaxf(v, 0.f), 255.f) - 128;
-        nrm += c * c;
-        pk[e >> 2] |= (unsigned)(c & 255) << (8 * (e & 3));
-    }
+    const i32x4 pk = codes16(src[0], src[1], nrm, bad);  // codes of a flagged set are never used
     nrm += __shfl_xor(nrm, 1);
     nrm += __shfl_xor(nrm, 2);
     nrm += __shfl_xor(nrm, 4);
     if (in) {
-        *reinterpret_cast<uint4*>(codes + ((size_t)st.row0 + row) * 128 + part * 16) =
-            make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        *reinterpret_cast<i32x4*>(codes + ((size_t)st.row0 + row) * 128 + part * 16) = pk;
         if (part == 0) rowkeys[st.row0 + row] = -(256 * nrm + (row & 255));  // the row's key bias (r = row mod 256)
         if (bad) flags[blockIdx.y] = epoch;  // every writer stores the same word
     }
@@ -185,32 +200,6 @@ __device__ __forceinline__ Best merge_best(const Best a, const Best b) {
     const int ne = bf ? b.e2 : a.e2, ni = bf ? b.i2 : a.i2;  // runner-up of the winner's list
     const bool ls = lt_ei(le, li, ne, ni);
     return Best{we, wi, ls ? le : ne, ls ? li : ni};
-}
-
-// 16 fp16 descriptor values -> int8 codes c = v - 128 (4 dwords), adding
-// sum c^2 to nrm; bad is set by a value that is not an integer 0..255 (NaN,
-// infinities and -0 included), whose code is then meaningless (the caller
-// falls back to the fp16 path).  Packed: v + 1024 puts an integer 0..1023 in
-// the mantissa bits exactly (0x6400 | v for v < 256), one v_perm gathers four
-// such low bytes, and v ^ 0x80 is v - 128 as int8; v_dot4 adds the squares.
-__device__ __forceinline__ i32x4 codes16(const uint4 a, const uint4 b, int& nrm, bool& bad) {
-    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-    const unsigned w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    unsigned y[8];
-#pragma unroll
-    for (int e = 0; e < 8; e++) {
-        const h2 yv = __builtin_bit_cast(h2, w[e]) + (h2){(_Float16)1024.f, (_Float16)1024.f};
-        const h2 back = yv - (h2){(_Float16)1024.f, (_Float16)1024.f};
-        y[e] = __builtin_bit_cast(unsigned, yv);
-        bad |= (y[e] & 0xff00ff00u) != 0x64006400u || __builtin_bit_cast(unsigned, back) != w[e];
-    }
-    i32x4 pk;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        pk[k] = (int)(__builtin_amdgcn_perm(y[2 * k + 1], y[2 * k], 0x06040200u) ^ 0x80808080u);
-        nrm = __builtin_amdgcn_sdot4(pk[k], pk[k], nrm, false);
-    }
-    return pk;
 }
 
 // ---------------------------------------------------------------------------

@@ -2,9 +2,15 @@
 
 Usage: python3 tools/mfma_summary.py TAG > profiles/roundN/mfma_counters.json
 Reads gpurun_out/mpmc_TAG_p{1,2}/run_counter_collection.csv; averages each
-counter over the dispatches of k_match with the same grid size.  MFMA busy
-fraction = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)
-(GRBM_GUI_ACTIVE is summed over the 8 XCDs).
+counter over the dispatches of a matcher kernel with the same grid size.
+
+MFMA busy fraction = SQ_VALU_MFMA_BUSY_CYCLES / (kernel duration x 2.4 GHz x
+1024 SIMDs), the duration from the same pass's kernel trace: the fraction of
+the chip's matrix-pipe cycles at the peak clock (under load the clock is lower,
+so this understates busy a little).  The round-2 figure divided by
+GRBM_GUI_ACTIVE / 8 instead; that counter does not track the dispatch's
+duration (it read 3.8 GHz-equivalent on the round-3 kernel), so it is kept
+only as a raw counter.
 """
 import csv
 import json
@@ -21,14 +27,19 @@ def main(tag):
         per = defaultdict(lambda: defaultdict(float))  # (grid, dispatch) -> counter -> sum over rows
         with open(f"gpurun_out/mpmc_{tag}_p{p}/run_counter_collection.csv") as f:
             for row in csv.DictReader(f):
-                if "k_match<" not in row["Kernel_Name"] and not row["Kernel_Name"].endswith("k_match"):
-                    if "k_match" not in row["Kernel_Name"] or "prep" in row["Kernel_Name"]:
-                        continue
+                if "k_match" not in row["Kernel_Name"] or "prep" in row["Kernel_Name"]:
+                    continue
                 per[(int(row["Grid_Size"]), row["Dispatch_Id"])][row["Counter_Name"]] += float(row["Counter_Value"])
         for (grid, _), cs in per.items():
             for c, v in cs.items():
                 if c in KEEP and not (p == 2 and c == "GRBM_GUI_ACTIVE"):
                     vals[grid][c].append(v)
+    dur = defaultdict(list)  # grid -> kernel durations (us) of pass 1
+    with open(f"gpurun_out/mpmc_{tag}_p1/run_kernel_trace.csv") as f:
+        for row in csv.DictReader(f):
+            if "k_match" in row["Kernel_Name"] and "prep" not in row["Kernel_Name"]:
+                grid = int(row["Grid_Size_X"]) * int(row["Grid_Size_Y"]) * int(row["Grid_Size_Z"])
+                dur[grid].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e3)
     out = []
     for grid in sorted(vals):
         d = {"grid_size": grid, "dispatches": len(vals[grid]["SQ_INSTS_MFMA"])}
@@ -36,14 +47,15 @@ def main(tag):
             xs = vals[grid][c]
             if xs:
                 d[c if c != "GRBM_GUI_ACTIVE" else "GRBM_GUI_ACTIVE_sum_xcd"] = round(sum(xs) / len(xs), 1)
-        g = d.get("GRBM_GUI_ACTIVE_sum_xcd")
-        if g:
-            d["mfma_busy_frac"] = round(d["SQ_VALU_MFMA_BUSY_CYCLES"] / (g / 8 * 1024), 4)
+        if dur.get(grid):
+            us = sum(dur[grid]) / len(dur[grid])
+            d["kernel_us"] = round(us, 3)
+            d["mfma_busy_frac"] = round(d["SQ_VALU_MFMA_BUSY_CYCLES"] / (us * 1e-6 * 2.4e9 * 1024), 4)
         out.append(d)
     json.dump({"command": f"tools/match_pmc.sh {tag} (two --pmc passes, kernel trace only, over tools/match_pmc.py); "
                           f"python3 tools/mfma_summary.py {tag}",
-               "note": "k_match (int8 MFMA) per dispatch; MFMA busy fraction = SQ_VALU_MFMA_BUSY_CYCLES / "
-                       "(GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs), GRBM_GUI_ACTIVE summed over the 8 XCDs",
+               "note": "matcher kernels (int8 MFMA) per dispatch; MFMA busy fraction = SQ_VALU_MFMA_BUSY_CYCLES / "
+                       "(kernel duration from the same pass's kernel trace x 2.4 GHz x 1024 SIMDs)",
                "kernels": out}, sys.stdout, indent=1)
 
 
