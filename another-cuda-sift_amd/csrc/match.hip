@@ -688,10 +688,6 @@ static int device_cus() {
     return cus;
 }
 
-#ifndef SIFT_MATCH_BATCH_SLOTS
-#define SIFT_MATCH_BATCH_SLOTS 2  // batched: workgroups per CU the splits aim for (one round)
-#endif
-
 MatchPlan match_plan(int max_nq, int max_nt, int P) {
     MatchPlan pl;
     const int ntiles = (max_nt + kMatchTileRows - 1) / kMatchTileRows;
@@ -703,17 +699,33 @@ MatchPlan match_plan(int max_nq, int max_nt, int P) {
         S = S < maxS ? S : maxS;
         pl.S = S < 1 ? 1 : S;
     } else {
-        // As many splits as fit the chip in one round (a second, partial
-        // round costs a whole split's time), each whole key groups.
+        // Splits (whole key groups each) that minimise the busiest CU's work
+        // within one round of workgroups: a CU's tile rate is the same with
+        // one workgroup (2 waves per SIMD) or two (4), so the time is
+        // (workgroups on the busiest CU) x (tiles per split), plus the split
+        // merge (~2.8 us, kMergeTiles tile-times) when S > 1.  C5 (224 query
+        // blocks on 256 CUs): S = 1, 64 tiles and no merge, instead of S = 2
+        // (two workgroups of 32 tiles on 192 CUs, then the merge).
         pl.nw = kMatchBatchNW;
         const int qblocks = (max_nq + 64 * pl.nw - 1) / (64 * pl.nw);
         const int groups = (ntiles + kGroupTiles - 1) / kGroupTiles;
-        int S = SIFT_MATCH_BATCH_SLOTS * device_cus() / (qblocks * P);
-        S = S < groups ? S : groups;
-        S = S < 1 ? 1 : S;
-        const int tps = ((ntiles + S - 1) / S + kGroupTiles - 1) / kGroupTiles * kGroupTiles;
-        S = tps > 0 ? (ntiles + tps - 1) / tps : 1;
-        pl.S = S < 1 ? 1 : S;
+        const int cus = device_cus(), units = qblocks * P;
+        constexpr int kMergeTiles = 6;
+        int best = 1;
+        long best_cost = -1;
+        for (int S = 1; S <= groups; S++) {
+            const int tps = ((ntiles + S - 1) / S + kGroupTiles - 1) / kGroupTiles * kGroupTiles;
+            const int s_eff = (ntiles + tps - 1) / tps;
+            if (s_eff != S) continue;  // same split sizes as a smaller S
+            const long wgs = (long)units * S;
+            if (S > 1 && wgs > (long)kMatchWgPerCu * cus) break;  // one round only
+            const long cost = (wgs + cus - 1) / cus * tps + (S > 1 ? kMergeTiles : 0);
+            if (best_cost < 0 || cost < best_cost) {
+                best_cost = cost;
+                best = S;
+            }
+        }
+        pl.S = best;
     }
     return pl;
 }
