@@ -40,6 +40,15 @@ def main(tag):
             if "k_match" in row["Kernel_Name"] and "prep" not in row["Kernel_Name"]:
                 grid = int(row["Grid_Size_X"]) * int(row["Grid_Size_Y"]) * int(row["Grid_Size_Z"])
                 dur[grid].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e3)
+    dur_kt = defaultdict(list)  # unprofiled durations (kernel-trace-only run), if present
+    try:
+        with open(f"gpurun_out/mpmc_{tag}_kt/run_kernel_trace.csv") as f:
+            for row in csv.DictReader(f):
+                if "k_match" in row["Kernel_Name"] and "prep" not in row["Kernel_Name"]:
+                    grid = int(row["Grid_Size_X"]) * int(row["Grid_Size_Y"]) * int(row["Grid_Size_Z"])
+                    dur_kt[grid].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e3)
+    except FileNotFoundError:
+        pass
     out = []
     for grid in sorted(vals):
         d = {"grid_size": grid, "dispatches": len(vals[grid]["SQ_INSTS_MFMA"])}
@@ -51,11 +60,19 @@ def main(tag):
             us = sum(dur[grid]) / len(dur[grid])
             d["kernel_us"] = round(us, 3)
             d["mfma_busy_frac"] = round(d["SQ_VALU_MFMA_BUSY_CYCLES"] / (us * 1e-6 * 2.4e9 * 1024), 4)
+        if dur_kt.get(grid):
+            ks = sorted(dur_kt[grid])[len(dur_kt[grid]) // 10:]  # first tenth: warm-up
+            ukt = sum(ks) / len(ks)
+            d["kernel_us_unprofiled"] = round(ukt, 3)
+            d["unprofiled_launches"] = len(ks)
+            d["mfma_busy_frac_unprofiled"] = round(d["SQ_VALU_MFMA_BUSY_CYCLES"] / (ukt * 1e-6 * 2.4e9 * 1024), 4)
         out.append(d)
     json.dump({"command": f"tools/match_pmc.sh {tag} (two --pmc passes, kernel trace only, over tools/match_pmc.py); "
                           f"python3 tools/mfma_summary.py {tag}",
                "note": "matcher kernels (int8 MFMA) per dispatch; MFMA busy fraction = SQ_VALU_MFMA_BUSY_CYCLES / "
-                       "(kernel duration from the same pass's kernel trace x 2.4 GHz x 1024 SIMDs)",
+                       "(kernel duration x 2.4 GHz x 1024 SIMDs), the duration from the same --pmc pass's kernel "
+                       "trace (stretched by the counters) and, _unprofiled, from a kernel-trace-only run of the "
+                       "same workload (40x the calls, first tenth dropped); SQ_VALU_MFMA_BUSY_CYCLES = 32 per MFMA",
                "kernels": out}, sys.stdout, indent=1)
 
 

@@ -21,7 +21,9 @@ typedef int i32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kIters = 2048, kChains = 8;
 
-// op 0: v_add_f32, 1: v_lshl_add_u32, 2: v_max3_i32, 3: v_med3_i32, 4: v_add_u32, 5: v_max_i32
+// op 0: v_add_f32, 1: v_lshl_add_u32, 2: v_max3_i32, 3: v_med3_i32, 4: v_add_u32, 5: v_max_i32,
+// 6: v_max3_f32, 7: v_med3_f32, 8: v_max_f32, 9: v_mad_i32_i24, 10: v_add3_u32, 11: v_fma_f32,
+// 12: v_lshlrev_b32, 13: v_max_u32, 14: v_pk_max_i16, 15: v_med3_u32
 template <int OP, bool MFMA>
 __global__ __launch_bounds__(256) void k_valu(int seed, unsigned long long* cyc, int* sink) {
     const int lane = threadIdx.x & 63;
@@ -46,6 +48,16 @@ __global__ __launch_bounds__(256) void k_valu(int seed, unsigned long long* cyc,
             if constexpr (OP == 3) __asm__ volatile("v_med3_i32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(k1), "v"(k2));
             if constexpr (OP == 4) __asm__ volatile("v_add_u32 %0, %0, %1" : "+v"(x[c]) : "v"(k1));
             if constexpr (OP == 5) __asm__ volatile("v_max_i32 %0, %0, %1" : "+v"(x[c]) : "v"(k1));
+            if constexpr (OP == 6) __asm__ volatile("v_max3_f32 %0, %0, %1, %2" : "+v"(f[c]) : "v"(k1), "v"(k2));
+            if constexpr (OP == 7) __asm__ volatile("v_med3_f32 %0, %0, %1, %2" : "+v"(f[c]) : "v"(k1), "v"(k2));
+            if constexpr (OP == 8) __asm__ volatile("v_max_f32 %0, %0, %1" : "+v"(f[c]) : "v"(k1));
+            if constexpr (OP == 9) __asm__ volatile("v_mad_i32_i24 %0, %0, 9, %1" : "+v"(x[c]) : "v"(k1));
+            if constexpr (OP == 10) __asm__ volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(k1), "v"(k2));
+            if constexpr (OP == 11) __asm__ volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(f[c]) : "v"(k1), "v"(k2));
+            if constexpr (OP == 12) __asm__ volatile("v_lshlrev_b32 %0, 9, %0" : "+v"(x[c]));
+            if constexpr (OP == 13) __asm__ volatile("v_max_u32 %0, %0, %1" : "+v"(x[c]) : "v"(k1));
+            if constexpr (OP == 14) __asm__ volatile("v_pk_max_i16 %0, %0, %1" : "+v"(x[c]) : "v"(k1));
+            if constexpr (OP == 15) __asm__ volatile("v_med3_u32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(k1), "v"(k2));
         }
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -80,15 +92,20 @@ static void run(const char* name, int wps) {
 }
 
 int main() {
-    for (int w : {1, 2, 4}) {
+    for (int w : {2, 4}) {
         run<0, false>("v_add_f32", w);
-        run<1, false>("v_lshl_add_u32", w);
         run<2, false>("v_max3_i32", w);
-        run<3, false>("v_med3_i32", w);
-        run<4, false>("v_add_u32", w);
-        run<5, false>("v_max_i32", w);
-        run<1, true>("v_lshl_add_u32", w);
-        run<2, true>("v_max3_i32", w);
+        run<6, false>("v_max3_f32", w);
+        run<7, false>("v_med3_f32", w);
+        run<8, false>("v_max_f32", w);
+        run<9, false>("v_mad_i32_i24", w);
+        run<10, false>("v_add3_u32", w);
+        run<11, false>("v_fma_f32", w);
+        run<12, false>("v_lshlrev_b32", w);
+        run<13, false>("v_max_u32", w);
+        run<14, false>("v_pk_max_i16", w);
+        run<15, false>("v_med3_u32", w);
+        run<6, true>("v_max3_f32", w);
     }
     return 0;
 }
