@@ -13,6 +13,6 @@ for P in "$P1" "$P2"; do
   i=$((i+1))
   timeout -k 10 120 rocprofv3 --pmc $P --kernel-trace -d gpurun_out/mpmc_${TAG}_p$i -o run --output-format csv -- python3 tools/match_pmc.py > gpurun_out/mpmc_${TAG}_p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/mpmc_${TAG}_p$i.log; exit 1; }
 done
-# unprofiled durations of the same kernels (kernel trace only, 40x the calls)
-timeout -k 10 120 rocprofv3 --kernel-trace -d gpurun_out/mpmc_${TAG}_kt -o run --output-format csv -- python3 tools/match_pmc.py 40 > gpurun_out/mpmc_${TAG}_kt.log 2>&1 || { echo "trace run failed"; tail -5 gpurun_out/mpmc_${TAG}_kt.log; exit 1; }
+# unprofiled durations of the same kernels (kernel trace only, 400x the calls: the clock settles)
+timeout -k 10 120 rocprofv3 --kernel-trace -d gpurun_out/mpmc_${TAG}_kt -o run --output-format csv -- python3 tools/match_pmc.py 400 > gpurun_out/mpmc_${TAG}_kt.log 2>&1 || { echo "trace run failed"; tail -5 gpurun_out/mpmc_${TAG}_kt.log; exit 1; }
 echo match pmc done

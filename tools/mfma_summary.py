@@ -72,7 +72,7 @@ def main(tag):
                "note": "matcher kernels (int8 MFMA) per dispatch; MFMA busy fraction = SQ_VALU_MFMA_BUSY_CYCLES / "
                        "(kernel duration x 2.4 GHz x 1024 SIMDs), the duration from the same --pmc pass's kernel "
                        "trace (stretched by the counters) and, _unprofiled, from a kernel-trace-only run of the "
-                       "same workload (40x the calls, first tenth dropped); SQ_VALU_MFMA_BUSY_CYCLES = 32 per MFMA",
+                       "same workload (400x the calls, first tenth dropped); SQ_VALU_MFMA_BUSY_CYCLES = 32 per MFMA",
                "kernels": out}, sys.stdout, indent=1)
 
 
