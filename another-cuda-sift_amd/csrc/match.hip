@@ -695,9 +695,16 @@ MatchPlan match_plan(int max_nq, int max_nt, int P) {
         pl.nw = SIFT_MATCH_NW_SINGLE;
         const int qblocks = (max_nq + 64 * pl.nw - 1) / (64 * pl.nw);
         int S = (SIFT_MATCH_WG_TARGET_SINGLE + qblocks - 1) / qblocks;
-        const int maxS = ntiles / 2 > 1 ? ntiles / 2 : 1;  // >= 2 tiles per split
+        // >= 4 tiles per split: every split converts its workgroup's query rows
+        // again (C3, 2000 x 2000: 4 tiles 11.5 us per call, 3 tiles 11.9, 2 12.4,
+        // 1 15.8, 6 12.3, 8 13.4; tools/r3_c3_dma.sh).
+        constexpr int kMinTilesSingle = 4;
+        const int maxS = (ntiles + kMinTilesSingle - 1) / kMinTilesSingle;
         S = S < maxS ? S : maxS;
-        pl.S = S < 1 ? 1 : S;
+        S = S < 1 ? 1 : S;
+        // No empty splits (tps rounded up can leave trailing ones empty).
+        const int tps = (ntiles + S - 1) / S;
+        pl.S = tps > 0 ? (ntiles + tps - 1) / tps : 1;
     } else {
         // Splits (whole key groups each) that minimise the busiest CU's work
         // within one round of workgroups: a CU's tile rate is the same with
