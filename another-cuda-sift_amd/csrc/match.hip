@@ -314,20 +314,30 @@ __device__ __forceinline__ void write_match(int i1, float e1, int i2, float e2, 
 // its LDS slot is lane x 16 B).
 // ---------------------------------------------------------------------------
 constexpr int kTileBytes = kMatchTileRows * 128;
-constexpr int kMatchBatchNW = 8;  // waves per k_match_batch workgroup (512 queries)
+#ifndef SIFT_MATCH_BATCH_NW
+#define SIFT_MATCH_BATCH_NW 8
+#endif
+#ifndef SIFT_MATCH_BATCH_QBW
+#define SIFT_MATCH_BATCH_QBW 2
+#endif
+constexpr int kMatchBatchNW = SIFT_MATCH_BATCH_NW;    // waves per k_match_batch workgroup
+constexpr int kMatchBatchQBW = SIFT_MATCH_BATCH_QBW;  // 32-query blocks per wave (512 queries per workgroup)
+constexpr int kMatchBatchQB = 32 * kMatchBatchQBW * kMatchBatchNW;
+constexpr int kMatchBatchWgPerCu = 2 * 8 / kMatchBatchNW > 0 ? 2 * 8 / kMatchBatchNW : 1;  // register budget: 16 waves per CU
 constexpr int kChunkRows = kChunkTiles * kMatchTileRows;
 static_assert(kChunkTiles == kGroupTiles, "a staged chunk is at most one key group");
 
 __device__ __forceinline__ int piece_swz(int row, int piece) { return piece ^ ((row >> 1) & 7); }
 
-// A wave's two 32-query B operands: lane (col, h) holds bytes [64h, 64h + 64)
+// A wave's QBW 32-query B operands: lane (col, h) holds bytes [64h, 64h + 64)
 // of query row q0w + 32 qb + col, one 16-byte fragment per MFMA; the A
 // fragments take the same bytes of the train rows, so both sides pair the same
 // descriptor dimensions in every K slot.  qn = |c_q|^2.
+template <int QBW>
 __device__ __forceinline__ void load_queries(const int8_t* __restrict__ qc, const int* __restrict__ qkeys, int nq,
-                                             int q0w, int col, int h, i32x4 (&bq)[2][4], int (&qn)[2]) {
+                                             int q0w, int col, int h, i32x4 (&bq)[QBW][4], int (&qn)[QBW]) {
 #pragma unroll
-    for (int qb = 0; qb < 2; qb++) {
+    for (int qb = 0; qb < QBW; qb++) {
         const int row = min(q0w + 32 * qb + col, nq - 1);
         const i32x4* src = reinterpret_cast<const i32x4*>(qc + (size_t)row * 128 + 64 * h);
 #pragma unroll
@@ -369,10 +379,12 @@ __device__ __forceinline__ void stage_dma(const int8_t* __restrict__ tc, const i
 // block (accumulator registers 0-7 / 8-15).  The chunk lies in one key group
 // (r = row - t0 < 256), so its top-2 is decoded once into (e, train index) and
 // merged into the running pair (earlier groups win ties).
+template <int QBW>
 __device__ __forceinline__ void chunk_top2(const int8_t* sc, const int* sk, int nc, int t0, int col, int h,
-                                           const i32x4 (&bq)[2][4], Best (&best)[2]) {
-    int m1e[2] = {INT_MIN, INT_MIN}, m2e[2] = {INT_MIN, INT_MIN};  // registers 0-7
-    int m1o[2] = {INT_MIN, INT_MIN}, m2o[2] = {INT_MIN, INT_MIN};  // registers 8-15
+                                           const i32x4 (&bq)[QBW][4], Best (&best)[QBW]) {
+    int m1e[QBW], m2e[QBW], m1o[QBW], m2o[QBW];  // registers 0-7 / 8-15
+#pragma unroll
+    for (int qb = 0; qb < QBW; qb++) m1e[qb] = m2e[qb] = m1o[qb] = m2o[qb] = INT_MIN;
     const int sw = (col >> 1) & 7;
     const int8_t* const ta0 = sc + col * 128;
     const int* const tk1 = sk + 4 * h;
@@ -386,14 +398,14 @@ __device__ __forceinline__ void chunk_top2(const int8_t* sc, const int* sk, int 
             // accumulator register i holds train row (i & 3) + 8 (i >> 2) + 4 h
 #pragma unroll
             for (int g = 0; g < 4; g++) tk[g] = *reinterpret_cast<const i32x4*>(tk1 + j * kMatchTileRows + 8 * g);
-            i32x16 acc[2] = {{}, {}};
+            i32x16 acc[QBW] = {};
 #pragma unroll
-            for (int qb = 0; qb < 2; qb++)
+            for (int qb = 0; qb < QBW; qb++)
 #pragma unroll
                 for (int kb = 0; kb < 4; kb++)
                     acc[qb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[kb], bq[qb][kb], acc[qb], 0, 0, 0);
 #pragma unroll
-            for (int qb = 0; qb < 2; qb++)
+            for (int qb = 0; qb < QBW; qb++)
 #pragma unroll
                 for (int i = 0; i < 8; i += 2) {
                     const int x0 = (acc[qb][i] << 9) + tk[i >> 2][i & 3];
@@ -408,7 +420,7 @@ __device__ __forceinline__ void chunk_top2(const int8_t* sc, const int* sk, int 
         }
     }
 #pragma unroll
-    for (int qb = 0; qb < 2; qb++) {
+    for (int qb = 0; qb < QBW; qb++) {
         const int a1 = m1e[qb], a2 = m2e[qb], b1 = m1o[qb], b2 = m2o[qb];
         best[qb] = fold_group(best[qb], max(a1, b1), max(min(a1, b1), max(a2, b2)), t0);
     }
@@ -595,13 +607,13 @@ __global__ __launch_bounds__(64 * NW, (kMatchWgPerCu * NW) / 4) void k_match_sin
 // 8 tiles).  With S > 1 the splits merge through the keys scratch and the one
 // that completes the query block's count writes the outputs.
 // ---------------------------------------------------------------------------
-template <int NW>
-__global__ __launch_bounds__(64 * NW, (kMatchWgPerCu * NW) / 4) void k_match_batch(
+template <int NW, int QBW>
+__global__ __launch_bounds__(64 * NW, (kMatchBatchWgPerCu * NW) / 4) void k_match_batch(
     MatchBatch batch, int S, int nq_stride, const int8_t* __restrict__ codes, const int* __restrict__ rowkeys,
     int sentinel, const unsigned* __restrict__ flags, unsigned epoch, unsigned long long* __restrict__ keys,
     unsigned* __restrict__ done, float ratio, int ratio_on_squared, int* __restrict__ idx2, float* __restrict__ d2out,
     int* __restrict__ match) {
-    constexpr int QB = 64 * NW;
+    constexpr int QB = 32 * QBW * NW;  // queries per workgroup
     __shared__ __attribute__((aligned(16))) int8_t s_codes[2][kChunkTiles * kTileBytes];
     __shared__ __attribute__((aligned(16))) int s_key[2][kChunkRows];
     __shared__ unsigned s_last;
@@ -615,18 +627,20 @@ __global__ __launch_bounds__(64 * NW, (kMatchWgPerCu * NW) / 4) void k_match_bat
     const int ntiles = (pr.nt + kMatchTileRows - 1) / kMatchTileRows;
     const int tps = ((ntiles + S - 1) / S + kGroupTiles - 1) / kGroupTiles * kGroupTiles;  // whole key groups
     const int tb = min(ntiles, (int)blockIdx.y * tps), te = min(ntiles, tb + tps);
-    const int q0w = q0 + 64 * w;
-    Top2 res[2];
+    const int q0w = q0 + 32 * QBW * w;
+    Top2 res[QBW];
     if (flags[pr.qset] != epoch && flags[pr.tset] != epoch) {
         // ---- integer path ----
         const int8_t* __restrict__ tc = codes + (size_t)pr.trow0 * 128;
         const int* __restrict__ tk = rowkeys + pr.trow0;
         const int8_t* __restrict__ zc = codes + (size_t)sentinel * 128;  // zero code row (padding)
         const int* __restrict__ zk = rowkeys + sentinel;
-        i32x4 bq[2][4];
-        int qn[2];
-        load_queries(codes + (size_t)pr.qrow0 * 128, rowkeys + pr.qrow0, pr.nq, q0w, col, h, bq, qn);
-        Best best[2] = {{kNone, kNone, kNone, kNone}, {kNone, kNone, kNone, kNone}};
+        i32x4 bq[QBW][4];
+        int qn[QBW];
+        load_queries<QBW>(codes + (size_t)pr.qrow0 * 128, rowkeys + pr.qrow0, pr.nq, q0w, col, h, bq, qn);
+        Best best[QBW];
+#pragma unroll
+        for (int qb = 0; qb < QBW; qb++) best[qb] = Best{kNone, kNone, kNone, kNone};
         if (tb < te)
             stage_dma<NW>(tc, tk, pr.nt, tb * kMatchTileRows, min(kChunkTiles, te - tb), zc, zk, s_codes[0], s_key[0],
                           w, lane);
@@ -643,21 +657,21 @@ __global__ __launch_bounds__(64 * NW, (kMatchWgPerCu * NW) / 4) void k_match_bat
                               s_key[buf ^ 1], w, lane);
             chunk_top2(s_codes[buf], s_key[buf], min(kChunkTiles, te - c0), c0 * kMatchTileRows, col, h, bq, best);
         }
-        res[0] = finish_best(best[0], qn[0]);
-        res[1] = finish_best(best[1], qn[1]);
+#pragma unroll
+        for (int qb = 0; qb < QBW; qb++) res[qb] = finish_best(best[qb], qn[qb]);
     } else {
         // ---- general path: fp16 values that are not integers 0..255 ----
-        res[0] = match_f16_block(pr, q0w, tb, te, col, h);
-        res[1] = match_f16_block(pr, q0w + 32, tb, te, col, h);
+#pragma unroll
+        for (int qb = 0; qb < QBW; qb++) res[qb] = match_f16_block(pr, q0w + 32 * qb, tb, te, col, h);
     }
     __syncthreads();  // s_res aliases the code tiles
     if (h == 0) {
-        s_res[64 * w + col] = res[0];
-        s_res[64 * w + 32 + col] = res[1];
+#pragma unroll
+        for (int qb = 0; qb < QBW; qb++) s_res[32 * QBW * w + 32 * qb + col] = res[qb];
     }
     __syncthreads();
     const int q = q0 + tid;
-    const bool qv = q < pr.nq;
+    const bool qv = tid < QB && q < pr.nq;  // (64 NW threads >= QB queries)
     const size_t o = (size_t)pr.out_off + q;
     if (S == 1) {
         if (qv) write_top2(s_res[tid], o, ratio, ratio_on_squared, idx2, d2out, match);
@@ -714,7 +728,7 @@ MatchPlan match_plan(int max_nq, int max_nt, int P) {
         // blocks on 256 CUs): S = 1, 64 tiles and no merge, instead of S = 2
         // (two workgroups of 32 tiles on 192 CUs, then the merge).
         pl.nw = kMatchBatchNW;
-        const int qblocks = (max_nq + 64 * pl.nw - 1) / (64 * pl.nw);
+        const int qblocks = (max_nq + kMatchBatchQB - 1) / kMatchBatchQB;
         const int groups = (ntiles + kGroupTiles - 1) / kGroupTiles;
         const int cus = device_cus(), units = qblocks * P;
         constexpr int kMergeTiles = 6;
@@ -725,7 +739,7 @@ MatchPlan match_plan(int max_nq, int max_nt, int P) {
             const int s_eff = (ntiles + tps - 1) / tps;
             if (s_eff != S) continue;  // same split sizes as a smaller S
             const long wgs = (long)units * S;
-            if (S > 1 && wgs > (long)kMatchWgPerCu * cus) break;  // one round only
+            if (S > 1 && wgs > (long)kMatchBatchWgPerCu * cus) break;  // one round only
             const long cost = (wgs + cus - 1) / cus * tps + (S > 1 ? kMergeTiles : 0);
             if (best_cost < 0 || cost < best_cost) {
                 best_cost = cost;
@@ -752,8 +766,8 @@ void launch_match(const MatchSets& sets, MatchBatch& batch, const MatchPlan& pla
                            flags, epoch);
     int max_nq = 1;
     for (int p = 0; p < batch.P; p++) max_nq = max(max_nq, batch.pair[p].nq);
-    dim3 g((max_nq + 64 * kMatchBatchNW - 1) / (64 * kMatchBatchNW), plan.S, batch.P);
-    hipLaunchKernelGGL(k_match_batch<kMatchBatchNW>, g, dim3(64 * kMatchBatchNW), 0, s, batch, plan.S, nq_stride, codes,
+    dim3 g((max_nq + kMatchBatchQB - 1) / kMatchBatchQB, plan.S, batch.P);
+    hipLaunchKernelGGL((k_match_batch<kMatchBatchNW, kMatchBatchQBW>), g, dim3(64 * kMatchBatchNW), 0, s, batch, plan.S, nq_stride, codes,
                        rowkeys, sentinel, flags, epoch, keys, done, ratio, ratio_on_squared, idx2, d2, match);
 }
 
