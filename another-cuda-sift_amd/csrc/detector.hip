@@ -106,11 +106,14 @@ const char* build_flags() {
 #ifdef SIFT_BLUR_IW112
            " SIFT_BLUR_IW112=" SIFT_STR(SIFT_BLUR_IW112)
 #endif
-#ifdef SIFT_BLUR_CHAIN
-           " SIFT_BLUR_CHAIN=" SIFT_STR(SIFT_BLUR_CHAIN)
+#ifdef SIFT_MATCH_BATCH_NW
+           " SIFT_MATCH_BATCH_NW=" SIFT_STR(SIFT_MATCH_BATCH_NW)
 #endif
-#ifdef SIFT_CHAIN_NW
-           " SIFT_CHAIN_NW=" SIFT_STR(SIFT_CHAIN_NW)
+#ifdef SIFT_MATCH_NW_SINGLE
+           " SIFT_MATCH_NW_SINGLE=" SIFT_STR(SIFT_MATCH_NW_SINGLE)
+#endif
+#ifdef SIFT_MATCH_BATCH_QBW
+           " SIFT_MATCH_BATCH_QBW=" SIFT_STR(SIFT_MATCH_BATCH_QBW)
 #endif
 #ifdef SIFT_BLUR_X4ST
            " SIFT_BLUR_X4ST=" SIFT_STR(SIFT_BLUR_X4ST)
@@ -248,10 +251,6 @@ struct sift_hip_detector {
     float* dDg = nullptr;
 
     bool timing = false;
-#ifndef SIFT_BLUR_CHAIN
-#define SIFT_BLUR_CHAIN 0  // measured slower: A/B builds -DSIFT_BLUR_CHAIN=1
-#endif
-    bool blurChains = SIFT_BLUR_CHAIN;  // chained blur units (launch_blur_chain)
     int blurReps = 1;  // timing mode: each blur launch repeated back to back inside its event pair
     std::vector<TimingRec> trecs;
     std::vector<TimingAgg> tagg;
@@ -547,7 +546,7 @@ void enqueue_head(sift_hip_detector* d, const void* img, int pitch, int fmt, int
                 pitch = d->inPitch;
                 s = d->afs;
             }
-            launch_blur((const float*)img, pitch, 1, W, H, g.base, g.pitch, nullptr, d->initTaps, fr, s, d->stream,
+            launch_blur((const float*)img, pitch, 1, W, H, g.base, g.pitch, DecOut{}, d->initTaps, fr, s, d->stream,
                         range_keys(d, parity), d->dCtr);
         });
     }
@@ -564,20 +563,20 @@ void enqueue_pyramid(sift_hip_detector* d, int nf, int parity) {
     if (d->firstOctave < 0) {
         const OctGeom& g = d->pyr.oct[0];
         d->timed("blur_init", (double)g.W * g.H * 8 * nf, [&] {
-            launch_blur(d->dUp, d->upPitch, 1, g.W, g.H, g.base, g.pitch, nullptr, d->initTaps, fr, d->afs, s,
+            launch_blur(d->dUp, d->upPitch, 1, g.W, g.H, g.base, g.pitch, DecOut{}, d->initTaps, fr, d->afs, s,
                         range_keys(d, parity), d->dCtr);
         });
     }
     static const char* blurNames[kMaxOctaves] = {"blur_o0", "blur_o1", "blur_o2", "blur_o3", "blur_o4", "blur_o5",
                                                  "blur_o6", "blur_o7", "blur_o8", "blur_o9", "blur_o10", "blur_o11",
                                                  "blur_o12", "blur_o13", "blur_o14", "blur_o15"};
-    // Blur jobs (o, i): plane i of octave o from plane i-1, or for i = 1 of
-    // octaves > 0 from plane L of octave o-1 (decimated, base plane copied
-    // out).  List-scheduled in (o, i) order: a job is ready once its input
-    // plane's job has been launched (stream order); the two oldest ready jobs
-    // share one launch when their radii have a pair kernel -- with L = 3,
-    // (o, 4) + (o+1, 1) and (o, 5) + (o+1, 2): 11 launches instead of 15 for
-    // three octaves.
+    // Blur jobs (o, i): plane i of octave o from plane i-1 (plane 0 of octave
+    // o+1 is written by job (o, L) as it stores: the INTER_NEAREST half-size
+    // copy of plane L).  List-scheduled in (o, i) order: a job is ready once
+    // its input plane's job has been launched (stream order); the two oldest
+    // ready jobs share one launch when their radii have a pair kernel -- with
+    // L = 3, (o, 4) + (o+1, 1) and (o, 5) + (o+1, 2): 11 launches instead of 15
+    // for three octaves.
     struct Job {
         int o, i;
         BlurDesc b;
@@ -588,109 +587,54 @@ void enqueue_pyramid(sift_hip_detector* d, int nf, int parity) {
         const OctGeom& g = d->pyr.oct[o];
         for (int i = 1; i < L + 3; i++) {
             Job j{o, i, {}, 0};
+            j.b.src = g.base + (size_t)(i - 1) * g.planeStride;
+            j.b.spitch = g.pitch;
+            j.b.sstep = 1;
             j.b.dst = g.base + (size_t)i * g.planeStride;
             j.b.dpitch = g.pitch;
             j.b.W = g.W;
             j.b.H = g.H;
             j.b.taps = &d->layerTaps[i];
-            if (i == 1 && o > 0) {
-                const OctGeom& p = d->pyr.oct[o - 1];
-                j.b.src = p.base + (size_t)L * p.planeStride;
-                j.b.spitch = p.pitch;
-                j.b.sstep = 2;
-                j.b.copy_out = g.base;
-                j.bytes = (double)g.W * g.H * 12 * nf;
-            } else {
-                j.b.src = g.base + (size_t)(i - 1) * g.planeStride;
-                j.b.spitch = g.pitch;
-                j.b.sstep = 1;
-                j.b.copy_out = nullptr;
-                j.bytes = (double)g.W * g.H * 8 * nf;
+            j.bytes = (double)g.W * g.H * 8 * nf;
+            if (i == L && o + 1 < d->nOct) {
+                const OctGeom& n = d->pyr.oct[o + 1];
+                j.b.dec = DecOut{n.base, n.pitch, n.W, n.H};
+                j.bytes += (double)n.W * n.H * 4 * nf;
             }
             jobs.push_back(j);
         }
     }
     auto idx = [&](int o, int i) { return o * (L + 2) + (i - 1); };
-    // Launch units: a chain of planes (i, i+1) of one octave in one tile pass
-    // (plane i written, not re-read: launch_blur_chain) where an instantiation
-    // exists for their radii, else single planes.  With L = 3 and sigma 1.6
-    // (radii 5, 6, 8, 10, 13): units (1,2), (3,4), 5 per octave.
-    struct Unit {
-        int o, i, n;  // planes i .. i + n - 1 of octave o
-    };
-    std::vector<Unit> units;
-    for (int o = 0; o < d->nOct; o++) {
-        const OctGeom& g = d->pyr.oct[o];
-        for (int i = 1; i < L + 3;) {
-            const bool chain = d->blurChains && i + 1 < L + 3 &&
-                               blur_chain_supported(d->layerTaps[i].n >> 1, d->layerTaps[i + 1].n >> 1, g.W, g.H);
-            units.push_back(Unit{o, i, chain ? 2 : 1});
-            i += chain ? 2 : 1;
-        }
-    }
-    std::vector<bool> planeDone(jobs.size(), false), unitDone(units.size(), false);
+    std::vector<bool> done(jobs.size(), false);
     auto ready = [&](size_t k) {
-        const Unit& u = units[k];
-        if (unitDone[k]) return false;
-        if (u.i >= 2) return (bool)planeDone[idx(u.o, u.i - 1)];
-        return u.o == 0 || (bool)planeDone[idx(u.o - 1, L)];
+        const Job& j = jobs[k];
+        if (done[k]) return false;
+        if (j.i >= 2) return (bool)done[idx(j.o, j.i - 1)];
+        return j.o == 0 || (bool)done[idx(j.o - 1, L)];
     };
-    auto finish = [&](size_t k) {
-        unitDone[k] = true;
-        for (int q = 0; q < units[k].n; q++) planeDone[idx(units[k].o, units[k].i + q)] = true;
-    };
-    auto unit_bytes = [&](const Unit& u) {  // algorithmic: one read of the input, a write per plane (+ base copy)
-        const Job& j = jobs[idx(u.o, u.i)];
-        return u.n == 1 ? j.bytes : j.bytes + (double)j.b.W * j.b.H * 4 * nf;
-    };
-    auto single = [&](const Job& j) {
-        d->timed(blurNames[j.o], j.bytes, [&] {
-            launch_blur(j.b.src, j.b.spitch, j.b.sstep, j.b.W, j.b.H, j.b.dst, j.b.dpitch, j.b.copy_out, *j.b.taps, fr,
-                        d->afs, s);
-        });
-    };
-    for (size_t left = units.size(); left > 0;) {
+    for (size_t left = jobs.size(); left > 0;) {
         int a = -1, b = -1;
-        for (size_t k = 0; k < units.size() && b < 0; k++)
+        for (size_t k = 0; k < jobs.size() && b < 0; k++)
             if (ready(k)) (a < 0 ? a : b) = (int)k;
-        const Unit& ua = units[a];
+        const Job& ja = jobs[a];
         bool paired = false;
         if (b >= 0) {
-            const Unit& ub = units[b];
+            const Job& jb = jobs[b];
             char name[16];
-            snprintf(name, sizeof name, "blur_o%d+o%d", ua.o, ub.o);
-            const double bytes = unit_bytes(ua) + unit_bytes(ub);
-            if (ua.n == 1 && ub.n == 1) {
-                d->timed(name, bytes,
-                         [&] { paired = launch_blur_pair(jobs[idx(ua.o, ua.i)].b, jobs[idx(ub.o, ub.i)].b, fr, s); });
-            } else if (ua.n + ub.n == 3) {
-                const Unit& uc = ua.n == 2 ? ua : ub;
-                const Unit& us = ua.n == 2 ? ub : ua;
-                d->timed(name, bytes, [&] {
-                    paired = launch_blur_chain(jobs[idx(uc.o, uc.i)].b, jobs[idx(uc.o, uc.i + 1)].b,
-                                               &jobs[idx(us.o, us.i)].b, fr, s);
-                });
-            }
+            snprintf(name, sizeof name, "blur_o%d+o%d", ja.o, jb.o);
+            d->timed(name, ja.bytes + jb.bytes, [&] { paired = launch_blur_pair(ja.b, jb.b, fr, s); });
             if (paired) {
-                finish(b);
+                done[b] = true;
                 left--;
             }
         }
         if (!paired) {
-            if (ua.n == 2) {
-                bool ok = false;
-                d->timed(blurNames[ua.o], unit_bytes(ua), [&] {
-                    ok = launch_blur_chain(jobs[idx(ua.o, ua.i)].b, jobs[idx(ua.o, ua.i + 1)].b, nullptr, fr, s);
-                });
-                if (!ok) {  // (unit built only where supported)
-                    single(jobs[idx(ua.o, ua.i)]);
-                    single(jobs[idx(ua.o, ua.i + 1)]);
-                }
-            } else {
-                single(jobs[idx(ua.o, ua.i)]);
-            }
+            d->timed(blurNames[ja.o], ja.bytes, [&] {
+                launch_blur(ja.b.src, ja.b.spitch, ja.b.sstep, ja.b.W, ja.b.H, ja.b.dst, ja.b.dpitch, ja.b.dec,
+                            *ja.b.taps, fr, d->afs, s);
+            });
         }
-        finish(a);
+        done[a] = true;
         left--;
     }
 }

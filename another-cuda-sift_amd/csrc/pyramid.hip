@@ -98,17 +98,17 @@ constexpr int BLUR_TH = SIFT_BLUR_TH;
 static_assert(BLUR_TH % 32 == 0, "blur tile height: 8-row column blocks for 4 or 8 waves");
 static int blur_waves(int tiles) { return tiles >= SIFT_BLUR_BIG_TILES ? 4 : 8; }
 
-// One blur launch's job: plane src (stride-sstep read = fused INTER_NEAREST
-// decimation) -> dst, optional decimated base copy, pixel range, counters.
+// One blur launch's job: plane src -> dst, optionally the next octave's base
+// plane (dec), the pixel range and the frame counters.
 struct BlurJob {
     const void* src;  // float, or uint8_t for the frame's first blur of an 8-bit frame
     float* dst;
-    float* copy_out;
+    DecOut dec;
     unsigned* range_keys;
     Counters* zero_ctr;
     int spitch, sstep, W, H, dpitch, tilesX, ntiles;
     int nf;         // frames; the launch has nf * ntiles tiles of this job
-    long sfs, dfs;  // byte strides between frames: source; dst / copy_out / range_keys / zero_ctr
+    long sfs, dfs;  // byte strides between frames: source; dst / dec / range_keys / zero_ctr
     Taps taps;
 };
 
@@ -178,7 +178,7 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
     const int f = t / J.ntiles, tile = t - f * J.ntiles;
     const T* __restrict__ src = fptr(static_cast<const T*>(J.src), f * J.sfs);
     float* __restrict__ dst = fptr(J.dst, f * J.dfs);
-    float* __restrict__ copy_out = J.copy_out ? fptr(J.copy_out, f * J.dfs) : nullptr;
+    float* __restrict__ dec_out = J.dec.p ? fptr(J.dec.p, f * J.dfs) : nullptr;
     unsigned* __restrict__ range_keys = J.range_keys ? fptr(J.range_keys, f * J.dfs) : nullptr;
     Counters* __restrict__ zero_ctr = J.zero_ctr ? fptr(J.zero_ctr, f * J.dfs) : nullptr;
     const int spitch = J.spitch, sstep = J.sstep, W = J.W, H = J.H, dpitch = J.dpitch;
@@ -298,17 +298,6 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
                     if (i < RPW - 1 || wv + BLUR_NW * i < IH) irow[BLUR_NW * i * IW + 64] = v1[i];
             }
         }
-        if (ES == 4 && copy_out) {  // decimated base plane of this octave = the tile's interior inputs
-#pragma unroll
-            for (int i = 0; i < RPW; i++) {
-                const int ly = wv + BLUR_NW * i, gy = y0 - R + ly;
-                if (ly >= R && ly < R + BLUR_TH && gy < H) {
-                    float* row = copy_out + (size_t)gy * dpitch + x0 - R;
-                    if (lane >= R && x0 - R + lane < W) row[lane] = v0[i];
-                    if (lane < R && x0 + 64 + lane - R < W) row[64 + lane] = v1[i];
-                }
-            }
-        }
     }
     __syncthreads();
 
@@ -418,6 +407,20 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
                 if (gy < H && gx < W) dst[(size_t)gy * dpitch + gx] = out[q];
             }
         }
+        if (dec_out) {
+            // The next octave's base plane: even rows and columns of this
+            // plane (y0, yb even), stored by the even lanes; other lanes get
+            // an offset past the buffer, which the hardware drops (no branch).
+            const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
+                dec_out, 0, (int)min((long)J.dec.pitch * J.dec.H * 4, 0x7fffffffL), 0x00020000);
+            const bool cx = (gx & 1) == 0 && (gx >> 1) < J.dec.W;
+#pragma unroll
+            for (int q = 0; q < 8; q += 2) {
+                const int dy = (y0 + yb + q) >> 1;
+                const unsigned off = cx && dy < J.dec.H ? (unsigned)(dy * J.dec.pitch + (gx >> 1)) * 4u : 0x80000000u;
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, out[q]), drs, off, 0, 0);
+            }
+        }
         if (range_keys) {
 #pragma unroll
             for (int q = 0; q < 8; q++) {
@@ -506,7 +509,7 @@ __global__ __launch_bounds__(64 * NW) void k_blur2(BlurJob A, BlurJob B) {
         blur_tile<RB, float, NW>(B, blockIdx.x - na, in);
 }
 
-static BlurJob make_job(const void* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, float* copy_out,
+static BlurJob make_job(const void* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, const DecOut& dec,
                         const Taps& taps, unsigned* range_keys, Counters* zero_ctr, const Frames& fr, long sfs) {
     BlurJob j;
     j.nf = fr.nf;
@@ -514,7 +517,7 @@ static BlurJob make_job(const void* src, int spitch, int sstep, int W, int H, fl
     j.dfs = fr.stride;
     j.src = src;
     j.dst = dst;
-    j.copy_out = copy_out;
+    j.dec = dec;
     j.range_keys = range_keys;
     j.zero_ctr = zero_ctr;
     j.spitch = spitch;
@@ -581,358 +584,16 @@ bool launch_blur_pair_jobs(const BlurJob& a, const BlurJob& b, hipStream_t s) {
 }
 
 bool launch_blur_pair(const BlurDesc& a, const BlurDesc& b, const Frames& fr, hipStream_t s) {
-    return launch_blur_pair_jobs(make_job(a.src, a.spitch, a.sstep, a.W, a.H, a.dst, a.dpitch, a.copy_out, *a.taps,
+    return launch_blur_pair_jobs(make_job(a.src, a.spitch, a.sstep, a.W, a.H, a.dst, a.dpitch, a.dec, *a.taps,
                                           nullptr, nullptr, fr, fr.stride),
-                                 make_job(b.src, b.spitch, b.sstep, b.W, b.H, b.dst, b.dpitch, b.copy_out, *b.taps,
+                                 make_job(b.src, b.spitch, b.sstep, b.W, b.H, b.dst, b.dpitch, b.dec, *b.taps,
                                           nullptr, nullptr, fr, fr.stride),
                                  s);
 }
 
-// ---------------------------------------------------------------------------
-// Chained blurs: planes i and i+1 of an octave from plane i-1 in one tile
-// pass.  The tile stages its input once with a halo of
-// RA + RB, runs blur A (row pass in place, column pass into registers) over
-// the tile plus blur B's halo, writes that intermediate back over the input
-// tile, stores its core as plane i, runs blur B over it and stores plane
-// i+1: 3 plane transfers instead of 4 (plane i is written but not re-read).
-// Every output is the same float operation sequence as k_blur's (row: the
-// sequential fma chain, or the symmetric form for 2R+1 <= 5; column: the
-// symmetric pk_fma chain), and the intermediate's out-of-image halo is the
-// reflect-101 copy of its in-image values -- what a separate blur of plane i
-// would read -- so both planes are bit-identical to two k_blur launches.
-// Reference: Filter.cu:8-51, applied twice (Detector.cu:163-176).
-// ---------------------------------------------------------------------------
-template <int RA, int RB>
-struct ChainGeom {
-    static constexpr int RT = RA + RB;
-    static constexpr int RUA = (RA + 3) & ~3, RUB = (RB + 3) & ~3;
-    static constexpr int ORG = RUA + RUB;                  // LDS column 0 = image column x0 - ORG
-    static constexpr int NA4 = (RUB + BLUR_TW + RB + 3) / 4;  // pass-A float4 outputs per row, from column RUA
-    static constexpr int IW = 2 * RUA + 4 * NA4;           // LDS row pitch (last pass-A window ends there)
-    static constexpr int IH = BLUR_TH + 2 * RT;            // staged rows: row 0 = image row y0 - RT
-    static constexpr int MH = BLUR_TH + 2 * RB;            // intermediate rows: row 0 = image row y0 - RB
-    static constexpr int WA = BLUR_TW + 2 * RB;            // intermediate columns from LDS column ORG - RB
-    static constexpr int LDS = IW * IH + 4;
-    static_assert(ORG - RT >= 0 && ORG + BLUR_TW + RT <= IW, "staged halo inside the LDS row");
-    static_assert(RUA + 4 * NA4 >= ORG + BLUR_TW + RB, "pass A covers blur B's halo");
-    static_assert(NA4 <= 64, "a pass-A row fits one wave");
-};
-
-struct BlurChainJob {
-    BlurJob a;   // src -> a.dst (plane i), taps A; decimation / copy_out as BlurJob
-    float* dst2;  // plane i+1
-    Taps taps2;
-};
-
-// Packed row pass over one LDS row: four outputs starting at LDS column c0
-// from a window read at the aligned column c0 - RU (RU = R rounded up to 4),
-// OpenCV's row-filter operation order (see blur_tile).
-template <int R>
-__device__ __forceinline__ f32x4 chain_row4(const float* __restrict__ rowp, int c0, const Taps& taps) {
-    constexpr int RU = (R + 3) & ~3, SS = RU - R, NWV = (SS + 2 * R + 4 + 3) / 4;
-    float win[4 * NWV];
-    const f32x4* p = reinterpret_cast<const f32x4*>(rowp + c0 - RU);
-#pragma unroll
-    for (int v = 0; v < NWV; v++) {
-        f32x4 f = p[v];
-        __asm__ volatile("" : "+v"(f));
-        win[4 * v] = f[0];
-        win[4 * v + 1] = f[1];
-        win[4 * v + 2] = f[2];
-        win[4 * v + 3] = f[3];
-    }
-    f32x2 pe[2 * NWV], po[2 * NWV - 1];
-#pragma unroll
-    for (int j = 0; j < 2 * NWV; j++) pe[j] = (f32x2){win[2 * j], win[2 * j + 1]};
-#pragma unroll
-    for (int j = 0; j < 2 * NWV - 1; j++) po[j] = pk_mov_hi_lo(pe[j], pe[j + 1]);
-    auto pr = [&](int i) -> f32x2 {
-        i += SS;
-        return (i & 1) ? po[i >> 1] : pe[i >> 1];
-    };
-    f32x2 s2[2];
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-        const int q = 2 * h;
-        if constexpr (2 * R + 1 > 5) {
-            f32x2 a = {0.f, 0.f};
-#pragma unroll
-            for (int k = 0; k <= 2 * R; k++) a = __builtin_elementwise_fma(pr(q + k), (f32x2)taps.w[k], a);
-            s2[h] = a;
-        } else {
-            f32x2 a = pr(q + R) * (f32x2)taps.w[R];
-#pragma unroll
-            for (int k = 1; k <= R; k++)
-                a = __builtin_elementwise_fma(pr(q + R - k) + pr(q + R + k), (f32x2)taps.w[R + k], a);
-            s2[h] = a;
-        }
-    }
-    return (f32x4){s2[0][0], s2[0][1], s2[1][0], s2[1][1]};
-}
-
-// Packed column pass: 8 outputs (rows base+R .. base+R+7 of the window) of
-// column `col`, window rows base .. base + 7 + 2R at pitch P.
-template <int R, int P>
-__device__ __forceinline__ void chain_col8(const float* __restrict__ base, const Taps& taps, float out[8]) {
-    const volatile __attribute__((address_space(3))) float* vm =
-        (const volatile __attribute__((address_space(3))) float*)base;
-    f32x2 cp[4 + 2 * R];
-#pragma unroll
-    for (int j = 0; j < 4 + 2 * R; j++) cp[j] = (f32x2){vm[j * P], vm[(j + 4) * P]};
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        f32x2 a = __builtin_elementwise_fma(cp[q + R], (f32x2)taps.w[R], (f32x2){0.f, 0.f});
-#pragma unroll
-        for (int k = 1; k <= R; k++) a = __builtin_elementwise_fma(cp[q + R + k] + cp[q + R - k], (f32x2)taps.w[R + k], a);
-        out[q] = a[0];
-        out[q + 4] = a[1];
-    }
-}
-
-// Store a 64 x BLUR_TH output tile held in LDS rows (pitch P, first column
-// c0, 4-aligned) to dst: 16-byte stores for full tiles, dwords at the edges.
-template <int P, int NT>
-__device__ __forceinline__ void chain_store_tile(const float* __restrict__ lds, int row0, int c0, float* __restrict__ dst,
-                                                 int dpitch, int x0, int y0, int W, int H) {
-    typedef unsigned u32x4t __attribute__((ext_vector_type(4)));
-    const int tid = threadIdx.x;
-    if (y0 + BLUR_TH <= H && x0 + BLUR_TW <= W) {
-        const __amdgpu_buffer_rsrc_t drs =
-            __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)min((long)dpitch * H * 4, 0x7fffffffL), 0x00020000);
-#pragma unroll
-        for (int u = 0; u < BLUR_TH * 16 / NT; u++) {
-            const int i = tid + NT * u, r = i >> 4, c4 = 4 * (i & 15);
-            const u32x4t v = *reinterpret_cast<const u32x4t*>(lds + (row0 + r) * P + c0 + c4);
-            __builtin_amdgcn_raw_buffer_store_b128(v, drs, (unsigned)((y0 + r) * dpitch + x0 + c4) * 4u, 0, 0);
-        }
-    } else {
-        for (int i = tid; i < BLUR_TH * BLUR_TW; i += NT) {
-            const int r = i >> 6, c = i & 63;
-            if (y0 + r < H && x0 + c < W) dst[(size_t)(y0 + r) * dpitch + x0 + c] = lds[(row0 + r) * P + c0 + c];
-        }
-    }
-}
-
-template <int RA, int RB, int NWAVES>
-__device__ __forceinline__ void chain_tile(const BlurChainJob& CJ, int blk, float* __restrict__ in) {
-    using G = ChainGeom<RA, RB>;
-    constexpr int NT = 64 * NWAVES, IW = G::IW, IH = G::IH, ORG = G::ORG, RT = G::RT;
-    const BlurJob& J = CJ.a;
-    const int t = xcd_tile(blk, J.ntiles * J.nf);
-    const int f = t / J.ntiles, tile = t - f * J.ntiles;
-    const float* __restrict__ src = fptr(static_cast<const float*>(J.src), f * J.sfs);
-    float* __restrict__ dstA = fptr(J.dst, f * J.dfs);
-    float* __restrict__ dstB = fptr(CJ.dst2, f * J.dfs);
-    float* __restrict__ copy_out = J.copy_out ? fptr(J.copy_out, f * J.dfs) : nullptr;
-    const int spitch = J.spitch, sstep = J.sstep, W = J.W, H = J.H, dpitch = J.dpitch;
-    const int x0 = (tile % J.tilesX) * BLUR_TW, y0 = (tile / J.tilesX) * BLUR_TH;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-
-    // ---- stage the (IH x IW) input tile: LDS (r, c) = image (y0 - RT + r, x0 - ORG + c)
-    {
-        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<float*>(src), 0, (int)min((long)spitch * sstep * H * 4, 0x7fffffffL), 0x00020000);
-        const bool x4 = sstep == 1 && x0 - ORG >= 0 && x0 - ORG + IW <= W && y0 - RT >= 0 && y0 - RT + IH <= H;
-        if (x4) {
-            typedef unsigned u32x4s __attribute__((ext_vector_type(4)));
-            constexpr int QR = IW / 4, NQ = QR * IH, QPT = (NQ + NT - 1) / NT;
-            u32x4s q4[QPT];
-            const int rb0 = (y0 - RT) * spitch + x0 - ORG;
-#pragma unroll
-            for (int u = 0; u < QPT; u++) {
-                const int idx = min(tid + NT * u, NQ - 1), row = idx / QR, qq = idx - row * QR;
-                q4[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (unsigned)(rb0 + row * spitch + 4 * qq) * 4u, 0, 0);
-            }
-#pragma unroll
-            for (int u = 0; u < QPT; u++)
-                if (u < QPT - 1 || tid + NT * u < NQ) *reinterpret_cast<u32x4s*>(in + 4 * (tid + NT * u)) = q4[u];
-        } else {
-            // Reflected dword loads (one bounce, then clamped: the host runs
-            // chains only when min(W, H) > RA + RB + 1, so every position that
-            // feeds an in-image output reflects exactly; the others only stay
-            // in bounds).
-            auto refl = [](int p, int len) {
-                p = p < 0 ? -p : (p >= len ? 2 * len - 2 - p : p);
-                return min(max(p, 0), len - 1);
-            };
-            constexpr int NE = IW * IH, EPT = (NE + NT - 1) / NT;
-            float v[EPT];
-#pragma unroll
-            for (int u = 0; u < EPT; u++) {
-                const int idx = min(tid + NT * u, NE - 1), r = idx / IW, c = idx - r * IW;
-                const int gy = refl(y0 - RT + r, H), gx = refl(x0 - ORG + c, W);
-                v[u] = __builtin_bit_cast(
-                    float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, (unsigned)((gy * spitch + gx) * sstep) * 4u, 0, 0));
-            }
-#pragma unroll
-            for (int u = 0; u < EPT; u++)
-                if (u < EPT - 1 || tid + NT * u < NE) in[tid + NT * u] = v[u];
-        }
-    }
-    lds_barrier();
-    if (copy_out) {  // decimated base plane of this octave = the tile's interior inputs
-        for (int i = tid; i < BLUR_TH * BLUR_TW; i += NT) {
-            const int r = i >> 6, c = i & 63;
-            if (y0 + r < H && x0 + c < W) copy_out[(size_t)(y0 + r) * dpitch + x0 + c] = in[(RT + r) * IW + ORG + c];
-        }
-        lds_barrier();  // read before the row pass overwrites the tile
-    }
-
-    // ---- blur A, row pass, in place: rows 0 .. IH-1, outputs at columns RUA .. RUA + 4 NA4
-    {
-        constexpr int NA4 = G::NA4, RPI = 64 / NA4;
-        const int sub = lane / NA4, q = lane - sub * NA4;
-        if (sub < RPI) {
-            for (int ly = wave * RPI + sub; ly < IH; ly += NWAVES * RPI) {
-                float* rowp = in + ly * IW;
-                const int c0 = G::RUA + 4 * q;
-                const f32x4 o = chain_row4<RA>(rowp, c0, J.taps);
-                *reinterpret_cast<f32x4*>(rowp + c0) = o;
-            }
-        }
-    }
-    lds_barrier();
-
-    // ---- blur A, column pass into registers: intermediate rows 0 .. MH-1 (8-row
-    // blocks, the last one aligned to MH), columns ORG - RB .. ORG - RB + WA
-    constexpr int NBA = (G::MH + 7) / 8, NIA = G::WA * NBA, IPT = (NIA + NT - 1) / NT;
-    float acc[IPT][8];
-#pragma unroll
-    for (int u = 0; u < IPT; u++) {
-        const int i = min(tid + NT * u, NIA - 1), b = i / G::WA, c = i - b * G::WA;
-        const int rb = min(8 * b, G::MH - 8);
-        chain_col8<RA, IW>(in + rb * IW + ORG - RB + c, J.taps, acc[u]);
-    }
-    lds_barrier();  // every read of the staged tile is done: the intermediate overwrites it
-#pragma unroll
-    for (int u = 0; u < IPT; u++) {
-        const int i = min(tid + NT * u, NIA - 1), b = i / G::WA, c = i - b * G::WA;
-        const int rb = min(8 * b, G::MH - 8);
-        if (u < IPT - 1 || tid + NT * u < NIA) {
-#pragma unroll
-            for (int qq = 0; qq < 8; qq++) in[(rb + qq) * IW + ORG - RB + c] = acc[u][qq];
-        }
-    }
-    lds_barrier();
-
-    // ---- intermediate halo outside the image = reflect-101 of its in-image
-    // values (what blur B of a stored plane i reads); only positions that feed
-    // in-image outputs.  Disjoint from the in-image core the store reads.
-    if (x0 - RB < 0 || x0 + BLUR_TW + RB > W || y0 - RB < 0 || y0 + BLUR_TH + RB > H) {
-        for (int i = tid; i < G::MH * G::WA; i += NT) {
-            const int r = i / G::WA, c = i - r * G::WA;
-            const int gy = y0 - RB + r, gx = x0 - RB + c;
-            if ((gy < 0 || gy >= H || gx < 0 || gx >= W) && gy <= H - 1 + RB && gx <= W - 1 + RB) {
-                const int ry = gy < 0 ? -gy : (gy >= H ? 2 * H - 2 - gy : gy);
-                const int rx = gx < 0 ? -gx : (gx >= W ? 2 * W - 2 - gx : gx);
-                in[r * IW + ORG - RB + c] = in[(ry - y0 + RB) * IW + ORG - RB + (rx - x0 + RB)];
-            }
-        }
-    }
-    chain_store_tile<IW, NT>(in, RB, ORG, dstA, dpitch, x0, y0, W, H);
-    lds_barrier();
-
-    // ---- blur B, row pass, in place: intermediate rows 0 .. MH-1, outputs at
-    // columns ORG .. ORG + 64 (16 lanes per row, the ds_read_b128 lane groups
-    // of blur_tile: each 16-lane group covers the 64 banks once)
-    {
-        const int l = lane & 31;
-        const bool grpB = (l >= 4 && l < 12) || (l >= 16 && l < 20) || l >= 28;
-        const int bq = grpB ? (l < 12 ? l - 4 : (l < 20 ? l - 8 : l - 16)) : (l < 4 ? l : (l < 16 ? l - 8 : l - 12));
-        for (int ly = wave * 4 + (lane >> 5) * 2 + (grpB ? 1 : 0); ly < G::MH; ly += 4 * NWAVES) {
-            float* rowp = in + ly * IW;
-            const int c0 = ORG + 4 * bq;
-            const f32x4 o = chain_row4<RB>(rowp, c0, CJ.taps2);
-            *reinterpret_cast<f32x4*>(rowp + c0) = o;
-        }
-    }
-    lds_barrier();
-
-    // ---- blur B, column pass: lane = column, 8-row blocks
-    constexpr int CB = BLUR_TH / (8 * NWAVES);
-    float outs[CB][8];
-#pragma unroll
-    for (int cbk = 0; cbk < CB; cbk++) {
-        const int yb = (wave + cbk * NWAVES) * 8;
-        chain_col8<RB, IW>(in + yb * IW + ORG + lane, CJ.taps2, outs[cbk]);
-    }
-    lds_barrier();  // the output tile overwrites rows 0 .. BLUR_TH of the intermediate
-#pragma unroll
-    for (int cbk = 0; cbk < CB; cbk++) {
-        const int yb = (wave + cbk * NWAVES) * 8;
-#pragma unroll
-        for (int qq = 0; qq < 8; qq++) in[(yb + qq) * IW + ORG + lane] = outs[cbk][qq];
-    }
-    lds_barrier();
-    chain_store_tile<IW, NT>(in, 0, ORG, dstB, dpitch, x0, y0, W, H);
-}
-
-template <int RA, int RB, int NW>
-__global__ __launch_bounds__(64 * NW) void k_blur_chain(BlurChainJob J) {
-    __shared__ __attribute__((aligned(16))) float in[ChainGeom<RA, RB>::LDS];
-    chain_tile<RA, RB, NW>(J, blockIdx.x, in);
-}
-
-// A chain (octave o+1's first two planes) beside a single blur (octave o's
-// last plane) in one launch, as k_blur2 pairs single jobs.
-template <int RA, int RB, int R, int NW>
-__global__ __launch_bounds__(64 * NW) void k_blur_chain1(BlurChainJob A, BlurJob B) {
-    constexpr int NA = ChainGeom<RA, RB>::LDS, NB = blur_lds_floats<R>();
-    __shared__ __attribute__((aligned(16))) float in[NA > NB ? NA : NB];
-    const int na = A.a.ntiles * A.a.nf;
-    if ((int)blockIdx.x < na)
-        chain_tile<RA, RB, NW>(A, blockIdx.x, in);
-    else
-        blur_tile<R, float, NW>(B, blockIdx.x - na, in);
-}
-
-#ifndef SIFT_CHAIN_NW
-#define SIFT_CHAIN_NW 8  // waves per chain tile
-#endif
-
-static BlurChainJob make_chain(const BlurDesc& a, const BlurDesc& b, const Frames& fr) {
-    BlurChainJob c;
-    c.a = make_job(a.src, a.spitch, a.sstep, a.W, a.H, a.dst, a.dpitch, a.copy_out, *a.taps, nullptr, nullptr, fr,
-                   fr.stride);
-    c.dst2 = b.dst;
-    c.taps2 = *b.taps;
-    return c;
-}
-
-bool blur_chain_supported(int ra, int rb, int W, int H) {
-    if (min(W, H) <= ra + rb + 1) return false;
-    return (ra == 5 && rb == 6) || (ra == 8 && rb == 10);
-}
-
-bool launch_blur_chain(const BlurDesc& a, const BlurDesc& b, const BlurDesc* single, const Frames& fr, hipStream_t s) {
-    const int ra = a.taps->n >> 1, rb = b.taps->n >> 1;
-    if (!blur_chain_supported(ra, rb, a.W, a.H)) return false;
-    constexpr int NW = SIFT_CHAIN_NW;
-    const BlurChainJob c = make_chain(a, b, fr);
-    const int na = c.a.ntiles * c.a.nf;
-    if (single) {
-        const BlurJob j = make_job(single->src, single->spitch, single->sstep, single->W, single->H, single->dst,
-                                   single->dpitch, single->copy_out, *single->taps, nullptr, nullptr, fr, fr.stride);
-        const int r = single->taps->n >> 1, nb = j.ntiles * j.nf;
-        if (ra == 5 && rb == 6 && r == 13) {
-            hipLaunchKernelGGL((k_blur_chain1<5, 6, 13, NW>), dim3(na + nb), dim3(64 * NW), 0, s, c, j);
-            return true;
-        }
-        return false;
-    }
-    if (ra == 5 && rb == 6)
-        hipLaunchKernelGGL((k_blur_chain<5, 6, NW>), dim3(na), dim3(64 * NW), 0, s, c);
-    else
-        hipLaunchKernelGGL((k_blur_chain<8, 10, NW>), dim3(na), dim3(64 * NW), 0, s, c);
-    return true;
-}
-
-// 8-bit frames: the first blur reads the bytes itself for the default init
-// radii (sigma 1.6: 13 taps without upscale); any other radius converts the
-// frame to float first (k_u8_to_f32) and runs the float blur.
 bool launch_blur_u8(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, const Taps& taps,
                     const Frames& fr, long sfs, hipStream_t s, unsigned* range_keys, Counters* zero_ctr) {
-    const BlurJob j = make_job(src, spitch, 1, W, H, dst, dpitch, nullptr, taps, range_keys, zero_ctr, fr, sfs);
+    const BlurJob j = make_job(src, spitch, 1, W, H, dst, dpitch, DecOut{}, taps, range_keys, zero_ctr, fr, sfs);
     const int tiles = j.ntiles * j.nf;
     const bool big = blur_waves(tiles) == 4;
     switch (taps.n >> 1) {
@@ -962,11 +623,11 @@ void launch_u8_to_f32(const uint8_t* src, int spitch, int W, int H, float* dst, 
                        sfs, fr.stride);
 }
 
-void launch_blur(const float* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, float* copy_out,
+void launch_blur(const float* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, const DecOut& dec,
                  const Taps& taps, const Frames& fr, long sfs, hipStream_t s, unsigned* range_keys,
                  Counters* zero_ctr) {
     const int r = taps.n >> 1;  // 1 .. kMaxTaps/2 (taps.n >= 3 by construction)
-    kBlurTable[r - 1](make_job(src, spitch, sstep, W, H, dst, dpitch, copy_out, taps, range_keys, zero_ctr, fr, sfs), s);
+    kBlurTable[r - 1](make_job(src, spitch, sstep, W, H, dst, dpitch, dec, taps, range_keys, zero_ctr, fr, sfs), s);
 }
 
 // ---------------------------------------------------------------------------

@@ -93,7 +93,14 @@ void launch_upsample2x(const float* src, int spitch, int W, int H, float* dst, i
 constexpr int kRangeSlots = 256;
 // range_keys (nullable): 2 * kRangeSlots keys, zeroed before the launch.
 // zero_ctr (nullable): counters to zero (the frame's first blur).
-void launch_blur(const float* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, float* copy_out,
+// The next octave's base plane, written by the blur of plane L of this octave
+// as it stores its tiles: dst[2y][2x] -> p[y][x] for x < W, y < H (OpenCV's
+// INTER_NEAREST half-size resize).  p == nullptr: none.
+struct DecOut {
+    float* p = nullptr;
+    int pitch = 0, W = 0, H = 0;
+};
+void launch_blur(const float* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, const DecOut& dec,
                  const Taps& taps, const Frames& fr, long sfs, hipStream_t s, unsigned* range_keys = nullptr,
                  Counters* zero_ctr = nullptr);
 // Two independent float blurs in one launch (no range keys / counters);
@@ -103,16 +110,10 @@ struct BlurDesc {
     int spitch, sstep, W, H;
     float* dst;
     int dpitch;
-    float* copy_out;
+    DecOut dec;
     const Taps* taps;
 };
 bool launch_blur_pair(const BlurDesc& a, const BlurDesc& b, const Frames& fr, hipStream_t s);
-// Chained blurs: plane a.dst from a.src, then plane b.dst from a.dst (b.src
-// ignored), in one tile pass; optionally beside an independent single blur
-// in the same launch.  false (nothing launched) without an instantiation for
-// the radii, or for planes too small for one-bounce reflection.
-bool blur_chain_supported(int ra, int rb, int W, int H);
-bool launch_blur_chain(const BlurDesc& a, const BlurDesc& b, const BlurDesc* single, const Frames& fr, hipStream_t s);
 // 8-bit frames (pitches in bytes).  launch_blur_u8 returns false (nothing
 // launched) for an init radius without a fused 8-bit instantiation; the caller
 // then converts with launch_u8_to_f32 and uses launch_blur.
