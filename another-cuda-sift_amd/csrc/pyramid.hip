@@ -123,11 +123,18 @@ struct BlurJob {
 #define SIFT_BLUR_IW16 1
 #endif
 // Tiles with every input in the image read their staging rows as aligned
-// 16-byte loads of columns x0 - 8 .. x0 + 71 (radius <= 8): a quarter of the
-// load instructions of the per-column dword staging.  The LDS tile then starts
-// at column x0 - 8 for every radius <= 8 (ORG), whichever staging ran.
+// 16-byte loads of columns x0 - ORG .. x0 + 63 + ORG, ORG = 8 for radius <= 8
+// and R rounded up to a multiple of 4 above (12 at R = 10, 16 at R = 13): a
+// quarter of the load instructions of the per-column dword staging.  The LDS
+// tile starts at column x0 - ORG whichever staging ran.
 #ifndef SIFT_BLUR_X4LD
 #define SIFT_BLUR_X4LD 1
+#endif
+#ifndef SIFT_BLUR_X4LD_BIG
+#define SIFT_BLUR_X4LD_BIG 1  // the 16-byte staging for radii > 8 too
+#endif
+#ifndef SIFT_BLUR_X4LD_MAXR
+#define SIFT_BLUR_X4LD_MAXR 24
 #endif
 // Full tiles store their output rows as 16-byte stores (each wave's 8-row
 // blocks transposed through the freed LDS tile) instead of one dword per
@@ -142,10 +149,14 @@ struct BlurJob {
 #endif
 template <int R>
 constexpr int blur_org() {  // tile column 0 = image column x0 - ORG
-    return SIFT_BLUR_X4LD && R <= 8 ? 8 : R;
+    return SIFT_BLUR_X4LD && R <= 8 ? 8 : SIFT_BLUR_X4LD && SIFT_BLUR_X4LD_BIG && R <= SIFT_BLUR_X4LD_MAXR ? (R + 3) & ~3 : R;
 }
+// Radius 11..24 with the dword staging: pitch 112 (16 mod 32, conflict-free
+// row-pass stores).  With the 16-byte staging (default) the rows stay unpadded
+// (R = 13: 96 floats) so the interior tiles stage by LDS-DMA: the paired
+// R = 13 launch 115.7 -> 113.0 us per 16 frames (tools/r3_blur_x4_ab.sh).
 #ifndef SIFT_BLUR_IW112
-#define SIFT_BLUR_IW112 1  // radius 11..24: pitch 112 (16 mod 32) -- 4 workgroups per CU either way at R = 13
+#define SIFT_BLUR_IW112 0
 #endif
 template <int R>
 constexpr int blur_iw() {  // radius 9, 10: the next 16-mod-32 pitch (112) costs a workgroup per CU -- kept at 64 + 2R
@@ -230,47 +241,50 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
                 v1[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, c1, roff, 0));
             }
         };
-        const bool x4 = ES == 4 && ORG == 8 && sstep == 1 && x0 >= 8 && x0 + BLUR_TW + 8 <= W && y0 - R >= 0 &&
-                        y0 - R + IH <= H;  // uniform
+        constexpr int QW = (BLUR_TW + 2 * ORG) / 4;  // float4s per staged row
+        const bool x4 = ES == 4 && ORG % 4 == 0 && ORG >= R && sstep == 1 && x0 >= ORG &&
+                        x0 + BLUR_TW + ORG <= W && y0 - R >= 0 && y0 - R + IH <= H;  // uniform
         if (x4) {
-            // Interior tile: 16-byte loads of the 80-column rows (IW = 80, so the
-            // LDS tile is one contiguous run of float4s), all in flight before
-            // the first LDS store.
-            static_assert(ES != 4 || ORG != 8 || IW == 80, "x4 staging assumes 80-float LDS rows");
-            constexpr int NQ = 20 * IH, NT = 64 * BLUR_NW, QPT = (NQ + NT - 1) / NT;
-            const int rb0 = (y0 - R) * spitch + x0 - 8;
-#if SIFT_BLUR_DMA
-            // LDS-DMA: float4 q of the tile goes from global memory straight
-            // to LDS float4 q (global_load_lds_dwordx4: a wave's 64 lanes fill
-            // 1 KiB at M0), no VGPR round trip and no ds_write_b128; the
-            // staging barrier below waits for vmcnt(0).
-            const float* fsrc = reinterpret_cast<const float*>(src);  // ES == 4 here
+            // Interior tile: 16-byte loads of the QW-float4 rows, all in
+            // flight before the first LDS store.
+            static_assert(!(ES == 4 && ORG % 4 == 0) || 4 * QW <= IW, "x4 staging row inside the LDS row");
+            constexpr int NQ = QW * IH, NT = 64 * BLUR_NW, QPT = (NQ + NT - 1) / NT;
+            const int rb0 = (y0 - R) * spitch + x0 - ORG;
+            if constexpr (SIFT_BLUR_DMA && IW == 4 * QW) {
+                // LDS-DMA (the LDS rows are unpadded: float4 q of the tile goes
+                // to LDS float4 q; global_load_lds_dwordx4: a wave's 64 lanes
+                // fill 1 KiB at M0), no VGPR round trip and no ds_write_b128.
+                const float* fsrc = reinterpret_cast<const float*>(src);  // ES == 4 here
 #pragma unroll
-            for (int u = 0; u < QPT; u++) {
-                const int idx = tid + NT * u;
-                if (u < QPT - 1 || idx < NQ) {
-                    const int row = idx / 20, qq = idx - row * 20;
-                    __builtin_amdgcn_global_load_lds(
-                        (const void*)(fsrc + rb0 + row * spitch + 4 * qq),
-                        (__attribute__((address_space(3))) void*)(in + 4 * (NT * u + 64 * (tid >> 6))), 16, 0, 0);
+                for (int u = 0; u < QPT; u++) {
+                    const int idx = tid + NT * u;
+                    if (u < QPT - 1 || idx < NQ) {
+                        const int row = idx / QW, qq = idx - row * QW;
+                        __builtin_amdgcn_global_load_lds(
+                            (const void*)(fsrc + rb0 + row * spitch + 4 * qq),
+                            (__attribute__((address_space(3))) void*)(in + 4 * (NT * u + 64 * (tid >> 6))), 16, 0, 0);
+                    }
+                }
+                // LDS-DMA writes are counted by vmcnt, not lgkmcnt: wait for this
+                // wave's copies explicitly so the staging barrier below publishes
+                // them whatever fence the compiler gives __syncthreads().
+                __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            } else {
+                // Padded LDS rows (R = 13: 96 floats staged in a 112-float pitch):
+                // 16-byte loads into VGPRs, then ds_write_b128 per float4.
+                typedef unsigned u32x4s __attribute__((ext_vector_type(4)));
+                u32x4s q4[QPT];
+#pragma unroll
+                for (int u = 0; u < QPT; u++) {
+                    const int idx = min(tid + NT * u, NQ - 1), row = idx / QW, qq = idx - row * QW;
+                    q4[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (unsigned)(rb0 + row * spitch + 4 * qq) * 4u, 0, 0);
+                }
+#pragma unroll
+                for (int u = 0; u < QPT; u++) {
+                    const int idx = tid + NT * u, row = idx / QW, qq = idx - row * QW;
+                    if (u < QPT - 1 || idx < NQ) *reinterpret_cast<u32x4s*>(in + row * IW + 4 * qq) = q4[u];
                 }
             }
-            // LDS-DMA writes are counted by vmcnt, not lgkmcnt: wait for this
-            // wave's copies explicitly so the staging barrier below publishes
-            // them whatever fence the compiler gives __syncthreads().
-            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#else
-            typedef unsigned u32x4s __attribute__((ext_vector_type(4)));
-            u32x4s q4[QPT];
-#pragma unroll
-            for (int u = 0; u < QPT; u++) {
-                const int idx = min(tid + NT * u, NQ - 1), row = idx / 20, qq = idx - row * 20;
-                q4[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (unsigned)(rb0 + row * spitch + 4 * qq) * 4u, 0, 0);
-            }
-#pragma unroll
-            for (int u = 0; u < QPT; u++)
-                if (u < QPT - 1 || tid + NT * u < NQ) *reinterpret_cast<u32x4s*>(in + 4 * (tid + NT * u)) = q4[u];
-#endif
         } else if (y0 - R >= 0 && y0 - R + IH <= H) {
             // Interior rows (most tiles): the row offset advances by a constant,
             // one s_add per row.  Rows past IH of the last step read in-range
