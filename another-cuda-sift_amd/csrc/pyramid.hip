@@ -421,10 +421,11 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
                 if (gy < H && gx < W) dst[(size_t)gy * dpitch + gx] = out[q];
             }
         }
-        if (dec_out) {
-            // The next octave's base plane: even rows and columns of this
-            // plane (y0, yb even), stored by the even lanes; other lanes get
-            // an offset past the buffer, which the hardware drops (no branch).
+        if (dec_out && !(SIFT_BLUR_X4ST && full)) {
+            // The next octave's base plane (edge tiles; full tiles store it
+            // from the LDS image below): even rows and columns of this plane
+            // (y0, yb even), stored by the even lanes; other lanes get an
+            // offset past the buffer, which the hardware drops (no branch).
             const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
                 dec_out, 0, (int)min((long)J.dec.pitch * J.dec.H * 4, 0x7fffffffL), 0x00020000);
             const bool cx = (gx & 1) == 0 && (gx >> 1) < J.dec.W;
@@ -469,6 +470,26 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
                 const int row = yb + 4 * hh + (lane >> 4), c4 = 4 * (lane & 15);
                 const u32x4t v = *reinterpret_cast<const u32x4t*>(in + row * BLUR_TW + c4);
                 __builtin_amdgcn_raw_buffer_store_b128(v, drs, (unsigned)((y0 + row) * dpitch + x0 + c4) * 4u, 0, 0);
+            }
+        }
+        if (dec_out) {
+            // The next octave's base plane from the same LDS image: an 8-row
+            // block gives 4 rows x 8 float4s of even rows and columns; lane l
+            // takes block 2 it + l / 32, row (l % 32) / 8, float4 l % 8 (two
+            // 16-byte LDS reads, the even elements, one 16-byte store).
+            const __amdgpu_buffer_rsrc_t ers = __builtin_amdgcn_make_buffer_rsrc(
+                dec_out, 0, (int)min((long)J.dec.pitch * J.dec.H * 4, 0x7fffffffL), 0x00020000);
+            const int r4 = (lane & 31) >> 3, c8 = 8 * (lane & 7);
+#pragma unroll
+            for (int it = 0; it < (BLUR_CB + 1) / 2; it++) {
+                const int cbk = 2 * it + (lane >> 5);
+                const int yb = (wave + min(cbk, BLUR_CB - 1) * BLUR_NW) * 8;
+                const f32x4* rp = reinterpret_cast<const f32x4*>(in + (yb + 2 * r4) * BLUR_TW + c8);
+                const f32x4 a = rp[0], b = rp[1];
+                const u32x4t v = __builtin_bit_cast(u32x4t, (f32x4){a[0], a[2], b[0], b[2]});
+                const unsigned off =
+                    cbk < BLUR_CB ? (unsigned)(((y0 + yb) / 2 + r4) * J.dec.pitch + x0 / 2 + c8 / 2) * 4u : 0x80000000u;
+                __builtin_amdgcn_raw_buffer_store_b128(v, ers, off, 0, 0);
             }
         }
     }
