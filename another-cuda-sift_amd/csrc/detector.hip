@@ -546,7 +546,7 @@ void enqueue_head(sift_hip_detector* d, const void* img, int pitch, int fmt, int
                 pitch = d->inPitch;
                 s = d->afs;
             }
-            launch_blur((const float*)img, pitch, 1, W, H, g.base, g.pitch, DecOut{}, d->initTaps, fr, s, d->stream,
+            launch_blur((const float*)img, pitch, W, H, g.base, g.pitch, DecOut{}, d->initTaps, fr, s, d->stream,
                         range_keys(d, parity), d->dCtr);
         });
     }
@@ -563,7 +563,7 @@ void enqueue_pyramid(sift_hip_detector* d, int nf, int parity) {
     if (d->firstOctave < 0) {
         const OctGeom& g = d->pyr.oct[0];
         d->timed("blur_init", (double)g.W * g.H * 8 * nf, [&] {
-            launch_blur(d->dUp, d->upPitch, 1, g.W, g.H, g.base, g.pitch, DecOut{}, d->initTaps, fr, d->afs, s,
+            launch_blur(d->dUp, d->upPitch, g.W, g.H, g.base, g.pitch, DecOut{}, d->initTaps, fr, d->afs, s,
                         range_keys(d, parity), d->dCtr);
         });
     }
@@ -589,7 +589,6 @@ void enqueue_pyramid(sift_hip_detector* d, int nf, int parity) {
             Job j{o, i, {}, 0};
             j.b.src = g.base + (size_t)(i - 1) * g.planeStride;
             j.b.spitch = g.pitch;
-            j.b.sstep = 1;
             j.b.dst = g.base + (size_t)i * g.planeStride;
             j.b.dpitch = g.pitch;
             j.b.W = g.W;
@@ -630,7 +629,7 @@ void enqueue_pyramid(sift_hip_detector* d, int nf, int parity) {
         }
         if (!paired) {
             d->timed(blurNames[ja.o], ja.bytes, [&] {
-                launch_blur(ja.b.src, ja.b.spitch, ja.b.sstep, ja.b.W, ja.b.H, ja.b.dst, ja.b.dpitch, ja.b.dec,
+                launch_blur(ja.b.src, ja.b.spitch, ja.b.W, ja.b.H, ja.b.dst, ja.b.dpitch, ja.b.dec,
                             *ja.b.taps, fr, d->afs, s);
             });
         }

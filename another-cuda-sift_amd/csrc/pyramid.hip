@@ -63,8 +63,9 @@ void launch_upsample2x_u8(const uint8_t* src, int spitch, int W, int H, float* d
 // Separable Gaussian blur, one 64 x BLUR_TH output tile per workgroup of
 // BLUR_NW waves (each BLUR_TH / BLUR_NW rows of the column pass),
 // instantiated per radius R (taps 2R+1) so every tap loop is fully unrolled.
-// The (BLUR_TH+2R) x (64+2R) input tile (reflect-101 borders, optional stride-2
-// read = INTER_NEAREST octave decimation fused in) is staged once in LDS.
+// The (BLUR_TH+2R) x (64+2R) input tile (reflect-101 borders) is staged once
+// in LDS; the blur of an octave's plane L also writes the next octave's base
+// plane (its even rows and columns, OpenCV's INTER_NEAREST half-size resize).
 // Row pass: 16 threads per row, each keeps a (2R+4)-float register window
 // (ds_read_b128) and runs 4 independent fma chains (4 adjacent outputs).
 // Column pass: one column per lane, 8 rows per thread, (2R+8)-float window.
@@ -106,7 +107,7 @@ struct BlurJob {
     DecOut dec;
     unsigned* range_keys;
     Counters* zero_ctr;
-    int spitch, sstep, W, H, dpitch, tilesX, ntiles;
+    int spitch, W, H, dpitch, tilesX, ntiles;
     int nf;         // frames; the launch has nf * ntiles tiles of this job
     long sfs, dfs;  // byte strides between frames: source; dst / dec / range_keys / zero_ctr
     Taps taps;
@@ -192,7 +193,7 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
     float* __restrict__ dec_out = J.dec.p ? fptr(J.dec.p, f * J.dfs) : nullptr;
     unsigned* __restrict__ range_keys = J.range_keys ? fptr(J.range_keys, f * J.dfs) : nullptr;
     Counters* __restrict__ zero_ctr = J.zero_ctr ? fptr(J.zero_ctr, f * J.dfs) : nullptr;
-    const int spitch = J.spitch, sstep = J.sstep, W = J.W, H = J.H, dpitch = J.dpitch;
+    const int spitch = J.spitch, W = J.W, H = J.H, dpitch = J.dpitch;
     const Taps& taps = J.taps;
     // Row-pass results (`mid`, pitch IW) overwrite their own input row of
     // `in` in place: a row is read and written only by the same 16 lanes of
@@ -228,9 +229,9 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
         const int gx0 = refl(x0 - R + lane, W), gx1 = refl(x0 - R + 64 + min(lane, RW - 65), W);
         constexpr int ES = (int)sizeof(T);
         const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<T*>(src), 0, (int)min((long)spitch * sstep * H * ES, 0x7fffffffL), 0x00020000);
-        const unsigned c0 = (unsigned)(gx0 * sstep) * ES, c1 = (unsigned)(gx1 * sstep) * ES;
-        const int rowB = spitch * sstep * ES;  // bytes per source row
+            const_cast<T*>(src), 0, (int)min((long)spitch * H * ES, 0x7fffffffL), 0x00020000);
+        const unsigned c0 = (unsigned)gx0 * ES, c1 = (unsigned)gx1 * ES;
+        const int rowB = spitch * ES;  // bytes per source row
         float v0[RPW], v1[RPW];
         auto ld = [&](int i, int roff) {
             if constexpr (ES == 1) {
@@ -242,7 +243,7 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
             }
         };
         constexpr int QW = (BLUR_TW + 2 * ORG) / 4;  // float4s per staged row
-        const bool x4 = ES == 4 && ORG % 4 == 0 && ORG >= R && sstep == 1 && x0 >= ORG &&
+        const bool x4 = ES == 4 && ORG % 4 == 0 && ORG >= R && x0 >= ORG &&
                         x0 + BLUR_TW + ORG <= W && y0 - R >= 0 && y0 - R + IH <= H;  // uniform
         if (x4) {
             // Interior tile: 16-byte loads of the QW-float4 rows, all in
@@ -544,7 +545,7 @@ __global__ __launch_bounds__(64 * NW) void k_blur2(BlurJob A, BlurJob B) {
         blur_tile<RB, float, NW>(B, blockIdx.x - na, in);
 }
 
-static BlurJob make_job(const void* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, const DecOut& dec,
+static BlurJob make_job(const void* src, int spitch, int W, int H, float* dst, int dpitch, const DecOut& dec,
                         const Taps& taps, unsigned* range_keys, Counters* zero_ctr, const Frames& fr, long sfs) {
     BlurJob j;
     j.nf = fr.nf;
@@ -556,7 +557,6 @@ static BlurJob make_job(const void* src, int spitch, int sstep, int W, int H, fl
     j.range_keys = range_keys;
     j.zero_ctr = zero_ctr;
     j.spitch = spitch;
-    j.sstep = sstep;
     j.W = W;
     j.H = H;
     j.dpitch = dpitch;
@@ -619,16 +619,16 @@ bool launch_blur_pair_jobs(const BlurJob& a, const BlurJob& b, hipStream_t s) {
 }
 
 bool launch_blur_pair(const BlurDesc& a, const BlurDesc& b, const Frames& fr, hipStream_t s) {
-    return launch_blur_pair_jobs(make_job(a.src, a.spitch, a.sstep, a.W, a.H, a.dst, a.dpitch, a.dec, *a.taps,
+    return launch_blur_pair_jobs(make_job(a.src, a.spitch, a.W, a.H, a.dst, a.dpitch, a.dec, *a.taps,
                                           nullptr, nullptr, fr, fr.stride),
-                                 make_job(b.src, b.spitch, b.sstep, b.W, b.H, b.dst, b.dpitch, b.dec, *b.taps,
+                                 make_job(b.src, b.spitch, b.W, b.H, b.dst, b.dpitch, b.dec, *b.taps,
                                           nullptr, nullptr, fr, fr.stride),
                                  s);
 }
 
 bool launch_blur_u8(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, const Taps& taps,
                     const Frames& fr, long sfs, hipStream_t s, unsigned* range_keys, Counters* zero_ctr) {
-    const BlurJob j = make_job(src, spitch, 1, W, H, dst, dpitch, DecOut{}, taps, range_keys, zero_ctr, fr, sfs);
+    const BlurJob j = make_job(src, spitch, W, H, dst, dpitch, DecOut{}, taps, range_keys, zero_ctr, fr, sfs);
     const int tiles = j.ntiles * j.nf;
     const bool big = blur_waves(tiles) == 4;
     switch (taps.n >> 1) {
@@ -658,11 +658,11 @@ void launch_u8_to_f32(const uint8_t* src, int spitch, int W, int H, float* dst, 
                        sfs, fr.stride);
 }
 
-void launch_blur(const float* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, const DecOut& dec,
+void launch_blur(const float* src, int spitch, int W, int H, float* dst, int dpitch, const DecOut& dec,
                  const Taps& taps, const Frames& fr, long sfs, hipStream_t s, unsigned* range_keys,
                  Counters* zero_ctr) {
     const int r = taps.n >> 1;  // 1 .. kMaxTaps/2 (taps.n >= 3 by construction)
-    kBlurTable[r - 1](make_job(src, spitch, sstep, W, H, dst, dpitch, dec, taps, range_keys, zero_ctr, fr, sfs), s);
+    kBlurTable[r - 1](make_job(src, spitch, W, H, dst, dpitch, dec, taps, range_keys, zero_ctr, fr, sfs), s);
 }
 
 // ---------------------------------------------------------------------------

@@ -100,14 +100,14 @@ struct DecOut {
     float* p = nullptr;
     int pitch = 0, W = 0, H = 0;
 };
-void launch_blur(const float* src, int spitch, int sstep, int W, int H, float* dst, int dpitch, const DecOut& dec,
+void launch_blur(const float* src, int spitch, int W, int H, float* dst, int dpitch, const DecOut& dec,
                  const Taps& taps, const Frames& fr, long sfs, hipStream_t s, unsigned* range_keys = nullptr,
                  Counters* zero_ctr = nullptr);
 // Two independent float blurs in one launch (no range keys / counters);
 // false (nothing launched) when the radius pair has no instantiation.
 struct BlurDesc {
     const float* src;
-    int spitch, sstep, W, H;
+    int spitch, W, H;
     float* dst;
     int dpitch;
     DecOut dec;

@@ -209,18 +209,15 @@ int main(int argc, char** argv) {
         lt[i] = taps_for(std::sqrt(st * st - sp * sp));
     }
     const Taps init = taps_for(std::sqrt(sigma * sigma - 0.25));
-    launch_blur(dIn, W0, 1, W0, H0, pyr.oct[0].base, pyr.oct[0].pitch, nullptr, init, kOne, 0, s);
+    launch_blur(dIn, W0, W0, H0, pyr.oct[0].base, pyr.oct[0].pitch, DecOut{}, init, kOne, 0, s);
     for (int o = 0; o < 3; o++) {
         const OctGeom& g = pyr.oct[o];
         for (int i = 1; i < L + 3; i++) {
-            float* dst = g.base + (size_t)i * g.planeStride;
-            if (i == 1 && o > 0) {
-                const OctGeom& p = pyr.oct[o - 1];
-                launch_blur(p.base + (size_t)L * p.planeStride, p.pitch, 2, g.W, g.H, dst, g.pitch, g.base, lt[i], kOne, 0, s);
-            } else {
-                launch_blur(g.base + (size_t)(i - 1) * g.planeStride, g.pitch, 1, g.W, g.H, dst, g.pitch, nullptr,
-                            lt[i], kOne, 0, s);
-            }
+            // plane L also writes the next octave's base plane (decimated)
+            DecOut dec;
+            if (i == L && o + 1 < 3) dec = DecOut{pyr.oct[o + 1].base, pyr.oct[o + 1].pitch, pyr.oct[o + 1].W, pyr.oct[o + 1].H};
+            launch_blur(g.base + (size_t)(i - 1) * g.planeStride, g.pitch, g.W, g.H, g.base + (size_t)i * g.planeStride,
+                        g.pitch, dec, lt[i], kOne, 0, s);
         }
     }
     CK(hipStreamSynchronize(s));
@@ -236,7 +233,7 @@ int main(int argc, char** argv) {
             float* src = g.base + (size_t)(i - 1) * g.planeStride;
             float* dst = g.base + (size_t)i * g.planeStride;
             const double bytes = 8.0 * g.W * g.H;
-            us = time_us(iters, s, [&] { launch_blur(src, g.pitch, 1, g.W, g.H, dst, g.pitch, nullptr, lt[i], kOne, 0, s); });
+            us = time_us(iters, s, [&] { launch_blur(src, g.pitch, g.W, g.H, dst, g.pitch, DecOut{}, lt[i], kOne, 0, s); });
             std::printf("{\"kernel\": \"k_blur<%d>\", \"octave\": %d, \"W\": %d, \"H\": %d, \"us\": %.3f, \"GBps\": %.1f}\n",
                         lt[i].n / 2, o, g.W, g.H, us, bytes / us / 1e3);
         }
