@@ -23,17 +23,22 @@ constexpr int kIters = 2048, kChains = 8;
 
 // op 0: v_add_f32, 1: v_lshl_add_u32, 2: v_max3_i32, 3: v_med3_i32, 4: v_add_u32, 5: v_max_i32,
 // 6: v_max3_f32, 7: v_med3_f32, 8: v_max_f32, 9: v_mad_i32_i24, 10: v_add3_u32, 11: v_fma_f32,
-// 12: v_lshlrev_b32, 13: v_max_u32, 14: v_pk_max_i16, 15: v_med3_u32
+// 12: v_lshlrev_b32, 13: v_max_u32, 14: v_pk_max_i16, 15: v_med3_u32,
+// 16: v_pk_fma_f32, 17: v_pk_mov_b32, 18: v_pk_add_f32, 19: v_fmac_f32 (VOP2)
 template <int OP, bool MFMA>
 __global__ __launch_bounds__(256) void k_valu(int seed, unsigned long long* cyc, int* sink) {
     const int lane = threadIdx.x & 63;
     int x[kChains];
     float f[kChains];
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 p2[kChains];
     for (int c = 0; c < kChains; c++) {
         x[c] = seed + lane * 3 + c;
         f[c] = (float)x[c];
+        p2[c] = (f2){f[c], f[c] + 1.f};
     }
     const int k1 = seed * 7 + lane, k2 = seed - lane;
+    const f2 q1 = {(float)k1, 1.5f}, q2 = {0.5f, (float)seed};
     const i32x4 a = {seed + lane, seed * 3, lane, 7}, b = {lane * 5, seed, 3, lane};
     i32x16 acc = {};
     __syncthreads();
@@ -58,11 +63,15 @@ __global__ __launch_bounds__(256) void k_valu(int seed, unsigned long long* cyc,
             if constexpr (OP == 13) __asm__ volatile("v_max_u32 %0, %0, %1" : "+v"(x[c]) : "v"(k1));
             if constexpr (OP == 14) __asm__ volatile("v_pk_max_i16 %0, %0, %1" : "+v"(x[c]) : "v"(k1));
             if constexpr (OP == 15) __asm__ volatile("v_med3_u32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(k1), "v"(k2));
+            if constexpr (OP == 16) __asm__ volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(p2[c]) : "v"(q1), "v"(q2));
+            if constexpr (OP == 17) __asm__ volatile("v_pk_mov_b32 %0, %0, %1 op_sel:[1,0]" : "+v"(p2[c]) : "v"(q1));
+            if constexpr (OP == 18) __asm__ volatile("v_pk_add_f32 %0, %0, %1" : "+v"(p2[c]) : "v"(q1));
+            if constexpr (OP == 19) __asm__ volatile("v_fmac_f32 %0, %1, %2" : "+v"(f[c]) : "v"(k1), "v"(k2));
         }
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     int s = acc[lane & 15];
-    for (int c = 0; c < kChains; c++) s += x[c] + (int)f[c];
+    for (int c = 0; c < kChains; c++) s += x[c] + (int)f[c] + (int)p2[c][0] + (int)p2[c][1];
     sink[blockIdx.x * blockDim.x + threadIdx.x] = s;
     if (lane == 0) cyc[blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)] = t1 - t0;
 }
@@ -92,20 +101,14 @@ static void run(const char* name, int wps) {
 }
 
 int main() {
-    for (int w : {2, 4}) {
+    for (int w : {2, 4, 6}) {
         run<0, false>("v_add_f32", w);
-        run<2, false>("v_max3_i32", w);
-        run<6, false>("v_max3_f32", w);
-        run<7, false>("v_med3_f32", w);
-        run<8, false>("v_max_f32", w);
-        run<9, false>("v_mad_i32_i24", w);
-        run<10, false>("v_add3_u32", w);
         run<11, false>("v_fma_f32", w);
-        run<12, false>("v_lshlrev_b32", w);
-        run<13, false>("v_max_u32", w);
-        run<14, false>("v_pk_max_i16", w);
-        run<15, false>("v_med3_u32", w);
-        run<6, true>("v_max3_f32", w);
+        run<19, false>("v_fmac_f32", w);
+        run<16, false>("v_pk_fma_f32", w);
+        run<17, false>("v_pk_mov_b32", w);
+        run<18, false>("v_pk_add_f32", w);
+        run<2, false>("v_max3_i32", w);
     }
     return 0;
 }
