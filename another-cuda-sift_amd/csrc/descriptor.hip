@@ -236,6 +236,9 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
     // them to the host's pinned copy directly (no D2H copy node in the graph).
     if (wg == 0 && tid < (int)(sizeof(Counters) / 4))
         reinterpret_cast<unsigned*>(host_ctr)[tid] = reinterpret_cast<const unsigned*>(ctr)[tid];
+    // A single frame's grid (8192) exceeds its keypoint count: the surplus
+    // workgroups leave before the pixel-range reduction below.
+    if (wg >= n) return;
     // Pixel range of the frame; it bounds every Gaussian plane (convex blurs).
     unsigned kmax = 0, knmn = 0;
     for (int i = lane; i < kRangeSlots; i += 64) {

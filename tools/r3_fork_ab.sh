@@ -1,5 +1,5 @@
 #!/bin/bash
-# Forked octave-0 extrema A/B: -m gpu suite on the working-tree build, then
+# Library A/B (bench lines): -m gpu suite on the working-tree build, then
 # bench lines (throughput, sync single-frame latency) of ab/{nofork,fork}, twice.
 set -o pipefail
 export TMPDIR=/tmp; mkdir -p gpurun_out
