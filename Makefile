@@ -11,6 +11,7 @@ PKG      := another-cuda-sift_amd
 SRC      := $(PKG)/csrc
 OUT      := $(PKG)/lib
 JOBS     ?= 8
+ROCM_LIB ?= /opt/rocm/lib
 
 # -ffp-contract=off + correctly rounded f32 div/sqrt: the float operation order
 # written in the kernels is the one executed (bit-exact parity with the oracle).
@@ -33,7 +34,8 @@ $(OUT)/obj/synth_frame.o: $(SRC)/synth_frame.cpp include/sift_hip.h
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
 $(OUT)/libsift_hip.so: $(HIP_OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HIP_OBJS) -ldl -Wl,-soname,libsift_hip.so
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HIP_OBJS) -ldl -L$(ROCM_LIB) -lrocprofiler-sdk-roctx \
+	    -Wl,-rpath,$(ROCM_LIB) -Wl,-soname,libsift_hip.so
 
 CXX_SRCS := $(SRC)/detector_cxx.cpp $(SRC)/multi_cxx.cpp
 
@@ -48,10 +50,26 @@ $(OUT)/%: tools/%.cpp $(OUT)/libsift_cuda.so
 oracle:
 	$(MAKE) -C oracle
 
+# Sanitizer builds of the host code (HIP kernels are not
+# instrumented, and GPU ASan is not available on the GPU pool): the CPU oracle,
+# and the C++ drop-in surface (detector_cxx.cpp, multi_cxx.cpp) linked into the
+# CPU orchestration test tests/cpp/test_multi.cpp, all with
+# -fsanitize=address,undefined.  tests/test_asan.py runs both.
+ASAN_DIR  := $(OUT)/asan
+SANFLAGS  := -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=undefined
+
+asan: $(ASAN_DIR)/test_multi
+	$(MAKE) -C oracle asan
+
+$(ASAN_DIR)/test_multi: tests/cpp/test_multi.cpp $(CXX_SRCS) $(wildcard include/sift_cuda/*.hh) include/sift_hip.h $(OUT)/libsift_hip.so
+	@mkdir -p $(ASAN_DIR)
+	$(CXX) -std=c++17 -Iinclude -Wall -Wextra $(SANFLAGS) -pthread -o $@ tests/cpp/test_multi.cpp $(CXX_SRCS) \
+	    -L$(OUT) -lsift_hip -Wl,-rpath,'$$ORIGIN/..'
+
 clean:
 	rm -rf $(OUT)
 
-.PHONY: all tools oracle clean
+.PHONY: all tools oracle asan clean
 
 # Isolated kernel timing (tools/kernel_bench.hip), not part of `all`.
 tools/kernel_bench: tools/kernel_bench.hip $(OUT)/obj/pyramid.o $(OUT)/obj/synth_frame.o

@@ -7,6 +7,7 @@
 // in device counters, every launch has a fixed grid, and the only host sync
 // per frame is the final 32-byte counter readback.
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <sys/stat.h>
 
@@ -282,9 +283,13 @@ struct sift_hip_detector {
         // repeated to time them back to back without per-launch event cost.
         const int reps = strncmp(name, "blur_", 5) == 0 ? blurReps : 1;
         TimingRec r{name_id(name), next_event(), next_event(), bytes * reps, reps};
+        // A roctx range per stage: rocprofv3
+        // --marker-trace shows the stage spans and the kernels launched in them.
+        roctxRangePushA(name);
         (void)hipEventRecord(r.e0, stream);
         for (int i = 0; i < reps; i++) fn();
         (void)hipEventRecord(r.e1, stream);
+        roctxRangePop();
         trecs.push_back(r);
     }
     void collect_timing() {
@@ -1070,16 +1075,9 @@ int replay_reset(sift_hip_detector* d) {
     return SIFT_HIP_OK;
 }
 
-int replay_stage(sift_hip_detector* d, const std::string& in, const std::string& stage, const std::string& out) {
-    static const char* kStages[] = {"pyramid", "extrema", "refine", "orientation", "order", "descriptor"};
-    bool known = false;
-    for (const char* k : kStages) known |= stage == k;
-    if (!known) return fail(SIFT_HIP_ERR_INVALID, "unknown stage '" + stage + "'");
-    if (!make_dirs(out)) return fail(SIFT_HIP_ERR_INVALID, "cannot create " + out);
-    HIPCHK(hipStreamSynchronize(d->stream));
-    const bool timing = d->timing;
-    d->timing = false;
-    if (int rc = replay_reset(d)) return rc;
+// The stage itself (replay_stage below owns the handle's state around it:
+// every return from here, error or not, is followed by the restore).
+int replay_stage_body(sift_hip_detector* d, const std::string& in, const std::string& stage, const std::string& out) {
     std::vector<Counters> dumped;  // the frame's final counters
     if (stage != "pyramid" && stage != "extrema") {
         if (int rc = read_vec(in + "/counters.u32", dumped)) return rc;
@@ -1202,9 +1200,28 @@ int replay_stage(sift_hip_detector* d, const std::string& in, const std::string&
         if (!jobs.empty()) HIPCHK(hipMemcpy(desc.data(), d->dDesc[0], sizeof(uint16_t) * desc.size(), hipMemcpyDeviceToHost));
         rc = write_file(out + "/desc.f16", desc.data(), sizeof(uint16_t) * desc.size());
     }
+    return rc;
+}
+
+// One cleanup path: once the arenas may have been touched (uploads, kernels),
+// the handle's timing mode and its post-warm-up scratch state (counters, the
+// dedupe bitmap, range keys) are restored on every exit, including a failed
+// read, capacity check, HIP call or output write, so the next frame starts
+// clean.  The first error is the one returned (and kept in last_error).
+int replay_stage(sift_hip_detector* d, const std::string& in, const std::string& stage, const std::string& out) {
+    static const char* kStages[] = {"pyramid", "extrema", "refine", "orientation", "order", "descriptor"};
+    bool known = false;
+    for (const char* k : kStages) known |= stage == k;
+    if (!known) return fail(SIFT_HIP_ERR_INVALID, "unknown stage '" + stage + "'");
+    if (!make_dirs(out)) return fail(SIFT_HIP_ERR_INVALID, "cannot create " + out);
+    HIPCHK(hipStreamSynchronize(d->stream));
+    const bool timing = d->timing;
+    d->timing = false;
+    int rc = replay_reset(d);
+    if (!rc) rc = replay_stage_body(d, in, stage, out);
     d->timing = timing;
-    if (rc) return rc;
-    return replay_reset(d);
+    const int rc_reset = replay_reset(d);
+    return rc ? rc : rc_reset;
 }
 
 #define CHECK_HANDLE(h)                                                                       \
@@ -1709,6 +1726,14 @@ int sift_hip_match_batched(sift_hip_matcher_t m, int P, const uint16_t* const* q
 int sift_hip_match_device(sift_hip_matcher_t m, const uint16_t* q, int nq, const uint16_t* t, int nt, float ratio,
                           int ratio_on_squared, int* idx2, float* d2, int* match, void* stream) {
     return sift_hip_match_batched(m, 1, &q, &nq, &t, &nt, ratio, ratio_on_squared, idx2, d2, match, stream);
+}
+
+int sift_hip_match_plan(int max_query, int max_train, int pairs, int* splits, int* waves) {
+    if (max_query < 0 || max_train < 0 || pairs < 1 || !splits) return fail(SIFT_HIP_ERR_INVALID, "bad match shape");
+    const MatchPlan pl = match_plan(max_query, max_train, pairs);
+    *splits = pl.S;
+    if (waves) *waves = pl.nw;
+    return SIFT_HIP_OK;
 }
 
 int sift_hip_match_host(sift_hip_matcher_t m, const uint16_t* q, int nq, const uint16_t* t, int nt, float ratio,

@@ -690,6 +690,11 @@ __global__ __launch_bounds__(64 * NW, (kMatchBatchWgPerCu * NW) / 4) void k_matc
 #ifndef SIFT_MATCH_FUSED_SINGLE
 #define SIFT_MATCH_FUSED_SINGLE 1  // single pairs: no prep launch (tools A/B builds set 0)
 #endif
+// The matcher's done counters are sized per (pair, kMatchQB-query block)
+// (sift_hip_matcher_create); a launch indexes them by its own block, which must
+// therefore hold at least kMatchQB queries.
+static_assert(64 * SIFT_MATCH_NW_SINGLE >= kMatchQB, "single-pair blocks smaller than the done-counter block");
+static_assert(kMatchBatchQB >= kMatchQB, "batched blocks smaller than the done-counter block");
 
 static int device_cus() {
     static int cus = [] {

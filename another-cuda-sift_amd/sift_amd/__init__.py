@@ -18,7 +18,9 @@ installed, so the load order no longer depends on the caller's imports.
 from __future__ import annotations
 
 import ctypes
+import importlib.util
 import os
+import sys
 from dataclasses import dataclass
 from typing import Optional, Sequence
 
@@ -60,10 +62,15 @@ def lib() -> ctypes.CDLL:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise SiftHipError(f"{LIB_PATH} not found: build it with `make` (or __graft_entry__.build())")
-    try:  # torch's bundled HIP runtime first (module docstring); importing torch does not touch the GPU
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    # torch's bundled HIP runtime first (module docstring), so one HIP runtime
+    # serves both; importing torch does not touch the GPU.  Only when torch is
+    # installed, and a broken torch install (OSError / RuntimeError from its
+    # bundled libraries) must not stop callers that never use torch.
+    if "torch" not in sys.modules and importlib.util.find_spec("torch") is not None:
+        try:
+            import torch  # noqa: F401
+        except Exception as e:  # noqa: BLE001
+            print(f"sift_amd: torch import failed ({e!r}); loading {LIB_PATH} on its own", file=sys.stderr)
     L = ctypes.CDLL(LIB_PATH)
     vp, ip, i, f, d, sz = ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_float, ctypes.c_double, ctypes.c_size_t
     sigs = {
@@ -106,6 +113,7 @@ def lib() -> ctypes.CDLL:
         "sift_hip_match_device": (i, [vp, vp, i, vp, i, f, i, vp, vp, vp, vp]),
         "sift_hip_match_batched": (i, [vp, i, vp, vp, vp, vp, f, i, vp, vp, vp, vp]),
         "sift_hip_match_host": (i, [vp, vp, i, vp, i, f, i, vp]),
+        "sift_hip_match_plan": (i, [i, i, i, ip, ip]),
         "sift_synth_frame": (i, [ctypes.c_uint, i, i, vp]),
         "sift_hip_device_count": (i, [ip]),
         "sift_hip_set_device": (i, [i]),
@@ -402,6 +410,14 @@ class Detector:
 
 class Matcher:
     """Brute-force L2 matcher (replaces Match.cu:8-177) with preallocated scratch."""
+
+    @staticmethod
+    def plan(max_query: int, max_train: int, pairs: int = 1) -> tuple:
+        """(train splits per query block, waves per workgroup) a call of this
+        shape launches with (sift_hip_match_plan; host-only)."""
+        S, nw = ctypes.c_int(), ctypes.c_int()
+        _check(lib().sift_hip_match_plan(max_query, max_train, pairs, ctypes.byref(S), ctypes.byref(nw)), "match_plan")
+        return S.value, nw.value
 
     def __init__(self, max_query: int, max_train: int, max_pairs: int = 1, device: int = -1):
         self._m = ctypes.c_void_p()

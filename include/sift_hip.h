@@ -245,6 +245,12 @@ int sift_hip_match_host(sift_hip_matcher_t m, const uint16_t* query, int nq,
                         const uint16_t* train, int nt, float ratio, int ratio_on_squared,
                         int* out);
 
+/* The launch plan a match call of this shape gets: train splits S per query
+ * block (S > 1: split workgroups merge their top-2 through the scratch's
+ * atomics) and waves per workgroup.  Host-only (no GPU call beyond reading the
+ * CU count; 256 without a device), for tests and tools. */
+int sift_hip_match_plan(int max_query, int max_train, int pairs, int* splits, int* waves);
+
 /* --- Multi-GPU (the reference binds one Detector to the current
  * device, Detector.hh:26-29, and has no multi-GPU path) ----------------------- */
 

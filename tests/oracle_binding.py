@@ -14,7 +14,10 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
-ORACLE_LIB = os.path.join(ORACLE_DIR, "_build", "libsift_oracle.so")
+# SIFT_ORACLE_BUILD=_build_asan: the sanitizer build (oracle/Makefile asan,
+# tests/test_asan.py); default: the optimised build.
+BUILD_DIR = os.environ.get("SIFT_ORACLE_BUILD", "_build")
+ORACLE_LIB = os.path.join(ORACLE_DIR, BUILD_DIR, "libsift_oracle.so")
 # Builds of the same restatement (oracle/Makefile): "pinned" is the parity pin
 # of the HIP path; the others model OpenCV's AVX2 / AVX-512 dispatch as GCC
 # compiles it (the ensemble the stated OpenCV tolerance comes from).
@@ -57,7 +60,8 @@ def lib(variant: str = "pinned") -> ctypes.CDLL:
     if variant not in _libs:
         path = VARIANTS[variant]
         if not os.path.exists(path):
-            subprocess.run(["make", "-C", ORACLE_DIR], check=True, capture_output=True)
+            subprocess.run(["make", "-C", ORACLE_DIR] + (["asan"] if BUILD_DIR == "_build_asan" else []), check=True,
+                           capture_output=True)
         L = ctypes.CDLL(path)
         vp, i, l, d = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_double
         P = ctypes.POINTER(Params)

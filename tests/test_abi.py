@@ -158,3 +158,15 @@ def test_batch_host_logic(sift):
     finally:
         L.sift_hip_destroy(h)
     assert L.sift_hip_set_batch(None, 2) == -1
+
+
+def test_match_plan_host_only(sift):
+    """sift_hip_match_plan needs no GPU: single pairs use 4-wave workgroups and
+    >= 4-tile splits; C5 (56 pairs of 2000 x 2000) runs one split per query
+    block; the ragged batched case of test_gpu_parity has S > 1."""
+    S, nw = sift.Matcher.plan(2000, 2000, 1)
+    assert nw == 4 and 1 < S <= 16
+    assert sift.Matcher.plan(2000, 2000, 56) == (1, 8)
+    assert sift.Matcher.plan(2000, 2500, 8)[0] > 1
+    with pytest.raises(sift.SiftHipError):
+        sift.Matcher.plan(10, 10, 0)

@@ -102,3 +102,38 @@ def test_stage_replay_uses_the_dumped_input(sift, tmp_path):
     assert list(rows) == [3]
     with pytest.raises(sift.SiftHipError):
         det.replayStage(dump, "no-such-stage", out)
+
+
+@pytest.mark.parametrize("stage", ["descriptor", "refine", "pyramid"])
+def test_stage_replay_failed_write_restores_handle(sift, tmp_path, stage):
+    """A replay whose output write fails after its kernels ran (the output file
+    name is taken by a directory) reports the error and still leaves the
+    handle as after warm-up: timing mode restored, the arena's
+    scratch invariants (counters, dedupe bitmap, range keys) reset, so the next
+    frame is bit-exact with the one before the replay."""
+    w, h = 320, 240
+    det = sift.Detector(sift.CudaSiftConfig(col_width=w, row_width=h, numFeatures=0), device=0)
+    det.gpuWarmUpAndAllocate()
+    dump = str(tmp_path / "dump")
+    img = sift.synth_frame(16, w, h)
+    det.setDataGen(dump)
+    det.detectAndCompute(img)
+    det.setDataGen("")
+    det.copyToHost(True)
+    want_k, want_d = det.final_kpts.copy(), det.descriptors.view(np.uint16).copy()
+    out = tmp_path / "out"
+    blocker = {"descriptor": "desc.f16", "refine": "refined.rec", "pyramid": "gauss_o0_l0.f32"}[stage]
+    os.makedirs(out / blocker)  # fopen(out/blocker, "wb") fails after the stage's kernels
+    det.set_timing(True)
+    with pytest.raises(sift.SiftHipError):
+        det.replayStage(dump, stage, str(out))
+    det.timing_reset()
+    det.detectAndCompute(img)  # timing mode still on: the stages record their launches
+    assert det.timing().get("descriptor", {}).get("launches", 0) == 1
+    det.copyToHost(True)
+    assert np.array_equal(det.final_kpts, want_k)
+    assert np.array_equal(det.descriptors.view(np.uint16), want_d)
+    det.set_timing(False)
+    det.detectAndCompute(img)
+    det.copyToHost(True)
+    assert np.array_equal(det.descriptors.view(np.uint16), want_d)

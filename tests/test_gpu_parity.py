@@ -262,12 +262,14 @@ def test_match_batched_equals_pairs(sift, oracle):
 
 
 def test_match_batched_ragged_ranges(sift, oracle):
-    """The persistent batched matcher cuts the (pair, query block, train tile)
-    sequence into equal ranges per workgroup: ragged pairs put range edges in
-    the middle of key groups and query blocks, so the same query block merges
-    contributions of several workgroups.  Ties between far-apart train rows,
-    a pair without train rows and a pair without queries, three calls on one
-    matcher (the merge restores keys and counters)."""
+    """The batched matcher splits every pair's train rows into S ranges of
+    whole 8-tile key groups (one 512-query block per workgroup): for these
+    ragged shapes the plan has S > 1 (asserted), so a query block's top-2 is
+    merged from several workgroups through the scratch's atomics, and pairs
+    shorter than a split leave some splits empty.  Ties between train rows in
+    different key groups / splits, a pair without train rows and a pair
+    without queries, three calls on one matcher (the merge restores keys and
+    counters)."""
     rng = np.random.default_rng(23)
     shapes = [(700, 1999), (513, 33), (1, 2500), (64, 0), (0, 100), (1200, 257), (37, 5), (2000, 2000)]
     qs, ts = [], []
@@ -285,6 +287,8 @@ def test_match_batched_ragged_ranges(sift, oracle):
     dt = [sift.DeviceArray.from_numpy(_half_rows(t)) if len(t) else None for t in ts]
     tot = sum(n for n, _ in shapes)
     m = sift.Matcher(2000, 2500, max_pairs=len(shapes))
+    splits, _ = sift.Matcher.plan(2000, 2500, len(shapes))
+    assert splits > 1, "this case exists to run the split merge"
     for rep in range(3):
         idx2, d2 = sift.DeviceArray(tot * 8), sift.DeviceArray(tot * 8)
         m.match_batched([d.value if d else 0 for d in dq], [n for n, _ in shapes],

@@ -66,13 +66,19 @@ def main(tag):
             d["kernel_us_unprofiled"] = round(ukt, 3)
             d["unprofiled_launches"] = len(ks)
             d["mfma_busy_frac_unprofiled"] = round(d["SQ_VALU_MFMA_BUSY_CYCLES"] / (ukt * 1e-6 * 2.4e9 * 1024), 4)
+            # Both methods side by side: same_pass divides by the
+            # --pmc pass's own (counter-stretched) duration; cross_run by a
+            # separate kernel-trace run's duration at a nominal 2.4 GHz.  Round 2
+            # reported same_pass only; compare rounds on the same method.
+            d["mfma_busy_methods"] = {"same_pass": d.get("mfma_busy_frac"), "cross_run_2p4ghz": d["mfma_busy_frac_unprofiled"]}
         out.append(d)
     json.dump({"command": f"tools/match_pmc.sh {tag} (two --pmc passes, kernel trace only, over tools/match_pmc.py); "
                           f"python3 tools/mfma_summary.py {tag}",
                "note": "matcher kernels (int8 MFMA) per dispatch; MFMA busy fraction = SQ_VALU_MFMA_BUSY_CYCLES / "
                        "(kernel duration x 2.4 GHz x 1024 SIMDs), the duration from the same --pmc pass's kernel "
                        "trace (stretched by the counters) and, _unprofiled, from a kernel-trace-only run of the "
-                       "same workload (400x the calls, first tenth dropped); SQ_VALU_MFMA_BUSY_CYCLES = 32 per MFMA",
+                       "same workload (400x the calls, first tenth dropped) at a nominal 2.4 GHz -- two runs mixed, so "
+                       "mfma_busy_methods lists both; round 2's numbers are same_pass; SQ_VALU_MFMA_BUSY_CYCLES = 32 per MFMA",
                "kernels": out}, sys.stdout, indent=1)
 
 
