@@ -16,7 +16,8 @@ ROCM_LIB ?= /opt/rocm/lib
 # -ffp-contract=off + correctly rounded f32 div/sqrt: the float operation order
 # written in the kernels is the one executed (bit-exact parity with the oracle).
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
-            -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -I$(SRC) -Wall -Wno-unused-result $(EXTRA_HIPFLAGS)
+            -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -I$(SRC) -Wall -Wno-unused-result $(EXTRA_HIPFLAGS) \
+            $(if $(strip $(EXTRA_HIPFLAGS)),-DSIFT_AB_FLAGS='"$(strip $(EXTRA_HIPFLAGS))"')
 CXXFLAGS := -O2 -std=c++17 -fPIC -Iinclude -Wall -Wextra
 
 HIP_SRCS := $(SRC)/detector.hip $(SRC)/pyramid.hip $(SRC)/keypoints.hip $(SRC)/descriptor.hip $(SRC)/match.hip \

@@ -47,36 +47,18 @@ constexpr int kCells = (kD + 2) * (kD + 2);  // 36 spatial cells incl. the borde
 constexpr int kCellW = 10;                   // dwords per cell in each fixed-point histogram
 constexpr int kMaxRows = kDescMaxRows;       // enumerated windows: side = 2R+1 <= kMaxRows
 constexpr int kGroup = 4;                    // samples whose loads are in flight together (raster path)
-#ifndef SIFT_DESC_ITEM
-#define SIFT_DESC_ITEM 2
-#endif
-constexpr int kItem = SIFT_DESC_ITEM;        // consecutive samples of one row per work item (enumerated path)
+// Consecutive samples of one row per work item (enumerated path).  Measured:
+// 4-sample items -2 %, 1-sample items (dword loads per sample) 304 vs 198 us.
+constexpr int kItem = 2;
 // Histogram copies: lane l adds into copy l % kCopies, so lanes working on
 // the same (cell, orientation) -- same LDS address, serialised atomics -- are
 // spread over kCopies addresses (banks 16 apart); the epilogue sums them.
-#ifndef SIFT_DESC_COPIES
-#define SIFT_DESC_COPIES 2  // 352 vs 381 us per 16-frame launch (1 copy), 378 (4 copies: LDS-limited occupancy)
-#endif
-constexpr int kCopies = SIFT_DESC_COPIES;
-static_assert(kCopies == 1 || kCopies == 2 || kCopies == 4, "histogram copies: 1, 2 or 4");
+// 352 vs 381 us per 16-frame launch (1 copy), 378 (4 copies: LDS-limited occupancy).
+constexpr int kCopies = 2;
 constexpr int kHistWords = 2 * kCells * kCellW;  // one copy: the even- and the odd-orientation histogram
-// Lane -> run permutation (odd multiplier, 1 = identity): a wave's lanes take
-// runs spread over the window instead of neighbouring runs, so fewer lanes of
-// one atomic instruction share a cell.
-#ifndef SIFT_DESC_PERM
-#define SIFT_DESC_PERM 1
-#endif
-static_assert(SIFT_DESC_PERM % 2 == 1, "lane permutation multiplier must be odd");
-// Transcendentals: 0 = native v_rcp / v_sqrt / v_exp (+-1 ulp); 1 = the
-// oracle's correctly rounded division / sqrt and OpenCV's exp32f table
-// polynomial (fewer +-1 descriptor flips, more VALU).
-#ifndef SIFT_DESC_PRECISE
-#define SIFT_DESC_PRECISE 0
-#endif
-
-#ifndef SIFT_DESC_SERIAL_SAMPLES
-#define SIFT_DESC_SERIAL_SAMPLES 1  // scheduling barrier between an item's samples
-#endif
+// (Measured and dropped: lane -> run permutations 5, 9, 17, 33 (equal or
+// worse); the oracle's correctly rounded division / sqrt / exp32f in the
+// sample loop (+16 % time, flip counts unchanged).)
 
 struct DescGeom {
     float cos_t, sin_t, exp_scale;
@@ -148,15 +130,7 @@ __device__ __forceinline__ void clip_interval(int& lo, int& hi, float s, float i
 // differences move a descriptor entry by ~1e-7 relative and flip its rounding
 // only at a .5 boundary: inside the |diff| <= 1 bar, at the same rate as the
 // summation-order difference.  The fastAtan2 polynomial itself is kept.
-__constant__ float c_exptab_desc[64];  // OpenCV expTab_f (SIFT_DESC_PRECISE)
-void upload_exp_table_desc(const float* tab64) {
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_exptab_desc), tab64, sizeof(float) * 64);
-}
-
 __device__ __forceinline__ float desc_atan2(float y, float x) {
-#if SIFT_DESC_PRECISE
-    return cv_fast_atan2(y, x);
-#endif
     const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
     const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
     const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
@@ -171,19 +145,7 @@ __device__ __forceinline__ float desc_atan2(float y, float x) {
     return a;
 }
 __device__ __forceinline__ float desc_magnitude(float x, float y) {
-#if SIFT_DESC_PRECISE
-    return cv_magnitude(x, y);
-#else
     return __builtin_amdgcn_sqrtf(__fmaf_rn(x, x, y * y));
-#endif
-}
-__device__ __forceinline__ float desc_exp(float x, const float* tab) {
-#if SIFT_DESC_PRECISE
-    return cv_exp32f(x, tab);
-#else
-    (void)tab;
-    return __builtin_amdgcn_exp2f(x * 1.44269504088896341f);
-#endif
 }
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -194,11 +156,11 @@ struct JobWords {
 // kDT threads per keypoint: 4 waves for a single frame (few keypoints, the
 // chip needs the parallelism inside each), 2 waves for frame batches (more
 // keypoints in flight per CU: 296 vs 311 us per 8-frame launch, tools/ab_*).
-#ifndef SIFT_DESC_WAVES
-#define SIFT_DESC_WAVES 6  // min waves per SIMD (VGPR budget <= 80): 198 us vs 208 (5) and 211 (8) per 8-frame launch
-#endif
+// Minimum waves per SIMD (VGPR budget <= 80): 198 us vs 208 (5) and 211 (8)
+// per 8-frame launch; re-swept in round 3 (5 / 7: 337 / 331 vs 334 us).
+constexpr int kDescWaves = 6;
 template <int kDT>
-__global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJob* __restrict__ jobs, const Counters* __restrict__ ctr,
+__global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* __restrict__ jobs, const Counters* __restrict__ ctr,
                                                    const unsigned* __restrict__ range_keys,
                                                    uint16_t* __restrict__ desc, Counters* __restrict__ host_ctr,
                                                    long fs, unsigned nf) {
@@ -209,12 +171,6 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
     // scale keeps every bin below 2^31, so no carry crosses the word boundary.
     __shared__ __attribute__((aligned(16))) unsigned histE[kCopies * kHistWords];  // copy c at c * kHistWords
     __shared__ __attribute__((aligned(16))) float sq[128];
-#if SIFT_DESC_PRECISE
-    __shared__ float s_tab[64];
-    for (int i = threadIdx.x; i < 64; i += kDT) s_tab[i] = c_exptab_desc[i];
-#else
-    [[maybe_unused]] float* const s_tab = nullptr;
-#endif
     __shared__ int rowpre[kMaxRows + 4], rowlo[kMaxRows], rowln[kMaxRows];
     __shared__ float s_norm[12];
     constexpr int kPer = kDT >= 128 ? 1 : 128 / kDT;  // descriptor entries per thread in the epilogue
@@ -329,13 +285,9 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
             valid = valid && rbin > -1 && rbin < kD && cbin > -1 && cbin < kD;
             const float dx = r - l, dy = u - d;
             const f32x2t sq = rot * rot;
-#if SIFT_DESC_PRECISE
-            const float wgt = desc_exp((sq[0] + sq[1]) * G.exp_scale, s_tab);
-#else
             // exp_scale = -1/8 is a power of two, so (r2 * -1/8) * log2(e)
             // = r2 * (-log2(e) / 8) with the same single rounding: one multiply.
             const float wgt = __builtin_amdgcn_exp2f((sq[0] + sq[1]) * (-1.44269504088896341f / (kD * kD * 0.5f)));
-#endif
             const float gori = desc_atan2(dy, dx);
             const float gmag = desc_magnitude(dx, dy);
             float obin = (gori - jb.angle) * bins_per_rad;
@@ -407,7 +359,7 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
             // oracle's bin-range test alone.
             const int N = rowpre[side];
             const int run = (N + kDT - 1) / kDT;
-            const int tq = (tid & ~63) | ((lane * SIFT_DESC_PERM) & 63);  // this thread's run
+            const int tq = tid;  // this thread's run
             const int k0 = min(N, tq * run), k1 = min(N, k0 + run);
             if (k0 < k1) {
                 int lo = 0, hi = side - 1;  // last row with rowpre[row] <= k0 (non-empty)
@@ -430,19 +382,10 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
                     float row6[kItem + 2], up[kItem], dn[kItem];
                     {
                         const f32x4d cm = __builtin_bit_cast(f32x4d, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o - 4u, 0, 0));
-                        if constexpr (kItem == 2) {
-                            const f32x2d u2 = __builtin_bit_cast(f32x2d, __builtin_amdgcn_raw_buffer_load_b64(rsrc, o - pitch4, 0, 0));
-                            const f32x2d d2 = __builtin_bit_cast(f32x2d, __builtin_amdgcn_raw_buffer_load_b64(rsrc, o + pitch4, 0, 0));
-                            for (int t = 0; t < 2; t++) up[t] = u2[t], dn[t] = d2[t];
-                        } else {
-                            static_assert(kItem == 4, "items of 2 or 4 samples");
-                            const f32x2d ce = __builtin_bit_cast(f32x2d, __builtin_amdgcn_raw_buffer_load_b64(rsrc, o + 12u, 0, 0));
-                            const f32x4d u4 = __builtin_bit_cast(f32x4d, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o - pitch4, 0, 0));
-                            const f32x4d d4 = __builtin_bit_cast(f32x4d, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o + pitch4, 0, 0));
-                            for (int t = 0; t < 4; t++) up[t] = u4[t], dn[t] = d4[t];
-                            row6[4] = ce[0];
-                            row6[5] = ce[1];
-                        }
+                        static_assert(kItem == 2, "items of two samples");
+                        const f32x2d u2 = __builtin_bit_cast(f32x2d, __builtin_amdgcn_raw_buffer_load_b64(rsrc, o - pitch4, 0, 0));
+                        const f32x2d d2 = __builtin_bit_cast(f32x2d, __builtin_amdgcn_raw_buffer_load_b64(rsrc, o + pitch4, 0, 0));
+                        for (int t = 0; t < 2; t++) up[t] = u2[t], dn[t] = d2[t];
                         for (int t = 0; t < 4; t++) row6[t] = cm[t];
                     }
                     const float fi = (float)i, is = fi * G.sin_t, ic = fi * G.cos_t;
@@ -456,9 +399,7 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
                         accum_rot(rot[0], rot[1], t < cnt, row6[t], row6[t + 2], up[t], dn[t]);
                         // One sample at a time: interleaving the four keeps
                         // ~90 VGPRs live (occupancy 5 instead of 8 waves/SIMD).
-#if SIFT_DESC_SERIAL_SAMPLES
                         __builtin_amdgcn_sched_barrier(0);
-#endif
                     }
                     jj += kItem;
                     if (k + 1 < k1 && jj >= jend) {  // next non-empty row
@@ -548,28 +489,21 @@ __global__ __launch_bounds__(kDT, SIFT_DESC_WAVES) void k_descriptor(const DescJ
 void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned* range_keys, uint16_t* desc,
                        Counters* host_ctr, const KeypointParams& kp, const Frames& fr, hipStream_t s) {
     (void)kp;
-#ifndef SIFT_DESC_SINGLE_DT
-#define SIFT_DESC_SINGLE_DT 256  // threads per keypoint for a single frame (tools A/B builds vary it)
-#endif
+    // Threads per keypoint: 256 for a single frame (128: 34.6 us, 512: 47.6 vs
+    // 36.1 per frame, round 3), 128 for frame batches.
+    constexpr int kSingleDT = 256, kBatchDT = 128;
     if (fr.nf <= 1) {
-        hipLaunchKernelGGL(k_descriptor<SIFT_DESC_SINGLE_DT>, dim3(8192), dim3(SIFT_DESC_SINGLE_DT), 0, s, jobs, ctr,
-                           range_keys, desc, host_ctr, fr.stride, 1u);
+        hipLaunchKernelGGL(k_descriptor<kSingleDT>, dim3(8192), dim3(kSingleDT), 0, s, jobs, ctr, range_keys, desc,
+                           host_ctr, fr.stride, 1u);
     } else {
         // Workgroups per frame: 2048 at 8 frames (16384 in all).  The bigger
         // grids this kernel once had filled every CU slot and kept the other
         // stream's pyramid kernels out; with fewer workgroups (each looping
         // over more keypoints) the two co-reside: +2-3 % frame rate
         // (tools/grid_sweep.sh).
-#ifdef SIFT_DESC_PER  // tools A/B builds
-        const int per = SIFT_DESC_PER;
-#else
         const int per = std::max(1024, 16384 / fr.nf);
-#endif
-#ifndef SIFT_DESC_BATCH_DT
-#define SIFT_DESC_BATCH_DT 128  // threads per keypoint for frame batches (tools A/B builds vary it)
-#endif
-        hipLaunchKernelGGL(k_descriptor<SIFT_DESC_BATCH_DT>, dim3(per * fr.nf), dim3(SIFT_DESC_BATCH_DT), 0, s, jobs,
-                           ctr, range_keys, desc, host_ctr, fr.stride, (unsigned)fr.nf);
+        hipLaunchKernelGGL(k_descriptor<kBatchDT>, dim3(per * fr.nf), dim3(kBatchDT), 0, s, jobs, ctr, range_keys,
+                           desc, host_ctr, fr.stride, (unsigned)fr.nf);
     }
 }
 

@@ -69,93 +69,17 @@ Taps gaussian_taps(double sigma) {
 }
 
 // Compile-time A/B and instrumentation switches of the kernels (tools/ab_*.sh
-// builds pass them through EXTRA_HIPFLAGS to every translation unit).  Any
-// of them makes this a non-default build: sift_hip_version() lists them
-// ("build=ab ..."), and bench.py and __graft_entry__.smoke() refuse such a
-// library, so a measured or tested line always names the code it ran.
-#define SIFT_XSTR(x) #x
-#define SIFT_STR(x) SIFT_XSTR(x)
+// builds pass them through EXTRA_HIPFLAGS, which the Makefile also records as
+// SIFT_AB_FLAGS).  Any of them makes this a non-default build:
+// sift_hip_version() lists them ("build=ab ..."), and bench.py and
+// __graft_entry__.smoke() refuse such a library, so a measured or tested line
+// always names the code it ran.
 const char* build_flags() {
-    return ""
-#ifdef SIFT_BLUR_TH
-           " SIFT_BLUR_TH=" SIFT_STR(SIFT_BLUR_TH)
+#ifdef SIFT_AB_FLAGS
+    return " " SIFT_AB_FLAGS;
+#else
+    return "";
 #endif
-#ifdef SIFT_BLUR_BIG_TILES
-           " SIFT_BLUR_BIG_TILES=" SIFT_STR(SIFT_BLUR_BIG_TILES)
-#endif
-#ifdef SIFT_BLUR_IW16
-           " SIFT_BLUR_IW16=" SIFT_STR(SIFT_BLUR_IW16)
-#endif
-#ifdef SIFT_BLUR_X4LD
-           " SIFT_BLUR_X4LD=" SIFT_STR(SIFT_BLUR_X4LD)
-#endif
-#ifdef SIFT_BLUR_DMA
-           " SIFT_BLUR_DMA=" SIFT_STR(SIFT_BLUR_DMA)
-#endif
-#ifdef SIFT_EX_TALL_MIN
-           " SIFT_EX_TALL_MIN=" SIFT_STR(SIFT_EX_TALL_MIN)
-#endif
-#ifdef SIFT_DESC_SERIAL_SAMPLES
-           " SIFT_DESC_SERIAL_SAMPLES=" SIFT_STR(SIFT_DESC_SERIAL_SAMPLES)
-#endif
-#ifdef SIFT_MATCH_WG_TARGET_SINGLE
-           " SIFT_MATCH_WG_TARGET_SINGLE=" SIFT_STR(SIFT_MATCH_WG_TARGET_SINGLE)
-#endif
-#ifdef SIFT_MATCH_FUSED_SINGLE
-           " SIFT_MATCH_FUSED_SINGLE=" SIFT_STR(SIFT_MATCH_FUSED_SINGLE)
-#endif
-#ifdef SIFT_BLUR_IW112
-           " SIFT_BLUR_IW112=" SIFT_STR(SIFT_BLUR_IW112)
-#endif
-#ifdef SIFT_MATCH_BATCH_NW
-           " SIFT_MATCH_BATCH_NW=" SIFT_STR(SIFT_MATCH_BATCH_NW)
-#endif
-#ifdef SIFT_MATCH_NW_SINGLE
-           " SIFT_MATCH_NW_SINGLE=" SIFT_STR(SIFT_MATCH_NW_SINGLE)
-#endif
-#ifdef SIFT_MATCH_BATCH_QBW
-           " SIFT_MATCH_BATCH_QBW=" SIFT_STR(SIFT_MATCH_BATCH_QBW)
-#endif
-#ifdef SIFT_BLUR_X4ST
-           " SIFT_BLUR_X4ST=" SIFT_STR(SIFT_BLUR_X4ST)
-#endif
-#ifdef SIFT_ORI_AHEAD
-           " SIFT_ORI_AHEAD=" SIFT_STR(SIFT_ORI_AHEAD)
-#endif
-#ifdef SIFT_DESC_SINGLE_DT
-           " SIFT_DESC_SINGLE_DT=" SIFT_STR(SIFT_DESC_SINGLE_DT)
-#endif
-#ifdef SIFT_ORI_PER
-           " SIFT_ORI_PER=" SIFT_STR(SIFT_ORI_PER)
-#endif
-#ifdef SIFT_DESC_PER
-           " SIFT_DESC_PER=" SIFT_STR(SIFT_DESC_PER)
-#endif
-#ifdef SIFT_DESC_BATCH_DT
-           " SIFT_DESC_BATCH_DT=" SIFT_STR(SIFT_DESC_BATCH_DT)
-#endif
-#ifdef SIFT_DESC_WAVES
-           " SIFT_DESC_WAVES=" SIFT_STR(SIFT_DESC_WAVES)
-#endif
-#ifdef SIFT_DESC_ITEM
-           " SIFT_DESC_ITEM=" SIFT_STR(SIFT_DESC_ITEM)
-#endif
-#ifdef SIFT_DESC_PERM
-           " SIFT_DESC_PERM=" SIFT_STR(SIFT_DESC_PERM)
-#endif
-#ifdef SIFT_DESC_COPIES
-           " SIFT_DESC_COPIES=" SIFT_STR(SIFT_DESC_COPIES)
-#endif
-#ifdef SIFT_DESC_PRECISE
-           " SIFT_DESC_PRECISE=" SIFT_STR(SIFT_DESC_PRECISE)
-#endif
-#ifdef SIFT_EX_CPL
-           " SIFT_EX_CPL=" SIFT_STR(SIFT_EX_CPL)
-#endif
-#ifdef SIFT_MATCH_WG_TARGET
-           " SIFT_MATCH_WG_TARGET=" SIFT_STR(SIFT_MATCH_WG_TARGET)
-#endif
-        ;
 }
 
 struct TimingRec {
@@ -179,6 +103,7 @@ struct sift_hip_detector {
     sift_hip_config cfg{};
     int device = 0;
     int L = 3, nOct = 0, firstOctave = 0;
+    int tailOct = 0;  // first octave of the pyramid-tail launch (nOct: none)
     int baseW = 0, baseH = 0;
     hipStream_t stream = nullptr;
     // Frame uploads and result downloads.  Created on first use: a stream
@@ -222,7 +147,7 @@ struct sift_hip_detector {
     float* dUp = nullptr;
     float* dPyr = nullptr;
     uint2* dCand = nullptr;
-    unsigned capCand = 1u << 20;
+    unsigned capCand = 1u << 20;  // sized to the frame in setup_taps
     RefKpt* dRef = nullptr;
     OriKpt* dOri = nullptr;
     int* dSlot = nullptr;
@@ -244,6 +169,14 @@ struct sift_hip_detector {
 
     hipGraphExec_t exec[kSlots] = {};   // B frames per launch
     hipGraphExec_t exec1[kSlots] = {};  // one frame (B > 1 only; exec when B = 1)
+    // The same graphs with the f32 head captured in (device input): the head
+    // node is re-pointed at each frame's image (hipGraphExecKernelNodeSetParams),
+    // so the frame is ONE graph launch -- a separate head launch left ~6 us
+    // between the head and the graph's first kernel on every single frame.
+    hipGraphExec_t execH[kSlots] = {}, execH1[kSlots] = {};
+    hipGraph_t graphH[kSlots] = {}, graphH1[kSlots] = {};
+    hipGraphNode_t headH[kSlots] = {}, headH1[kSlots] = {};
+    HeadNode headNode{};
     bool useGraph = true;
 
     // Stage dumps (sift_hip_set_datagen): directory, and a device copy of the
@@ -311,6 +244,12 @@ struct sift_hip_detector {
                 if (e) (void)hipGraphExecDestroy(e);
             for (auto& e : exec1)
                 if (e) (void)hipGraphExecDestroy(e);
+            for (int k = 0; k < kSlots; k++) {
+                if (execH[k]) (void)hipGraphExecDestroy(execH[k]);
+                if (execH1[k]) (void)hipGraphExecDestroy(execH1[k]);
+                if (graphH[k]) (void)hipGraphDestroy(graphH[k]);
+                if (graphH1[k]) (void)hipGraphDestroy(graphH1[k]);
+            }
             if (dArena) (void)hipFree(dArena);
             for (int k = 0; k < kSlots; k++)
                 if (evFrame[k]) (void)hipEventDestroy(evFrame[k]);
@@ -391,14 +330,34 @@ void setup_taps(sift_hip_detector* d) {
     }
     d->layerTaps.resize(L + 3);
     for (int i = 0; i < L + 3; i++) d->layerTaps[i] = gaussian_taps(sig[i]);
+#ifndef SIFT_TAIL
+#define SIFT_TAIL 1  // the pyramid tail for the small octaves (A/B builds: 0)
+#endif
+    d->tailOct = SIFT_TAIL && L + 3 <= kTailMaxPlanes ? tail_first_octave(d->pyr, d->layerTaps.data(), L) : d->nOct;
     d->threshold = (float)(int)std::floor(0.5 * d->cfg.contrastThreshould / L * 255 * 1.0);
     d->kp.contrastThreshold = (float)d->cfg.contrastThreshould;
     d->kp.edgeThreshold = (float)d->cfg.edgeThreshould;
     d->kp.sigma = (float)d->cfg.sigma;
     d->kp.numFeatures = d->cfg.numFeatures;
-    d->kp.capRefined = 1u << 18;
-    d->kp.capOriented = 1u << 19;
-    d->kp.capFinal = (unsigned)(d->cfg.maxKeypoints > 0 ? d->cfg.maxKeypoints : 65536);
+    // Capacities sized to the frame (were fixed 1M / 2^18 / 2^19 / 65536, so a
+    // small frame held 128 MiB against the reference's 84, readme.md:16).
+    // Candidates: 1/8 of the scale-space samples (a 3x3x3 extremum test passes
+    // ~7 % of samples of pure noise before the contrast threshold; natural and
+    // synthetic frames stay far below); refined <= candidates; oriented: one
+    // slot per refined keypoint + as many extra peaks; results: numFeatures
+    // (+ a quarter for retainBest's response ties), or 1/32 of the pyramid's
+    // pixels without a feature limit (C1 frames keep ~1/3000).  Every stage
+    // clamps to its capacity and sets its overflow bit (sift_hip_overflow_flags).
+    double sumPx = 0;
+    for (int o = 0; o < d->nOct; o++) sumPx += (double)d->pyr.oct[o].W * d->pyr.oct[o].H;
+    auto clampu = [](double v, double lo, double hi) { return (unsigned)std::max(lo, std::min(v, hi)); };
+    d->capCand = clampu(sumPx * L / 8, 16384, 1u << 20);
+    d->kp.capRefined = std::min(d->capCand, 1u << 18);
+    d->kp.capOriented = 2 * d->kp.capRefined;
+    const int nfeat = d->cfg.numFeatures;
+    d->kp.capFinal = d->cfg.maxKeypoints > 0 ? (unsigned)d->cfg.maxKeypoints
+                     : nfeat > 0             ? clampu(nfeat + std::max(nfeat / 4, 512), 1024, 65536)
+                                             : clampu(sumPx / 32, 4096, 65536);
     // LDS patch bounds: scl_octv = sigma * 2^((layer + xi) / L) <= sigma * 2^((L + 0.5) / L).
     // Larger radii (not reachable from accepted keypoints) fall back to HBM reads.
     const double sclMax = d->cfg.sigma * std::pow(2.0, (L + 0.5) / L);
@@ -427,6 +386,7 @@ int allocate(sift_hip_detector* d) {
     HIPCHK(hipSetDevice(d->device));
     HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     d->allocated = true;
+    HIPCHK(tail_init());
     HIPCHK(hipEventCreateWithFlags(&d->evIn, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&d->evOut, hipEventDisableTiming));
     const int W = d->cfg.col_width, H = d->cfg.row_width;
@@ -557,6 +517,16 @@ void enqueue_head(sift_hip_detector* d, const void* img, int pitch, int fmt, int
     }
 }
 
+// Pyramid tail: octaves d->tailOct.. in one launch (one workgroup per frame,
+// planes in LDS), none when every octave is too large for it.
+void left_tail(sift_hip_detector* d, int nf, hipStream_t s) {
+    if (d->tailOct >= d->nOct) return;
+    double bytes = 0;
+    for (int o = d->tailOct; o < d->nOct; o++)
+        bytes += (double)d->pyr.oct[o].W * d->pyr.oct[o].H * 4 * (o == d->tailOct ? 1 + (d->L + 2) : (d->L + 2)) * nf;
+    d->timed("pyr_tail", bytes, [&] { launch_blur_tail(d->pyr, d->layerTaps.data(), d->L, d->tailOct, Frames{nf, d->afs}, s); });
+}
+
 // The frame pipeline after the head, as the stages tool/perf.cu replays one
 // at a time (sift_hip_replay_stage): pyramid (blur jobs), extrema, refine,
 // orientation, order (retainBest + deterministic order + descriptor jobs),
@@ -588,7 +558,9 @@ void enqueue_pyramid(sift_hip_detector* d, int nf, int parity) {
         double bytes;
     };
     std::vector<Job> jobs;
-    for (int o = 0; o < d->nOct; o++) {
+    // Octaves from d->tailOct on: one pyramid-tail launch after the jobs
+    // (launch_blur_tail; their base plane is written by job (tailOct - 1, L)).
+    for (int o = 0; o < d->tailOct; o++) {
         const OctGeom& g = d->pyr.oct[o];
         for (int i = 1; i < L + 3; i++) {
             Job j{o, i, {}, 0};
@@ -616,6 +588,7 @@ void enqueue_pyramid(sift_hip_detector* d, int nf, int parity) {
         if (j.i >= 2) return (bool)done[idx(j.o, j.i - 1)];
         return j.o == 0 || (bool)done[idx(j.o - 1, L)];
     };
+    if (jobs.empty()) left_tail(d, nf, s);
     for (size_t left = jobs.size(); left > 0;) {
         int a = -1, b = -1;
         for (size_t k = 0; k < jobs.size() && b < 0; k++)
@@ -641,6 +614,7 @@ void enqueue_pyramid(sift_hip_detector* d, int nf, int parity) {
         done[a] = true;
         left--;
     }
+    if (!jobs.empty()) left_tail(d, nf, s);
 }
 
 void enqueue_extrema(sift_hip_detector* d, int nf) {
@@ -723,11 +697,46 @@ int capture(sift_hip_detector* d, int slot, int nf, hipGraphExec_t* out) {
     return SIFT_HIP_OK;
 }
 
+// The head for f32 device input (the frame's first blur, or the 2x upsample)
+// as node parameters for image `img` (pitch in floats, nf frames at byte
+// stride sfs): what enqueue_head launches.
+void head_node(sift_hip_detector* d, HeadNode& h, const float* img, int pitch, int parity, int nf, long sfs) {
+    const int W = d->cfg.col_width, H = d->cfg.row_width;
+    const Frames fr{nf, d->afs};
+    if (d->firstOctave < 0) {
+        head_upsample_node(h, img, pitch, W, H, d->dUp, d->upPitch, fr, sfs);
+    } else {
+        const OctGeom& g = d->pyr.oct[0];
+        head_blur_node(h, img, pitch, W, H, g.base, g.pitch, d->initTaps, fr, sfs, range_keys(d, parity), d->dCtr);
+    }
+}
+
+// head + body captured together; the graph is kept for its head node.
+int capture_with_head(sift_hip_detector* d, int slot, int nf, hipGraphExec_t* out, hipGraph_t* graph,
+                      hipGraphNode_t* head) {
+    HIPCHK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
+    enqueue_head(d, d->dInput, d->inPitch, SIFT_HIP_F32, slot & 1, nf, d->afs);
+    enqueue_body(d, slot, nf);
+    HIPCHK(hipStreamEndCapture(d->stream, graph));
+    size_t nroot = 0;
+    HIPCHK(hipGraphGetRootNodes(*graph, nullptr, &nroot));
+    if (nroot != 1) return fail(SIFT_HIP_ERR_RUNTIME, "captured frame graph: expected one root (the head)");
+    HIPCHK(hipGraphGetRootNodes(*graph, head, &nroot));
+    hipGraphNodeType ty;
+    HIPCHK(hipGraphNodeGetType(*head, &ty));
+    if (ty != hipGraphNodeTypeKernel) return fail(SIFT_HIP_ERR_RUNTIME, "captured frame graph: the head is not a kernel");
+    HIPCHK(hipGraphInstantiate(out, *graph, nullptr, nullptr, 0));
+    return SIFT_HIP_OK;
+}
+
 int build_graphs(sift_hip_detector* d) {
     for (int b = 0; b < d->kSlots; b++) {
         if (int rc = capture(d, b, d->B, &d->exec[b])) return rc;
-        if (d->B > 1)
+        if (int rc = capture_with_head(d, b, d->B, &d->execH[b], &d->graphH[b], &d->headH[b])) return rc;
+        if (d->B > 1) {
             if (int rc = capture(d, b, 1, &d->exec1[b])) return rc;
+            if (int rc = capture_with_head(d, b, 1, &d->execH1[b], &d->graphH1[b], &d->headH1[b])) return rc;
+        }
     }
     return SIFT_HIP_OK;
 }
@@ -754,13 +763,25 @@ int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEven
             HIPCHK(hipMemcpy2DAsync(d->dDg, sizeof(float) * W, img, sizeof(float) * (size_t)pitch, sizeof(float) * W,
                                     H, hipMemcpyDeviceToDevice, d->stream));
     }
-    enqueue_head(d, img, pitch, fmt, slot & 1, nf, sfs);
-    if (consumed) HIPCHK(hipEventRecord(consumed, d->stream));
-    hipGraphExec_t g = nf == d->B ? d->exec[slot] : (nf == 1 ? d->exec1[slot] : nullptr);
-    if (d->useGraph && !d->timing && g) {
-        HIPCHK(hipGraphLaunch(g, d->stream));
-    } else {  // timing mode, or a partial batch: the same launches, eagerly
-        enqueue_body(d, slot, nf);
+    const bool graphs = d->useGraph && !d->timing;
+    hipGraphExec_t gh = !graphs || consumed || fmt != SIFT_HIP_F32 ? nullptr
+                        : nf == d->B                                 ? d->execH[slot]
+                        : nf == 1                                    ? d->execH1[slot]
+                                                                     : nullptr;
+    if (gh) {  // device f32 input: one launch for the whole frame, the head re-pointed at img
+        HeadNode& h = d->headNode;
+        head_node(d, h, static_cast<const float*>(img), pitch, slot & 1, nf, sfs);
+        HIPCHK(hipGraphExecKernelNodeSetParams(gh, nf == d->B ? d->headH[slot] : d->headH1[slot], &h.p));
+        HIPCHK(hipGraphLaunch(gh, d->stream));
+    } else {
+        enqueue_head(d, img, pitch, fmt, slot & 1, nf, sfs);
+        if (consumed) HIPCHK(hipEventRecord(consumed, d->stream));
+        hipGraphExec_t g = nf == d->B ? d->exec[slot] : (nf == 1 ? d->exec1[slot] : nullptr);
+        if (graphs && g) {
+            HIPCHK(hipGraphLaunch(g, d->stream));
+        } else {  // timing mode, or a partial batch: the same launches, eagerly
+            enqueue_body(d, slot, nf);
+        }
     }
     HIPCHK(hipEventRecord(d->evFrame[slot], d->stream));
     d->nfOf[slot] = nf;
@@ -1491,6 +1512,15 @@ int sift_hip_overflow_flags(sift_hip_t d, int* flags) {
         if (int rc = ensure_counts(d)) return rc;
     }
     *flags = d->hCtr ? (int)d->hCtr[(size_t)d->cur * d->B].overflow : 0;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_capacities(sift_hip_t d, int* cand, int* refined, int* oriented, int* results) {
+    if (!d) return fail(SIFT_HIP_ERR_INVALID, "null handle");
+    if (cand) *cand = (int)d->capCand;
+    if (refined) *refined = (int)d->kp.capRefined;
+    if (oriented) *oriented = (int)d->kp.capOriented;
+    if (results) *results = (int)d->kp.capFinal;
     return SIFT_HIP_OK;
 }
 

@@ -24,7 +24,6 @@ __constant__ float c_exptab[64];
 
 void upload_exp_table(const float* tab64) {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(c_exptab), tab64, 64 * sizeof(float));
-    upload_exp_table_desc(tab64);
 }
 
 constexpr int kOriBins = 36;

@@ -501,11 +501,11 @@ __device__ __forceinline__ void merge_contribution(const Top2* s_res, unsigned* 
 // exact integers below 2^24, so both paths return the same (d^2, index) pairs
 // with the same tie order.  Key groups start at the split's first tile.
 // ---------------------------------------------------------------------------
-template <int NW>
+template <int NW, int QBW>
 __global__ __launch_bounds__(64 * NW, (kMatchWgPerCu * NW) / 4) void k_match_single(
     MatchPair pr, int S, unsigned long long* __restrict__ keys, unsigned* __restrict__ done, float ratio,
     int ratio_on_squared, int* __restrict__ idx2, float* __restrict__ d2out, int* __restrict__ match) {
-    constexpr int NT = 64 * NW, QB = 64 * NW;
+    constexpr int NT = 64 * NW, QB = 32 * QBW * NW;  // threads, queries per workgroup (QBW 32-query blocks per wave)
     __shared__ __attribute__((aligned(16))) int8_t s_codes[2][kChunkTiles * kTileBytes];
     __shared__ __attribute__((aligned(16))) int s_key[2][kChunkRows];
     __shared__ unsigned s_last;
@@ -516,14 +516,14 @@ __global__ __launch_bounds__(64 * NW, (kMatchWgPerCu * NW) / 4) void k_match_sin
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, col = lane & 31, h = lane >> 5;
     const int ntiles = (pr.nt + kMatchTileRows - 1) / kMatchTileRows, tps = (ntiles + S - 1) / S;
     const int tbeg = min(ntiles, (int)blockIdx.y * tps), tend = min(ntiles, tbeg + tps);
-    const int q0w = q0 + 64 * w;
-    Top2 res[2];
+    const int q0w = q0 + 32 * QBW * w;
+    Top2 res[QBW];
     bool bad = false;  // a non-integer value among this workgroup's rows
     {
-        i32x4 bq[2][4];
-        int qn[2];
+        i32x4 bq[QBW][4];
+        int qn[QBW];
 #pragma unroll
-        for (int qb = 0; qb < 2; qb++) {
+        for (int qb = 0; qb < QBW; qb++) {
             const int row = min(q0w + 32 * qb + col, pr.nq - 1);
             const uint4* src = reinterpret_cast<const uint4*>(pr.q + (size_t)row * 128 + 64 * h);
             int nrm = 0;
@@ -565,7 +565,9 @@ __global__ __launch_bounds__(64 * NW, (kMatchWgPerCu * NW) / 4) void k_match_sin
                 }
             }
         };
-        Best best[2] = {{kNone, kNone, kNone, kNone}, {kNone, kNone, kNone, kNone}};
+        Best best[QBW];
+#pragma unroll
+        for (int qb = 0; qb < QBW; qb++) best[qb] = Best{kNone, kNone, kNone, kNone};
         if (tbeg < tend) stage(tbeg, 0);
         int buf = 0;
         for (int c0 = tbeg; c0 < tend; c0 += kChunkTiles, buf ^= 1) {
@@ -573,22 +575,22 @@ __global__ __launch_bounds__(64 * NW, (kMatchWgPerCu * NW) / 4) void k_match_sin
             if (c0 + kChunkTiles < tend) stage(c0 + kChunkTiles, buf ^ 1);
             chunk_top2(s_codes[buf], s_key[buf], min(kChunkTiles, tend - c0), c0 * kMatchTileRows, col, h, bq, best);
         }
-        res[0] = finish_best(best[0], qn[0]);
-        res[1] = finish_best(best[1], qn[1]);
+#pragma unroll
+        for (int qb = 0; qb < QBW; qb++) res[qb] = finish_best(best[qb], qn[qb]);
     }
     if (__syncthreads_or(bad)) {
         // ---- general path: fp16 values that are not integers 0..255 ----
-        res[0] = match_f16_block(pr, q0w, tbeg, tend, col, h);
-        res[1] = match_f16_block(pr, q0w + 32, tbeg, tend, col, h);
+#pragma unroll
+        for (int qb = 0; qb < QBW; qb++) res[qb] = match_f16_block(pr, q0w + 32 * qb, tbeg, tend, col, h);
     }
     __syncthreads();  // s_res aliases the code tiles
     if (h == 0) {
-        s_res[64 * w + col] = res[0];
-        s_res[64 * w + 32 + col] = res[1];
+#pragma unroll
+        for (int qb = 0; qb < QBW; qb++) s_res[32 * QBW * w + 32 * qb + col] = res[qb];
     }
     __syncthreads();
     const int q = q0 + tid;
-    const bool qv = q < pr.nq;
+    const bool qv = tid < QB && q < pr.nq;
     const size_t o = (size_t)pr.out_off + q;
     if (S == 1) {
         if (qv) write_top2(s_res[tid], o, ratio, ratio_on_squared, idx2, d2out, match);
@@ -685,15 +687,19 @@ __global__ __launch_bounds__(64 * NW, (kMatchBatchWgPerCu * NW) / 4) void k_matc
 #define SIFT_MATCH_WG_TARGET_SINGLE 256  // single pairs: workgroups a launch aims for when choosing train splits
 #endif
 #ifndef SIFT_MATCH_NW_SINGLE
-#define SIFT_MATCH_NW_SINGLE 4  // single pairs: waves per workgroup (256 queries)
+#define SIFT_MATCH_NW_SINGLE 4  // single pairs: waves per workgroup
 #endif
+#ifndef SIFT_MATCH_QBW_SINGLE
+#define SIFT_MATCH_QBW_SINGLE 2  // single pairs: 32-query blocks per wave (4 x 2: 256 queries per workgroup)
+#endif
+constexpr int kMatchSingleQB = 32 * SIFT_MATCH_QBW_SINGLE * SIFT_MATCH_NW_SINGLE;
 #ifndef SIFT_MATCH_FUSED_SINGLE
 #define SIFT_MATCH_FUSED_SINGLE 1  // single pairs: no prep launch (tools A/B builds set 0)
 #endif
 // The matcher's done counters are sized per (pair, kMatchQB-query block)
 // (sift_hip_matcher_create); a launch indexes them by its own block, which must
 // therefore hold at least kMatchQB queries.
-static_assert(64 * SIFT_MATCH_NW_SINGLE >= kMatchQB, "single-pair blocks smaller than the done-counter block");
+static_assert(kMatchSingleQB >= kMatchQB, "single-pair blocks smaller than the done-counter block");
 static_assert(kMatchBatchQB >= kMatchQB, "batched blocks smaller than the done-counter block");
 
 static int device_cus() {
@@ -712,7 +718,7 @@ MatchPlan match_plan(int max_nq, int max_nt, int P) {
     const int ntiles = (max_nt + kMatchTileRows - 1) / kMatchTileRows;
     if (P == 1 && SIFT_MATCH_FUSED_SINGLE) {
         pl.nw = SIFT_MATCH_NW_SINGLE;
-        const int qblocks = (max_nq + 64 * pl.nw - 1) / (64 * pl.nw);
+        const int qblocks = (max_nq + kMatchSingleQB - 1) / kMatchSingleQB;
         int S = (SIFT_MATCH_WG_TARGET_SINGLE + qblocks - 1) / qblocks;
         // >= 4 tiles per split: every split converts its workgroup's query rows
         // again (C3, 2000 x 2000: 4 tiles 11.5 us per call, 3 tiles 11.9, 2 12.4,
@@ -761,9 +767,9 @@ void launch_match(const MatchSets& sets, MatchBatch& batch, const MatchPlan& pla
                   unsigned* done, float ratio, int ratio_on_squared, int* idx2, float* d2, int* match, hipStream_t s) {
     if (batch.P == 1 && SIFT_MATCH_FUSED_SINGLE) {
         const MatchPair& pr = batch.pair[0];
-        dim3 g((max(pr.nq, 1) + 64 * SIFT_MATCH_NW_SINGLE - 1) / (64 * SIFT_MATCH_NW_SINGLE), plan.S, 1);
-        hipLaunchKernelGGL(k_match_single<SIFT_MATCH_NW_SINGLE>, g, dim3(64 * SIFT_MATCH_NW_SINGLE), 0, s, pr, plan.S,
-                           keys, done, ratio, ratio_on_squared, idx2, d2, match);
+        dim3 g((max(pr.nq, 1) + kMatchSingleQB - 1) / kMatchSingleQB, plan.S, 1);
+        hipLaunchKernelGGL((k_match_single<SIFT_MATCH_NW_SINGLE, SIFT_MATCH_QBW_SINGLE>), g, dim3(64 * SIFT_MATCH_NW_SINGLE),
+                           0, s, pr, plan.S, keys, done, ratio, ratio_on_squared, idx2, d2, match);
         return;
     }
     if (sets.maxn > 0)

@@ -5,6 +5,7 @@
 // operation order is the oracle's (oracle/sift_oracle.cpp gaussianBlur /
 // upsample2x / isExtremum), so planes and candidate lists are bit-exact.
 #include <array>
+#include <cstring>
 #include <utility>
 
 #include "sift_kernels.h"
@@ -658,11 +659,322 @@ void launch_u8_to_f32(const uint8_t* src, int spitch, int W, int H, float* dst, 
                        sfs, fr.stride);
 }
 
+// The kernel node launch_blur (without a decimated output) and
+// launch_upsample2x would make, for a captured frame graph whose head node
+// is re-pointed at each frame's input (hipGraphExecKernelNodeSetParams).
+template <int R>
+const void* blur_fn(int nw) {
+    return nw == 4 ? reinterpret_cast<const void*>(&k_blur<R, float, 4>)
+                   : reinterpret_cast<const void*>(&k_blur<R, float, 8>);
+}
+template <int... Rs>
+constexpr std::array<const void* (*)(int), sizeof...(Rs)> blur_fn_table(std::integer_sequence<int, Rs...>) {
+    return {&blur_fn<Rs + 1>...};
+}
+static const std::array<const void* (*)(int), kMaxTaps / 2> kBlurFnTable =
+    blur_fn_table(std::make_integer_sequence<int, kMaxTaps / 2>{});
+static_assert(sizeof(BlurJob) <= sizeof(HeadNode::args), "head node argument storage");
+
+void head_blur_node(HeadNode& h, const float* src, int spitch, int W, int H, float* dst, int dpitch, const Taps& taps,
+                    const Frames& fr, long sfs, unsigned* range_keys, Counters* zero_ctr) {
+    const BlurJob j = make_job(src, spitch, W, H, dst, dpitch, DecOut{}, taps, range_keys, zero_ctr, fr, sfs);
+    const int tiles = j.ntiles * j.nf, nw = blur_waves(tiles);
+    std::memcpy(h.args, &j, sizeof j);
+    h.argv[0] = h.args;
+    h.p = hipKernelNodeParams{};
+    h.p.func = const_cast<void*>(kBlurFnTable[(taps.n >> 1) - 1](nw));
+    h.p.gridDim = dim3(tiles);
+    h.p.blockDim = dim3(64 * nw);
+    h.p.sharedMemBytes = 0;
+    h.p.kernelParams = h.argv;
+    h.p.extra = nullptr;
+}
+
+void head_upsample_node(HeadNode& h, const float* src, int spitch, int W, int H, float* dst, int dpitch,
+                        const Frames& fr, long sfs) {
+    // k_upsample2x<float>(src, spitch, W, H, dst, dpitch, sfs, dfs): each argument at its own slot.
+    unsigned char* a = h.args;
+    auto put = [&](int i, const void* v, size_t n) {
+        std::memcpy(a + 16 * i, v, n);
+        h.argv[i] = a + 16 * i;
+    };
+    put(0, &src, sizeof src);
+    put(1, &spitch, sizeof spitch);
+    put(2, &W, sizeof W);
+    put(3, &H, sizeof H);
+    put(4, &dst, sizeof dst);
+    put(5, &dpitch, sizeof dpitch);
+    put(6, &sfs, sizeof sfs);
+    put(7, &fr.stride, sizeof fr.stride);
+    h.p = hipKernelNodeParams{};
+    h.p.func = reinterpret_cast<void*>(&k_upsample2x<float>);
+    h.p.gridDim = dim3((2 * W + 63) / 64, (2 * H + 3) / 4, fr.nf);
+    h.p.blockDim = dim3(256);
+    h.p.sharedMemBytes = 0;
+    h.p.kernelParams = h.argv;
+    h.p.extra = nullptr;
+}
+
 void launch_blur(const float* src, int spitch, int W, int H, float* dst, int dpitch, const DecOut& dec,
                  const Taps& taps, const Frames& fr, long sfs, hipStream_t s, unsigned* range_keys,
                  Counters* zero_ctr) {
     const int r = taps.n >> 1;  // 1 .. kMaxTaps/2 (taps.n >= 3 by construction)
     kBlurTable[r - 1](make_job(src, spitch, W, H, dst, dpitch, dec, taps, range_keys, zero_ctr, fr, sfs), s);
+}
+
+// ---------------------------------------------------------------------------
+// Pyramid tail: every blur of the small octaves o >= T of a frame in ONE
+// workgroup (1024 threads, one per frame), planes held in LDS.  A single
+// frame's small octaves were one launch per blur job (752x480, auto octaves:
+// 14 launches of 1-2 tiles for octaves 3..6, ~5 us each: the launch and one
+// tile's load -> LDS -> passes -> store chain, almost none of it work); here
+// octave T's base plane is read once and every plane is blurred LDS -> LDS
+// with the operations of blur_tile in the same order (OpenCV's sepFilter2D:
+// the row filter, then the symmetric column filter; reflect-101 borders,
+// looping for kernels wider than the octave), stored for the keypoint stages,
+// and plane L's even rows and columns become the next octave's base (LDS and
+// HBM).  Row pass A -> B, column pass B -> A; the LDS rows have an odd pitch:
+// the row pass gives consecutive lanes consecutive rows, the column pass
+// consecutive columns (conflict-free both ways).  The taps of the plane are
+// staged in LDS (wave-uniform reads).  The octaves it takes are bounded by
+// work, not LDS: one CU's VALU runs the whole tail (tail_first_octave).
+// ---------------------------------------------------------------------------
+constexpr int kTailThreads = 1024;
+constexpr int kTailRun = 4;     // outputs per thread and run (along the pass)
+constexpr int kTailRmax = 16;   // radius bound of the tail's unrolled windows
+constexpr int kTailMaxDim = 512;  // octave width / height bound (reflection tables)
+
+__host__ __device__ __forceinline__ int tail_pitch(int W) { return W | 1; }
+
+// HBM stores as global_store (not flat: a flat store counts on lgkmcnt too,
+// so the next run's LDS wait would also wait for it).  The tail's barriers
+// fence LDS only (lds_barrier): __syncthreads() would wait for every plane
+// store to be acknowledged before the next pass (56 us for 752x480's tail);
+// the planes are read by later launches only.
+__device__ __forceinline__ void gstore(float* p, size_t i, float v) {
+    ((__attribute__((address_space(1))) float*)p)[i] = v;
+}
+__device__ __forceinline__ float gload(const float* p, size_t i) {
+    return ((const __attribute__((address_space(1))) float*)p)[i];
+}
+
+// One instantiation per radius class RP (the largest radius of the tail's
+// planes, rounded up to 4, 8, 13 or 16), every plane's taps zero-padded to
+// 2 RP + 1: in these sums every term is >= 0 (non-negative pixels and taps),
+// so a zero-weight fma adds a signed zero to a non-negative sum and leaves it
+// bit-identical, and a leading one leaves s = +0 until the first real tap --
+// the padded chain is OpenCV's chain.  (Per-radius instantiations dispatched
+// per plane: 56 us for 752x480's tail, its code cold in the instruction cache
+// at every plane.)  The window loads of a run are all issued before its
+// first fma.
+template <int RP>
+__device__ __forceinline__ void tail_row_pass(const float* __restrict__ A, float* __restrict__ B, int W, int H, int P,
+                                              bool small, const float* __restrict__ wp, const int* __restrict__ xo) {
+    constexpr int NWIN = kTailRun + 2 * RP;
+    const int nrx = (W + kTailRun - 1) / kTailRun, nruns = nrx * H;
+    for (int r = threadIdx.x; r < nruns; r += kTailThreads) {
+        const int y = r % H, xb = (r / H) * kTailRun;  // consecutive lanes: consecutive rows
+        const float* row = A + y * P;
+        // Source column of window slot k: xb - RP + k (runs at the borders
+        // through the reflection table xo[j] = reflect101(j - RP), j = xb + k).
+        float win[NWIN];
+        if (xb - RP >= 0 && xb + kTailRun - 1 + RP < W) {
+#pragma unroll
+            for (int k = 0; k < NWIN; k++) win[k] = row[xb - RP + k];
+        } else {
+            int ix[NWIN];
+#pragma unroll
+            for (int k = 0; k < NWIN; k++) ix[k] = xo[xb + k];
+#pragma unroll
+            for (int k = 0; k < NWIN; k++) win[k] = row[ix[k]];
+        }
+        float s[kTailRun];
+        if (!small) {  // RowFilter: s = 0; s = fma(x[k], w[k], s), k = 0..2R
+#pragma unroll
+            for (int q = 0; q < kTailRun; q++) s[q] = 0.f;
+#pragma unroll
+            for (int k = 0; k <= 2 * RP; k++) {
+                const float wk = wp[k];
+#pragma unroll
+                for (int q = 0; q < kTailRun; q++) s[q] = __fmaf_rn(win[q + k], wk, s[q]);
+            }
+        } else {  // SymmRowSmall (2R + 1 <= 5): s = x0 w0; s = fma(x[-k] + x[+k], w_k, s)
+            const float wc = wp[RP];
+#pragma unroll
+            for (int q = 0; q < kTailRun; q++) s[q] = win[q + RP] * wc;
+#pragma unroll
+            for (int k = 1; k <= 2 && k <= RP; k++) {
+                const float wk = wp[RP + k];
+#pragma unroll
+                for (int q = 0; q < kTailRun; q++) s[q] = __fmaf_rn(win[q + RP - k] + win[q + RP + k], wk, s[q]);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kTailRun; q++)
+            if (xb + q < W) B[y * P + xb + q] = s[q];
+    }
+}
+
+// Column pass (SymmColumnFilter: s = fma(c, w_R, 0); s = fma(down_k + up_k,
+// w_{R+k}, s)) B -> A and the plane to HBM; with `dec`, the even rows and
+// columns also go to the next octave's base (LDS N and HBM).
+template <int RP>
+__device__ __forceinline__ void tail_col_pass(const float* __restrict__ B, float* __restrict__ A, int W, int H, int P,
+                                              const float* __restrict__ wp, const int* __restrict__ yo,
+                                              float* __restrict__ gdst, int gpitch, bool dec, float* __restrict__ N,
+                                              int NP, float* __restrict__ gnext, int gnpitch) {
+    constexpr int NWIN = kTailRun + 2 * RP;
+    const int nry = (H + kTailRun - 1) / kTailRun, nruns = nry * W;
+    for (int r = threadIdx.x; r < nruns; r += kTailThreads) {
+        const int x = r % W, yb = (r / W) * kTailRun;  // consecutive lanes: consecutive columns
+        float win[NWIN];
+        if (yb - RP >= 0 && yb + kTailRun - 1 + RP < H) {
+#pragma unroll
+            for (int k = 0; k < NWIN; k++) win[k] = B[(yb - RP + k) * P + x];
+        } else {
+            int iy[NWIN];
+#pragma unroll
+            for (int k = 0; k < NWIN; k++) iy[k] = yo[yb + k];
+#pragma unroll
+            for (int k = 0; k < NWIN; k++) win[k] = B[iy[k] * P + x];
+        }
+        float s[kTailRun];
+        const float wc = wp[RP];
+#pragma unroll
+        for (int q = 0; q < kTailRun; q++) s[q] = __fmaf_rn(win[q + RP], wc, 0.f);
+#pragma unroll
+        for (int k = 1; k <= RP; k++) {
+            const float wk = wp[RP + k];
+#pragma unroll
+            for (int q = 0; q < kTailRun; q++) s[q] = __fmaf_rn(win[q + RP + k] + win[q + RP - k], wk, s[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < kTailRun; q++) {
+            const int y = yb + q;
+            if (y < H) {
+                A[y * P + x] = s[q];
+                gstore(gdst, (size_t)y * gpitch + x, s[q]);
+                if (dec && !((x | y) & 1) && (x >> 1) < (W >> 1) && (y >> 1) < (H >> 1)) {
+                    N[(y >> 1) * NP + (x >> 1)] = s[q];
+                    gstore(gnext, (size_t)(y >> 1) * gnpitch + (x >> 1), s[q]);
+                }
+            }
+        }
+    }
+}
+
+template <int RP>
+__device__ __forceinline__ void tail_octaves(const TailDesc& T, float* lds, const float (*wall)[2 * kTailRmax + 1],
+                                             int* xo, int* yo, long foff) {
+    int aOff = 0, nOff = T.regionX;
+    const int bOff = T.regionX + T.regionY;
+    for (int o = T.o0; o < T.nOct; o++) {
+        const OctGeom& g = T.oct[o];
+        const OctGeom& gn = T.oct[o + 1 < T.nOct ? o + 1 : o];
+        float* base = fptr(g.base, foff);
+        const int P = tail_pitch(g.W);
+        // Reflection tables for the padded radius (the same for every plane).
+        lds_barrier();
+        const int t = threadIdx.x;
+        if (t < g.W + 2 * RP + kTailRun) xo[t] = reflect101(min(t - RP, g.W - 1 + RP), g.W);
+        if (t < g.H + 2 * RP + kTailRun) yo[t] = reflect101(min(t - RP, g.H - 1 + RP), g.H);
+        for (int i = 1; i < T.L + 3; i++) {
+            const bool small = T.taps[i].n <= 5, dec = o + 1 < T.nOct && i == T.L;
+            const float* wp = wall[i];
+            lds_barrier();  // A written (load / previous column pass); tables set
+#if !defined(SIFT_TAIL_DIAG) || SIFT_TAIL_DIAG != 1  // timing-variant builds only (tools/ab_variant.sh)
+            tail_row_pass<RP>(lds + aOff, lds + bOff, g.W, g.H, P, small, wp, xo);
+#endif
+            lds_barrier();
+#if !defined(SIFT_TAIL_DIAG) || SIFT_TAIL_DIAG != 2
+            tail_col_pass<RP>(lds + bOff, lds + aOff, g.W, g.H, P, wp, yo, base + (size_t)i * g.planeStride, g.pitch,
+                              dec, lds + nOff, tail_pitch(gn.W), dec ? fptr(gn.base, foff) : base, gn.pitch);
+#endif
+        }
+        const int tt = aOff;  // the next octave works on its base; its own next base goes where this plane was
+        aOff = nOff;
+        nOff = tt;
+    }
+}
+
+__global__ __launch_bounds__(kTailThreads) void k_blur_tail(TailDesc T, long fs) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ float wall[kTailMaxPlanes][2 * kTailRmax + 1];  // every plane's taps, zero-padded to 2 RP + 1
+    __shared__ int xo[kTailMaxDim + 2 * kTailRmax + kTailRun], yo[kTailMaxDim + 2 * kTailRmax + kTailRun];
+    const long foff = (long)blockIdx.x * fs;
+    const int RP = T.rpad;
+    // LDS (float offsets into lds, not pointers, so every access stays a
+    // ds_*): A = the plane (region X, then the next base's region,
+    // alternating), B = the row pass's output, N = the next octave's base.
+    {
+        // Taps from the kernel arguments, padded: one round of loads here
+        // instead of a dependent kernarg load before every plane.
+        for (int t = threadIdx.x; t < kTailMaxPlanes * (2 * kTailRmax + 1); t += kTailThreads) {
+            const int i = t / (2 * kTailRmax + 1), k = t - i * (2 * kTailRmax + 1);
+            float v = 0.f;
+            if (i < T.L + 3 && k <= 2 * RP) {
+                const int R = T.taps[i].n >> 1, kk = k - RP + R;
+                if (kk >= 0 && kk <= 2 * R) v = T.taps[i].w[kk];
+            }
+            wall[i][k] = v;
+        }
+        const OctGeom& g = T.oct[T.o0];
+        const float* src = fptr(g.base, foff);
+        const int P = tail_pitch(g.W);
+        for (int i = threadIdx.x; i < g.W * g.H; i += kTailThreads) {
+            const int y = i / g.W, x = i - y * g.W;
+            lds[y * P + x] = gload(src, (size_t)y * g.pitch + x);
+        }
+    }
+#if defined(SIFT_TAIL_DIAG) && SIFT_TAIL_DIAG == 3
+    return;
+#endif
+    switch (RP) {
+        case 4: tail_octaves<4>(T, lds, wall, xo, yo, foff); break;
+        case 8: tail_octaves<8>(T, lds, wall, xo, yo, foff); break;
+        case 13: tail_octaves<13>(T, lds, wall, xo, yo, foff); break;
+        default: tail_octaves<16>(T, lds, wall, xo, yo, foff); break;
+    }
+}
+
+#ifndef SIFT_TAIL_MAX_PX
+#define SIFT_TAIL_MAX_PX 10000  // largest octave the tail takes (one CU's VALU: 752x480 octave 3 = 94x60)
+#endif
+int tail_first_octave(const PyrDesc& pyr, const Taps* taps, int L) {
+    for (int i = 1; i < L + 3; i++)
+        if ((taps[i].n >> 1) > kTailRmax) return pyr.nOct;
+    int T = pyr.nOct;
+    for (int o = pyr.nOct - 1; o >= 0; o--) {
+        const OctGeom& g = pyr.oct[o];
+        const long px = (long)tail_pitch(g.W) * g.H;
+        const long nxt = o + 1 < pyr.nOct ? (long)tail_pitch(pyr.oct[o + 1].W) * pyr.oct[o + 1].H : 0;
+        if ((long)g.W * g.H > SIFT_TAIL_MAX_PX || 2 * px + nxt > kTailLdsFloats || g.W > kTailMaxDim ||
+            g.H > kTailMaxDim)
+            break;
+        T = o;
+    }
+    return T;
+}
+
+hipError_t tail_init() {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_blur_tail),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)(sizeof(float) * kTailLdsFloats));
+}
+
+void launch_blur_tail(const PyrDesc& pyr, const Taps* taps, int L, int o0, const Frames& fr, hipStream_t s) {
+    TailDesc T{};
+    T.o0 = o0;
+    T.nOct = pyr.nOct;
+    T.L = L;
+    for (int o = 0; o < pyr.nOct; o++) T.oct[o] = pyr.oct[o];
+    for (int i = 0; i < L + 3 && i < kTailMaxPlanes; i++) T.taps[i] = taps[i];
+    int rmax = 0;
+    for (int i = 1; i < L + 3; i++) rmax = std::max(rmax, taps[i].n >> 1);
+    T.rpad = rmax <= 4 ? 4 : rmax <= 8 ? 8 : rmax <= 13 ? 13 : 16;
+    T.regionX = tail_pitch(pyr.oct[o0].W) * pyr.oct[o0].H;
+    T.regionY = o0 + 1 < pyr.nOct ? tail_pitch(pyr.oct[o0 + 1].W) * pyr.oct[o0 + 1].H : 0;
+    const size_t lds = sizeof(float) * (size_t)(2 * T.regionX + T.regionY);
+    hipLaunchKernelGGL(k_blur_tail, dim3(fr.nf), dim3(kTailThreads), lds, s, T, fr.stride);
 }
 
 // ---------------------------------------------------------------------------
@@ -843,16 +1155,24 @@ __device__ __forceinline__ float dpp_right_or(float own, float v) {  // lane i <
 
 // One workgroup = 4 waves stacked vertically over a 256-column strip: block
 // `tile` of the octave (strips across; the caller picks the XCD order).
-template <int LT, int EX4_TR, int EX4_AHEAD, int CPL = SIFT_EX_CPL>
+// A wave tests NB * EX4_TR consecutive rows as one stream (the 3-row DoG ring
+// and the loads ahead carry across its EX4_TR-row steps), so the two halo
+// rows above and below are read once per NB * EX4_TR rows instead of once per
+// EX4_TR: strips of 6 rows read 8 (1.20x algorithmic HBM bytes measured at
+// 16 frames, round-3 verdict), 24-row streams read 26.
+template <int LT, int EX4_TR, int EX4_AHEAD, int NB = 1, int CPL = SIFT_EX_CPL>
 __device__ __forceinline__ void extrema_block(const OctGeom& g, int o, float thr, uint2* __restrict__ cand,
                                               Counters* __restrict__ ctr, unsigned cap, int tile, int strips,
                                               uint2* s_list, unsigned& s_cnt, unsigned& s_base) {
     constexpr int NG = LT + 3, ND = LT + 2;
     static_assert(CPL * LT <= 31 && (CPL == 2 || CPL == 4), "hit bits per row");
+    static_assert(NB == 1 || (EX4_TR % 3 == 0 && EX4_TR % (EX4_AHEAD + 1) == 0),
+                  "multi-step streams: the ring and the load sets repeat every EX4_TR rows");
     typedef float f4 __attribute__((ext_vector_type(CPL)));  // CPL columns of one lane
     constexpr int EX4_COLS = 64 * CPL;                          // columns per wave
+    constexpr int TR = EX4_TR * NB;                             // rows per wave
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int x0 = (tile % strips) * EX4_COLS, y0 = ((tile / strips) * 4 + wave) * EX4_TR;
+    const int x0 = (tile % strips) * EX4_COLS, y0 = ((tile / strips) * 4 + wave) * TR;
     const int W = g.W, H = g.H, pitch = g.pitch;
     const int xl = x0 + CPL * lane;
     const int xe = min(max(lane == 0 ? x0 - 1 : x0 + EX4_COLS, 0), W - 1);
@@ -872,9 +1192,18 @@ __device__ __forceinline__ void extrema_block(const OctGeom& g, int o, float thr
     // rows ahead of the row being formed.
     f4 rv[EX4_AHEAD + 1][NG];
     float rev[EX4_AHEAD + 1][NG];
+    // Lanes whose columns start past the octave's width (the last strip of a
+    // row overhangs it: 1920 = 7.5 strips) and the lanes that do not use the
+    // outer column (all but lanes 0 and 63) load from an offset past the
+    // buffer: the hardware returns 0 without a memory request.
+#ifndef SIFT_EX_MASK_LOADS
+#define SIFT_EX_MASK_LOADS 1
+#endif
+    const bool l4 = !SIFT_EX_MASK_LOADS || xl < W, le = !SIFT_EX_MASK_LOADS || lane == 0 || lane == 63;
     auto issue_row = [&](int y, f4 (&v)[NG], float (&e)[NG]) {
         const int yc = min(max(y, 0), H - 1);
-        const unsigned off4 = (unsigned)(yc * pitch + xl) * 4u, offe = (unsigned)(yc * pitch + xe) * 4u;
+        const unsigned off4 = l4 ? (unsigned)(yc * pitch + xl) * 4u : 0x80000000u;
+        const unsigned offe = le ? (unsigned)(yc * pitch + xe) * 4u : 0x80000000u;
 #pragma unroll
         for (int d = 0; d < NG; d++) {
             const int so = (int)((long)d * g.planeStride * 4);
@@ -957,28 +1286,35 @@ __device__ __forceinline__ void extrema_block(const OctGeom& g, int o, float thr
     };
 
     if (y0 < H) {
-        // Strip row m = 0 .. EX4_TR + 1 (image row y0 - 1 + m) is loaded into raw
-        // set m % NS; once formed, its set is reloaded with strip row m + NS.
-        constexpr int NS = EX4_AHEAD + 1, NR = EX4_TR + 2;
-        auto form = [&](int m, f4 (&d4)[ND], float (&de)[ND]) {
-            const int k = m % NS;
+        // Strip row m = 0 .. TR + 1 (image row y0 - 1 + m) is loaded into raw
+        // set m % NS; once formed, its set is reloaded with strip row m + NS
+        // (rows past the image: clamped reads, never tested).
+        constexpr int NS = EX4_AHEAD + 1, NR = TR + 2;
+        // Streams end at the image's last tested row (H - 6): no load or test
+        // past it (uniform).
+        const int nsteps = NB == 1 ? 1 : min(NB, (min(H - 5, y0 + TR) - y0 + EX4_TR - 1) / EX4_TR);
+        auto form = [&](int m, int km, f4 (&d4)[ND], float (&de)[ND]) {  // km = m % NS (compile-time)
 #pragma unroll
             for (int d = 0; d < ND; d++) {
-                d4[d] = rv[k][d + 1] - rv[k][d];
-                de[d] = rev[k][d + 1] - rev[k][d];
+                d4[d] = rv[km][d + 1] - rv[km][d];
+                de[d] = rev[km][d + 1] - rev[km][d];
             }
-            if (m + NS < NR) issue_row(y0 - 1 + m + NS, rv[k], rev[k]);
+            if (m + NS < NR) issue_row(y0 - 1 + m + NS, rv[km], rev[km]);
         };
 #pragma unroll
         for (int m = 0; m < NS && m < NR; m++) issue_row(y0 - 1 + m, rv[m], rev[m]);
-        form(0, rd[0], re[0]);
-        form(1, rd[1], re[1]);
+        form(0, 0, rd[0], re[0]);
+        form(1, 1 % NS, rd[1], re[1]);
         // Row y0 + k + 1 (strip row k + 2) enters ring slot (k + 2) % 3, row y0 + k is tested.
+#pragma unroll 1
+        for (int kb = 0; kb < nsteps * EX4_TR; kb += EX4_TR) {
 #pragma unroll
-        for (int k = 0; k < EX4_TR; k++) {
-            const int A = k % 3, B = (k + 1) % 3, C = (k + 2) % 3;
-            form(k + 2, rd[C], re[C]);
-            emit_row(y0 + k, test_row(y0 + k, A, B, C));
+            for (int k6 = 0; k6 < EX4_TR; k6++) {
+                const int k = kb + k6;
+                const int A = k6 % 3, B = (k6 + 1) % 3, C = (k6 + 2) % 3;
+                form(k + 2, (k6 + 2) % NS, rd[C], re[C]);
+                emit_row(y0 + k, test_row(y0 + k, A, B, C));
+            }
         }
     }
     __syncthreads();
@@ -1001,6 +1337,9 @@ __device__ __forceinline__ void extrema_block(const OctGeom& g, int o, float thr
 // rows vs 19.8 at 2; 960x600 9.2 us at 2 rows vs 10.8 at 6).
 #ifndef SIFT_EX_TALL_MIN
 #define SIFT_EX_TALL_MIN 2048  // single frames: 6-row wave strips from this many strips per launch, else 2-row (1920x1200: 1600 -> 2-row, 26.4 -> 25.5 us); batches: 1024
+#endif
+#ifndef SIFT_EX_STREAM
+#define SIFT_EX_STREAM 2  // 6-row steps per tall wave stream (12 rows: 247 vs 251 us per 16-frame launch; 18, 24 rows slower)
 #endif
 struct ExtremaPlan {
     int start[kMaxOctaves + 1];  // start[nOct] = blocks per frame
@@ -1028,7 +1367,7 @@ __global__ __launch_bounds__(256) void k_extrema_all(PyrDesc pyr, ExtremaPlan pl
     ctr = fptr(ctr, f * fs);
     const int blk = b - plan.start[o];
     if (plan.tall[o])
-        extrema_block<LT, 6, 2>(g, o, thr, cand, ctr, cap, blk, plan.strips[o], s_list, s_cnt, s_base);
+        extrema_block<LT, 6, 2, SIFT_EX_STREAM>(g, o, thr, cand, ctr, cap, blk, plan.strips[o], s_list, s_cnt, s_base);
     else
         extrema_block<LT, 2, 2>(g, o, thr, cand, ctr, cap, blk, plan.strips[o], s_list, s_cnt, s_base);
 }
@@ -1053,7 +1392,7 @@ bool launch_extrema_all(const PyrDesc& pyr, float threshold, uint2* cand, Counte
         // Frames of a batch count too: each brings its own strips.
         // (8, 12 or 20 rows per wave for batches: 147, 149, 582 us vs 131 at 6.)
         const bool tall = strips * ((g.H + 5) / 6) * fr.nf >= (fr.nf > 1 ? 1024 : SIFT_EX_TALL_MIN);
-        const int tr = tall ? 6 : 2;
+        const int tr = tall ? 6 * SIFT_EX_STREAM : 2;
         plan.start[o] = total;
         plan.strips[o] = strips;
         plan.tall[o] = tall;

@@ -103,6 +103,18 @@ struct DecOut {
 void launch_blur(const float* src, int spitch, int W, int H, float* dst, int dpitch, const DecOut& dec,
                  const Taps& taps, const Frames& fr, long sfs, hipStream_t s, unsigned* range_keys = nullptr,
                  Counters* zero_ctr = nullptr);
+// Kernel node parameters of the f32 head launches (the frame's first blur with
+// range keys and counter zeroing, or the 2x upsample), for re-pointing a
+// captured graph's head node at each frame's input.
+struct HeadNode {
+    hipKernelNodeParams p;
+    alignas(16) unsigned char args[512];  // argument values (argv[i] -> args)
+    void* argv[8];
+};
+void head_blur_node(HeadNode& h, const float* src, int spitch, int W, int H, float* dst, int dpitch, const Taps& taps,
+                    const Frames& fr, long sfs, unsigned* range_keys, Counters* zero_ctr);
+void head_upsample_node(HeadNode& h, const float* src, int spitch, int W, int H, float* dst, int dpitch,
+                        const Frames& fr, long sfs);
 // Two independent float blurs in one launch (no range keys / counters);
 // false (nothing launched) when the radius pair has no instantiation.
 struct BlurDesc {
@@ -114,6 +126,20 @@ struct BlurDesc {
     const Taps* taps;
 };
 bool launch_blur_pair(const BlurDesc& a, const BlurDesc& b, const Frames& fr, hipStream_t s);
+// Pyramid tail (pyramid.hip): planes 1..L+2 of octaves o0..nOct-1 of each
+// frame in one workgroup, in LDS, from octave o0's base plane (already in
+// HBM).  tail_first_octave: the first octave from which every later octave
+// fits (nOct: none).  taps[i] = the blur of plane i (i = 1..L+2).
+constexpr int kTailLdsFloats = 32768;  // 128 KiB of dynamic LDS (+ ~4.6 KiB static: taps, reflection tables)
+constexpr int kTailMaxPlanes = 9;           // L <= 6
+struct TailDesc {
+    OctGeom oct[kMaxOctaves];
+    Taps taps[kTailMaxPlanes];
+    int o0, nOct, L, regionX, regionY, rpad;
+};
+int tail_first_octave(const PyrDesc& pyr, const Taps* taps, int L);
+hipError_t tail_init();  // lets the tail kernel take up to 160 KiB of dynamic LDS (once, before capture)
+void launch_blur_tail(const PyrDesc& pyr, const Taps* taps, int L, int o0, const Frames& fr, hipStream_t s);
 // 8-bit frames (pitches in bytes).  launch_blur_u8 returns false (nothing
 // launched) for an init radius without a fused 8-bit instantiation; the caller
 // then converts with launch_u8_to_f32 and uses launch_blur.
@@ -202,6 +228,5 @@ void set_last_error(const std::string& msg);
 // Exp table (OpenCV expTab_f) uploaded once per device (orientation and
 // descriptor translation units each hold a copy).
 void upload_exp_table(const float* tab64);
-void upload_exp_table_desc(const float* tab64);
 
 }  // namespace sift_amd

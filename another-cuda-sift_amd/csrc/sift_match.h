@@ -6,7 +6,7 @@
 namespace sift_amd {
 
 constexpr int kMaxMatchPairs = 64;
-constexpr int kMatchQB = 256;       // queries per workgroup, smallest plan (4 waves x 64; 8 waves: 512)
+constexpr int kMatchQB = 128;       // queries per workgroup, smallest plan (done counters are sized per kMatchQB block)
 constexpr int kMatchTileRows = 32;  // train rows per MFMA tile
 constexpr int kChunkTiles = 8;      // train tiles per LDS chunk (32 KiB of codes + 1 KiB of keys, double buffered)
 constexpr int kMatchWgPerCu = 2;    // workgroups per CU the kernel is register-budgeted for

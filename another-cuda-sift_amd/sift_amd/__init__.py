@@ -91,6 +91,7 @@ def lib() -> ctypes.CDLL:
         "sift_hip_sync": (i, [vp]),
         "sift_hip_set_batch": (i, [vp, i]),
         "sift_hip_batch_capacity": (i, [vp, ip]),
+        "sift_hip_capacities": (i, [vp, ip, ip, ip, ip]),
         "sift_hip_detect_batch_device": (i, [vp, vp, i, sz, sz, i, vp]),
         "sift_hip_batch_frames": (i, [vp, ip]),
         "sift_hip_batch_results_device": (i, [vp, i, ip, ip, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp)]),
@@ -354,6 +355,12 @@ class Detector:
         self.final_kpts, self.final_features = k3, f4
         if d is not None:
             self.descriptors = d.view(np.float16)
+
+    def capacities(self) -> dict:
+        """Per-frame buffer capacities (sift_hip_capacities; host-only)."""
+        v = [ctypes.c_int() for _ in range(4)]
+        _check(lib().sift_hip_capacities(self._h, *[ctypes.byref(x) for x in v]), "capacities")
+        return dict(zip(("candidates", "refined", "oriented", "results"), (x.value for x in v)))
 
     def overflow_flags(self) -> int:
         v = ctypes.c_int()

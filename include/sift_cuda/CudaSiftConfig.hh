@@ -13,5 +13,5 @@ struct CudaSiftConfig {
     double sigma{1.6};
     bool upscale{false};         // true = OpenCV default firstOctave -1 (works here)
     int numOctaves{0};           // 0 = auto: cvRound(log2(min(W,H)) - 2) - firstOctave
-    int maxKeypoints{0};         // result capacity, 0 = 65536
+    int maxKeypoints{0};         // result capacity; 0 = sized from numFeatures / the frame (sift_hip.h)
 };

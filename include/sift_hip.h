@@ -47,7 +47,7 @@ typedef struct {
     int    upscale;             /* 1 = double the base image = OpenCV default   */
                                 /* firstOctave -1 (.hh:12, broken there)        */
     int    numOctaves;          /* extra: 0 = auto (OpenCV formula)             */
-    int    maxKeypoints;        /* extra: result capacity, 0 = 65536            */
+    int    maxKeypoints;        /* extra: result capacity; 0 = numFeatures + 25 % (or pyramid pixels / 32 when numFeatures = 0), at most 65536 */
 } sift_hip_config;
 
 /* Fills the reference defaults (CudaSiftConfig.hh:6-12) for a w x h image. */
@@ -141,6 +141,12 @@ int sift_hip_wait(sift_hip_t h, long long ticket);
 
 /* Detector::total_size (Detector.hh:62, Detector.cu:584-604). */
 int sift_hip_num_keypoints(sift_hip_t h, int* n);
+/* Capacities of the handle's per-frame buffers (host-only, valid right after
+ * sift_hip_create): 3x3x3 candidates, refined keypoints, oriented slots and
+ * results.  Sized from the octave geometry and numFeatures (maxKeypoints
+ * overrides the result capacity); NULL arguments are skipped. */
+int sift_hip_capacities(sift_hip_t h, int* candidates, int* refined, int* oriented, int* results);
+
 /* Non-zero when a capacity (candidates / keypoints / results) overflowed. */
 int sift_hip_overflow_flags(sift_hip_t h, int* flags);
 

@@ -170,3 +170,22 @@ def test_match_plan_host_only(sift):
     assert sift.Matcher.plan(2000, 2500, 8)[0] > 1
     with pytest.raises(sift.SiftHipError):
         sift.Matcher.plan(10, 10, 0)
+
+
+def test_capacities_sized_to_the_frame(sift):
+    """Per-frame capacities follow the geometry and numFeatures (host-only,
+    before warm-up): the reference-config 752x480 handle's result ring is
+    numFeatures + 25 %, its candidate list 1/8 of the scale-space samples;
+    maxKeypoints overrides the result capacity; numFeatures = 0 sizes results
+    from the pyramid's pixels.  Every capacity stays within the old fixed caps."""
+    d = sift.Detector(sift.CudaSiftConfig(col_width=752, row_width=480, numFeatures=5000, upscale=False), device=0)
+    c = d.capacities()
+    sum_px = sum(d.octave_dims(o)[0] * d.octave_dims(o)[1] for o in range(d.nOctaves))
+    assert c["results"] == 6250
+    assert c["candidates"] == max(16384, min(sum_px * 3 // 8, 1 << 20))
+    assert c["refined"] == min(c["candidates"], 1 << 18) and c["oriented"] == 2 * c["refined"]
+    d2 = sift.Detector(sift.CudaSiftConfig(col_width=752, row_width=480, numFeatures=5000, maxKeypoints=777), device=0)
+    assert d2.capacities()["results"] == 777
+    d3 = sift.Detector(sift.CudaSiftConfig(col_width=1920, row_width=1200, numFeatures=0, upscale=True), device=0)
+    c3 = d3.capacities()
+    assert 4096 <= c3["results"] <= 65536 and c3["candidates"] <= 1 << 20 and c3["oriented"] <= 1 << 19

@@ -87,3 +87,21 @@ def test_order_many_entries_slot_path(sift, oracle):
     assert det.overflow_flags() == 0
     assert det.total_size > 8192, det.total_size
     check_vs_oracle(sift, oracle, cfg, det, img)
+
+
+def test_device_memory_reference_configs(sift):
+    """One Detector at the reference's published configurations (tool default:
+    auto octaves, upscale=false, numFeatures=5000) holds at most the device
+    memory the reference's readme.md:16 reports (84 / 298 / 214 MiB): the
+    per-frame capacities are sized to the frame (sift_hip_capacities)."""
+    torch = pytest.importorskip("torch")
+    for (w, h, ref_mib) in ((752, 480, 84), (1920, 1200, 298), (1600, 900, 214)):
+        torch.cuda.synchronize()
+        free0 = torch.cuda.mem_get_info(0)[0]
+        det = sift.Detector(sift.CudaSiftConfig(col_width=w, row_width=h, numFeatures=5000, upscale=False), device=0)
+        det.gpuWarmUpAndAllocate()
+        torch.cuda.synchronize()
+        used = (free0 - torch.cuda.mem_get_info(0)[0]) / 2**20
+        print(f"{w}x{h}: {used:.1f} MiB (reference {ref_mib})")
+        assert used <= ref_mib, (w, h, used)
+        del det

@@ -1,0 +1,15 @@
+#!/bin/bash
+# HBM traffic (FETCH_SIZE, WRITE_SIZE passes, kernel trace only) of
+# tools/profile_frames.py --batch 16 for each ab/NAME.so; summarise with
+# tools/pmc_summary.py NAMEtraffic.  Usage: tools/ab_pmc_traffic.sh NAME1 ...
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+for N in "$@"; do
+  i=2
+  for C in FETCH_SIZE WRITE_SIZE; do
+    i=$((i+1))
+    SIFT_HIP_LIB=ab/$N.so timeout -k 10 120 rocprofv3 --pmc $C --kernel-trace -d gpurun_out/${N}traffic_p$i -o run --output-format csv -- python3 tools/profile_frames.py --frames 5 --batch ${AB_BATCH:-16} > gpurun_out/${N}traffic_p$i.log 2>&1 || { echo "$N $C failed"; tail -5 gpurun_out/${N}traffic_p$i.log; exit 1; }
+  done
+done
+echo traffic done
