@@ -318,10 +318,11 @@ __device__ __forceinline__ void ori_clear_bit(uint32_t* bitmap, const OctGeom& g
     atomicAnd(&bitmap[bit >> 5], ~(1u << (bit & 31)));
 }
 
-#ifndef SIFT_ORI_AHEAD
-#define SIFT_ORI_AHEAD 1  // 2, 3, 4 measured equal on one frame and on batches (A/B builds)
-#endif
-constexpr int kOriAhead = SIFT_ORI_AHEAD;  // chunks whose gradient loads are in flight
+// Chunks whose gradient loads are in flight: 2, 3, 4 measured equal on one
+// frame and on batches (round 2).  Two chunks sorted per step (their
+// dependence chains interleaved in one wave, round 4): 140 vs 131 us per
+// 16-frame launch, single frames equal.
+constexpr int kOriAhead = 1;
 __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* __restrict__ in,
                                                     Counters* __restrict__ ctr, OriKpt* __restrict__ out,
                                                     uint32_t* __restrict__ bitmap, KeypointParams kp, long fs) {

@@ -853,7 +853,9 @@ __device__ __forceinline__ void tail_col_pass(const float* __restrict__ B, float
             const int y = yb + q;
             if (y < H) {
                 A[y * P + x] = s[q];
+#if !defined(SIFT_TAIL_DIAG) || SIFT_TAIL_DIAG != 4
                 gstore(gdst, (size_t)y * gpitch + x, s[q]);
+#endif
                 if (dec && !((x | y) & 1) && (x >> 1) < (W >> 1) && (y >> 1) < (H >> 1)) {
                     N[(y >> 1) * NP + (x >> 1)] = s[q];
                     gstore(gnext, (size_t)(y >> 1) * gnpitch + (x >> 1), s[q]);
@@ -879,6 +881,15 @@ __device__ __forceinline__ void tail_octaves(const TailDesc& T, float* lds, cons
         if (t < g.W + 2 * RP + kTailRun) xo[t] = reflect101(min(t - RP, g.W - 1 + RP), g.W);
         if (t < g.H + 2 * RP + kTailRun) yo[t] = reflect101(min(t - RP, g.H - 1 + RP), g.H);
         for (int i = 1; i < T.L + 3; i++) {
+#if defined(SIFT_TAIL_DIAG) && SIFT_TAIL_DIAG == 5  // timing builds only: s_memtime per plane -> octave 0, plane 0
+            if (threadIdx.x == 0) {
+                const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+                unsigned* st = reinterpret_cast<unsigned*>(fptr(T.oct[0].base, foff));
+                const int slot = (o - T.o0) * (T.L + 2) + (i - 1);
+                st[2 * slot] = (unsigned)t0;
+                st[2 * slot + 1] = (unsigned)(t0 >> 32);
+            }
+#endif
             const bool small = T.taps[i].n <= 5, dec = o + 1 < T.nOct && i == T.L;
             const float* wp = wall[i];
             lds_barrier();  // A written (load / previous column pass); tables set
@@ -938,7 +949,7 @@ __global__ __launch_bounds__(kTailThreads) void k_blur_tail(TailDesc T, long fs)
 }
 
 #ifndef SIFT_TAIL_MAX_PX
-#define SIFT_TAIL_MAX_PX 10000  // largest octave the tail takes (one CU's VALU: 752x480 octave 3 = 94x60)
+#define SIFT_TAIL_MAX_PX 6000  // largest octave the tail takes (one CU's VALU: 752x480 octave 3 = 94x60; 1920x1200 octave 4 (120x75) lost 10-20 us)
 #endif
 int tail_first_octave(const PyrDesc& pyr, const Taps* taps, int L) {
     for (int i = 1; i < L + 3; i++)
