@@ -486,9 +486,227 @@ __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* _
     }
 }
 
+// ---------------------------------------------------------------------------
+// Exact mode (sift_hip_set_descriptor_mode(h, SIFT_HIP_DESC_EXACT)): OpenCV's
+// histogram bit for bit.  calcSIFTDescriptor sums each bin's float
+// contributions sequentially in raster order of the window; float addition is
+// not associative, so the fixed-point histogram above can land one byte off.
+// Here every bin has ONE owner lane that adds its contributions in that order:
+//   * one wave per keypoint; the enumerated samples are taken in chunks of 64
+//     consecutive samples (raster order), one per lane;
+//   * phase 1: each lane computes its sample with the oracle's correctly
+//     rounded math (cv_exp32f table exp, fastAtan2 with IEEE division,
+//     magnitude with IEEE sqrt), writes its 8 contributions and its
+//     (r0, c0, o0) to LDS, and 12 ballots give, per interior cell row, cell
+//     column and orientation pair, the samples that touch it;
+//   * phase 2: lane = (cell 0..15, orientation pair g 0..3) ANDs its three
+//     masks and walks the set bits in ascending order (= raster order), adding
+//     into its bins 2g, 2g+1 (and bin 8 for g = 0, wrapped into bin 0 at the
+//     end as OpenCV does).  A sample touching the lane only through one bin
+//     adds an exact +0 to the other (every contribution is >= +0, so x + 0 = x).
+// Measured cost: DESIGN.md section 2.
+constexpr int kExactWG = 64;
+__constant__ float c_desc_exptab[64];
+void upload_desc_exp_table(const float* tab64) {
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_desc_exptab), tab64, 64 * sizeof(float));
+}
+
+__global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __restrict__ jobs,
+                                                               const Counters* __restrict__ ctr,
+                                                               uint16_t* __restrict__ desc,
+                                                               Counters* __restrict__ host_ctr, long fs, unsigned nf) {
+    __shared__ float s_tab[64];
+    __shared__ __attribute__((aligned(16))) float rec[64 * 8];  // chunk sample s: its 8 contributions, OpenCV order
+    __shared__ int meta[64];                                    // (r0 + 1) | (c0 + 1) << 4 | o0 << 8
+    __shared__ int rowpre[kMaxRows + 1], rowlo[kMaxRows];
+    __shared__ __attribute__((aligned(16))) float raw[128];
+    __shared__ float s_norm[12];
+
+    const int lane = threadIdx.x;
+    const unsigned frame = blockIdx.x % nf, wg = blockIdx.x / nf, nwg = gridDim.x / nf;
+    const long foff = frame * fs;
+    jobs = fptr(jobs, foff);
+    ctr = fptr(ctr, foff);
+    desc = fptr(desc, foff);
+    host_ctr += frame;
+    const unsigned n = ctr->final_n;
+    static_assert(sizeof(Counters) <= 4 * kExactWG, "counters handed over by one wave");
+    if (wg == 0 && lane < (int)(sizeof(Counters) / 4))
+        reinterpret_cast<unsigned*>(host_ctr)[lane] = reinterpret_cast<const unsigned*>(ctr)[lane];
+    if (wg >= n) return;
+    s_tab[lane] = c_desc_exptab[lane];
+    const float bins_per_rad = kN / 360.f;
+    const float exp_scale = -1.f / (kD * kD * 0.5f);
+    // This lane's bins: interior cell (ci, cj), orientations 2g and 2g + 1.
+    const int cell = lane >> 2, g = lane & 3, ci = cell >> 2, cj = cell & 3;
+
+    for (unsigned p = wg; p < n; p += nwg) {
+        const DescJob jb = jobs[p];
+        DescGeom G;
+        G.cos_t = jb.cos_t;
+        G.sin_t = jb.sin_t;
+        G.exp_scale = exp_scale;
+        G.ptx = jb.ptx;
+        G.pty = jb.pty;
+        G.rows = jb.rows;
+        G.cols = jb.cols;
+        const int radius = jb.radius, side = 2 * radius + 1;
+        const bool enumerated = side <= kMaxRows;
+        const __amdgpu_buffer_rsrc_t rsrc =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(jb.img), 0, jb.rows * jb.pitch * 4, 0x00020000);
+        int N;
+        if (enumerated) {
+            // Per-row j-intervals (supersets of the in-square samples, clipped
+            // to the image interior) and their prefix sum: two rows per lane.
+            const float inv_sin = __builtin_amdgcn_rcpf(G.sin_t), inv_cos = __builtin_amdgcn_rcpf(G.cos_t);
+            int len2[2];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int t = 2 * lane + h, i = t - radius, r = G.pty + i;
+                int lo = max(-radius, 1 - G.ptx), hi = min(radius, G.cols - 2 - G.ptx);
+                if (r <= 0 || r >= G.rows - 1 || t >= side) hi = lo - 1;
+                clip_interval(lo, hi, G.sin_t, inv_sin, (float)i * G.cos_t + (kD / 2 - 0.5f), radius);
+                clip_interval(lo, hi, G.cos_t, inv_cos, -(float)i * G.sin_t + (kD / 2 - 0.5f), radius);
+                len2[h] = max(hi - lo + 1, 0);
+                if (t < side) rowlo[t] = lo;
+            }
+            const int sum = wave_incl_scan(len2[0] + len2[1]);
+            if (2 * lane + 1 <= side) rowpre[2 * lane + 1] = sum - len2[1];
+            if (2 * lane + 2 <= side) rowpre[2 * lane + 2] = sum;
+            if (lane == 0) rowpre[0] = 0;
+            N = __builtin_amdgcn_readlane(sum, 63);
+        } else {
+            N = side * side;  // huge window: the full raster, the oracle's test per sample
+        }
+        lds_barrier();
+
+        float accA = 0.f, accB = 0.f, accW = 0.f;  // bins 2g, 2g + 1, and 8 (g = 0)
+        for (int k0 = 0; k0 < N; k0 += 64) {
+            // ---- phase 1: sample k0 + lane ----
+            const int k = min(k0 + lane, N - 1);
+            int i, j;
+            if (enumerated) {
+                int lo = 0, hi = side - 1;  // last row with rowpre[row] <= k
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (rowpre[mid] <= k) lo = mid;
+                    else hi = mid - 1;
+                }
+                i = lo - radius;
+                j = rowlo[lo] + (k - rowpre[lo]);
+            } else {
+                i = k / side - radius;
+                j = k % side - radius;
+            }
+            float rbin, cbin, c_rot, r_rot;
+            const bool valid = desc_sample(G, i, j, rbin, cbin, c_rot, r_rot) && k0 + lane < N;
+            const unsigned o = (unsigned)((G.pty + i) * jb.pitch + G.ptx + j) * 4u;
+            const float l = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o - 4u, 0, 0));
+            const float r = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o + 4u, 0, 0));
+            const float u = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o - 4u * jb.pitch, 0, 0));
+            const float d = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o + 4u * jb.pitch, 0, 0));
+            const float dx = r - l, dy = u - d;
+            const float wgt = cv_exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, s_tab);
+            const float gori = cv_fast_atan2(dy, dx);
+            const float gmag = cv_magnitude(dx, dy);
+            float obin = (gori - jb.angle) * bins_per_rad;
+            const float mag = gmag * wgt;
+            const int r0 = cv_floor(rbin), c0 = cv_floor(cbin);
+            int o0 = cv_floor(obin);
+            rbin -= (float)r0;
+            cbin -= (float)c0;
+            obin -= (float)o0;
+            if (o0 < 0) o0 += kN;
+            if (o0 >= kN) o0 -= kN;
+            float v[8];
+            trilinear(mag, rbin, cbin, obin, v);
+            float4* rp = reinterpret_cast<float4*>(rec + lane * 8);
+            rp[0] = make_float4(v[0], v[1], v[2], v[3]);
+            rp[1] = make_float4(v[4], v[5], v[6], v[7]);
+            meta[lane] = (r0 + 1) | (c0 + 1) << 4 | o0 << 8;
+            // Samples touching interior cell row / column q (r0 in {q - 1, q})
+            // and orientation pair q (o0 in {2q - 1 mod 8, 2q, 2q + 1}).
+            unsigned long long RR[kD], CC[kD], OO[kD];
+#pragma unroll
+            for (int q = 0; q < kD; q++) {
+                RR[q] = __ballot(valid && (r0 == q || r0 == q - 1));
+                CC[q] = __ballot(valid && (c0 == q || c0 == q - 1));
+                OO[q] = __ballot(valid && (o0 == 2 * q || o0 == 2 * q + 1 || o0 == ((2 * q + kN - 1) & (kN - 1))));
+            }
+            unsigned long long M = (ci == 0 ? RR[0] : ci == 1 ? RR[1] : ci == 2 ? RR[2] : RR[3]) &
+                                   (cj == 0 ? CC[0] : cj == 1 ? CC[1] : cj == 2 ? CC[2] : CC[3]) &
+                                   (g == 0 ? OO[0] : g == 1 ? OO[1] : g == 2 ? OO[2] : OO[3]);
+            // rec / meta writes of every lane before any lane reads them (one
+            // wave: LDS executes its instructions in order; this keeps the
+            // compiler from moving the reads up).
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+            // ---- phase 2: this lane's samples in ascending (raster) order ----
+            while (M) {
+                const int s = __builtin_ctzll(M);
+                M &= M - 1;
+                const int mt = meta[s];
+                const int dr = ci - ((mt & 15) - 1), dc = cj - (((mt >> 4) & 15) - 1), so = mt >> 8;
+                const float2 pv = *reinterpret_cast<const float2*>(rec + s * 8 + dr * 4 + dc * 2);
+                const bool lo_pair = so == 2 * g;      // bins (2g, 2g + 1) <- (o0, o0 + 1)
+                const bool hi_only = so == 2 * g + 1;  // bin 2g + 1 <- o0
+                const bool below = !lo_pair && !hi_only;  // o0 = 2g - 1: bin 2g (bin 8 for g = 0) <- o0 + 1
+                accA = accA + (lo_pair ? pv.x : (below && g != 0 ? pv.y : 0.f));
+                accB = accB + (lo_pair ? pv.y : (hi_only ? pv.x : 0.f));
+                accW = accW + (below && g == 0 ? pv.y : 0.f);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+        }
+        // OpenCV's wrap: hist[0] += hist[8] (hist[1] += hist[9] adds +0).
+        raw[cell * kN + 2 * g] = g == 0 ? accA + accW : accA;
+        raw[cell * kN + 2 * g + 1] = accB;
+        lds_barrier();
+        // L2 norm (8 fma lanes, v_reduce_sum's pairing), 0.2 clip, sequential
+        // renorm, x512 rounding: the oracle's float operations.
+        if (lane < 8) {
+            float a = 0.f;
+#pragma unroll
+            for (int q = 0; q < 16; q++) a = __fmaf_rn(raw[lane + 8 * q], raw[lane + 8 * q], a);
+            s_norm[lane] = a;
+        }
+        lds_barrier();
+        const float t0 = s_norm[0] + s_norm[4], t1 = s_norm[1] + s_norm[5], t2 = s_norm[2] + s_norm[6],
+                    t3 = s_norm[3] + s_norm[7];
+        const float thr = __builtin_sqrtf((t0 + t2) + (t1 + t3)) * 0.2f;
+        const float v0 = fminf(raw[2 * lane], thr), v1 = fminf(raw[2 * lane + 1], thr);
+        lds_barrier();
+        raw[2 * lane] = v0;
+        raw[2 * lane + 1] = v1;
+        lds_barrier();
+        if (lane == 0) {
+            float nrm2 = 0.f;
+            for (int q = 0; q < 128; q++) nrm2 = nrm2 + raw[q] * raw[q];
+            s_norm[8] = 512.f / fmaxf(__builtin_sqrtf(nrm2), FLT_EPSILON);
+        }
+        lds_barrier();
+        const float scale = s_norm[8];
+        int b0 = cv_round(v0 * scale), b1 = cv_round(v1 * scale);
+        b0 = b0 < 0 ? 0 : (b0 > 255 ? 255 : b0);
+        b1 = b1 < 0 ? 0 : (b1 > 255 ? 255 : b1);
+        const _Float16 h0 = (_Float16)(float)b0, h1 = (_Float16)(float)b1;
+        reinterpret_cast<unsigned*>(desc + (size_t)p * 128)[lane] =
+            (unsigned)__builtin_bit_cast(uint16_t, h0) | (unsigned)__builtin_bit_cast(uint16_t, h1) << 16;
+        lds_barrier();  // rowpre / raw / s_norm are rewritten by the next keypoint
+    }
+}
+
 void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned* range_keys, uint16_t* desc,
                        Counters* host_ctr, const KeypointParams& kp, const Frames& fr, hipStream_t s) {
-    (void)kp;
+    if (kp.descExact) {
+        // One wave per keypoint; each workgroup loops over keypoints.
+        const int per = fr.nf <= 1 ? 8192 : std::max(2048, 32768 / fr.nf);
+        hipLaunchKernelGGL(k_descriptor_exact, dim3(per * fr.nf), dim3(kExactWG), 0, s, jobs, ctr, desc, host_ctr,
+                           fr.stride, (unsigned)fr.nf);
+        return;
+    }
     // Threads per keypoint: 256 for a single frame (128: 34.6 us, 512: 47.6 vs
     // 36.1 per frame, round 3), 128 for frame batches.
     constexpr int kSingleDT = 256, kBatchDT = 128;

@@ -373,6 +373,7 @@ void upload_exp_tab() {
     float tab[64];
     for (int j = 0; j < 64; j++) tab[j] = (float)(std::exp2((double)j / 64.0) * A0);
     upload_exp_table(tab);
+    upload_desc_exp_table(tab);
 }
 
 template <class T>
@@ -1406,6 +1407,20 @@ int sift_hip_set_batch(sift_hip_t d, int frames) {
     if (frames < 1 || frames > kMaxBatch) return fail(SIFT_HIP_ERR_INVALID, "batch size out of range (1..64)");
     if (d->allocated) return fail(SIFT_HIP_ERR_STATE, "sift_hip_set_batch after sift_hip_warmup");
     d->B = frames;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_set_descriptor_mode(sift_hip_t d, int mode) {
+    if (!d) return fail(SIFT_HIP_ERR_INVALID, "null handle");
+    if (mode != SIFT_HIP_DESC_FAST && mode != SIFT_HIP_DESC_EXACT) return fail(SIFT_HIP_ERR_INVALID, "unknown descriptor mode");
+    if (d->allocated) return fail(SIFT_HIP_ERR_STATE, "sift_hip_set_descriptor_mode after sift_hip_warmup");
+    d->kp.descExact = mode == SIFT_HIP_DESC_EXACT;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_descriptor_mode(sift_hip_t d, int* mode) {
+    if (!d || !mode) return fail(SIFT_HIP_ERR_INVALID, "null argument");
+    *mode = d->kp.descExact ? SIFT_HIP_DESC_EXACT : SIFT_HIP_DESC_FAST;
     return SIFT_HIP_OK;
 }
 

@@ -163,6 +163,7 @@ struct KeypointParams {
     int numBuckets;
     int oriRmax, descRmax;  // LDS patch bounds for orientation / descriptor radii
     int descNrec;           // LDS record bound of the descriptor's counting sort
+    int descExact;          // 1: OpenCV's sequential float histogram (k_descriptor_exact)
 };
 void launch_refine(const PyrDesc& pyr, const uint2* cand, unsigned capCand, Counters* ctr, uint32_t* bitmap,
                    RefKpt* out, const KeypointParams& kp, const Frames& fr, hipStream_t s);
@@ -228,5 +229,6 @@ void set_last_error(const std::string& msg);
 // Exp table (OpenCV expTab_f) uploaded once per device (orientation and
 // descriptor translation units each hold a copy).
 void upload_exp_table(const float* tab64);
+void upload_desc_exp_table(const float* tab64);
 
 }  // namespace sift_amd

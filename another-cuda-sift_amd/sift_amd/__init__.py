@@ -33,6 +33,7 @@ LIB_PATH = os.environ.get("SIFT_HIP_LIB") or os.path.join(LIB_DIR, "libsift_hip.
 
 SIFT_HIP_OK = 0
 SIFT_HIP_F32, SIFT_HIP_U8 = 0, 1  # pixel formats (include/sift_hip.h)
+SIFT_HIP_DESC_FAST, SIFT_HIP_DESC_EXACT = 0, 1  # descriptor modes (sift_hip_set_descriptor_mode)
 _lib = None
 
 
@@ -91,6 +92,8 @@ def lib() -> ctypes.CDLL:
         "sift_hip_sync": (i, [vp]),
         "sift_hip_set_batch": (i, [vp, i]),
         "sift_hip_batch_capacity": (i, [vp, ip]),
+        "sift_hip_set_descriptor_mode": (i, [vp, i]),
+        "sift_hip_descriptor_mode": (i, [vp, ip]),
         "sift_hip_capacities": (i, [vp, ip, ip, ip, ip]),
         "sift_hip_detect_batch_device": (i, [vp, vp, i, sz, sz, i, vp]),
         "sift_hip_batch_frames": (i, [vp, ip]),
@@ -209,15 +212,20 @@ class DeviceBuffer:
 class Detector:
     """sift_cuda::Detector (Detector.hh:24-96) over the C ABI."""
 
-    def __init__(self, config: CudaSiftConfig, device: int = -1, batch: int = 1):
+    def __init__(self, config: CudaSiftConfig, device: int = -1, batch: int = 1, exact_descriptors: bool = False):
         """batch > 1: frame-batch handle (sift_hip_set_batch): detectBatchDevice runs up to `batch`
-        frames per launch; the single-frame methods keep working (frame 0's arena)."""
+        frames per launch; the single-frame methods keep working (frame 0's arena).
+        exact_descriptors: OpenCV's sequential float histogram (SIFT_HIP_DESC_EXACT), descriptors
+        bit-identical to the oracle; default the fixed-point histogram (+-1 on a byte)."""
         self.config = config
         self.batch = int(batch)
+        self.exact_descriptors = bool(exact_descriptors)
         self._h = ctypes.c_void_p()
         _check(lib().sift_hip_create(ctypes.byref(config._abi()), device, ctypes.byref(self._h)), "sift_hip_create")
         if self.batch != 1:
             _check(lib().sift_hip_set_batch(self._h, self.batch), "set_batch")
+        if self.exact_descriptors:
+            _check(lib().sift_hip_set_descriptor_mode(self._h, SIFT_HIP_DESC_EXACT), "set_descriptor_mode")
         n = ctypes.c_int()
         lib().sift_hip_num_octaves(self._h, ctypes.byref(n))
         self.nOctaves = n.value

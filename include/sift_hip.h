@@ -110,6 +110,22 @@ int sift_hip_sync(sift_hip_t h);
 int sift_hip_set_batch(sift_hip_t h, int frames);
 int sift_hip_batch_capacity(sift_hip_t h, int* frames);
 
+/* Descriptor histogram summation, called before sift_hip_warmup (the mode is
+ * part of the captured graphs).  The reference sums each bin with float
+ * shared-memory atomics in scheduling order (SiftOps.cu:561-595); OpenCV sums
+ * it sequentially in raster order (sift.simd.hpp calcSIFTDescriptor).
+ *   SIFT_HIP_DESC_FAST  (default) fixed-point integer histogram: deterministic,
+ *                       the exact sum of the rounded contributions; a byte can
+ *                       differ from OpenCV's by +-1 (float summation order).
+ *   SIFT_HIP_DESC_EXACT OpenCV's sequential float sum and correctly rounded
+ *                       sample math: descriptors bit-identical to the oracle,
+ *                       at a higher descriptor cost.
+ * Keypoints are identical in both modes. */
+#define SIFT_HIP_DESC_FAST  0
+#define SIFT_HIP_DESC_EXACT 1
+int sift_hip_set_descriptor_mode(sift_hip_t h, int mode);
+int sift_hip_descriptor_mode(sift_hip_t h, int* mode);
+
 /* n (1..B) device frames, frame i at dev_frames + i * frame_stride_bytes (0 =
  * row_stride * height), enqueued on `stream` (NULL = internal), NOT
  * synchronised (sift_hip_sync).  The batch becomes the current launch group. */

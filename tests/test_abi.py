@@ -189,3 +189,24 @@ def test_capacities_sized_to_the_frame(sift):
     d3 = sift.Detector(sift.CudaSiftConfig(col_width=1920, row_width=1200, numFeatures=0, upscale=True), device=0)
     c3 = d3.capacities()
     assert 4096 <= c3["results"] <= 65536 and c3["candidates"] <= 1 << 20 and c3["oriented"] <= 1 << 19
+
+
+def test_descriptor_mode_host_logic(sift):
+    """sift_hip_set_descriptor_mode: two modes, set before warm-up (host-only)."""
+    L = sift.lib()
+    h = ctypes.c_void_p()
+    c = sift._Config()
+    L.sift_hip_default_config(ctypes.byref(c), 64, 64)
+    assert L.sift_hip_create(ctypes.byref(c), 0, ctypes.byref(h)) == 0
+    try:
+        m = ctypes.c_int(-1)
+        assert L.sift_hip_descriptor_mode(h, ctypes.byref(m)) == 0 and m.value == sift.SIFT_HIP_DESC_FAST
+        assert L.sift_hip_set_descriptor_mode(h, 2) == -1
+        assert L.sift_hip_set_descriptor_mode(h, sift.SIFT_HIP_DESC_EXACT) == 0
+        assert L.sift_hip_descriptor_mode(h, ctypes.byref(m)) == 0 and m.value == sift.SIFT_HIP_DESC_EXACT
+        assert L.sift_hip_set_descriptor_mode(h, sift.SIFT_HIP_DESC_FAST) == 0
+    finally:
+        L.sift_hip_destroy(h)
+    assert L.sift_hip_set_descriptor_mode(None, 0) == -1
+    d = sift.Detector(sift.CudaSiftConfig(col_width=64, row_width=64), device=0, exact_descriptors=True)
+    assert d.exact_descriptors

@@ -16,8 +16,8 @@ from parity_bar import assert_descriptor_bar
 pytestmark = pytest.mark.gpu
 
 
-def single_results(sift, cfg, frames):
-    det = sift.Detector(cfg, device=0)
+def single_results(sift, cfg, frames, exact=False):
+    det = sift.Detector(cfg, device=0, exact_descriptors=exact)
     det.gpuWarmUpAndAllocate()
     out = []
     for f in frames:
@@ -27,8 +27,8 @@ def single_results(sift, cfg, frames):
     return out
 
 
-def batch_results(sift, cfg, frames, B, u8=False):
-    det = sift.Detector(cfg, device=0, batch=B)
+def batch_results(sift, cfg, frames, B, u8=False, exact=False):
+    det = sift.Detector(cfg, device=0, batch=B, exact_descriptors=exact)
     det.gpuWarmUpAndAllocate()
     dt = torch.uint8 if u8 else torch.float32
     t = torch.from_numpy(np.stack(frames)).to(dtype=dt, device="cuda:0").contiguous()
@@ -107,3 +107,21 @@ def test_single_frame_call_on_batch_handle(sift, oracle):
     gi, oi = np.lexsort(gk[:, :4].T[::-1]), np.lexsort(o.T[::-1])
     assert np.array_equal(gk[gi, :4], o[oi])
     assert_descriptor_bar(got[2][2].view(np.float16).astype(np.float32)[gi], od[oi], "batch frame 2")
+
+
+def test_batch_exact_descriptors(sift, oracle):
+    """SIFT_HIP_DESC_EXACT on a batch handle (full batch through the graph):
+    frame results equal the single-frame exact handle's, and a frame's
+    descriptors equal the oracle's byte for byte."""
+    w, h = 752, 480
+    cfg = sift.CudaSiftConfig(col_width=w, row_width=h, numFeatures=0, numOctaves=3)
+    frames = [sift.synth_frame(90 + i, w, h) for i in range(4)]
+    _, got = batch_results(sift, cfg, frames, 4, exact=True)
+    assert_equal_results(got, single_results(sift, cfg, frames, exact=True))
+    k3, f4, d = got[3]
+    gk = np.stack([k3[:, 0], k3[:, 1], f4[:, 1], f4[:, 3], f4[:, 2]], 1)
+    ok, od = oracle.detect_and_compute(frames[3], oracle.from_config(cfg))
+    o = np.stack([ok["x"], ok["y"], ok["size"], ok["angle"], ok["response"]], 1)
+    gi, oi = np.lexsort(gk.T[::-1]), np.lexsort(o.T[::-1])
+    assert np.array_equal(gk[gi], o[oi])
+    assert np.array_equal(d.view(np.float16).astype(np.float32)[gi], od[oi])

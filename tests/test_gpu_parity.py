@@ -19,9 +19,9 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def make_detector(sift, w, h, **kw):
+def make_detector(sift, w, h, exact_descriptors=False, **kw):
     cfg = sift.CudaSiftConfig(col_width=w, row_width=h, **kw)
-    det = sift.Detector(cfg)
+    det = sift.Detector(cfg, exact_descriptors=exact_descriptors)
     det.gpuWarmUpAndAllocate()
     return cfg, det
 
@@ -106,6 +106,25 @@ def test_keypoints_and_descriptors(sift, oracle, w, h, upscale, nOct, nfeat, fra
     gi, oi = sort_keys(gk), sort_keys(ok)
     assert_descriptor_bar(gd[gi], od[oi], f"{w}x{h} up={upscale} nOct={nOct} nfeat={nfeat}")
     assert gd.min() >= 0 and gd.max() <= 255 and np.all(gd == np.round(gd))
+
+
+@pytest.mark.parametrize("w,h,upscale,nOct,nfeat,frame", CONFIGS)
+def test_exact_descriptors_bitexact(sift, oracle, w, h, upscale, nOct, nfeat, frame):
+    """SIFT_HIP_DESC_EXACT: OpenCV's sequential float histogram, so every
+    descriptor byte equals the pinned oracle's (no +-1 bar), keypoints as in
+    the default mode."""
+    img = sift.synth_frame(frame, w, h)
+    cfg, det = make_detector(sift, w, h, exact_descriptors=True, upscale=upscale, numOctaves=nOct, numFeatures=nfeat)
+    det.detectAndCompute(img)
+    assert det.overflow_flags() == 0
+    gk, gd, _ = gpu_keypoints(det)
+    ok, od = oracle.detect_and_compute(img, oracle.from_config(cfg))
+    assert_same_keypoints(gk, ok)
+    gi, oi = sort_keys(gk), sort_keys(ok)
+    diff = np.abs(gd[gi] - od[oi])
+    bad = np.nonzero(diff.max(axis=1))[0]
+    assert len(bad) == 0, (f"{len(bad)} of {len(gk)} descriptors differ, {np.count_nonzero(diff)} bytes, "
+                           f"max |d| {diff.max()}, first keypoint {gk[gi][bad[0]]}")
 
 
 ENSEMBLE = ["avx2-fma", "avx512-fma"]
