@@ -505,7 +505,21 @@ __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* _
 //     end as OpenCV does).  A sample touching the lane only through one bin
 //     adds an exact +0 to the other (every contribution is >= +0, so x + 0 = x).
 // Measured cost: DESIGN.md section 2.
-constexpr int kExactWG = 64;
+// Waves per workgroup, each on its own keypoints with private LDS (no
+// workgroup barrier inside the keypoint loop).
+constexpr int kExactWaves = 4;
+#ifndef SIFT_EXACT_WALK32
+#define SIFT_EXACT_WALK32 1
+#endif
+constexpr int kExactWG = 64 * kExactWaves;
+// Orders one wave's LDS writes before its later LDS reads by other lanes (LDS
+// executes a wave's instructions in order; the fences keep the compiler from
+// moving accesses across).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
 __constant__ float c_desc_exptab[64];
 void upload_desc_exp_table(const float* tab64) {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(c_desc_exptab), tab64, 64 * sizeof(float));
@@ -516,13 +530,19 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
                                                                uint16_t* __restrict__ desc,
                                                                Counters* __restrict__ host_ctr, long fs, unsigned nf) {
     __shared__ float s_tab[64];
-    __shared__ __attribute__((aligned(16))) float rec[64 * 8];  // chunk sample s: its 8 contributions, OpenCV order
-    __shared__ int meta[64];                                    // (r0 + 1) | (c0 + 1) << 4 | o0 << 8
-    __shared__ int rowpre[kMaxRows + 1], rowlo[kMaxRows];
-    __shared__ __attribute__((aligned(16))) float raw[128];
-    __shared__ float s_norm[12];
+    __shared__ __attribute__((aligned(16))) float s_rec[kExactWaves][64 * 8];  // chunk sample s: its 8 contributions, OpenCV order
+    __shared__ int s_meta[kExactWaves][64];  // pair base | o0 << 16 (below)
+    __shared__ int s_rowpre[kExactWaves][kMaxRows + 1], s_rowlo[kExactWaves][kMaxRows];
+    __shared__ __attribute__((aligned(16))) float s_raw[kExactWaves][128];
+    __shared__ float s_nrm[kExactWaves][12];
 
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float* rec = s_rec[w];
+    int* meta = s_meta[w];
+    int* rowpre = s_rowpre[w];
+    int* rowlo = s_rowlo[w];
+    float* raw = s_raw[w];
+    float* s_norm = s_nrm[w];
     const unsigned frame = blockIdx.x % nf, wg = blockIdx.x / nf, nwg = gridDim.x / nf;
     const long foff = frame * fs;
     jobs = fptr(jobs, foff);
@@ -530,18 +550,25 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
     desc = fptr(desc, foff);
     host_ctr += frame;
     const unsigned n = ctr->final_n;
-    static_assert(sizeof(Counters) <= 4 * kExactWG, "counters handed over by one wave");
-    if (wg == 0 && lane < (int)(sizeof(Counters) / 4))
-        reinterpret_cast<unsigned*>(host_ctr)[lane] = reinterpret_cast<const unsigned*>(ctr)[lane];
-    if (wg >= n) return;
-    s_tab[lane] = c_desc_exptab[lane];
+    static_assert(sizeof(Counters) <= 4 * kExactWG, "counters handed over by one workgroup");
+    if (wg == 0 && threadIdx.x < sizeof(Counters) / 4)
+        reinterpret_cast<unsigned*>(host_ctr)[threadIdx.x] = reinterpret_cast<const unsigned*>(ctr)[threadIdx.x];
+    if (wg * kExactWaves >= n) return;  // workgroup-uniform
+    if (w == 0) s_tab[lane] = c_desc_exptab[lane];
+    lds_barrier();
     const float bins_per_rad = kN / 360.f;
     const float exp_scale = -1.f / (kD * kD * 0.5f);
     // This lane's bins: interior cell (ci, cj), orientations 2g and 2g + 1.
     const int cell = lane >> 2, g = lane & 3, ci = cell >> 2, cj = cell & 3;
 
-    for (unsigned p = wg; p < n; p += nwg) {
-        const DescJob jb = jobs[p];
+    for (unsigned p = wg * kExactWaves + w; p < n; p += nwg * kExactWaves) {
+        // The job through SGPRs: a VGPR copy of jb.img would put every buffer
+        // load of the chunk loop in a waterfall loop.
+        JobWords jwd;
+        const unsigned* __restrict__ jw = reinterpret_cast<const unsigned*>(jobs + p);
+#pragma unroll
+        for (int q = 0; q < 16; q++) jwd.w[q >> 2][q & 3] = __builtin_amdgcn_readfirstlane(jw[q]);
+        const DescJob jb = __builtin_bit_cast(DescJob, jwd);
         DescGeom G;
         G.cos_t = jb.cos_t;
         G.sin_t = jb.sin_t;
@@ -578,13 +605,10 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
         } else {
             N = side * side;  // huge window: the full raster, the oracle's test per sample
         }
-        lds_barrier();
+        wave_lds_sync();
 
-        float accA = 0.f, accB = 0.f, accW = 0.f;  // bins 2g, 2g + 1, and 8 (g = 0)
-        for (int k0 = 0; k0 < N; k0 += 64) {
-            // ---- phase 1: sample k0 + lane ----
-            const int k = min(k0 + lane, N - 1);
-            int i, j;
+        // Window sample k -> (i, j): row by binary search over the prefix sums.
+        auto locate = [&](int k, int& i, int& j) {
             if (enumerated) {
                 int lo = 0, hi = side - 1;  // last row with rowpre[row] <= k
                 while (lo < hi) {
@@ -598,13 +622,40 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
                 i = k / side - radius;
                 j = k % side - radius;
             }
+        };
+        auto gload = [&](unsigned o) {
+            return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o, 0, 0));
+        };
+        const unsigned pitch4 = 4u * jb.pitch;
+        // Gradient loads run two chunks ahead of the math and walk
+        // (unconditionally: past the end they re-read a valid sample), so
+        // their latency hides behind two chunks' work.
+        struct Fetch {
+            int i, j;
+            float l, r, u, d;
+        };
+        auto fetch = [&](int k) {
+            Fetch f;
+            locate(min(k, N - 1), f.i, f.j);
+            const unsigned o = (unsigned)((G.pty + f.i) * jb.pitch + G.ptx + f.j) * 4u;
+            f.l = gload(o - 4u);
+            f.r = gload(o + 4u);
+            f.u = gload(o - pitch4);
+            f.d = gload(o + pitch4);
+            return f;
+        };
+        Fetch f1 = fetch(lane), f2 = fetch(64 + lane);
+        // Walk constants: pair address = meta's base + this lane's cell offset.
+        const int lane_off = ci * 4 + cj * 2 - 32;
+        float accA = 0.f, accB = 0.f, accW = 0.f;  // bins 2g, 2g + 1, and 8 (g = 0)
+        for (int k0 = 0; k0 < N; k0 += 64) {
+            // ---- phase 1: sample k0 + lane ----
+            const int i = f1.i, j = f1.j;
+            const float l = f1.l, r = f1.r, u = f1.u, d = f1.d;
+            f1 = f2;
+            f2 = fetch(k0 + 128 + lane);
             float rbin, cbin, c_rot, r_rot;
             const bool valid = desc_sample(G, i, j, rbin, cbin, c_rot, r_rot) && k0 + lane < N;
-            const unsigned o = (unsigned)((G.pty + i) * jb.pitch + G.ptx + j) * 4u;
-            const float l = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o - 4u, 0, 0));
-            const float r = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o + 4u, 0, 0));
-            const float u = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o - 4u * jb.pitch, 0, 0));
-            const float d = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o + 4u * jb.pitch, 0, 0));
             const float dx = r - l, dy = u - d;
             const float wgt = cv_exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, s_tab);
             const float gori = cv_fast_atan2(dy, dx);
@@ -623,7 +674,10 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
             float4* rp = reinterpret_cast<float4*>(rec + lane * 8);
             rp[0] = make_float4(v[0], v[1], v[2], v[3]);
             rp[1] = make_float4(v[4], v[5], v[6], v[7]);
-            meta[lane] = (r0 + 1) | (c0 + 1) << 4 | o0 << 8;
+            // Owner lane (ci, cj) reads pair (dr, dc) = (ci - r0, cj - c0) at
+            // lane*8 + dr*4 + dc*2 = base - 32 + ci*4 + cj*2 (base >= 14 for
+            // valid samples: r0, c0 <= 3); o0 in the high half.
+            meta[lane] = (lane * 8 + 32 - r0 * 4 - c0 * 2) | o0 << 16;
             // Samples touching interior cell row / column q (r0 in {q - 1, q})
             // and orientation pair q (o0 in {2q - 1 mod 8, 2q, 2q + 1}).
             unsigned long long RR[kD], CC[kD], OO[kD];
@@ -639,31 +693,58 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
             // rec / meta writes of every lane before any lane reads them (one
             // wave: LDS executes its instructions in order; this keeps the
             // compiler from moving the reads up).
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-            // ---- phase 2: this lane's samples in ascending (raster) order ----
-            while (M) {
-                const int s = __builtin_ctzll(M);
-                M &= M - 1;
-                const int mt = meta[s];
-                const int dr = ci - ((mt & 15) - 1), dc = cj - (((mt >> 4) & 15) - 1), so = mt >> 8;
-                const float2 pv = *reinterpret_cast<const float2*>(rec + s * 8 + dr * 4 + dc * 2);
+            wave_lds_sync();
+            // ---- phase 2: this lane's samples in ascending (raster) order,
+            // two per iteration (their LDS reads in flight together; a missing
+            // second one adds +0) ----
+            auto add = [&](int mt, float2 pv, bool use) {
+                const int so = mt >> 16;
                 const bool lo_pair = so == 2 * g;      // bins (2g, 2g + 1) <- (o0, o0 + 1)
                 const bool hi_only = so == 2 * g + 1;  // bin 2g + 1 <- o0
                 const bool below = !lo_pair && !hi_only;  // o0 = 2g - 1: bin 2g (bin 8 for g = 0) <- o0 + 1
-                accA = accA + (lo_pair ? pv.x : (below && g != 0 ? pv.y : 0.f));
-                accB = accB + (lo_pair ? pv.y : (hi_only ? pv.x : 0.f));
-                accW = accW + (below && g == 0 ? pv.y : 0.f);
+                accA = accA + (use && lo_pair ? pv.x : (use && below && g != 0 ? pv.y : 0.f));
+                accB = accB + (use && lo_pair ? pv.y : (use && hi_only ? pv.x : 0.f));
+                accW = accW + (use && below && g == 0 ? pv.y : 0.f);
+            };
+            // 32-bit halves (samples 0-31, then 32-63: raster order kept),
+            // so the bit scans and clears are single VALU ops.
+#if SIFT_EXACT_WALK32
+            auto walk = [&](unsigned m, int base) {
+                while (m) {
+                    const int s0 = base + __builtin_ctz(m);
+                    m &= m - 1;
+                    const bool two = m != 0;
+                    const int s1 = two ? base + __builtin_ctz(m) : s0;
+                    m &= m - 1;
+                    const int mt0 = meta[s0], mt1 = meta[s1];
+                    const float2 pv0 = *reinterpret_cast<const float2*>(rec + (mt0 & 0xffff) + lane_off);
+                    const float2 pv1 = *reinterpret_cast<const float2*>(rec + (mt1 & 0xffff) + lane_off);
+                    add(mt0, pv0, true);
+                    add(mt1, pv1, two);
+                }
+            };
+            walk((unsigned)M, 0);
+            walk((unsigned)(M >> 32), 32);
+#else
+            while (M) {
+                const int s0 = __builtin_ctzll(M);
+                M &= M - 1;
+                const bool two = M != 0;
+                const int s1 = two ? __builtin_ctzll(M) : s0;
+                M &= M - 1;
+                const int mt0 = meta[s0], mt1 = meta[s1];
+                const float2 pv0 = *reinterpret_cast<const float2*>(rec + (mt0 & 0xffff) + lane_off);
+                const float2 pv1 = *reinterpret_cast<const float2*>(rec + (mt1 & 0xffff) + lane_off);
+                add(mt0, pv0, true);
+                add(mt1, pv1, two);
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+#endif
+            wave_lds_sync();
         }
         // OpenCV's wrap: hist[0] += hist[8] (hist[1] += hist[9] adds +0).
         raw[cell * kN + 2 * g] = g == 0 ? accA + accW : accA;
         raw[cell * kN + 2 * g + 1] = accB;
-        lds_barrier();
+        wave_lds_sync();
         // L2 norm (8 fma lanes, v_reduce_sum's pairing), 0.2 clip, sequential
         // renorm, x512 rounding: the oracle's float operations.
         if (lane < 8) {
@@ -672,21 +753,21 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
             for (int q = 0; q < 16; q++) a = __fmaf_rn(raw[lane + 8 * q], raw[lane + 8 * q], a);
             s_norm[lane] = a;
         }
-        lds_barrier();
+        wave_lds_sync();
         const float t0 = s_norm[0] + s_norm[4], t1 = s_norm[1] + s_norm[5], t2 = s_norm[2] + s_norm[6],
                     t3 = s_norm[3] + s_norm[7];
         const float thr = __builtin_sqrtf((t0 + t2) + (t1 + t3)) * 0.2f;
         const float v0 = fminf(raw[2 * lane], thr), v1 = fminf(raw[2 * lane + 1], thr);
-        lds_barrier();
+        wave_lds_sync();
         raw[2 * lane] = v0;
         raw[2 * lane + 1] = v1;
-        lds_barrier();
+        wave_lds_sync();
         if (lane == 0) {
             float nrm2 = 0.f;
             for (int q = 0; q < 128; q++) nrm2 = nrm2 + raw[q] * raw[q];
             s_norm[8] = 512.f / fmaxf(__builtin_sqrtf(nrm2), FLT_EPSILON);
         }
-        lds_barrier();
+        wave_lds_sync();
         const float scale = s_norm[8];
         int b0 = cv_round(v0 * scale), b1 = cv_round(v1 * scale);
         b0 = b0 < 0 ? 0 : (b0 > 255 ? 255 : b0);
@@ -694,7 +775,7 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
         const _Float16 h0 = (_Float16)(float)b0, h1 = (_Float16)(float)b1;
         reinterpret_cast<unsigned*>(desc + (size_t)p * 128)[lane] =
             (unsigned)__builtin_bit_cast(uint16_t, h0) | (unsigned)__builtin_bit_cast(uint16_t, h1) << 16;
-        lds_barrier();  // rowpre / raw / s_norm are rewritten by the next keypoint
+        wave_lds_sync();  // rowpre / raw / s_norm are rewritten by the next keypoint
     }
 }
 
@@ -702,7 +783,7 @@ void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned*
                        Counters* host_ctr, const KeypointParams& kp, const Frames& fr, hipStream_t s) {
     if (kp.descExact) {
         // One wave per keypoint; each workgroup loops over keypoints.
-        const int per = fr.nf <= 1 ? 8192 : std::max(2048, 32768 / fr.nf);
+        const int per = fr.nf <= 1 ? 2048 : std::max(512, 8192 / fr.nf);
         hipLaunchKernelGGL(k_descriptor_exact, dim3(per * fr.nf), dim3(kExactWG), 0, s, jobs, ctr, desc, host_ctr,
                            fr.stride, (unsigned)fr.nf);
         return;

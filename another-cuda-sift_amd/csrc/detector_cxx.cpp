@@ -149,6 +149,12 @@ void Detector::setDataGen(const std::string& path) {
     if (m_handle) check(sift_hip_set_datagen(m_handle, path.c_str()), "setDataGen");
 }
 
+void Detector::setExactDescriptors(bool exact) {
+    if (m_handle)
+        check(sift_hip_set_descriptor_mode(m_handle, exact ? SIFT_HIP_DESC_EXACT : SIFT_HIP_DESC_FAST),
+              "setExactDescriptors");
+}
+
 void Detector::replayStage(const std::string& dump_dir, const std::string& stage, const std::string& out_dir) {
     if (!m_initialized && !gpuWarmUpAndAllocate()) return;
     check(sift_hip_replay_stage(m_handle, dump_dir.c_str(), stage.c_str(), out_dir.c_str()), "replayStage");

@@ -53,6 +53,10 @@ public:
     // input, every Gaussian plane, candidates, keypoints, descriptors);
     // tests/stage_check.py replays them.  An empty path switches it off.
     void setDataGen(const std::string& path);
+    // Extra: OpenCV's sequential float descriptor histogram (bit-identical
+    // descriptors; sift_hip_set_descriptor_mode(SIFT_HIP_DESC_EXACT)).  Call
+    // before gpuWarmUpAndAllocate; the default is the fixed-point histogram.
+    void setExactDescriptors(bool exact);
     // tool/perf.cu:43-100 (HostInterface.hh:11-69 run<Stage>): one stage --
     // "pyramid", "extrema", "refine", "orientation", "order", "descriptor" --
     // alone on a setDataGen dump's recorded input; its outputs go to out_dir

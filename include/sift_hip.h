@@ -112,7 +112,7 @@ int sift_hip_batch_capacity(sift_hip_t h, int* frames);
 
 /* Descriptor histogram summation, called before sift_hip_warmup (the mode is
  * part of the captured graphs).  The reference sums each bin with float
- * shared-memory atomics in scheduling order (SiftOps.cu:561-595); OpenCV sums
+ * shared-memory atomics in scheduling order (SiftOps.cu:587-600); OpenCV sums
  * it sequentially in raster order (sift.simd.hpp calcSIFTDescriptor).
  *   SIFT_HIP_DESC_FAST  (default) fixed-point integer histogram: deterministic,
  *                       the exact sum of the rounded contributions; a byte can

@@ -60,6 +60,7 @@ def test_libsift_cuda_exports_dropin_surface():
               "sift_cuda::Detector::gpuWarmUpAndAllocate()",
               "sift_cuda::Detector::detectAndCompute(Image<float> const&)",
               "sift_cuda::Detector::copyToHost(bool)",
+              "sift_cuda::Detector::setExactDescriptors(bool)",
               "sift_cuda::matchBruteForce("]:
         assert s in out, s
 

@@ -16,9 +16,10 @@ ap.add_argument("--octaves", type=int, default=3)
 ap.add_argument("--upscale", action="store_true")
 ap.add_argument("--eager", action="store_true", help="timing mode: un-graphed launches")
 ap.add_argument("--batch", type=int, default=1, help="frames per launch (sift_hip_set_batch)")
+ap.add_argument("--exact", action="store_true", help="exact descriptor mode (SIFT_HIP_DESC_EXACT)")
 a = ap.parse_args()
 cfg = sift.CudaSiftConfig(col_width=a.width, row_width=a.height, numOctaves=a.octaves, upscale=a.upscale)
-det = sift.Detector(cfg, device=0, batch=a.batch)
+det = sift.Detector(cfg, device=0, batch=a.batch, exact_descriptors=a.exact)
 det.gpuWarmUpAndAllocate()
 det.set_timing(a.eager)
 img = sift.synth_frame(0, a.width, a.height)
