@@ -515,6 +515,17 @@ constexpr int kExactWG = 64 * kExactWaves;
 // Orders one wave's LDS writes before its later LDS reads by other lanes (LDS
 // executes a wave's instructions in order; the fences keep the compiler from
 // moving accesses across).
+// Inclusive prefix maximum over the 64 lanes (non-negative values; DPP as
+// wave_incl_scan).
+__device__ __forceinline__ int wave_incl_max(int x) {
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false));
+    return x;
+}
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
     __builtin_amdgcn_wave_barrier();
@@ -535,6 +546,7 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
     __shared__ int s_rowpre[kExactWaves][kMaxRows + 1], s_rowlo[kExactWaves][kMaxRows];
     __shared__ __attribute__((aligned(16))) float s_raw[kExactWaves][128];
     __shared__ float s_nrm[kExactWaves][12];
+    __shared__ int s_rowmap[kExactWaves][64];
 
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float* rec = s_rec[w];
@@ -543,6 +555,7 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
     int* rowlo = s_rowlo[w];
     float* raw = s_raw[w];
     float* s_norm = s_nrm[w];
+    int* rowmap = s_rowmap[w];
     const unsigned frame = blockIdx.x % nf, wg = blockIdx.x / nf, nwg = gridDim.x / nf;
     const long foff = frame * fs;
     jobs = fptr(jobs, foff);
@@ -608,35 +621,60 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
         wave_lds_sync();
 
         // Window sample k -> (i, j): row by binary search over the prefix sums.
-        auto locate = [&](int k, int& i, int& j) {
-            if (enumerated) {
-                int lo = 0, hi = side - 1;  // last row with rowpre[row] <= k
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (rowpre[mid] <= k) lo = mid;
-                    else hi = mid - 1;
-                }
-                i = lo - radius;
-                j = rowlo[lo] + (k - rowpre[lo]);
-            } else {
-                i = k / side - radius;
-                j = k % side - radius;
+        // Enumerated sample k -> its row: binary search over the prefix sums.
+        auto row_search = [&](int k) {
+            int lo = 0, hi = side - 1;  // last row with rowpre[row] <= k
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (rowpre[mid] <= k) lo = mid;
+                else hi = mid - 1;
             }
+            return lo;
         };
         auto gload = [&](unsigned o) {
             return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o, 0, 0));
         };
         const unsigned pitch4 = 4u * jb.pitch;
         // Gradient loads run two chunks ahead of the math and walk
-        // (unconditionally: past the end they re-read a valid sample), so
-        // their latency hides behind two chunks' work.
+        // (unconditionally: past the end they re-read an in-buffer address),
+        // so their latency hides behind two chunks' work.
         struct Fetch {
             int i, j;
             float l, r, u, d;
         };
-        auto fetch = [&](int k) {
+        // Rows of a chunk [kf, kf + 64) without a per-lane search: frb is the
+        // row of sample kf; rows frb+1 .. frb+64 that start inside the chunk
+        // mark their start position (ds_max: of several rows starting at one
+        // position -- empty rows -- the last is the non-empty one) and a wave
+        // prefix maximum gives every position its row.  Non-empty rows are
+        // contiguous, so 64 rows cover the chunk; if not, the search.
+        int frb = N > 0 ? __builtin_amdgcn_readfirstlane(enumerated ? row_search(0) : 0) : 0;
+        auto fetch = [&](int kf) {
             Fetch f;
-            locate(min(k, N - 1), f.i, f.j);
+            if (enumerated) {
+                int row;
+                const bool covered = rowpre[min(frb + 65, side)] >= min(kf + 64, N);  // uniform
+                if (covered) {
+                    rowmap[lane] = frb;
+                    wave_lds_sync();
+                    const int r = frb + 1 + lane;
+                    if (r < side) {
+                        const int st = rowpre[r] - kf;
+                        if (st >= 0 && st < 64) atomicMax(&rowmap[st], r);
+                    }
+                    wave_lds_sync();
+                    row = wave_incl_max(rowmap[lane]);
+                } else {
+                    row = row_search(min(kf + lane, N - 1));
+                }
+                frb = __builtin_amdgcn_readlane(row, 63);
+                f.i = row - radius;
+                f.j = rowlo[row] + (kf + lane - rowpre[row]);
+            } else {
+                const int k = min(kf + lane, N - 1);
+                f.i = k / side - radius;
+                f.j = k % side - radius;
+            }
             const unsigned o = (unsigned)((G.pty + f.i) * jb.pitch + G.ptx + f.j) * 4u;
             f.l = gload(o - 4u);
             f.r = gload(o + 4u);
@@ -644,16 +682,23 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
             f.d = gload(o + pitch4);
             return f;
         };
-        Fetch f1 = fetch(lane), f2 = fetch(64 + lane);
+        Fetch f1 = fetch(0), f2 = fetch(64);
         // Walk constants: pair address = meta's base + this lane's cell offset.
         const int lane_off = ci * 4 + cj * 2 - 32;
+        unsigned sel_ci[kD], sel_cj[kD], sel_g[kD];  // all ones where this lane's index is q
+#pragma unroll
+        for (int q = 0; q < kD; q++) {
+            sel_ci[q] = ci == q ? ~0u : 0u;
+            sel_cj[q] = cj == q ? ~0u : 0u;
+            sel_g[q] = g == q ? ~0u : 0u;
+        }
         float accA = 0.f, accB = 0.f, accW = 0.f;  // bins 2g, 2g + 1, and 8 (g = 0)
         for (int k0 = 0; k0 < N; k0 += 64) {
             // ---- phase 1: sample k0 + lane ----
             const int i = f1.i, j = f1.j;
             const float l = f1.l, r = f1.r, u = f1.u, d = f1.d;
             f1 = f2;
-            f2 = fetch(k0 + 128 + lane);
+            f2 = fetch(k0 + 128);
             float rbin, cbin, c_rot, r_rot;
             const bool valid = desc_sample(G, i, j, rbin, cbin, c_rot, r_rot) && k0 + lane < N;
             const float dx = r - l, dy = u - d;
@@ -680,16 +725,28 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
             meta[lane] = (lane * 8 + 32 - r0 * 4 - c0 * 2) | o0 << 16;
             // Samples touching interior cell row / column q (r0 in {q - 1, q})
             // and orientation pair q (o0 in {2q - 1 mod 8, 2q, 2q + 1}).
+            // Plain compares (an invalid sample's row 64 touches no cell), so
+            // each ballot is one v_cmp into an SGPR pair.
+            const int r0v = valid ? r0 : 64;
             unsigned long long RR[kD], CC[kD], OO[kD];
 #pragma unroll
             for (int q = 0; q < kD; q++) {
-                RR[q] = __ballot(valid && (r0 == q || r0 == q - 1));
-                CC[q] = __ballot(valid && (c0 == q || c0 == q - 1));
-                OO[q] = __ballot(valid && (o0 == 2 * q || o0 == 2 * q + 1 || o0 == ((2 * q + kN - 1) & (kN - 1))));
+                RR[q] = __builtin_amdgcn_ballot_w64((unsigned)(r0v - q + 1) < 2u);
+                CC[q] = __builtin_amdgcn_ballot_w64((unsigned)(c0 - q + 1) < 2u);
+                OO[q] = __builtin_amdgcn_ballot_w64((unsigned)((o0 - 2 * q + 1) & (kN - 1)) < 3u);
             }
-            unsigned long long M = (ci == 0 ? RR[0] : ci == 1 ? RR[1] : ci == 2 ? RR[2] : RR[3]) &
-                                   (cj == 0 ? CC[0] : cj == 1 ? CC[1] : cj == 2 ? CC[2] : CC[3]) &
-                                   (g == 0 ? OO[0] : g == 1 ? OO[1] : g == 2 ? OO[2] : OO[3]);
+            // This lane's three masks by bitfield inserts with lane-constant
+            // selectors (no branches).
+            auto pick = [](const unsigned long long (&X)[kD], const unsigned (&sel)[kD]) {
+                unsigned lo = (unsigned)X[0], hi = (unsigned)(X[0] >> 32);
+#pragma unroll
+                for (int q = 1; q < kD; q++) {
+                    lo = ((unsigned)X[q] & sel[q]) | (lo & ~sel[q]);
+                    hi = ((unsigned)(X[q] >> 32) & sel[q]) | (hi & ~sel[q]);
+                }
+                return (unsigned long long)hi << 32 | lo;
+            };
+            unsigned long long M = pick(RR, sel_ci) & pick(CC, sel_cj) & pick(OO, sel_g);
             // rec / meta writes of every lane before any lane reads them (one
             // wave: LDS executes its instructions in order; this keeps the
             // compiler from moving the reads up).

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Counters of the exact-descriptor kernel (kernel trace only, one pass per
 # counter group) over tools/profile_frames.py --exact --batch 16.
-# Usage: tools/exact_pmc.sh TAG  -> gpurun_out/TAG_x{1,2}/
+# Usage: tools/exact_pmc.sh TAG  -> gpurun_out/TAG_p{1,2}/ (tools/pmc_summary.py TAG)
 set -o pipefail
 TAG=${1:-xpmc}
 export TMPDIR=/tmp
@@ -11,6 +11,6 @@ P2="SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ
 i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $P --kernel-trace -d gpurun_out/${TAG}_x$i -o run --output-format csv -- python3 tools/profile_frames.py --frames 5 --batch 16 --exact > gpurun_out/${TAG}_x$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/${TAG}_x$i.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $P --kernel-trace -d gpurun_out/${TAG}_p$i -o run --output-format csv -- python3 tools/profile_frames.py --frames 5 --batch 16 --exact > gpurun_out/${TAG}_p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/${TAG}_p$i.log; exit 1; }
 done
 echo done
