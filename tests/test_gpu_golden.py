@@ -80,3 +80,45 @@ def test_camera_rot90_match(sift, oracle, gold):
     n_gpu = int((od[:, 0] < 0.8 * od[:, 1]).sum())
     n_ref = int((ref[:, 0] < 0.8 * ref[:, 1]).sum())
     assert nq == len(ref) and abs(n_gpu - n_ref) <= 0.02 * n_ref, (n_gpu, n_ref)
+
+
+@pytest.mark.parametrize("name", ["default", "base_n60"])
+def test_camera_golden_exact_descriptors(sift, gold, name):
+    """Exact descriptor mode (SIFT_HIP_DESC_EXACT): the golden fixture's uint8
+    descriptors byte for byte."""
+    data, meta = gold
+    img = data["camera256"].astype(np.float32)
+    det = sift.Detector(config_for(sift, meta["configs"][name]), exact_descriptors=True)
+    det.gpuWarmUpAndAllocate()
+    det.detectAndCompute(img)
+    gk, gd, _ = gpu_keypoints(det)
+    ok, od = data[f"{name}_kpts"], data[f"{name}_desc"].astype(np.float32)
+    assert_same_keypoints(gk, ok)
+    assert np.array_equal(gd[sort_keys(gk)], od[sort_keys(ok)])
+
+
+def test_camera_rot90_match_exact(sift, gold):
+    """Exact descriptors of the crop and its rotation through the HIP matcher:
+    the golden knn-2 distances (oracle descriptors, oracle matcher) exactly."""
+    data, _ = gold
+    img = data["camera256"].astype(np.float32)
+    cfg = sift.CudaSiftConfig(col_width=256, row_width=256, upscale=True, numFeatures=0)
+    descs, keys = [], []
+    for im in (img, np.ascontiguousarray(np.rot90(img))):
+        det = sift.Detector(cfg, exact_descriptors=True)
+        det.gpuWarmUpAndAllocate()
+        det.detectAndCompute(im)
+        gk, d, _ = gpu_keypoints(det)
+        descs.append(d)
+        keys.append(gk)
+    da, db = descs
+    nq, nt = len(da), len(db)
+    dq = sift.DeviceArray.from_numpy(da.astype(np.float16))
+    dt = sift.DeviceArray.from_numpy(db.astype(np.float16))
+    idx2, d2 = sift.DeviceArray(nq * 8), sift.DeviceArray(nq * 8)
+    sift.Matcher(nq, nt).match_device(dq.value, nq, dt.value, nt, 0.8, False, idx2.value, d2.value)
+    gd = d2.to_numpy(np.float32, (nq, 2))
+    ref, ok = data["rot90_knn_dist"], data["default_kpts"]  # the golden's queries: the "default" config's keypoints
+    assert nq == len(ref) == len(ok)
+    # a query's distances depend on its descriptor and the train set only: compare in keypoint order
+    assert np.array_equal(np.sqrt(gd).astype(np.float32)[sort_keys(keys[0])], ref[sort_keys(ok)])

@@ -2,7 +2,10 @@
 tests do not use) through the HIP path and the CPU oracle, keypoints compared
 bit for bit and descriptor flips counted.
 
-    python3 tools/parity_sweep.py [FRAMES_PER_CONFIG] > gpurun_out/parity_sweep.json   (GPU box)
+    python3 tools/parity_sweep.py [FRAMES_PER_CONFIG] [--exact] > gpurun_out/parity_sweep.json   (GPU box)
+
+--exact: the exact descriptor mode (SIFT_HIP_DESC_EXACT), where every
+descriptor byte must equal the oracle's (flips = 0).
 
 Configurations: BASELINE C2 (1920x1200, 3 octaves, numFeatures 5000) and
 OpenCV defaults (doubled base, keep all) at 752x480 (C1's frame).
@@ -19,7 +22,9 @@ import oracle_binding as oracle  # noqa: E402
 import sift_amd as sift  # noqa: E402
 from test_gpu_parity import gpu_keypoints, sort_keys  # noqa: E402
 
-N = int(sys.argv[1]) if len(sys.argv) > 1 else 10  # frames per configuration (seeds unused by the tests)
+ARGS = [a for a in sys.argv[1:] if not a.startswith("--")]
+EXACT = "--exact" in sys.argv[1:]
+N = int(ARGS[0]) if ARGS else 10  # frames per configuration (seeds unused by the tests)
 CONFIGS = [("C2", 1920, 1200, dict(upscale=False, numOctaves=3, numFeatures=5000), range(1000, 1000 + N)),
            ("C1 OpenCV defaults", 752, 480, dict(upscale=True, numOctaves=0, numFeatures=0), range(5000, 5000 + N))]
 
@@ -29,7 +34,7 @@ def main():
                      "max_abs_diff": 0}
     for name, w, h, kw, seeds in CONFIGS:
         cfg = sift.CudaSiftConfig(col_width=w, row_width=h, **kw)
-        det = sift.Detector(cfg)
+        det = sift.Detector(cfg, exact_descriptors=EXACT)
         det.gpuWarmUpAndAllocate()
         for seed in seeds:
             img = sift.synth_frame(seed, w, h)
@@ -57,7 +62,9 @@ def main():
             rows.append(row)
             print(json.dumps(row), file=sys.stderr, flush=True)
     tot["exact_fraction"] = 1.0 - tot["flips"] / max(1, tot["entries"])
-    json.dump({"command": f"python3 tools/parity_sweep.py {N}", "total": tot, "frames": rows}, sys.stdout, indent=1)
+    cmd = f"python3 tools/parity_sweep.py {N}" + (" --exact" if EXACT else "")
+    json.dump({"command": cmd, "descriptor_mode": "exact" if EXACT else "fast", "total": tot, "frames": rows},
+              sys.stdout, indent=1)
     print()
 
 
