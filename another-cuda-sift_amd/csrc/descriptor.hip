@@ -508,9 +508,7 @@ __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* _
 // Waves per workgroup, each on its own keypoints with private LDS (no
 // workgroup barrier inside the keypoint loop).
 constexpr int kExactWaves = 4;
-#ifndef SIFT_EXACT_WALK32
-#define SIFT_EXACT_WALK32 1
-#endif
+constexpr int kZeroRec = 40;  // zero floats after the 64 records (absent second hit of a walk step)
 constexpr int kExactWG = 64 * kExactWaves;
 // Orders one wave's LDS writes before its later LDS reads by other lanes (LDS
 // executes a wave's instructions in order; the fences keep the compiler from
@@ -541,21 +539,24 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
                                                                uint16_t* __restrict__ desc,
                                                                Counters* __restrict__ host_ctr, long fs, unsigned nf) {
     __shared__ float s_tab[64];
-    __shared__ __attribute__((aligned(16))) float s_rec[kExactWaves][64 * 8];  // chunk sample s: its 8 contributions, OpenCV order
-    __shared__ int s_meta[kExactWaves][64];  // pair base | o0 << 16 (below)
-    __shared__ int s_rowpre[kExactWaves][kMaxRows + 1], s_rowlo[kExactWaves][kMaxRows];
-    __shared__ __attribute__((aligned(16))) float s_raw[kExactWaves][128];
+    // Chunk sample s: per target cell (dr, dc) one float4 {P.x, P.y, S.x, S.y}
+    // (below), at s*16 + (dr*2 + dc)*4; then a zero record for absent hits.
+    __shared__ __attribute__((aligned(16))) float s_rec[kExactWaves][64 * 16 + kZeroRec];
+    // 16-bit / 8-bit tables and the epilogue's raw[] and fetch's row map
+    // inside the records (dead at those points): 4.8 KB per wave, 8 waves/SIMD.
+    __shared__ unsigned short s_meta[kExactWaves][65];  // record base | (o0 >> 1) << 14 (below); [64]: the zero record
+    __shared__ unsigned short s_rowpre[kExactWaves][kMaxRows + 1];  // <= 128^2 samples
+    __shared__ signed char s_rowlo[kExactWaves][kMaxRows];           // |j| <= radius + 2 <= 66
     __shared__ float s_nrm[kExactWaves][12];
-    __shared__ int s_rowmap[kExactWaves][64];
 
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float* rec = s_rec[w];
-    int* meta = s_meta[w];
-    int* rowpre = s_rowpre[w];
-    int* rowlo = s_rowlo[w];
-    float* raw = s_raw[w];
+    unsigned short* meta = s_meta[w];
+    unsigned short* rowpre = s_rowpre[w];
+    signed char* rowlo = s_rowlo[w];
+    float* raw = rec;  // after the chunk loop
     float* s_norm = s_nrm[w];
-    int* rowmap = s_rowmap[w];
+    int* rowmap = reinterpret_cast<int*>(rec);  // inside fetch(), between a chunk's walk and the next chunk's records
     const unsigned frame = blockIdx.x % nf, wg = blockIdx.x / nf, nwg = gridDim.x / nf;
     const long foff = frame * fs;
     jobs = fptr(jobs, foff);
@@ -568,6 +569,8 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
         reinterpret_cast<unsigned*>(host_ctr)[threadIdx.x] = reinterpret_cast<const unsigned*>(ctr)[threadIdx.x];
     if (wg * kExactWaves >= n) return;  // workgroup-uniform
     if (w == 0) s_tab[lane] = c_desc_exptab[lane];
+    if (lane < kZeroRec) rec[64 * 16 + lane] = 0.f;
+    if (lane == 0) meta[64] = 64 * 16 + 64;  // + any lane offset (-64 .. -28) lands in the zero floats
     lds_barrier();
     const float bins_per_rad = kN / 360.f;
     const float exp_scale = -1.f / (kD * kD * 0.5f);
@@ -684,7 +687,7 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
         };
         Fetch f1 = fetch(0), f2 = fetch(64);
         // Walk constants: pair address = meta's base + this lane's cell offset.
-        const int lane_off = ci * 4 + cj * 2 - 32;
+        const int lane_off = ci * 8 + cj * 4 - 64;
         unsigned sel_ci[kD], sel_cj[kD], sel_g[kD];  // all ones where this lane's index is q
 #pragma unroll
         for (int q = 0; q < kD; q++) {
@@ -716,13 +719,25 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
             if (o0 >= kN) o0 -= kN;
             float v[8];
             trilinear(mag, rbin, cbin, obin, v);
-            float4* rp = reinterpret_cast<float4*>(rec + lane * 8);
-            rp[0] = make_float4(v[0], v[1], v[2], v[3]);
-            rp[1] = make_float4(v[4], v[5], v[6], v[7]);
-            // Owner lane (ci, cj) reads pair (dr, dc) = (ci - r0, cj - c0) at
-            // lane*8 + dr*4 + dc*2 = base - 32 + ci*4 + cj*2 (base >= 14 for
-            // valid samples: r0, c0 <= 3); o0 in the high half.
-            meta[lane] = (lane * 8 + 32 - r0 * 4 - c0 * 2) | o0 << 16;
+            // Per target cell (dr, dc) the values its owner lanes add, arranged
+            // by orientation so the walk needs no case analysis.  The primary
+            // owner (pair g = o0 >> 1) adds P to bins (2g, 2g + 1); for odd o0
+            // the secondary owner (g = (o0 + 1) >> 1 mod 4) adds S.x to bin 2g
+            // and S.y to bin 8:
+            //   o0 even:   P = (v_o0, v_o0+1), S = (0, 0)
+            //   o0 odd:    P = (0, v_o0),      S = (v_o0+1, 0)
+            //   o0 = 7:    P = (0, v_7),       S = (0, v_8)   (bin 8: g = 0's third bin)
+            const bool odd = o0 & 1, seven = o0 == kN - 1;
+            float4* rp = reinterpret_cast<float4*>(rec + lane * 16);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const float x = v[2 * q], y = v[2 * q + 1];
+                rp[q] = make_float4(odd ? 0.f : x, odd ? x : y, odd && !seven ? y : 0.f, seven ? y : 0.f);
+            }
+            // Owner lane (ci, cj) reads the float4 of (dr, dc) = (ci - r0, cj - c0)
+            // at lane*16 + dr*8 + dc*4 = base - 64 + ci*8 + cj*4 (base >= 28 for
+            // valid samples: r0, c0 <= 3); o0 >> 1 in bits 14-15.
+            meta[lane] = (unsigned short)((lane * 16 + 64 - r0 * 8 - c0 * 4) | (o0 >> 1) << 14);
             // Samples touching interior cell row / column q (r0 in {q - 1, q})
             // and orientation pair q (o0 in {2q - 1 mod 8, 2q, 2q + 1}).
             // Plain compares (an invalid sample's row 64 touches no cell), so
@@ -752,50 +767,31 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
             // compiler from moving the reads up).
             wave_lds_sync();
             // ---- phase 2: this lane's samples in ascending (raster) order,
-            // two per iteration (their LDS reads in flight together; a missing
-            // second one adds +0) ----
-            auto add = [&](int mt, float2 pv, bool use) {
-                const int so = mt >> 16;
-                const bool lo_pair = so == 2 * g;      // bins (2g, 2g + 1) <- (o0, o0 + 1)
-                const bool hi_only = so == 2 * g + 1;  // bin 2g + 1 <- o0
-                const bool below = !lo_pair && !hi_only;  // o0 = 2g - 1: bin 2g (bin 8 for g = 0) <- o0 + 1
-                accA = accA + (use && lo_pair ? pv.x : (use && below && g != 0 ? pv.y : 0.f));
-                accB = accB + (use && lo_pair ? pv.y : (use && hi_only ? pv.x : 0.f));
-                accW = accW + (use && below && g == 0 ? pv.y : 0.f);
+            // two per iteration (their LDS reads in flight together) ----
+            auto add = [&](int mt, float4 pv) {
+                const bool prim = (mt >> 14) == g;  // else this lane is the secondary owner (o0 = 2g - 1)
+                accA = accA + (prim ? pv.x : pv.z);
+                accB = accB + (prim ? pv.y : 0.f);
+                accW = accW + (prim ? 0.f : pv.w);
             };
-            // 32-bit halves (samples 0-31, then 32-63: raster order kept),
-            // so the bit scans and clears are single VALU ops.
-#if SIFT_EXACT_WALK32
+            // 32-bit halves (samples 0-31, then 32-63: raster order kept), so
+            // the bit scans and clears are single VALU ops; a missing second
+            // hit reads the zero record (adds +0).
             auto walk = [&](unsigned m, int base) {
                 while (m) {
                     const int s0 = base + __builtin_ctz(m);
                     m &= m - 1;
-                    const bool two = m != 0;
-                    const int s1 = two ? base + __builtin_ctz(m) : s0;
+                    const int s1 = m ? base + __builtin_ctz(m) : 64;
                     m &= m - 1;
                     const int mt0 = meta[s0], mt1 = meta[s1];
-                    const float2 pv0 = *reinterpret_cast<const float2*>(rec + (mt0 & 0xffff) + lane_off);
-                    const float2 pv1 = *reinterpret_cast<const float2*>(rec + (mt1 & 0xffff) + lane_off);
-                    add(mt0, pv0, true);
-                    add(mt1, pv1, two);
+                    const float4 pv0 = *reinterpret_cast<const float4*>(rec + (mt0 & 0x3fff) + lane_off);
+                    const float4 pv1 = *reinterpret_cast<const float4*>(rec + (mt1 & 0x3fff) + lane_off);
+                    add(mt0, pv0);
+                    add(mt1, pv1);
                 }
             };
             walk((unsigned)M, 0);
             walk((unsigned)(M >> 32), 32);
-#else
-            while (M) {
-                const int s0 = __builtin_ctzll(M);
-                M &= M - 1;
-                const bool two = M != 0;
-                const int s1 = two ? __builtin_ctzll(M) : s0;
-                M &= M - 1;
-                const int mt0 = meta[s0], mt1 = meta[s1];
-                const float2 pv0 = *reinterpret_cast<const float2*>(rec + (mt0 & 0xffff) + lane_off);
-                const float2 pv1 = *reinterpret_cast<const float2*>(rec + (mt1 & 0xffff) + lane_off);
-                add(mt0, pv0, true);
-                add(mt1, pv1, two);
-            }
-#endif
             wave_lds_sync();
         }
         // OpenCV's wrap: hist[0] += hist[8] (hist[1] += hist[9] adds +0).

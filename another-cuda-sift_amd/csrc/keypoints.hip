@@ -570,9 +570,6 @@ void launch_bucket_scatter(const OriKpt* kpts, const Counters* ctr, const unsign
 // the counts), and order[].  Used when the buckets fit in LDS
 // (kOrderMaxBuckets); the four kernels above remain for larger pyramids.
 // ---------------------------------------------------------------------------
-#ifndef SIFT_ORDER_REGSEL
-#define SIFT_ORDER_REGSEL 1  // radix select over the register copy of the responses
-#endif
 __global__ __launch_bounds__(1024) void k_order(const OriKpt* __restrict__ kpts, Counters* __restrict__ ctr,
                                                 unsigned* __restrict__ zero_range, unsigned* __restrict__ bcount,
                                                 unsigned* __restrict__ boff, int* __restrict__ slot,
@@ -598,20 +595,6 @@ __global__ __launch_bounds__(1024) void k_order(const OriKpt* __restrict__ kpts,
         s_k = (unsigned)kp.numFeatures;
     }
     __syncthreads();
-    // Up to kOrderRegs * 1024 entries (a frame's usual count) are loaded once
-    // into registers -- one 16-byte load of {response, octave, bucket, sub}
-    // per entry -- and serve the radix select's passes, the counts and the
-    // scatter below; larger lists are re-read from memory (slot[] round trip).
-    constexpr int kOrderRegs = 8;
-    static_assert(sizeof(OriKpt) == 32 && offsetof(OriKpt, response) == 16 && offsetof(OriKpt, bucket) == 24,
-                  "k_order reads {response, octave, bucket, sub} as the entry's second float4");
-    const bool inreg = n <= kOrderRegs * 1024u;
-    float4 q[kOrderRegs];
-    if (inreg) {
-        const float4* kq = reinterpret_cast<const float4*>(kpts);
-#pragma unroll
-        for (int u = 0; u < kOrderRegs; u++) q[u] = kq[2 * min(tid + 1024u * u, n - 1) + 1];
-    }
     // retainBest threshold (k_select's radix select)
     const bool sel = kp.numFeatures > 0 && n > (unsigned)kp.numFeatures;
     if (sel) {
@@ -620,17 +603,9 @@ __global__ __launch_bounds__(1024) void k_order(const OriKpt* __restrict__ kpts,
             for (int i = tid; i < 256; i += 1024) hist[i] = 0;
             __syncthreads();
             const unsigned prefix = s_prefix;
-            if (SIFT_ORDER_REGSEL && inreg) {
-#pragma unroll
-                for (int u = 0; u < kOrderRegs; u++) {
-                    const unsigned b = __float_as_uint(q[u].x);
-                    if (tid + 1024u * u < n && (b & pmask) == prefix) atomicAdd(&hist[(b >> shift) & 255u], 1u);
-                }
-            } else {
-                for (unsigned i = tid; i < n; i += 1024) {
-                    const unsigned b = __float_as_uint(kpts[i].response);
-                    if ((b & pmask) == prefix) atomicAdd(&hist[(b >> shift) & 255u], 1u);
-                }
+            for (unsigned i = tid; i < n; i += 1024) {
+                const unsigned b = __float_as_uint(kpts[i].response);
+                if ((b & pmask) == prefix) atomicAdd(&hist[(b >> shift) & 255u], 1u);
             }
             __syncthreads();
             if (tid < 64) {
@@ -650,8 +625,20 @@ __global__ __launch_bounds__(1024) void k_order(const OriKpt* __restrict__ kpts,
     if (tid == 0) ctr->thr_bits = thr_bits;
     const float thr = __uint_as_float(thr_bits);
     // counts (the slot order inside a bucket is re-ranked by k_bucket_rank).
+    // Up to kOrderRegs * 1024 entries (a frame's usual count) keep their
+    // bucket and slot in registers for the scatter below (one 16-byte load
+    // of {response, octave, bucket, sub} per entry, no slot[] round trip);
+    // larger lists go through slot[], four entries' loads in flight.
+    constexpr int kOrderRegs = 8;
+    static_assert(sizeof(OriKpt) == 32 && offsetof(OriKpt, response) == 16 && offsetof(OriKpt, bucket) == 24,
+                  "k_order reads {response, octave, bucket, sub} as the entry's second float4");
+    const bool inreg = n <= kOrderRegs * 1024u;
     int rbk[kOrderRegs], rsl[kOrderRegs];
     if (inreg) {
+        float4 q[kOrderRegs];
+        const float4* kq = reinterpret_cast<const float4*>(kpts);
+#pragma unroll
+        for (int u = 0; u < kOrderRegs; u++) q[u] = kq[2 * min(tid + 1024u * u, n - 1) + 1];
 #pragma unroll
         for (int u = 0; u < kOrderRegs; u++) {
             const unsigned i = tid + 1024u * u;
