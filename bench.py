@@ -615,6 +615,38 @@ def main():
     single = max_over_ranks(time.perf_counter() - t)
     single_value = world * n1 * W * H / 1e6 / single
 
+    # The C2 step with the exact descriptor mode (SIFT_HIP_DESC_EXACT: OpenCV's
+    # sequential float histogram, descriptors bit-identical to the oracle):
+    # its cost next to the default fixed-point mode (value above).
+    detx = [sift.Detector(cfg, device=local, batch=B, exact_descriptors=True) for _ in range(nstreams)]
+    for d in detx:
+        d.gpuWarmUpAndAllocate()
+
+    def stepx(s):
+        d = detx[s % len(detx)]
+        if B == 1:
+            d.detectAndComputeDevice(frames[s % nframes].data_ptr(), stride, sync=False)
+        else:
+            d.detectBatchDevice(fb.data_ptr(), B, stride, W * H * 4, sync=False)
+
+    nx = max(a.steps // 4, 1)
+    for s in range(2 * len(detx)):
+        stepx(s)
+    for d in detx:
+        d.sync()
+    barrier()
+    t = time.perf_counter()
+    for s in range(nx):
+        stepx(s)
+    for d in detx:
+        d.sync()
+    exact_t = max_over_ranks(time.perf_counter() - t)
+    exact_leg = {"value": round(world * nx * B * W * H / 1e6 / exact_t, 2), "unit": "Mpix/s",
+                 "ms_per_frame": round(exact_t / (nx * B) * 1e3, 4), "steps": nx,
+                 "note": "same C2 steps with sift_hip_set_descriptor_mode(SIFT_HIP_DESC_EXACT): descriptors "
+                         "bit-identical to the oracle (tests/test_gpu_parity.py::test_exact_descriptors_bitexact)"}
+    del detx
+
     # ---- C4: 256 synthetic 1600x900 frames sharded per image over the ranks -------
     W4, H4, N4 = 1600, 900, 256
     mine4 = multi.frame_shard(N4, rank, world)
@@ -890,6 +922,7 @@ def main():
             "pipeline_hbm_frac": round(88.0 * sum_px / (ms_per_frame / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             "sync_ms_per_frame": round(sync_ms, 4),
             "single_stream": {"value": round(single_value, 2), "ms_per_frame": round(single / n1 * 1e3, 4)},
+            "exact_descriptors": exact_leg,
             "host_input": host_input,
             "stage_us_per_frame_eager": stages,
             "stage_sum_us_eager": round(total_ms / nt * 1e3, 1),
