@@ -6,8 +6,11 @@
 // no input row is read twice vertically inside a segment.  Same arithmetic as
 // the product (pyramid.hip header comment): outputs compared bit for bit.
 //
-//   make -C tools blur_strip_ab   (or the hipcc line in tools/Makefile)
-//   tools/blur_strip_ab > gpurun_out/blur_strip_ab.jsonl       (GPU box)
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off \
+//     -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -Ianother-cuda-sift_amd/csrc \
+//     tools/blur_strip_ab.hip -Lanother-cuda-sift_amd/lib -lsift_hip \
+//     -Wl,-rpath,'$ORIGIN/../another-cuda-sift_amd/lib' -o tools/blur_strip_ab     (here, after make)
+//   tools/blur_strip_ab > gpurun_out/blur_strip_ab.jsonl                           (GPU box)
 //
 // One JSON line per (radius, kernel): us per 16-frame 1920x1200 launch, the
 // algorithmic 8 B/px rate, and whether the planes equal the product's.
