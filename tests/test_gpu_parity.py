@@ -221,17 +221,22 @@ def test_prev_descriptor_is_previous_frame(sift):
     del prev
 
 
-def test_blank_and_tiny_images(sift, oracle):
+@pytest.mark.parametrize("exact", [False, True])
+def test_blank_and_tiny_images(sift, oracle, exact):
+    """No keypoints on a flat frame; tiny frames (windows clipped by every
+    border) match the oracle -- descriptors byte for byte in the exact mode."""
     for (w, h, up) in [(64, 48, False), (33, 17, True), (128, 128, False)]:
         img = np.full((h, w), 128.0, np.float32)
-        cfg, det = make_detector(sift, w, h, upscale=up)
+        cfg, det = make_detector(sift, w, h, exact_descriptors=exact, upscale=up)
         det.detectAndCompute(img)
         assert det.total_size == 0
         img = sift.synth_frame(9, w, h)
         det.detectAndCompute(img)
-        gk, _, _ = gpu_keypoints(det)
-        ok, _ = oracle.detect_and_compute(img, oracle.from_config(cfg))
+        gk, gd, _ = gpu_keypoints(det)
+        ok, od = oracle.detect_and_compute(img, oracle.from_config(cfg))
         assert_same_keypoints(gk, ok)
+        if exact:
+            assert np.array_equal(gd[sort_keys(gk)], od[sort_keys(ok)])
 
 
 def test_size_mismatch_rejected(sift):
