@@ -52,14 +52,16 @@ def test_stage_check_cli(sift, tmp_path):
     assert json.loads(r.stdout)["oracle"]["keypoints_bitexact"]
 
 
-@pytest.mark.parametrize("w,h,upscale", [(400, 300, False), (257, 191, True)])
-def test_stage_replay_each_stage(sift, tmp_path, w, h, upscale):
+@pytest.mark.parametrize("w,h,upscale,exact", [(400, 300, False, False), (257, 191, True, False),
+                                              (400, 300, False, True)])
+def test_stage_replay_each_stage(sift, tmp_path, w, h, upscale, exact):
     """Per-stage replay (tool/perf.cu:43-100): every stage's kernels alone on
     the dump's recorded input reproduce the dump's output of that stage bit for
     bit (as record sets where the device appends with atomics); the handle then
-    detects normally again."""
+    detects normally again.  Also with the exact descriptor mode (the replayed
+    descriptor stage is the exact kernel)."""
     cfg = sift.CudaSiftConfig(col_width=w, row_width=h, upscale=upscale, numFeatures=0)
-    det = sift.Detector(cfg, device=0)
+    det = sift.Detector(cfg, device=0, exact_descriptors=exact)
     det.gpuWarmUpAndAllocate()
     dump = str(tmp_path / "dump")
     det.setDataGen(dump)
