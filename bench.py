@@ -76,6 +76,8 @@ def parse():
                          "rocprofv3 --kernel-trace --stats summary is committed beside the roofline numbers")
     ap.add_argument("--traffic-summary", default=os.path.join(ROOT, "profiles", "round4", "pmc_summary.json"),
                     help="PMC summary (tools/pmc_summary.py) with FETCH_SIZE/WRITE_SIZE of this code")
+    ap.add_argument("--exact-descriptors", action="store_true",
+                    help="run the C2 steps in the exact descriptor mode (SIFT_HIP_DESC_EXACT) instead of the default")
     ap.add_argument("--allow-ab-build", action="store_true",
                     help="run on a library built with A/B or instrumentation macros (never for reported numbers)")
     ap.add_argument("--launcher-selftest", action="store_true",
@@ -555,7 +557,7 @@ def main():
     # is still one complete frame.
     B = max(a.batch, 1)
     nstreams = 1 if a.roofline_only else a.streams
-    dets = [sift.Detector(cfg, device=local, batch=B) for _ in range(nstreams)]
+    dets = [sift.Detector(cfg, device=local, batch=B, exact_descriptors=a.exact_descriptors) for _ in range(nstreams)]
     for d in dets:
         d.gpuWarmUpAndAllocate()
     det = dets[0]
@@ -913,6 +915,7 @@ def main():
                 "frames_per_launch": B,
                 "streams_per_gpu": a.streams,
                 "parallelism": f"frame-sharded x{world}, no data-path collective",
+                "descriptor_mode": "exact" if a.exact_descriptors else "fixed-point (default)",
                 "keypoints_per_frame": kcount,
             },
             "roofline": rl["roofline"],
