@@ -496,9 +496,10 @@ __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* _
 //     consecutive samples (raster order), one per lane;
 //   * phase 1: each lane computes its sample with the oracle's correctly
 //     rounded math (cv_exp32f table exp, fastAtan2 with IEEE division,
-//     magnitude with IEEE sqrt), writes its 8 contributions and its
-//     (r0, c0, o0) to LDS, and 12 ballots give, per interior cell row, cell
-//     column and orientation pair, the samples that touch it;
+//     magnitude with IEEE sqrt), writes per target cell the float4 its owner
+//     lanes add ({P, S}, below) and a 16-bit (record base, o0 >> 1) word to
+//     LDS, and 12 ballots give, per interior cell row, cell column and
+//     orientation pair, the samples that touch it;
 //   * phase 2: lane = (cell 0..15, orientation pair g 0..3) ANDs its three
 //     masks and walks the set bits in ascending order (= raster order), adding
 //     into its bins 2g, 2g+1 (and bin 8 for g = 0, wrapped into bin 0 at the
