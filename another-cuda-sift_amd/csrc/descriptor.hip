@@ -509,6 +509,9 @@ __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* _
 // Waves per workgroup, each on its own keypoints with private LDS (no
 // workgroup barrier inside the keypoint loop).
 constexpr int kExactWaves = 4;
+// Hits per walk step (their LDS reads in flight together): 2, 3, 4 measured
+// 0.158 / 0.157 / 0.160 ms per frame (profiles/round4/exact_ab_hits*.jsonl).
+constexpr int kExactHits = 2;
 constexpr int kZeroRec = 40;  // zero floats after the 64 records (absent second hit of a walk step)
 constexpr int kExactWG = 64 * kExactWaves;
 // Orders one wave's LDS writes before its later LDS reads by other lanes (LDS
@@ -780,15 +783,21 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
             // hit reads the zero record (adds +0).
             auto walk = [&](unsigned m, int base) {
                 while (m) {
-                    const int s0 = base + __builtin_ctz(m);
-                    m &= m - 1;
-                    const int s1 = m ? base + __builtin_ctz(m) : 64;
-                    m &= m - 1;
-                    const int mt0 = meta[s0], mt1 = meta[s1];
-                    const float4 pv0 = *reinterpret_cast<const float4*>(rec + (mt0 & 0x3fff) + lane_off);
-                    const float4 pv1 = *reinterpret_cast<const float4*>(rec + (mt1 & 0x3fff) + lane_off);
-                    add(mt0, pv0);
-                    add(mt1, pv1);
+                    int sx[kExactHits];
+#pragma unroll
+                    for (int h = 0; h < kExactHits; h++) {
+                        sx[h] = m ? base + __builtin_ctz(m) : 64;
+                        m &= m - 1;
+                    }
+                    int mt[kExactHits];
+#pragma unroll
+                    for (int h = 0; h < kExactHits; h++) mt[h] = meta[sx[h]];
+                    float4 pv[kExactHits];
+#pragma unroll
+                    for (int h = 0; h < kExactHits; h++)
+                        pv[h] = *reinterpret_cast<const float4*>(rec + (mt[h] & 0x3fff) + lane_off);
+#pragma unroll
+                    for (int h = 0; h < kExactHits; h++) add(mt[h], pv[h]);
                 }
             };
             walk((unsigned)M, 0);
