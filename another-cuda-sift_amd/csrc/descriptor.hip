@@ -512,6 +512,11 @@ constexpr int kExactWaves = 4;
 // Hits per walk step (their LDS reads in flight together): 2, 3, 4 measured
 // 0.158 / 0.157 / 0.160 ms per frame (profiles/round4/exact_ab_hits*.jsonl).
 constexpr int kExactHits = 2;
+// Floats per sample record (its 4 float4s).  The walk's record reads run at
+// LDS bank conflicts ~1.1x their active cycles (tools/exact_pmc.sh); padded
+// strides 20 / 24: 0.157 / 0.158 vs 0.159 ms per frame, within box noise.
+constexpr int kRecStride = 16;
+static_assert(kRecStride % 4 == 0 && 64 * kRecStride + 64 < (1 << 14), "record bases in 14 bits, float4-aligned");
 constexpr int kZeroRec = 40;  // zero floats after the 64 records (absent second hit of a walk step)
 constexpr int kExactWG = 64 * kExactWaves;
 // Orders one wave's LDS writes before its later LDS reads by other lanes (LDS
@@ -545,7 +550,7 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
     __shared__ float s_tab[64];
     // Chunk sample s: per target cell (dr, dc) one float4 {P.x, P.y, S.x, S.y}
     // (below), at s*16 + (dr*2 + dc)*4; then a zero record for absent hits.
-    __shared__ __attribute__((aligned(16))) float s_rec[kExactWaves][64 * 16 + kZeroRec];
+    __shared__ __attribute__((aligned(16))) float s_rec[kExactWaves][64 * kRecStride + kZeroRec];
     // 16-bit / 8-bit tables and the epilogue's raw[] and fetch's row map
     // inside the records (dead at those points): 4.8 KB per wave, 8 waves/SIMD.
     __shared__ unsigned short s_meta[kExactWaves][65];  // record base | (o0 >> 1) << 14 (below); [64]: the zero record
@@ -573,8 +578,8 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
         reinterpret_cast<unsigned*>(host_ctr)[threadIdx.x] = reinterpret_cast<const unsigned*>(ctr)[threadIdx.x];
     if (wg * kExactWaves >= n) return;  // workgroup-uniform
     if (w == 0) s_tab[lane] = c_desc_exptab[lane];
-    if (lane < kZeroRec) rec[64 * 16 + lane] = 0.f;
-    if (lane == 0) meta[64] = 64 * 16 + 64;  // + any lane offset (-64 .. -28) lands in the zero floats
+    if (lane < kZeroRec) rec[64 * kRecStride + lane] = 0.f;
+    if (lane == 0) meta[64] = 64 * kRecStride + 64;  // + any lane offset (-64 .. -28) lands in the zero floats
     lds_barrier();
     const float bins_per_rad = kN / 360.f;
     const float exp_scale = -1.f / (kD * kD * 0.5f);
@@ -732,7 +737,7 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
             //   o0 odd:    P = (0, v_o0),      S = (v_o0+1, 0)
             //   o0 = 7:    P = (0, v_7),       S = (0, v_8)   (bin 8: g = 0's third bin)
             const bool odd = o0 & 1, seven = o0 == kN - 1;
-            float4* rp = reinterpret_cast<float4*>(rec + lane * 16);
+            float4* rp = reinterpret_cast<float4*>(rec + lane * kRecStride);
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 const float x = v[2 * q], y = v[2 * q + 1];
@@ -741,7 +746,7 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
             // Owner lane (ci, cj) reads the float4 of (dr, dc) = (ci - r0, cj - c0)
             // at lane*16 + dr*8 + dc*4 = base - 64 + ci*8 + cj*4 (base >= 28 for
             // valid samples: r0, c0 <= 3); o0 >> 1 in bits 14-15.
-            meta[lane] = (unsigned short)((lane * 16 + 64 - r0 * 8 - c0 * 4) | (o0 >> 1) << 14);
+            meta[lane] = (unsigned short)((lane * kRecStride + 64 - r0 * 8 - c0 * 4) | (o0 >> 1) << 14);
             // Samples touching interior cell row / column q (r0 in {q - 1, q})
             // and orientation pair q (o0 in {2q - 1 mod 8, 2q, 2q + 1}).
             // Plain compares (an invalid sample's row 64 touches no cell), so
