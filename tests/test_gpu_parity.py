@@ -435,6 +435,10 @@ def test_cpp_tools(sift):
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
     assert p.stdout == r.stdout
+    # the exact descriptor mode through the C++ surface (setExactDescriptors)
+    x = subprocess.run([os.path.join(lib, "extract_and_match_example"), "--frames", "3", "--exact"],
+                       capture_output=True, text=True, timeout=300)
+    assert x.returncode == 0, x.stdout + x.stderr
 
 
 def test_match_batched_c5_size(sift, oracle):

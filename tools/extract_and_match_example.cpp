@@ -4,7 +4,8 @@
 // copies shifted by (k*dx, k*dy) pixels, so good matches must agree with the shift.
 // --pipelined: 8-bit frames through Detector::submit / wait, frame f+1 staged
 // and uploaded while frame f computes; prints the same lines as the default
-// synchronous Imagef loop.
+// synchronous Imagef loop.  --exact: Detector::setExactDescriptors(true)
+// (OpenCV's descriptor bytes, sift_hip_set_descriptor_mode).
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -15,10 +16,11 @@
 
 int main(int argc, char** argv) {
     int W = 752, H = 480, frames = 4, dx = 3, dy = 2;
-    bool pipelined = false;
+    bool pipelined = false, exact = false;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         if (a == "--pipelined") pipelined = true;
+        else if (a == "--exact") exact = true;
         else if (a == "--width" && i + 1 < argc) W = std::atoi(argv[++i]);
         else if (a == "--height" && i + 1 < argc) H = std::atoi(argv[++i]);
         else if (a == "--frames" && i + 1 < argc) frames = std::atoi(argv[++i]);
@@ -33,6 +35,7 @@ int main(int argc, char** argv) {
     config.col_width = W;
     config.row_width = H;
     sift_cuda::Detector detector(config);
+    if (exact) detector.setExactDescriptors(true);  // before the warm-up: part of the captured graphs
     detector.gpuWarmUpAndAllocate();
     int prev_size = 0;
     std::vector<sift_cuda::Float3> prev_kpts;
