@@ -25,7 +25,8 @@ void check(int rc, const char* what) {
 
 class HipFrameWorker : public FrameWorker {
 public:
-    HipFrameWorker(const CudaSiftConfig& config, int device) : m_device(device), m_det(config, device) {
+    HipFrameWorker(const CudaSiftConfig& config, int device, bool exact) : m_device(device), m_det(config, device) {
+        if (exact) m_det.setExactDescriptors(true);  // before the warm-up (captured graphs)
         m_det.gpuWarmUpAndAllocate();
     }
     int device() const override { return m_device; }
@@ -52,8 +53,8 @@ std::vector<int> shardFrames(int frames, int w, int n) {
     return out;
 }
 
-MultiDetector::MultiDetector(const CudaSiftConfig& config, const std::vector<int>& devices) {
-    for (int d : devices) m_workers.emplace_back(new HipFrameWorker(config, d));
+MultiDetector::MultiDetector(const CudaSiftConfig& config, const std::vector<int>& devices, bool exactDescriptors) {
+    for (int d : devices) m_workers.emplace_back(new HipFrameWorker(config, d, exactDescriptors));
 }
 
 MultiDetector::MultiDetector(std::vector<std::unique_ptr<FrameWorker>> workers) : m_workers(std::move(workers)) {}

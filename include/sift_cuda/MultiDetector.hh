@@ -47,8 +47,9 @@ std::vector<int> shardFrames(int frames, int w, int n);
 class MultiDetector {
 public:
     // One sift_cuda::Detector per entry of `devices` (a device may repeat: several
-    // detectors, i.e. HIP streams, on one GPU).
-    MultiDetector(const CudaSiftConfig& config, const std::vector<int>& devices);
+    // detectors, i.e. HIP streams, on one GPU); exactDescriptors: every detector
+    // in the exact descriptor mode (Detector::setExactDescriptors).
+    MultiDetector(const CudaSiftConfig& config, const std::vector<int>& devices, bool exactDescriptors = false);
     explicit MultiDetector(std::vector<std::unique_ptr<FrameWorker>> workers);
     ~MultiDetector();
     MultiDetector(const MultiDetector&) = delete;
