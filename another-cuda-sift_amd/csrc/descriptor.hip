@@ -676,6 +676,10 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
                     }
                     wave_lds_sync();
                     row = wave_incl_max(rowmap[lane]);
+                    // rowmap aliases the float records of rec[]: keep the
+                    // record stores that follow from being scheduled above
+                    // this int read (TBAA would allow it).
+                    wave_lds_sync();
                 } else {
                     row = row_search(min(kf + lane, N - 1));
                 }

@@ -387,7 +387,17 @@ int allocate(sift_hip_detector* d) {
     HIPCHK(hipSetDevice(d->device));
     HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     d->allocated = true;
-    HIPCHK(tail_init());
+    // The pyramid tail is an optimisation: without the LDS it asks for (a
+    // device whose opt-in limit is lower, or a refused attribute) the small
+    // octaves take the per-plane blur launches instead.
+    if (d->tailOct < d->nOct) {
+        int optin = 0;
+        if (hipDeviceGetAttribute(&optin, hipDeviceAttributeSharedMemPerBlockOptin, d->device) != hipSuccess ||
+            optin < (int)(sizeof(float) * kTailLdsFloats) || tail_init() != hipSuccess) {
+            (void)hipGetLastError();
+            d->tailOct = d->nOct;
+        }
+    }
     HIPCHK(hipEventCreateWithFlags(&d->evIn, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&d->evOut, hipEventDisableTiming));
     const int W = d->cfg.col_width, H = d->cfg.row_width;
@@ -769,6 +779,14 @@ int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEven
                         : nf == d->B                                 ? d->execH[slot]
                         : nf == 1                                    ? d->execH1[slot]
                                                                      : nullptr;
+    // The head node of execH[slot] is re-pointed only once that exec's last
+    // launch (frame f - kSlots, whose completion evFrame[slot] still records)
+    // has finished: a queued launch never sees its kernel arguments change.
+    // Otherwise the frame takes the separate head launch and the plain exec.
+    if (gh && hipEventQuery(d->evFrame[slot]) != hipSuccess) {
+        (void)hipGetLastError();  // hipErrorNotReady
+        gh = nullptr;
+    }
     if (gh) {  // device f32 input: one launch for the whole frame, the head re-pointed at img
         HeadNode& h = d->headNode;
         head_node(d, h, static_cast<const float*>(img), pitch, slot & 1, nf, sfs);

@@ -82,6 +82,21 @@ void Detector::refreshViews() {
     device_descriptor = DeviceBuffer<Half>(reinterpret_cast<Half*>(const_cast<uint16_t*>(desc)), (size_t)cap * 128);
     prev_descriptor = DeviceBuffer<Half>(reinterpret_cast<Half*>(const_cast<uint16_t*>(prev)), (size_t)cap * 128);
     sift_hip_num_keypoints(m_handle, &total_size);
+    warnOverflow();
+}
+
+// A stage that hit its capacity (sift_hip_capacities) clamps and sets a bit:
+// results may then be missing keypoints the reference would keep.  Reported
+// on stderr once per detector and flag set (maxKeypoints raises the limit).
+void Detector::warnOverflow() {
+    int flags = 0;
+    if (!m_handle || sift_hip_overflow_flags(m_handle, &flags) != SIFT_HIP_OK || !flags) return;
+    if ((flags & ~m_overflowWarned) == 0) return;
+    m_overflowWarned |= flags;
+    std::fprintf(stderr,
+                 "sift_cuda::Detector: capacity overflow (flags 0x%x: 1 candidates, 2 refined, 4 oriented, "
+                 "8 results); keypoints were dropped -- raise CudaSiftConfig::maxKeypoints\n",
+                 flags);
 }
 
 void Detector::detectAndCompute(const Imagef& image) {

@@ -510,6 +510,7 @@ __global__ __launch_bounds__(64 * NW, (kMatchWgPerCu * NW) / 4) void k_match_sin
     __shared__ __attribute__((aligned(16))) int s_key[2][kChunkRows];
     __shared__ unsigned s_last;
     static_assert(sizeof(Top2) * QB <= sizeof(s_codes), "results alias the code tiles");
+    static_assert(QB <= NT, "the write-out gives each thread one query: at most 2 query blocks per wave");
     Top2* const s_res = reinterpret_cast<Top2*>(&s_codes[0][0]);
     const int q0 = blockIdx.x * QB;
     if (q0 >= pr.nq) return;
@@ -616,6 +617,7 @@ __global__ __launch_bounds__(64 * NW, (kMatchBatchWgPerCu * NW) / 4) void k_matc
     unsigned* __restrict__ done, float ratio, int ratio_on_squared, int* __restrict__ idx2, float* __restrict__ d2out,
     int* __restrict__ match) {
     constexpr int QB = 32 * QBW * NW;  // queries per workgroup
+    static_assert(QB <= 64 * NW, "the write-out gives each thread one query: at most 2 query blocks per wave");
     __shared__ __attribute__((aligned(16))) int8_t s_codes[2][kChunkTiles * kTileBytes];
     __shared__ __attribute__((aligned(16))) int s_key[2][kChunkRows];
     __shared__ unsigned s_last;

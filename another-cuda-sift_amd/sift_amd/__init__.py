@@ -21,6 +21,7 @@ import ctypes
 import importlib.util
 import os
 import sys
+import warnings
 from dataclasses import dataclass
 from typing import Optional, Sequence
 
@@ -39,6 +40,10 @@ _lib = None
 
 class SiftHipError(RuntimeError):
     pass
+
+
+class SiftCapacityWarning(RuntimeWarning):
+    """A per-frame capacity (candidates, refined, oriented, results) overflowed; see overflow_flags()."""
 
 
 class _Config(ctypes.Structure):
@@ -272,6 +277,17 @@ class Detector:
         n = ctypes.c_int()
         lib().sift_hip_num_keypoints(self._h, ctypes.byref(n))
         self.total_size = n.value
+        self._warn_overflow()
+
+    def _warn_overflow(self) -> None:
+        """A stage that hit its capacity clamps and sets a bit (keypoints the reference would keep are
+        dropped): warned once per detector and flag (SiftCapacityWarning)."""
+        flags = self.overflow_flags()
+        new = flags & ~getattr(self, "_overflow_warned", 0)
+        if new:
+            self._overflow_warned = getattr(self, "_overflow_warned", 0) | flags
+            warnings.warn(f"capacity overflow (flags {flags:#x}: 1 candidates, 2 refined, 4 oriented, 8 results); "
+                          f"keypoints were dropped -- raise CudaSiftConfig.maxKeypoints", SiftCapacityWarning, stacklevel=3)
 
     def _host_frame(self, image: np.ndarray):
         """(array, format): uint8 frames stay 8-bit (Image8U); anything else is float32 (Imagef)."""

@@ -79,10 +79,12 @@ public:
 
 private:
     void refreshViews();
+    void warnOverflow();
     CudaSiftConfig m_config{};
     sift_hip_detector* m_handle{nullptr};
     bool m_initialized{false};
     int m_nOctaves{0};
+    int m_overflowWarned{0};  // overflow flags already reported on stderr
     std::string m_debug_path;
 };
 

@@ -560,3 +560,51 @@ def ctypes_count(sift, det):
     n = ctypes.c_int()
     sift._check(sift.lib().sift_hip_num_keypoints(det.handle, ctypes.byref(n)), "num_keypoints")
     return n.value
+
+
+def tiled_frame(seed, w=320, h=240, period=16):
+    """A smoothed random 16x16 tile repeated over the frame: translated copies
+    of one pattern give large groups of keypoints with identical responses
+    (retainBest keeps every keypoint tied at the n-th response)."""
+    from scipy.ndimage import gaussian_filter
+
+    rng = np.random.default_rng(seed)
+    t = gaussian_filter(rng.integers(0, 256, (period, period)).astype(np.float32), 1.5, mode="wrap")
+    t = (t - t.min()) / (t.max() - t.min()) * 255
+    return np.ascontiguousarray(np.round(np.tile(t, (h // period, w // period))).astype(np.float32))
+
+
+@pytest.mark.parametrize("seed,nfeat", [(0, 500), (1, 500), (1, 2000), (2, 0)])
+def test_dense_ties_no_overflow(sift, oracle, seed, nfeat):
+    """Default capacities on a tie-heavy dense texture (25 distinct responses
+    among ~1,700 keypoints; with nfeat 2000, 2,469 kept against a result
+    capacity of 2,512): no stage overflows and the results are the oracle's."""
+    img = tiled_frame(seed)
+    h, w = img.shape
+    cfg, det = make_detector(sift, w, h, upscale=True, numFeatures=nfeat)
+    det.detectAndCompute(img)
+    assert det.overflow_flags() == 0
+    gk, gd, _ = gpu_keypoints(det)
+    ok, od = oracle.detect_and_compute(img, oracle.from_config(cfg))
+    assert_same_keypoints(gk, ok)
+    if nfeat:
+        assert len(np.unique(ok["response"])) < len(ok) // 10, "the fixture should be tie-heavy"
+    gi, oi = sort_keys(gk), sort_keys(ok)
+    assert_descriptor_bar(gd[gi], od[oi], f"tiled seed {seed} nfeat {nfeat}")
+
+
+def test_overflow_warns(sift):
+    """A result capacity below the frame's keypoints: the overflow bit is set
+    and the wrapper warns (SiftCapacityWarning), once per detector and flag."""
+    import warnings
+
+    img = sift.synth_frame(0, 320, 240)
+    cfg, det = make_detector(sift, 320, 240, upscale=True, numFeatures=0, maxKeypoints=64)
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        det.detectAndCompute(img)
+        det.detectAndCompute(img)
+    assert det.overflow_flags() & 8
+    assert det.total_size == 64
+    hits = [r for r in rec if issubclass(r.category, sift.SiftCapacityWarning)]
+    assert len(hits) == 1, [str(r.message) for r in rec]
