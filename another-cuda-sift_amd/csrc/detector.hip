@@ -14,9 +14,13 @@
 #include <algorithm>
 #include <cerrno>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "sift_hip.h"
@@ -82,6 +86,81 @@ const char* build_flags() {
 #endif
 }
 
+// Host copies of large frames split over a few persistent threads (the
+// staging copy of a host frame: one thread moves ~10 GB/s, a 1920x1200 f32
+// frame is 9.2 MB).  run(parts, fn) calls fn(0..parts-1), part 0 on the
+// calling thread, and returns when every part is done.
+class CopyPool {
+public:
+    explicit CopyPool(int workers) {
+        for (int i = 0; i < workers; i++) th_.emplace_back([this, i] { loop(i + 1); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    int parts() const { return (int)th_.size() + 1; }
+    void run(const std::function<void(int)>& fn) {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            fn_ = &fn;
+            pending_ = (int)th_.size();
+            gen_++;
+        }
+        cv_.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> g(m_);
+        done_.wait(g, [this] { return pending_ == 0; });
+        fn_ = nullptr;
+    }
+
+private:
+    void loop(int part) {
+        unsigned long long seen = 0;
+        for (;;) {
+            const std::function<void(int)>* fn;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                fn = fn_;
+            }
+            (*fn)(part);
+            std::lock_guard<std::mutex> g(m_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)>* fn_ = nullptr;
+    int pending_ = 0;
+    unsigned long long gen_ = 0;
+    bool stop_ = false;
+};
+
+// Row copy (dst pitch / src stride in bytes), split over the pool when large.
+void copy_rows(CopyPool* pool, char* dst, size_t dpitch, const char* src, size_t sstride, size_t rowB, int rows) {
+    auto part = [&](int lo, int hi) {
+        if (dpitch == sstride && dpitch == rowB) {
+            if (hi > lo) memcpy(dst + dpitch * lo, src + sstride * lo, rowB * (hi - lo));
+        } else {
+            for (int y = lo; y < hi; y++) memcpy(dst + dpitch * y, src + sstride * y, rowB);
+        }
+    };
+    if (!pool || rowB * rows < (1u << 20)) {
+        part(0, rows);
+        return;
+    }
+    const int P = pool->parts();
+    pool->run([&](int k) { part((int)((long)rows * k / P), (int)((long)rows * (k + 1) / P)); });
+}
+
 struct TimingRec {
     int name;
     hipEvent_t e0, e1;
@@ -99,13 +178,58 @@ struct TimingAgg {
 
 void sift_amd::set_last_error(const std::string& msg) { g_err = msg; }
 
+// Results slots per compute lane: frames f-1 .. f+2 of a lane never share one.
+constexpr int kResultSlots = 4;
+constexpr int kMaxLanes = 4;
+constexpr int kFrameRing = 64;  // per-frame (lane, slot) records; far more than can be alive at once
+
+// A compute lane: one HIP stream, its B frame arenas (every per-frame buffer of
+// the pipeline, sift_kernels.h Frames), the graphs captured on them and a ring
+// of kResultSlots results slots.  A lane runs its frames in order; frames on
+// different lanes run concurrently ("Frames in flight").
+struct Lane {
+    hipStream_t stream = nullptr;
+    char* arena = nullptr;
+    Counters* hCtr = nullptr;     // kResultSlots x B pinned host copies of the counters (written by k_descriptor)
+    Counters* hCtrDev = nullptr;  // their device-side address
+    hipEvent_t evFrame[kResultSlots] = {};  // recorded after each slot's last frame
+    hipGraphExec_t exec[kResultSlots] = {};   // B frames per launch
+    hipGraphExec_t exec1[kResultSlots] = {};  // one frame (B > 1 only; exec when B = 1)
+    // The same graphs with the f32 head captured in (device input): the head
+    // node is re-pointed at each frame's image (hipGraphExecKernelNodeSetParams),
+    // so the frame is ONE graph launch -- a separate head launch left ~6 us
+    // between the head and the graph's first kernel on every single frame.
+    hipGraphExec_t execH[kResultSlots] = {}, execH1[kResultSlots] = {};
+    hipGraph_t graphH[kResultSlots] = {}, graphH1[kResultSlots] = {};
+    hipGraphNode_t headH[kResultSlots] = {}, headH1[kResultSlots] = {};
+    int nfOf[kResultSlots] = {};  // frames of the launch group that wrote each slot
+    long long slotFrame[kResultSlots] = {-1, -1, -1, -1};  // the frame whose results each slot holds
+    long long launched = 0;  // launch groups run on this lane; the next takes slot launched % kResultSlots
+    long long last = -1;     // the last frame launched here (-1: none since warm-up)
+    // Host-input frames: results copied to mapped pinned host memory right
+    // after the frame (k_results_to_host), one region per slot (created at the
+    // lane's first host-input frame).
+    char* hRes = nullptr;
+    char* hResDev = nullptr;
+    hipEvent_t evHost[kResultSlots] = {};
+    long long hostFrame[kResultSlots] = {-1, -1, -1, -1};  // the frame each host region holds
+};
+
+// Byte offsets of every per-frame buffer inside a frame arena (the same for
+// every arena of every lane).
+struct ArenaLayout {
+    size_t input = 0, up = 0, pyr = 0, cand = 0, ref = 0, ori = 0, slot = 0, order = 0, jobs = 0, range = 0,
+           bcount = 0, boff = 0, bitmap = 0, ctr = 0;
+    size_t k3[kResultSlots] = {}, f4[kResultSlots] = {}, desc[kResultSlots] = {};
+    size_t octave[kMaxOctaves] = {};  // float offset of each octave's planes inside the pyramid
+};
+
 struct sift_hip_detector {
     sift_hip_config cfg{};
     int device = 0;
     int L = 3, nOct = 0, firstOctave = 0;
     int tailOct = 0;  // first octave of the pyramid-tail launch (nOct: none)
     int baseW = 0, baseH = 0;
-    hipStream_t stream = nullptr;
     // Frame uploads and result downloads.  Created on first use: a stream
     // holds a hardware queue, and device-input callers (several detectors per
     // GPU, one stream each) need none.
@@ -113,28 +237,37 @@ struct sift_hip_detector {
     hipEvent_t evIn = nullptr, evOut = nullptr;
     bool allocated = false;
 
-    // Frames are numbered in submission order.  Frame f writes results slot
-    // f % kSlots; `current` is the frame the result accessors expose (its
-    // predecessor's descriptors are prev_descriptor).  At most two frames may
-    // be in flight past `current`, so frames current-1 .. current+2 never
-    // share a slot.
-    static constexpr int kSlots = 4;
-    static constexpr int kInSlots = 2;  // upload ring (pinned staging + device)
+    // Frames are numbered in submission order.  Frame f runs on lane
+    // frec(f).lane and writes that lane's results slot frec(f).slot; `current`
+    // is the frame the result accessors expose (its predecessor's descriptors
+    // are prev_descriptor).  A frame may take a lane's slot only if the slot
+    // holds no frame from current - 1 on, and at most 2 frames per lane may be
+    // in flight past `current`.
+    static constexpr int kSlots = kResultSlots;
+    Lane lanes[kMaxLanes];
+    int nLanes = 0;    // lanes created (lane 0 at warm-up, more on demand)
+    int maxLanes = 2;  // sift_hip_set_lanes
+    int ln = 0;        // the lane the pointer views below are bound to (bind_lane)
+    int curLane = 0;   // lane of `current`
+    struct FrameRec {
+        int lane = 0, slot = 0;
+    };
+    FrameRec frecs[kFrameRing];
+    FrameRec& frec(long long f) { return frecs[f & (kFrameRing - 1)]; }
+    Lane& lane() { return lanes[ln]; }
     long long submitted = 0, current = -1, firstFrame = 0, uploads = 0;
-    int slot_of(long long f) const { return (int)(f & (kSlots - 1)); }
-    hipEvent_t evFrame[kSlots] = {};                     // recorded after each frame's last kernel
-    void* dIn[kInSlots] = {};                            // uploaded frames (f32 or u8)
-    void* hStage[kInSlots] = {};                         // pinned staging
-    hipEvent_t evUp[kInSlots] = {}, evRead[kInSlots] = {};  // upload done / first kernel done
+    static constexpr int kMaxInSlots = kMaxLanes + 1;
+    int nIn = 2;                                            // upload ring slots: lanes + 1
+    void* dIn[kMaxInSlots] = {};                            // uploaded frames (f32 or u8)
+    void* hStage[kMaxInSlots] = {};                         // pinned staging
+    hipEvent_t evUp[kMaxInSlots] = {}, evRead[kMaxInSlots] = {};  // upload done / first kernel done
 
     // Frame batches: up to B frames per launch (sift_hip_set_batch).  Every
-    // per-frame buffer below lives in frame 0's arena; frame f's copy is at
-    // + f * afs bytes (Frames, sift_kernels.h).  nfOf[slot] = frames of the
-    // launch group that wrote results slot `slot`.
+    // per-frame buffer below lives in frame 0's arena of the bound lane; frame
+    // f's copy is at + f * afs bytes (Frames, sift_kernels.h).
     int B = 1;
     long afs = 0;
-    char* dArena = nullptr;
-    int nfOf[kSlots] = {};
+    ArenaLayout lay;
 
     PyrDesc pyr{};
     Taps initTaps{};
@@ -142,6 +275,8 @@ struct sift_hip_detector {
     float threshold = 1.f;
     KeypointParams kp{};
 
+    // Views of the bound lane (bind_lane): its stream and frame-0 arena pointers.
+    hipStream_t stream = nullptr;
     int inPitch = 0, upPitch = 0;
     float* dInput = nullptr;  // blank warm-up frame; f32 scratch for 8-bit frames at other init radii
     float* dUp = nullptr;
@@ -164,20 +299,13 @@ struct sift_hip_detector {
     float* dKpts3[kSlots] = {};
     float* dFeats4[kSlots] = {};
     uint16_t* dDesc[kSlots] = {};
-    int cur = 0, count = 0, prevCount = 0;  // slot_of(current) and the counts of current, current - 1
+    int cur = 0, count = 0, prevCount = 0;  // frec(current).slot and the counts of current, current - 1
     bool countsValid = true;  // count / prevCount / the slot's host counters read after the frame completed
 
-    hipGraphExec_t exec[kSlots] = {};   // B frames per launch
-    hipGraphExec_t exec1[kSlots] = {};  // one frame (B > 1 only; exec when B = 1)
-    // The same graphs with the f32 head captured in (device input): the head
-    // node is re-pointed at each frame's image (hipGraphExecKernelNodeSetParams),
-    // so the frame is ONE graph launch -- a separate head launch left ~6 us
-    // between the head and the graph's first kernel on every single frame.
-    hipGraphExec_t execH[kSlots] = {}, execH1[kSlots] = {};
-    hipGraph_t graphH[kSlots] = {}, graphH1[kSlots] = {};
-    hipGraphNode_t headH[kSlots] = {}, headH1[kSlots] = {};
     HeadNode headNode{};
     bool useGraph = true;
+
+    CopyPool* pool = nullptr;  // staging copies of large host frames (created at the first one)
 
     // Stage dumps (sift_hip_set_datagen): directory, and a device copy of the
     // frame's input as float (the caller's buffer may change before the dump).
@@ -240,33 +368,36 @@ struct sift_hip_detector {
     ~sift_hip_detector() {
         if (allocated) {
             (void)hipSetDevice(device);
-            for (auto& e : exec)
-                if (e) (void)hipGraphExecDestroy(e);
-            for (auto& e : exec1)
-                if (e) (void)hipGraphExecDestroy(e);
-            for (int k = 0; k < kSlots; k++) {
-                if (execH[k]) (void)hipGraphExecDestroy(execH[k]);
-                if (execH1[k]) (void)hipGraphExecDestroy(execH1[k]);
-                if (graphH[k]) (void)hipGraphDestroy(graphH[k]);
-                if (graphH1[k]) (void)hipGraphDestroy(graphH1[k]);
+            for (int k = 0; k < nLanes; k++) {
+                Lane& L = lanes[k];
+                if (L.stream) (void)hipStreamSynchronize(L.stream);
+                for (int b = 0; b < kSlots; b++) {
+                    for (hipGraphExec_t e : {L.exec[b], L.exec1[b], L.execH[b], L.execH1[b]})
+                        if (e) (void)hipGraphExecDestroy(e);
+                    for (hipGraph_t g : {L.graphH[b], L.graphH1[b]})
+                        if (g) (void)hipGraphDestroy(g);
+                    if (L.evFrame[b]) (void)hipEventDestroy(L.evFrame[b]);
+                }
+                if (L.arena) (void)hipFree(L.arena);
+                if (L.hCtr) (void)hipHostFree(L.hCtr);
+                if (L.hRes) (void)hipHostFree(L.hRes);
+                for (hipEvent_t e : L.evHost)
+                    if (e) (void)hipEventDestroy(e);
+                if (L.stream) (void)hipStreamDestroy(L.stream);
             }
-            if (dArena) (void)hipFree(dArena);
-            for (int k = 0; k < kSlots; k++)
-                if (evFrame[k]) (void)hipEventDestroy(evFrame[k]);
-            for (int k = 0; k < kInSlots; k++) {
+            for (int k = 0; k < kMaxInSlots; k++) {
                 if (dIn[k]) (void)hipFree(dIn[k]);
                 if (hStage[k]) (void)hipHostFree(hStage[k]);
                 if (evUp[k]) (void)hipEventDestroy(evUp[k]);
                 if (evRead[k]) (void)hipEventDestroy(evRead[k]);
             }
-            if (hCtr) (void)hipHostFree(hCtr);
             if (dDg) (void)hipFree(dDg);
             for (auto e : evPool) (void)hipEventDestroy(e);
             if (evIn) (void)hipEventDestroy(evIn);
             if (evOut) (void)hipEventDestroy(evOut);
-            for (hipStream_t st : {stream, copyStream})
-                if (st) (void)hipStreamDestroy(st);
+            if (copyStream) (void)hipStreamDestroy(copyStream);
         }
+        delete pool;
     }
 };
 
@@ -299,7 +430,8 @@ int setup_geometry(sift_hip_detector* d) {
         g.H = H;
         g.pitch = (W + 63) / 64 * 64;
         g.planeStride = (long)g.pitch * H;
-        g.base = reinterpret_cast<float*>(off);  // relocated after allocation
+        g.base = nullptr;  // bound to a lane's arena by bind_lane
+        d->lay.octave[o] = off;
         g.rowBase = rowBase;
         g.bitBase = bitBase;
         off += (size_t)g.planeStride * (d->L + 3);
@@ -383,9 +515,53 @@ int dalloc(T** p, size_t count) {
     return SIFT_HIP_OK;
 }
 
+// Points the handle's buffer views (stream, frame-0 arena pointers, host
+// counters) at lane k.  Every entry point binds the lane it works on: the
+// submitting lane for a new frame, the current frame's lane for accessors.
+void bind_lane(sift_hip_detector* d, int k) {
+    Lane& L = d->lanes[k];
+    const ArenaLayout& a = d->lay;
+    char* A = L.arena;
+    d->ln = k;
+    d->stream = L.stream;
+    d->dInput = reinterpret_cast<float*>(A + a.input);
+    d->dUp = d->firstOctave < 0 ? reinterpret_cast<float*>(A + a.up) : nullptr;
+    d->dPyr = reinterpret_cast<float*>(A + a.pyr);
+    for (int o = 0; o < d->nOct; o++) d->pyr.oct[o].base = d->dPyr + a.octave[o];
+    d->dCand = reinterpret_cast<uint2*>(A + a.cand);
+    d->dRef = reinterpret_cast<RefKpt*>(A + a.ref);
+    d->dOri = reinterpret_cast<OriKpt*>(A + a.ori);
+    d->dSlot = reinterpret_cast<int*>(A + a.slot);
+    d->dOrder = reinterpret_cast<int*>(A + a.order);
+    d->dJobs = reinterpret_cast<DescJob*>(A + a.jobs);
+    d->dRange = reinterpret_cast<unsigned*>(A + a.range);
+    d->dBcount = reinterpret_cast<unsigned*>(A + a.bcount);
+    d->dBoff = reinterpret_cast<unsigned*>(A + a.boff);
+    d->dBitmap = reinterpret_cast<uint32_t*>(A + a.bitmap);
+    d->dCtr = reinterpret_cast<Counters*>(A + a.ctr);
+    for (int b = 0; b < d->kSlots; b++) {
+        d->dKpts3[b] = reinterpret_cast<float*>(A + a.k3[b]);
+        d->dFeats4[b] = reinterpret_cast<float*>(A + a.f4[b]);
+        d->dDesc[b] = reinterpret_cast<uint16_t*>(A + a.desc[b]);
+    }
+    d->hCtr = L.hCtr;
+    d->hCtrDev = L.hCtrDev;
+}
+
+// Results of frame f (lane and slot from its record), without binding.
+const uint16_t* frame_desc(const sift_hip_detector* d, long long f) {
+    const auto& r = d->frecs[f & (kFrameRing - 1)];
+    return reinterpret_cast<const uint16_t*>(d->lanes[r.lane].arena + d->lay.desc[r.slot]);
+}
+const Counters& frame_counters(const sift_hip_detector* d, long long f, int i = 0) {
+    const auto& r = d->frecs[f & (kFrameRing - 1)];
+    return d->lanes[r.lane].hCtr[(size_t)r.slot * d->B + i];
+}
+
+// Per-handle allocations shared by the lanes: the upload ring and the frame
+// arena layout (the lanes themselves: add_lane).
 int allocate(sift_hip_detector* d) {
     HIPCHK(hipSetDevice(d->device));
-    HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     d->allocated = true;
     // The pyramid tail is an optimisation: without the LDS it asks for (a
     // device whose opt-in limit is lower, or a refused attribute) the small
@@ -402,21 +578,16 @@ int allocate(sift_hip_detector* d) {
     HIPCHK(hipEventCreateWithFlags(&d->evOut, hipEventDisableTiming));
     const int W = d->cfg.col_width, H = d->cfg.row_width;
     d->inPitch = (W + 63) / 64 * 64;
-    // Upload ring (host input path, one frame at a time): sized for f32 rows
-    // of pitch inPitch (an 8-bit frame uses the first quarter with a byte
-    // pitch of inPitch).
+    // Upload ring (host input path): one slot per lane + 1, sized for f32
+    // rows of pitch inPitch (an 8-bit frame uses the first quarter with a
+    // byte pitch of inPitch).
+    d->nIn = d->maxLanes + 1;
     const size_t inBytes = sizeof(float) * (size_t)d->inPitch * H;
-    for (int k = 0; k < d->kInSlots; k++) {
+    for (int k = 0; k < d->nIn; k++) {
         if (hipMalloc(&d->dIn[k], inBytes) != hipSuccess) return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc failed");
         HIPCHK(hipHostMalloc(&d->hStage[k], inBytes, hipHostMallocDefault));
         HIPCHK(hipEventCreateWithFlags(&d->evUp[k], hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&d->evRead[k], hipEventDisableTiming));
-        HIPCHK(hipEventRecord(d->evUp[k], d->stream));
-        HIPCHK(hipEventRecord(d->evRead[k], d->stream));
-    }
-    for (int k = 0; k < d->kSlots; k++) {
-        HIPCHK(hipEventCreateWithFlags(&d->evFrame[k], hipEventDisableTiming));
-        HIPCHK(hipEventRecord(d->evFrame[k], d->stream));
     }
     if (d->firstOctave < 0) d->upPitch = (2 * W + 63) / 64 * 64;
     size_t pyrFloats = 0;
@@ -424,68 +595,69 @@ int allocate(sift_hip_detector* d) {
     const unsigned capO = d->kp.capOriented, capF = d->kp.capFinal;
 
     // Frame arena: every per-frame buffer at a 256-B aligned offset; B arenas
-    // back to back.  Zeroed once here; afterwards the kernels keep the
-    // scratch zero for the next frame (first blur: counters, k_order /
-    // k_select: range keys, k_bucket_rank: bucket counts, k_orientation:
-    // dedupe bits), so the frame graph has no memset node.
+    // back to back per lane.  Zeroed once at allocation; afterwards the
+    // kernels keep the scratch zero for the next frame (first blur: counters,
+    // k_order / k_select: range keys, k_bucket_rank: bucket counts,
+    // k_orientation: dedupe bits), so the frame graph has no memset node.
     size_t off = 0;
     auto take = [&](size_t bytes) {
         const size_t o = off;
         off += (std::max<size_t>(bytes, 1) + 255) & ~(size_t)255;
         return o;
     };
-    const size_t oInput = take(sizeof(float) * (size_t)d->inPitch * H);  // blank warm-up frame / u8 -> f32 scratch
-    const size_t oUp = d->firstOctave < 0 ? take(sizeof(float) * (size_t)d->upPitch * 2 * H) : 0;
-    const size_t oPyr = take(sizeof(float) * pyrFloats);
-    const size_t oCand = take(sizeof(uint2) * d->capCand);
-    const size_t oRef = take(sizeof(RefKpt) * d->kp.capRefined);
-    const size_t oOri = take(sizeof(OriKpt) * capO);
-    const size_t oSlot = take(sizeof(int) * capO);
-    const size_t oOrder = take(sizeof(int) * capO);
-    const size_t oJobs = take(sizeof(DescJob) * capF);
-    const size_t oRange = take(sizeof(unsigned) * 2 * 2 * kRangeSlots);  // one set per frame parity
-    const size_t oBcount = take(sizeof(unsigned) * (size_t)d->kp.numBuckets);
-    const size_t oBoff = take(sizeof(unsigned) * (size_t)d->kp.numBuckets);
-    const size_t oBitmap = take(sizeof(uint32_t) * d->bitmapWords);
-    const size_t oCtr = take(sizeof(Counters));
-    size_t oK3[sift_hip_detector::kSlots], oF4[sift_hip_detector::kSlots], oDesc[sift_hip_detector::kSlots];
+    ArenaLayout& a = d->lay;
+    a.input = take(sizeof(float) * (size_t)d->inPitch * H);  // blank warm-up frame / u8 -> f32 scratch
+    a.up = d->firstOctave < 0 ? take(sizeof(float) * (size_t)d->upPitch * 2 * H) : 0;
+    a.pyr = take(sizeof(float) * pyrFloats);
+    a.cand = take(sizeof(uint2) * d->capCand);
+    a.ref = take(sizeof(RefKpt) * d->kp.capRefined);
+    a.ori = take(sizeof(OriKpt) * capO);
+    a.slot = take(sizeof(int) * capO);
+    a.order = take(sizeof(int) * capO);
+    a.jobs = take(sizeof(DescJob) * capF);
+    a.range = take(sizeof(unsigned) * 2 * 2 * kRangeSlots);  // one set per frame parity
+    a.bcount = take(sizeof(unsigned) * (size_t)d->kp.numBuckets);
+    a.boff = take(sizeof(unsigned) * (size_t)d->kp.numBuckets);
+    a.bitmap = take(sizeof(uint32_t) * d->bitmapWords);
+    a.ctr = take(sizeof(Counters));
     for (int b = 0; b < d->kSlots; b++) {
-        oK3[b] = take(sizeof(float) * 3 * (size_t)capF);
-        oF4[b] = take(sizeof(float) * 4 * (size_t)capF);
-        oDesc[b] = take(sizeof(uint16_t) * 128 * (size_t)capF);
+        a.k3[b] = take(sizeof(float) * 3 * (size_t)capF);
+        a.f4[b] = take(sizeof(float) * 4 * (size_t)capF);
+        a.desc[b] = take(sizeof(uint16_t) * 128 * (size_t)capF);
     }
     d->afs = (long)off;
-    if (hipMalloc((void**)&d->dArena, off * d->B) != hipSuccess)
-        return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc of the frame arenas failed");
-    HIPCHK(hipMemset(d->dArena, 0, off * d->B));
-    char* A = d->dArena;
-    d->dInput = reinterpret_cast<float*>(A + oInput);
-    d->dUp = d->firstOctave < 0 ? reinterpret_cast<float*>(A + oUp) : nullptr;
-    d->dPyr = reinterpret_cast<float*>(A + oPyr);
-    for (int o = 0; o < d->nOct; o++)
-        d->pyr.oct[o].base = d->dPyr + reinterpret_cast<size_t>(d->pyr.oct[o].base);
-    d->dCand = reinterpret_cast<uint2*>(A + oCand);
-    d->dRef = reinterpret_cast<RefKpt*>(A + oRef);
-    d->dOri = reinterpret_cast<OriKpt*>(A + oOri);
-    d->dSlot = reinterpret_cast<int*>(A + oSlot);
-    d->dOrder = reinterpret_cast<int*>(A + oOrder);
-    d->dJobs = reinterpret_cast<DescJob*>(A + oJobs);
-    d->dRange = reinterpret_cast<unsigned*>(A + oRange);
-    d->dBcount = reinterpret_cast<unsigned*>(A + oBcount);
-    d->dBoff = reinterpret_cast<unsigned*>(A + oBoff);
-    d->dBitmap = reinterpret_cast<uint32_t*>(A + oBitmap);
-    d->dCtr = reinterpret_cast<Counters*>(A + oCtr);
-    for (int b = 0; b < d->kSlots; b++) {
-        d->dKpts3[b] = reinterpret_cast<float*>(A + oK3[b]);
-        d->dFeats4[b] = reinterpret_cast<float*>(A + oF4[b]);
-        d->dDesc[b] = reinterpret_cast<uint16_t*>(A + oDesc[b]);
-    }
-    const size_t nh = (size_t)d->kSlots * d->B;
-    HIPCHK(hipHostMalloc((void**)&d->hCtr, sizeof(Counters) * nh, hipHostMallocMapped | hipHostMallocCoherent));
-    memset(d->hCtr, 0, sizeof(Counters) * nh);
-    HIPCHK(hipHostGetDevicePointer((void**)&d->hCtrDev, d->hCtr, 0));
     upload_exp_tab();
     return SIFT_HIP_OK;
+}
+
+int build_graphs(sift_hip_detector* d);
+
+// A new compute lane: stream, zeroed arenas, host counters, events and the
+// captured graphs (bound on return).
+int add_lane(sift_hip_detector* d) {
+    if (d->nLanes >= kMaxLanes) return fail(SIFT_HIP_ERR_STATE, "no lane left");
+    const int k = d->nLanes;
+    Lane& L = d->lanes[k];
+    d->nLanes++;  // from here the destructor releases what the lane holds
+    HIPCHK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
+    if (hipMalloc((void**)&L.arena, (size_t)d->afs * d->B) != hipSuccess)
+        return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc of the frame arenas failed");
+    HIPCHK(hipMemsetAsync(L.arena, 0, (size_t)d->afs * d->B, L.stream));
+    const size_t nh = (size_t)d->kSlots * d->B;
+    HIPCHK(hipHostMalloc((void**)&L.hCtr, sizeof(Counters) * nh, hipHostMallocMapped | hipHostMallocCoherent));
+    memset(L.hCtr, 0, sizeof(Counters) * nh);
+    HIPCHK(hipHostGetDevicePointer((void**)&L.hCtrDev, L.hCtr, 0));
+    for (int b = 0; b < d->kSlots; b++) {
+        HIPCHK(hipEventCreateWithFlags(&L.evFrame[b], hipEventDisableTiming));
+        HIPCHK(hipEventRecord(L.evFrame[b], L.stream));
+    }
+    if (k == 0)  // upload-ring events start complete (recorded on the first lane)
+        for (int i = 0; i < d->nIn; i++) {
+            HIPCHK(hipEventRecord(d->evUp[i], L.stream));
+            HIPCHK(hipEventRecord(d->evRead[i], L.stream));
+        }
+    bind_lane(d, k);
+    return build_graphs(d);
 }
 
 // The first kernel reads the caller's image (upload ring slot or a device
@@ -741,12 +913,13 @@ int capture_with_head(sift_hip_detector* d, int slot, int nf, hipGraphExec_t* ou
 }
 
 int build_graphs(sift_hip_detector* d) {
+    Lane& L = d->lane();
     for (int b = 0; b < d->kSlots; b++) {
-        if (int rc = capture(d, b, d->B, &d->exec[b])) return rc;
-        if (int rc = capture_with_head(d, b, d->B, &d->execH[b], &d->graphH[b], &d->headH[b])) return rc;
+        if (int rc = capture(d, b, d->B, &L.exec[b])) return rc;
+        if (int rc = capture_with_head(d, b, d->B, &L.execH[b], &L.graphH[b], &L.headH[b])) return rc;
         if (d->B > 1) {
-            if (int rc = capture(d, b, 1, &d->exec1[b])) return rc;
-            if (int rc = capture_with_head(d, b, 1, &d->execH1[b], &d->graphH1[b], &d->headH1[b])) return rc;
+            if (int rc = capture(d, b, 1, &L.exec1[b])) return rc;
+            if (int rc = capture_with_head(d, b, 1, &L.execH1[b], &L.graphH1[b], &L.headH1[b])) return rc;
         }
     }
     return SIFT_HIP_OK;
@@ -755,14 +928,69 @@ int build_graphs(sift_hip_detector* d) {
 int dump_stage_files(sift_hip_detector* d);
 void complete_counts(sift_hip_detector* d);
 
-// Enqueues launch group d->submitted (nf frames at byte stride sfs) on
-// d->stream; `consumed` (nullable) is recorded once the input has been read.
-// With stage dumps on (single frames after warm-up) the frame's input is kept
-// as float, the frame is completed synchronously and dumped.
+bool event_done(hipEvent_t e) {
+    const hipError_t r = hipEventQuery(e);
+    if (r == hipSuccess) return true;
+    (void)hipGetLastError();  // hipErrorNotReady is not an error of the handle
+    return false;
+}
+
+// Blank launch groups through every graph of a lane created after warm-up
+// (first-launch costs, as sift_hip_warmup's blank frames pay them for lane 0).
+// They take no frame numbers; slots 0..kSlots-1 in order keep the lane's
+// range-key parity alternating, and the lane's next frame takes slot 0.
+int warm_lane(sift_hip_detector* d) {
+    Lane& L = d->lane();
+    const int nb = d->B > 1 ? 2 : 1;
+    for (int r = 0; r < nb; r++)
+        for (int b = 0; b < d->kSlots; b++) {
+            HIPCHK(hipGraphLaunch(r == 0 ? L.execH[b] : L.execH1[b], L.stream));
+            HIPCHK(hipEventRecord(L.evFrame[b], L.stream));
+            L.nfOf[b] = r == 0 ? d->B : 1;
+        }
+    L.launched = (long long)nb * d->kSlots;
+    return SIFT_HIP_OK;
+}
+
+// The lane for the next frame, bound on return: the first idle lane (its last
+// frame complete), else a new lane (up to maxLanes), else the busy lane whose
+// last frame is the oldest.  A lane qualifies only if its next results slot
+// holds no frame the caller may still read (current - 1 onwards).
+int pick_lane(sift_hip_detector* d) {
+    auto slot_free = [&](int k) {
+        const Lane& L = d->lanes[k];
+        const long long occ = L.slotFrame[L.launched % d->kSlots];
+        return occ < 0 || occ < d->firstFrame || occ < d->current - 1;
+    };
+    int busy = -1;
+    for (int k = 0; k < d->nLanes; k++) {
+        if (!slot_free(k)) continue;
+        const Lane& L = d->lanes[k];
+        if (L.last < 0 || event_done(L.evFrame[(L.launched + d->kSlots - 1) % d->kSlots])) {
+            bind_lane(d, k);
+            return SIFT_HIP_OK;
+        }
+        if (busy < 0 || L.last < d->lanes[busy].last) busy = k;
+    }
+    if (d->nLanes < d->maxLanes) {  // (lane 0 comes from sift_hip_warmup)
+        if (int rc = add_lane(d)) return rc;
+        return warm_lane(d);
+    }
+    if (busy < 0)
+        return fail(SIFT_HIP_ERR_STATE, "every lane's next results slot is still held: sift_hip_wait first");
+    bind_lane(d, busy);
+    return SIFT_HIP_OK;
+}
+
+// Enqueues launch group d->submitted (nf frames at byte stride sfs) on the
+// bound lane (pick_lane); `consumed` (nullable) is recorded once the input has
+// been read.  With stage dumps on (single frames after warm-up) the frame's
+// input is kept as float, the frame is completed synchronously and dumped.
 int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEvent_t consumed, int nf = 1,
               long sfs = 0) {
     const long long f = d->submitted;
-    const int slot = d->slot_of(f);
+    Lane& L = d->lane();
+    const int slot = (int)(L.launched % d->kSlots);
     const bool dump = !d->dgDir.empty() && nf == 1 && d->firstFrame > 0;
     const int W = d->cfg.col_width, H = d->cfg.row_width;
     if (dump) {
@@ -776,39 +1004,41 @@ int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEven
     }
     const bool graphs = d->useGraph && !d->timing;
     hipGraphExec_t gh = !graphs || consumed || fmt != SIFT_HIP_F32 ? nullptr
-                        : nf == d->B                                 ? d->execH[slot]
-                        : nf == 1                                    ? d->execH1[slot]
+                        : nf == d->B                                 ? L.execH[slot]
+                        : nf == 1                                    ? L.execH1[slot]
                                                                      : nullptr;
     // The head node of execH[slot] is re-pointed only once that exec's last
-    // launch (frame f - kSlots, whose completion evFrame[slot] still records)
-    // has finished: a queued launch never sees its kernel arguments change.
-    // Otherwise the frame takes the separate head launch and the plain exec.
-    if (gh && hipEventQuery(d->evFrame[slot]) != hipSuccess) {
-        (void)hipGetLastError();  // hipErrorNotReady
-        gh = nullptr;
-    }
+    // launch (whose completion evFrame[slot] still records) has finished: a
+    // queued launch never sees its kernel arguments change.  Otherwise the
+    // frame takes the separate head launch and the plain exec.
+    if (gh && !event_done(L.evFrame[slot])) gh = nullptr;
     if (gh) {  // device f32 input: one launch for the whole frame, the head re-pointed at img
         HeadNode& h = d->headNode;
         head_node(d, h, static_cast<const float*>(img), pitch, slot & 1, nf, sfs);
-        HIPCHK(hipGraphExecKernelNodeSetParams(gh, nf == d->B ? d->headH[slot] : d->headH1[slot], &h.p));
+        HIPCHK(hipGraphExecKernelNodeSetParams(gh, nf == d->B ? L.headH[slot] : L.headH1[slot], &h.p));
         HIPCHK(hipGraphLaunch(gh, d->stream));
     } else {
         enqueue_head(d, img, pitch, fmt, slot & 1, nf, sfs);
         if (consumed) HIPCHK(hipEventRecord(consumed, d->stream));
-        hipGraphExec_t g = nf == d->B ? d->exec[slot] : (nf == 1 ? d->exec1[slot] : nullptr);
+        hipGraphExec_t g = nf == d->B ? L.exec[slot] : (nf == 1 ? L.exec1[slot] : nullptr);
         if (graphs && g) {
             HIPCHK(hipGraphLaunch(g, d->stream));
         } else {  // timing mode, or a partial batch: the same launches, eagerly
             enqueue_body(d, slot, nf);
         }
     }
-    HIPCHK(hipEventRecord(d->evFrame[slot], d->stream));
-    d->nfOf[slot] = nf;
+    HIPCHK(hipEventRecord(L.evFrame[slot], d->stream));
+    L.nfOf[slot] = nf;
+    L.slotFrame[slot] = f;
+    L.launched++;
+    L.last = f;
+    d->frec(f) = sift_hip_detector::FrameRec{d->ln, slot};
     d->submitted = f + 1;
     if (dump) {
         HIPCHK(hipStreamSynchronize(d->stream));
         if (d->timing) d->collect_timing();
         d->current = f;
+        d->curLane = d->ln;
         d->cur = slot;
         complete_counts(d);
         return dump_stage_files(d);
@@ -816,19 +1046,20 @@ int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEven
     return SIFT_HIP_OK;
 }
 
-// Exposes frame f through the result accessors.  Its counts are read once the
-// frame is complete (complete_counts).
+// Exposes frame f through the result accessors (and binds its lane).  Its
+// counts are read once the frame is complete (complete_counts).
 void make_current(sift_hip_detector* d, long long f) {
     d->current = f;
-    d->cur = d->slot_of(f);
+    d->curLane = d->frec(f).lane;
+    d->cur = d->frec(f).slot;
     d->countsValid = false;
+    bind_lane(d, d->curLane);
 }
 
 void complete_counts(sift_hip_detector* d) {
     const long long f = d->current;
     auto n = [&](long long g) {
-        return g < d->firstFrame ? 0
-                                 : (int)std::min<unsigned>(d->hCtr[(size_t)d->slot_of(g) * d->B].final_n, d->kp.capFinal);
+        return g < d->firstFrame ? 0 : (int)std::min<unsigned>(frame_counters(d, g).final_n, d->kp.capFinal);
     };
     d->count = n(f);
     d->prevCount = n(f - 1);
@@ -837,17 +1068,27 @@ void complete_counts(sift_hip_detector* d) {
 
 // Counts of the current launch group are read from the pinned host copies its
 // last kernel writes: an accessor called before sift_hip_sync / sift_hip_wait
-// (e.g. straight after sift_hip_detect_device) first waits for that group.
+// (e.g. straight after sift_hip_detect_device) first waits for that group.  The
+// previous frame may run on another lane: its counts are waited for too.
 int ensure_counts(sift_hip_detector* d) {
     if (d->countsValid) return SIFT_HIP_OK;
-    if (d->current >= d->firstFrame) HIPCHK(hipEventSynchronize(d->evFrame[d->cur]));
+    for (long long g : {d->current - 1, d->current})
+        if (g >= d->firstFrame) {
+            const auto& r = d->frec(g);
+            HIPCHK(hipEventSynchronize(d->lanes[r.lane].evFrame[r.slot]));
+        }
     complete_counts(d);
     return SIFT_HIP_OK;
 }
 
-int finish_frame(sift_hip_detector* d) {
-    HIPCHK(hipStreamSynchronize(d->stream));
+int sync_lanes(sift_hip_detector* d) {
+    for (int k = 0; k < d->nLanes; k++) HIPCHK(hipStreamSynchronize(d->lanes[k].stream));
     if (d->timing) d->collect_timing();
+    return SIFT_HIP_OK;
+}
+
+int finish_frame(sift_hip_detector* d) {
+    if (int rc = sync_lanes(d)) return rc;
     if (d->submitted > 0) {
         make_current(d, d->submitted - 1);
         complete_counts(d);
@@ -863,9 +1104,53 @@ int copy_stream(sift_hip_detector* d, hipStream_t* s) {
 
 int format_size(int fmt) { return fmt == SIFT_HIP_U8 ? 1 : (fmt == SIFT_HIP_F32 ? 4 : 0); }
 
+// Frames in flight past `current` (host-input and device submits): at most 2
+// per lane the handle may use.
+int check_in_flight(sift_hip_detector* d) {
+    if (d->submitted > d->current + 2LL * d->maxLanes)
+        return fail(SIFT_HIP_ERR_STATE, "every lane already has two frames in flight past the current one: sift_hip_wait first");
+    return SIFT_HIP_OK;
+}
+
+// Host results region of a lane slot: kpts3 | feats4 | descriptors at capacity.
+size_t host_res_bytes(const sift_hip_detector* d) {
+    const size_t c = d->kp.capFinal;
+    return ((12 * c + 255) & ~(size_t)255) + 16 * c + 256 * c;
+}
+void host_res(const sift_hip_detector* d, char* base, int slot, float** k3, float** f4, uint16_t** desc) {
+    const size_t c = d->kp.capFinal;
+    char* p = base + host_res_bytes(d) * slot;
+    *k3 = reinterpret_cast<float*>(p);
+    p += (12 * c + 255) & ~(size_t)255;
+    *f4 = reinterpret_cast<float*>(p);
+    *desc = reinterpret_cast<uint16_t*>(p + 16 * c);
+}
+
+// After a host-input frame: its results into the lane slot's pinned host
+// region on the lane's stream (the next frame of the lane follows it; other
+// lanes keep computing), evHost[slot] once they are there.
+int prefetch_results(sift_hip_detector* d, long long f) {
+    Lane& L = d->lane();
+    const int slot = d->frec(f).slot;
+    if (!L.hRes) {
+        const size_t bytes = host_res_bytes(d) * d->kSlots;
+        HIPCHK(hipHostMalloc((void**)&L.hRes, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostGetDevicePointer((void**)&L.hResDev, L.hRes, 0));
+        for (hipEvent_t& e : L.evHost) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    float *k3, *f4;
+    uint16_t* desc;
+    host_res(d, L.hResDev, slot, &k3, &f4, &desc);
+    launch_results_to_host(d->dKpts3[slot], d->dFeats4[slot], d->dDesc[slot], d->dCtr, d->kp.capFinal, k3, f4, desc,
+                           d->stream);
+    HIPCHK(hipEventRecord(L.evHost[slot], d->stream));
+    L.hostFrame[slot] = f;
+    return SIFT_HIP_OK;
+}
+
 // Host frame -> pinned staging (the caller's buffer is free on return) ->
 // device upload ring on copyStream (overlapping the frames in flight) ->
-// pipeline on d->stream.
+// pipeline on the frame's lane -> results to pinned host memory.
 int submit_host(sift_hip_detector* d, const void* img, size_t stride, int fmt, long long* ticket) {
     const int es = format_size(fmt);
     if (!es) return fail(SIFT_HIP_ERR_INVALID, "unknown pixel format");
@@ -874,19 +1159,14 @@ int submit_host(sift_hip_detector* d, const void* img, size_t stride, int fmt, l
     const size_t rowB = (size_t)es * W, pitchB = (size_t)es * d->inPitch;
     if (stride == 0) stride = rowB;
     if (stride < rowB) return fail(SIFT_HIP_ERR_INVALID, "row stride smaller than width");
-    if (d->submitted > d->current + 2)
-        return fail(SIFT_HIP_ERR_STATE, "two frames already in flight past the current one: sift_hip_wait first");
+    if (int rc = check_in_flight(d)) return rc;
     hipStream_t cs;
     if (int rc = copy_stream(d, &cs)) return rc;
-    const int k = (int)(d->uploads & (d->kInSlots - 1));
+    if (int rc = pick_lane(d)) return rc;
+    const int k = (int)(d->uploads % d->nIn);
     HIPCHK(hipEventSynchronize(d->evUp[k]));  // staging slot k no longer being read
-    char* dst = (char*)d->hStage[k];
-    const char* src = (const char*)img;
-    if (stride == pitchB) {
-        memcpy(dst, src, pitchB * (H - 1) + rowB);
-    } else {
-        for (int y = 0; y < H; y++) memcpy(dst + pitchB * y, src + stride * y, rowB);
-    }
+    if (!d->pool && rowB * H >= (1u << 20)) d->pool = new CopyPool(3);
+    copy_rows(d->pool, (char*)d->hStage[k], pitchB, (const char*)img, stride, rowB, H);
     HIPCHK(hipStreamWaitEvent(cs, d->evRead[k], 0));  // device slot k read by its last frame
     HIPCHK(hipMemcpyAsync(d->dIn[k], d->hStage[k], pitchB * H, hipMemcpyHostToDevice, cs));
     HIPCHK(hipEventRecord(d->evUp[k], cs));
@@ -895,15 +1175,42 @@ int submit_host(sift_hip_detector* d, const void* img, size_t stride, int fmt, l
     const long long f = d->submitted;
     int rc = run_frame(d, d->dIn[k], d->inPitch, fmt, d->evRead[k]);
     if (rc) return rc;
+    if (d->dgDir.empty() && (rc = prefetch_results(d, f))) return rc;
+    if (ticket) *ticket = f;
+    return SIFT_HIP_OK;
+}
+
+// Device frame (HBM-resident, fp32 or u8) -> the frame's lane; the lane waits
+// for `stream` (the caller's producer) before reading it.
+int submit_device(sift_hip_detector* d, const void* img, size_t stride, int fmt, void* stream, int nf, size_t fstride,
+                  long long* ticket) {
+    hipStream_t ext = (hipStream_t)stream;
+    if (int rc = pick_lane(d)) return rc;
+    if (ext) {
+        HIPCHK(hipEventRecord(d->evIn, ext));
+        HIPCHK(hipStreamWaitEvent(d->stream, d->evIn, 0));
+    }
+    const long long f = d->submitted;
+    if (int rc = run_frame(d, img, (int)(stride / format_size(fmt)), fmt, nullptr, nf, (long)fstride)) return rc;
     if (ticket) *ticket = f;
     return SIFT_HIP_OK;
 }
 
 int wait_frame(sift_hip_detector* d, long long f) {
-    if (f < d->firstFrame || f >= d->submitted) return fail(SIFT_HIP_ERR_INVALID, "unknown frame ticket");
-    if (f < d->submitted - (d->kSlots - 1)) return fail(SIFT_HIP_ERR_STATE, "frame results already recycled");
-    HIPCHK(hipEventSynchronize(d->evFrame[d->slot_of(f)]));
-    if (d->timing && f == d->submitted - 1) d->collect_timing();
+    if (f < d->firstFrame || f >= d->submitted || f < d->submitted - kFrameRing)
+        return fail(SIFT_HIP_ERR_INVALID, "unknown frame ticket");
+    const auto& r = d->frec(f);
+    Lane& L = d->lanes[r.lane];
+    if (L.slotFrame[r.slot] != f) return fail(SIFT_HIP_ERR_STATE, "frame results already recycled");
+    if (d->timing) {
+        if (int rc = sync_lanes(d)) return rc;
+    } else {
+        HIPCHK(hipEventSynchronize(L.evFrame[r.slot]));
+        if (f - 1 >= d->firstFrame) {  // prev_descriptor may come from another lane
+            const auto& p = d->frec(f - 1);
+            HIPCHK(hipEventSynchronize(d->lanes[p.lane].evFrame[p.slot]));
+        }
+    }
     make_current(d, f);
     complete_counts(d);
     return SIFT_HIP_OK;
@@ -1105,11 +1412,13 @@ int write_planes(sift_hip_detector* d, const std::string& dir) {
 // kernels keep (zeroed counters, range keys, dedupe bitmap) restored by one
 // memset of the arenas; the handle has no current frame afterwards.
 int replay_reset(sift_hip_detector* d) {
-    HIPCHK(hipMemsetAsync(d->dArena, 0, (size_t)d->afs * d->B, d->stream));
-    HIPCHK(hipStreamSynchronize(d->stream));
+    bind_lane(d, 0);
+    HIPCHK(hipMemsetAsync(d->lanes[0].arena, 0, (size_t)d->afs * d->B, d->stream));
+    if (int rc = sync_lanes(d)) return rc;
     d->firstFrame = d->submitted;
     d->current = d->submitted - 1;
-    d->cur = d->current >= 0 ? d->slot_of(d->current) : 0;
+    d->curLane = 0;
+    d->cur = 0;
     d->count = d->prevCount = 0;
     d->countsValid = true;
     return SIFT_HIP_OK;
@@ -1264,11 +1573,15 @@ int replay_stage(sift_hip_detector* d, const std::string& in, const std::string&
     return rc ? rc : rc_reset;
 }
 
+// Every entry point starts bound to the current frame's lane (the accessors
+// address it); submitting entry points re-bind to the lane they pick.
 #define CHECK_HANDLE(h)                                                                       \
     do {                                                                                      \
         if (!(h)) return fail(SIFT_HIP_ERR_INVALID, "null handle");                          \
-        if (!(h)->allocated) return fail(SIFT_HIP_ERR_STATE, "sift_hip_warmup not called"); \
+        if (!(h)->allocated || !(h)->nLanes)                                                  \
+            return fail(SIFT_HIP_ERR_STATE, "sift_hip_warmup not called");                    \
         HIPCHK(hipSetDevice((h)->device));                                                    \
+        bind_lane((h), (h)->curLane);                                                         \
     } while (0)
 
 }  // namespace
@@ -1333,10 +1646,10 @@ int sift_hip_destroy(sift_hip_t h) {
 
 int sift_hip_warmup(sift_hip_t d) {
     if (!d) return fail(SIFT_HIP_ERR_INVALID, "null handle");
-    if (d->allocated) return SIFT_HIP_OK;
+    if (d->allocated) return d->nLanes ? SIFT_HIP_OK : fail(SIFT_HIP_ERR_STATE, "an earlier warm-up failed");
     int rc = allocate(d);
     if (rc) return rc;
-    rc = build_graphs(d);
+    rc = add_lane(d);  // lane 0; more lanes on demand (pick_lane)
     if (rc) return rc;
     // One blank frame (batch) through each graph: first-touch, code-object load.
     for (int i = 0; i < d->kSlots * (d->B > 1 ? 2 : 1); i++) {
@@ -1396,24 +1709,30 @@ int sift_hip_detect_device_fmt(sift_hip_t d, const void* img, size_t stride, int
     if (stride == 0) stride = (size_t)es * W;
     if (stride % es || stride < (size_t)es * W)
         return fail(SIFT_HIP_ERR_INVALID, "row stride must be a multiple of the pixel size and >= width");
-    if (d->submitted > d->current + 2)
-        return fail(SIFT_HIP_ERR_STATE, "two frames already in flight past the current one: sift_hip_wait first");
-    hipStream_t ext = (hipStream_t)stream;
-    if (ext) {
-        HIPCHK(hipEventRecord(d->evIn, ext));
-        HIPCHK(hipStreamWaitEvent(d->stream, d->evIn, 0));
-    }
-    const long long f = d->submitted;
-    int rc = run_frame(d, img, (int)(stride / es), format, nullptr);
-    if (rc) return rc;
+    if (int rc = check_in_flight(d)) return rc;
+    long long f = 0;
+    if (int rc = submit_device(d, img, stride, format, stream, 1, 0, &f)) return rc;
     // Device-ordered consumers see this frame's buffers at once; counts
     // follow at sift_hip_sync / sift_hip_wait.
     make_current(d, f);
-    if (ext) {
+    if (stream) {
         HIPCHK(hipEventRecord(d->evOut, d->stream));
-        HIPCHK(hipStreamWaitEvent(ext, d->evOut, 0));
+        HIPCHK(hipStreamWaitEvent((hipStream_t)stream, d->evOut, 0));
     }
     return SIFT_HIP_OK;
+}
+
+int sift_hip_submit_device(sift_hip_t d, const void* img, size_t stride, int format, void* stream, long long* ticket) {
+    CHECK_HANDLE(d);
+    if (!img) return fail(SIFT_HIP_ERR_INVALID, "null image");
+    const int es = format_size(format);
+    if (!es) return fail(SIFT_HIP_ERR_INVALID, "unknown pixel format");
+    const int W = d->cfg.col_width;
+    if (stride == 0) stride = (size_t)es * W;
+    if (stride % es || stride < (size_t)es * W)
+        return fail(SIFT_HIP_ERR_INVALID, "row stride must be a multiple of the pixel size and >= width");
+    if (int rc = check_in_flight(d)) return rc;
+    return submit_device(d, img, stride, format, stream, 1, 0, ticket);
 }
 
 int sift_hip_detect_device(sift_hip_t d, const float* img, size_t stride, void* stream) {
@@ -1425,6 +1744,21 @@ int sift_hip_set_batch(sift_hip_t d, int frames) {
     if (frames < 1 || frames > kMaxBatch) return fail(SIFT_HIP_ERR_INVALID, "batch size out of range (1..64)");
     if (d->allocated) return fail(SIFT_HIP_ERR_STATE, "sift_hip_set_batch after sift_hip_warmup");
     d->B = frames;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_set_lanes(sift_hip_t d, int lanes) {
+    if (!d) return fail(SIFT_HIP_ERR_INVALID, "null handle");
+    if (lanes < 1 || lanes > kMaxLanes) return fail(SIFT_HIP_ERR_INVALID, "lanes out of range (1..4)");
+    if (d->allocated) return fail(SIFT_HIP_ERR_STATE, "sift_hip_set_lanes after sift_hip_warmup");
+    d->maxLanes = lanes;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_lanes(sift_hip_t d, int* max_lanes, int* created) {
+    if (!d) return fail(SIFT_HIP_ERR_INVALID, "null handle");
+    if (max_lanes) *max_lanes = d->maxLanes;
+    if (created) *created = d->nLanes;
     return SIFT_HIP_OK;
 }
 
@@ -1462,20 +1796,13 @@ int sift_hip_detect_batch_device(sift_hip_t d, const void* frames, int n, size_t
     if (frame_stride == 0) frame_stride = stride * H;
     if (n > 1 && frame_stride < stride * (H - 1) + (size_t)es * W)
         return fail(SIFT_HIP_ERR_INVALID, "frame stride smaller than one frame");
-    if (d->submitted > d->current + 2)
-        return fail(SIFT_HIP_ERR_STATE, "two launch groups already in flight past the current one: sync first");
-    hipStream_t ext = (hipStream_t)stream;
-    if (ext) {
-        HIPCHK(hipEventRecord(d->evIn, ext));
-        HIPCHK(hipStreamWaitEvent(d->stream, d->evIn, 0));
-    }
-    const long long f = d->submitted;
-    int rc = run_frame(d, frames, (int)(stride / es), format, nullptr, n, (long)frame_stride);
-    if (rc) return rc;
+    if (int rc = check_in_flight(d)) return rc;
+    long long f = 0;
+    if (int rc = submit_device(d, frames, stride, format, stream, n, frame_stride, &f)) return rc;
     make_current(d, f);
-    if (ext) {
+    if (stream) {
         HIPCHK(hipEventRecord(d->evOut, d->stream));
-        HIPCHK(hipStreamWaitEvent(ext, d->evOut, 0));
+        HIPCHK(hipStreamWaitEvent((hipStream_t)stream, d->evOut, 0));
     }
     return SIFT_HIP_OK;
 }
@@ -1483,14 +1810,14 @@ int sift_hip_detect_batch_device(sift_hip_t d, const void* frames, int n, size_t
 int sift_hip_batch_frames(sift_hip_t d, int* n) {
     CHECK_HANDLE(d);
     if (!n) return fail(SIFT_HIP_ERR_INVALID, "null argument");
-    *n = d->current < d->firstFrame ? 0 : d->nfOf[d->cur];
+    *n = d->current < d->firstFrame ? 0 : d->lane().nfOf[d->cur];
     return SIFT_HIP_OK;
 }
 
 int sift_hip_batch_results_device(sift_hip_t d, int i, int* count, int* overflow, const float** k3,
                                   const float** f4, const uint16_t** desc) {
     CHECK_HANDLE(d);
-    if (d->current < d->firstFrame || i < 0 || i >= d->nfOf[d->cur])
+    if (d->current < d->firstFrame || i < 0 || i >= d->lane().nfOf[d->cur])
         return fail(SIFT_HIP_ERR_INVALID, "no such frame in the current batch");
     if (count || overflow)
         if (int rc = ensure_counts(d)) return rc;
@@ -1513,7 +1840,7 @@ int sift_hip_batch_copy_to_host(sift_hip_t d, int i, float* k3, float* f4, uint1
     if (count) *count = n;
     hipStream_t s;
     if (int rc = copy_stream(d, &s)) return rc;
-    HIPCHK(hipStreamWaitEvent(s, d->evFrame[d->cur], 0));
+    HIPCHK(hipStreamWaitEvent(s, d->lane().evFrame[d->cur], 0));
     if (n > 0) {
         if (k3) HIPCHK(hipMemcpyAsync(k3, dk, sizeof(float) * 3 * n, hipMemcpyDeviceToHost, s));
         if (f4) HIPCHK(hipMemcpyAsync(f4, df, sizeof(float) * 4 * n, hipMemcpyDeviceToHost, s));
@@ -1530,8 +1857,9 @@ int sift_hip_sync(sift_hip_t d) {
 
 int sift_hip_num_keypoints(sift_hip_t d, int* n) {
     if (!d || !n) return fail(SIFT_HIP_ERR_INVALID, "null argument");
-    if (d->allocated) {
+    if (d->allocated && d->nLanes) {
         HIPCHK(hipSetDevice(d->device));
+        bind_lane(d, d->curLane);
         if (int rc = ensure_counts(d)) return rc;
     }
     *n = d->count;
@@ -1540,8 +1868,9 @@ int sift_hip_num_keypoints(sift_hip_t d, int* n) {
 
 int sift_hip_overflow_flags(sift_hip_t d, int* flags) {
     if (!d || !flags) return fail(SIFT_HIP_ERR_INVALID, "null argument");
-    if (d->allocated) {
+    if (d->allocated && d->nLanes) {
         HIPCHK(hipSetDevice(d->device));
+        bind_lane(d, d->curLane);
         if (int rc = ensure_counts(d)) return rc;
     }
     *flags = d->hCtr ? (int)d->hCtr[(size_t)d->cur * d->B].overflow : 0;
@@ -1565,7 +1894,7 @@ int sift_hip_results_device(sift_hip_t d, const float** k3, const float** f4, co
     if (k3) *k3 = d->dKpts3[d->cur];
     if (f4) *f4 = d->dFeats4[d->cur];
     if (desc) *desc = d->dDesc[d->cur];
-    if (prev) *prev = d->dDesc[d->slot_of(d->current - 1)];
+    if (prev) *prev = d->current - 1 >= d->firstFrame ? frame_desc(d, d->current - 1) : d->dDesc[(d->cur + d->kSlots - 1) % d->kSlots];
     if (prevCount) *prevCount = d->prevCount;
     if (capacity) *capacity = (int)d->kp.capFinal;
     return SIFT_HIP_OK;
@@ -1575,11 +1904,25 @@ int sift_hip_copy_to_host(sift_hip_t d, float* k3, float* f4, uint16_t* desc, in
     CHECK_HANDLE(d);
     if (int rc = ensure_counts(d)) return rc;
     const int n = std::min(d->count, cap);
+    Lane& L = d->lane();
+    if (L.hRes && L.hostFrame[d->cur] == d->current && d->current >= d->firstFrame) {
+        // A host-input frame: its results already went to pinned host memory.
+        HIPCHK(hipEventSynchronize(L.evHost[d->cur]));
+        float *hk3, *hf4;
+        uint16_t* hdesc;
+        host_res(d, L.hRes, d->cur, &hk3, &hf4, &hdesc);
+        if (n > 0) {
+            if (k3) memcpy(k3, hk3, sizeof(float) * 3 * n);
+            if (f4) memcpy(f4, hf4, sizeof(float) * 4 * n);
+            if (desc) memcpy(desc, hdesc, sizeof(uint16_t) * 128 * n);
+        }
+        return SIFT_HIP_OK;
+    }
     // On the copy stream, ordered after the current frame only: frames
     // submitted after it keep running.
     hipStream_t s;
     if (int rc = copy_stream(d, &s)) return rc;
-    HIPCHK(hipStreamWaitEvent(s, d->evFrame[d->cur], 0));
+    HIPCHK(hipStreamWaitEvent(s, d->lane().evFrame[d->cur], 0));
     if (n > 0) {
         if (k3) HIPCHK(hipMemcpyAsync(k3, d->dKpts3[d->cur], sizeof(float) * 3 * n, hipMemcpyDeviceToHost, s));
         if (f4) HIPCHK(hipMemcpyAsync(f4, d->dFeats4[d->cur], sizeof(float) * 4 * n, hipMemcpyDeviceToHost, s));
@@ -1595,7 +1938,7 @@ int sift_hip_copy_descriptors_device(sift_hip_t d, uint16_t* dst, int cap, void*
     if (int rc = ensure_counts(d)) return rc;
     const int n = std::min(d->count, cap);
     hipStream_t s = stream ? (hipStream_t)stream : d->stream;
-    if (s != d->stream) HIPCHK(hipStreamWaitEvent(s, d->evFrame[d->cur], 0));
+    if (s != d->stream) HIPCHK(hipStreamWaitEvent(s, d->lane().evFrame[d->cur], 0));
     if (n > 0) HIPCHK(hipMemcpyAsync(dst, d->dDesc[d->cur], sizeof(uint16_t) * 128 * n, hipMemcpyDeviceToDevice, s));
     if (!stream) HIPCHK(hipStreamSynchronize(s));
     return SIFT_HIP_OK;

@@ -147,6 +147,17 @@ long long Detector::submit(const Image8U& image) {
     return t;
 }
 
+long long Detector::submitDevice(const void* dev, size_t stride, bool u8, void* stream) {
+    if (!m_initialized && !gpuWarmUpAndAllocate()) return -1;
+    long long t = -1;
+    check(sift_hip_submit_device(m_handle, dev, stride, u8 ? SIFT_HIP_U8 : SIFT_HIP_F32, stream, &t), "submitDevice");
+    return t;
+}
+
+void Detector::setLanes(int lanes) {
+    if (m_handle) check(sift_hip_set_lanes(m_handle, lanes), "setLanes");
+}
+
 void Detector::wait(long long ticket) {
     check(sift_hip_wait(m_handle, ticket), "wait");
     refreshViews();

@@ -37,21 +37,30 @@ constexpr float kOriPeakRatio = 0.8f;
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_refine(PyrDesc pyr, const uint2* __restrict__ cand, unsigned capCand,
                                                 Counters* __restrict__ ctr, uint32_t* __restrict__ bitmap,
-                                                RefKpt* __restrict__ out, KeypointParams kp, long fs) {
-    const long foff = blockIdx.y * fs;  // frame blockIdx.y
+                                                RefKpt* __restrict__ out, KeypointParams kp, long fs,
+                                                unsigned nf) {
+    // XCD-aware mapping as k_orientation's: frame = w % nf; a frame's q XCDs
+    // each take a contiguous range of its candidates (scan order: neighbours
+    // share their 3x3x4 rows in one L2).
+    const unsigned w = blockIdx.x, per = gridDim.x / nf;
+    const unsigned frame = w % nf, l = w / nf;
+    const unsigned q = (nf < 8 && 8 % nf == 0) ? 8 / nf : 1;
+    const unsigned range = l % q, j = l / q, step = per / q;
+    const long foff = (long)frame * fs;
     cand = fptr(cand, foff);
     ctr = fptr(ctr, foff);
     bitmap = fptr(bitmap, foff);
     out = fptr(out, foff);
     const unsigned n = min(ctr->cand, capCand);
+    const unsigned span = (n + q - 1) / q, iend = min(n, (range + 1) * span);
     const int lane = threadIdx.x & 63;
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
     // Wave-uniform loop (the append below is a wave collective).
-    for (unsigned i0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < n; i0 += gridDim.x * blockDim.x) {
+    for (unsigned i0 = range * span + j * blockDim.x + (threadIdx.x & ~63u); i0 < iend; i0 += step * blockDim.x) {
         const unsigned i = i0 + lane;
         RefKpt k;
         long bit = 0;
-        const bool acc = i < n && refine_candidate(pyr, cand[i], bitmap, kp, foff, k, bit);
+        const bool acc = i < iend && refine_candidate(pyr, cand[i], bitmap, kp, foff, k, bit);
         // One counter atomic per wave (a per-lane atomic on one address
         // serialises in L2).
         const unsigned long long mask = __ballot(acc);
@@ -78,8 +87,9 @@ static int per_frame_blocks(int one, int nf) { return nf <= 1 ? one : std::max(o
 
 void launch_refine(const PyrDesc& pyr, const uint2* cand, unsigned capCand, Counters* ctr, uint32_t* bitmap,
                    RefKpt* out, const KeypointParams& kp, const Frames& fr, hipStream_t s) {
-    hipLaunchKernelGGL(k_refine, dim3(per_frame_blocks(512, fr.nf), fr.nf), dim3(256), 0, s, pyr, cand, capCand, ctr,
-                       bitmap, out, kp, fr.stride);
+    const int per = per_frame_blocks(512, fr.nf) & ~7;
+    hipLaunchKernelGGL(k_refine, dim3(per * fr.nf), dim3(256), 0, s, pyr, cand, capCand, ctr, bitmap, out, kp,
+                       fr.stride, (unsigned)fr.nf);
 }
 
 // ---------------------------------------------------------------------------
@@ -323,11 +333,25 @@ __device__ __forceinline__ void ori_clear_bit(uint32_t* bitmap, const OctGeom& g
 // dependence chains interleaved in one wave, round 4): 140 vs 131 us per
 // 16-frame launch, single frames equal.
 constexpr int kOriAhead = 1;
+// XCD-aware keypoint mapping (a 1-D grid of nf * per one-wave workgroups;
+// the dispatcher hands workgroup w to XCD w % 8, and each XCD has its own L2).
+// Frame = w % nf, so with nf a multiple of 8 every frame lives on one XCD (its
+// windows are fetched into one L2); with nf dividing 8 a frame's q = 8 / nf
+// XCDs each take a contiguous range of its keypoints (the refined list is in
+// scan order, so neighbouring keypoints -- overlapping windows -- share an
+// L2).  The round-4 mapping (frame = blockIdx.y, keypoint round-robin over
+// blockIdx.x) put every frame's neighbouring keypoints on all 8 XCDs: 2.2x the
+// window bytes fetched from HBM.
 __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* __restrict__ in,
                                                     Counters* __restrict__ ctr, OriKpt* __restrict__ out,
-                                                    uint32_t* __restrict__ bitmap, KeypointParams kp, long fs) {
+                                                    uint32_t* __restrict__ bitmap, KeypointParams kp, long fs,
+                                                    unsigned nf) {
     __shared__ __attribute__((aligned(16))) float chunk[64 + 3 * kOriBins];  // bin runs padded to 4
-    const long foff = blockIdx.y * fs;  // frame blockIdx.y
+    const unsigned w = blockIdx.x, per = gridDim.x / nf;
+    const unsigned frame = w % nf, l = w / nf;
+    const unsigned q = (nf < 8 && 8 % nf == 0) ? 8 / nf : 1;  // XCDs sharing this frame
+    const unsigned range = l % q, j = l / q, step = per / q;
+    const long foff = (long)frame * fs;
     in = fptr(in, foff);
     ctr = fptr(ctr, foff);
     out = fptr(out, foff);
@@ -340,7 +364,8 @@ __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* _
     for (int bit = 0; bit < 6; bit++) lane_nb[bit] = ((lane >> bit) & 1) ? 0ull : ~0ull;
     const unsigned n = min(ctr->refined, kp.capRefined);
     const int fo = pyr.firstOctave;
-    for (unsigned k = blockIdx.x; k < n; k += gridDim.x) {  // round-robin (see k_descriptor)
+    const unsigned span = (n + q - 1) / q, kend = min(n, (range + 1) * span);
+    for (unsigned k = range * span + j; k < kend; k += step) {
         const RefKpt kpt = load_ref(in, k);
         const OctGeom* gp;
         const OriWin wn = ori_window(pyr, kpt, foff, gp);
@@ -373,12 +398,11 @@ void launch_orientation(const PyrDesc& pyr, const RefKpt* in, Counters* ctr, Ori
     // One-wave workgroups per frame: 8192 for a single frame, 1024 at 8 frames.
     // Grids that fill every wave slot keep the other stream's pyramid kernels
     // out; this size lets them co-reside (+2-4 % frame rate, tools/grid_sweep.sh).
-#ifdef SIFT_ORI_PER  // tools A/B builds
-    const int per = fr.nf <= 1 ? 8192 : SIFT_ORI_PER;
-#else
-    const int per = fr.nf <= 1 ? 8192 : std::max(256, 8192 / fr.nf);
-#endif
-    hipLaunchKernelGGL(k_orientation, dim3(per, fr.nf), dim3(64), 0, s, pyr, in, ctr, out, bitmap, kp, fr.stride);
+    // (512 per frame at 16 frames; 256 measured equal, round 2.)  per is a
+    // multiple of 8: every XCD range gets the same number of workgroups.
+    const int per = fr.nf <= 1 ? 8192 : std::max(256, 8192 / fr.nf) & ~7;
+    hipLaunchKernelGGL(k_orientation, dim3(per * fr.nf), dim3(64), 0, s, pyr, in, ctr, out, bitmap, kp, fr.stride,
+                       (unsigned)fr.nf);
 }
 
 // ---------------------------------------------------------------------------
@@ -859,6 +883,34 @@ void launch_bucket_rank(const PyrDesc& pyr, const OriKpt* kpts, unsigned* bcount
                         const KeypointParams& kp, const Frames& fr, hipStream_t s) {
     hipLaunchKernelGGL(k_bucket_rank, dim3(per_frame_blocks(256, fr.nf), fr.nf), dim3(256), 0, s, pyr, kpts, bcount,
                        boff, order, ctr, jobs, kpts3, feats4, kp, fr.stride);
+}
+
+// ---------------------------------------------------------------------------
+// Results of a host-input frame copied into mapped pinned host memory right
+// after the frame (sift_hip_submit): the caller's copyToHost then reads host
+// memory instead of a pageable device-to-host copy (Detector.cu:606-634 copies
+// after the frame, synchronously).  n = min(final_n, cap) rows, the count read
+// on the device; 16-byte stores where the layouts allow.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_results_to_host(const float* __restrict__ k3, const float* __restrict__ f4,
+                                                         const uint16_t* __restrict__ desc,
+                                                         const Counters* __restrict__ ctr, unsigned cap,
+                                                         float* __restrict__ hk3, float* __restrict__ hf4,
+                                                         uint16_t* __restrict__ hdesc) {
+    const unsigned n = min(ctr->final_n, cap);
+    const unsigned tid = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
+    const uint4* __restrict__ sd = reinterpret_cast<const uint4*>(desc);
+    uint4* __restrict__ dd = reinterpret_cast<uint4*>(hdesc);
+    for (unsigned i = tid; i < n * 16; i += nt) dd[i] = sd[i];
+    const float4* __restrict__ sf = reinterpret_cast<const float4*>(f4);
+    float4* __restrict__ df = reinterpret_cast<float4*>(hf4);
+    for (unsigned i = tid; i < n; i += nt) df[i] = sf[i];
+    for (unsigned i = tid; i < n * 3; i += nt) hk3[i] = k3[i];
+}
+
+void launch_results_to_host(const float* k3, const float* f4, const uint16_t* desc, const Counters* ctr, unsigned cap,
+                            float* hk3, float* hf4, uint16_t* hdesc, hipStream_t s) {
+    hipLaunchKernelGGL(k_results_to_host, dim3(128), dim3(256), 0, s, k3, f4, desc, ctr, cap, hk3, hf4, hdesc);
 }
 
 }  // namespace sift_amd

@@ -204,6 +204,9 @@ static_assert(sizeof(DescJob) == 64, "DescJob is one 64-byte scalar load");
 void launch_rank_final(const PyrDesc& pyr, const OriKpt* kpts, const unsigned* bcount, const unsigned* boff,
                        const int* order, const Counters* ctr, DescJob* jobs, float* kpts3, float* feats4,
                        const KeypointParams& kp, const Frames& fr, hipStream_t s);
+// Results of a finished frame -> mapped pinned host buffers (host-input frames).
+void launch_results_to_host(const float* k3, const float* f4, const uint16_t* desc, const Counters* ctr, unsigned cap,
+                            float* hk3, float* hf4, uint16_t* hdesc, hipStream_t s);
 void launch_bucket_rank(const PyrDesc& pyr, const OriKpt* kpts, unsigned* bcount, const unsigned* boff,
                         const int* order, const Counters* ctr, DescJob* jobs, float* kpts3, float* feats4,
                         const KeypointParams& kp, const Frames& fr, hipStream_t s);

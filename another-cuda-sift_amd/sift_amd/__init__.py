@@ -94,6 +94,9 @@ def lib() -> ctypes.CDLL:
         "sift_hip_detect_device_fmt": (i, [vp, vp, sz, i, vp]),
         "sift_hip_submit": (i, [vp, vp, sz, i, ctypes.POINTER(ctypes.c_longlong)]),
         "sift_hip_wait": (i, [vp, ctypes.c_longlong]),
+        "sift_hip_submit_device": (i, [vp, vp, sz, i, vp, ctypes.POINTER(ctypes.c_longlong)]),
+        "sift_hip_set_lanes": (i, [vp, i]),
+        "sift_hip_lanes": (i, [vp, ip, ip]),
         "sift_hip_sync": (i, [vp]),
         "sift_hip_set_batch": (i, [vp, i]),
         "sift_hip_batch_capacity": (i, [vp, ip]),
@@ -138,6 +141,8 @@ def lib() -> ctypes.CDLL:
         "sift_hip_device_sync": (i, []),
     }
     for name, (res, args) in sigs.items():
+        if os.environ.get("SIFT_HIP_LIB") and not hasattr(L, name):
+            continue  # an older A/B build (tools/ab_build.sh) may predate an entry point
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
@@ -217,11 +222,14 @@ class DeviceBuffer:
 class Detector:
     """sift_cuda::Detector (Detector.hh:24-96) over the C ABI."""
 
-    def __init__(self, config: CudaSiftConfig, device: int = -1, batch: int = 1, exact_descriptors: bool = False):
+    def __init__(self, config: CudaSiftConfig, device: int = -1, batch: int = 1, exact_descriptors: bool = False,
+                 lanes: Optional[int] = None):
         """batch > 1: frame-batch handle (sift_hip_set_batch): detectBatchDevice runs up to `batch`
         frames per launch; the single-frame methods keep working (frame 0's arena).
         exact_descriptors: OpenCV's sequential float histogram (SIFT_HIP_DESC_EXACT), descriptors
-        bit-identical to the oracle; default the fixed-point histogram (+-1 on a byte)."""
+        bit-identical to the oracle; default the fixed-point histogram (+-1 on a byte).
+        lanes: compute lanes for frames in flight (sift_hip_set_lanes, 1..4, library default 2):
+        frames submitted before the previous one completes run concurrently on another lane."""
         self.config = config
         self.batch = int(batch)
         self.exact_descriptors = bool(exact_descriptors)
@@ -229,6 +237,8 @@ class Detector:
         _check(lib().sift_hip_create(ctypes.byref(config._abi()), device, ctypes.byref(self._h)), "sift_hip_create")
         if self.batch != 1:
             _check(lib().sift_hip_set_batch(self._h, self.batch), "set_batch")
+        if lanes is not None:
+            _check(lib().sift_hip_set_lanes(self._h, int(lanes)), "set_lanes")
         if self.exact_descriptors:
             _check(lib().sift_hip_set_descriptor_mode(self._h, SIFT_HIP_DESC_EXACT), "set_descriptor_mode")
         n = ctypes.c_int()
@@ -317,6 +327,21 @@ class Detector:
         _check(lib().sift_hip_submit(self._h, _ptr(img), img.strides[0], fmt, ctypes.byref(t)), "submit")
         return t.value
 
+    def submitDevice(self, dev_ptr: int, row_stride_bytes: int = 0, stream: Optional[int] = None, u8: bool = False) -> int:
+        """Pipelined device input (sift_hip_submit_device): the frame at dev_ptr is enqueued on a free lane
+        after `stream`; returns the ticket for wait().  The buffer must stay unchanged until wait(ticket)."""
+        self.gpuWarmUpAndAllocate()
+        t = ctypes.c_longlong()
+        _check(lib().sift_hip_submit_device(self._h, dev_ptr, row_stride_bytes, SIFT_HIP_U8 if u8 else SIFT_HIP_F32,
+                                            stream, ctypes.byref(t)), "submitDevice")
+        return t.value
+
+    def lanes(self) -> tuple:
+        """(lane limit, lanes created so far)."""
+        m, c = ctypes.c_int(), ctypes.c_int()
+        _check(lib().sift_hip_lanes(self._h, ctypes.byref(m), ctypes.byref(c)), "lanes")
+        return m.value, c.value
+
     def wait(self, ticket: int) -> None:
         """Block until frame `ticket` is complete and expose its results (prev = frame ticket-1)."""
         _check(lib().sift_hip_wait(self._h, ticket), "wait")
@@ -372,9 +397,9 @@ class Detector:
     def copyToHost(self, descriptor: bool = True) -> None:
         """Detector.cu:606-634."""
         n = self.total_size
-        k3 = np.zeros((n, 3), np.float32)
-        f4 = np.zeros((n, 4), np.float32)
-        d = np.zeros((n, 128), np.uint16) if descriptor else None
+        k3 = np.empty((n, 3), np.float32)
+        f4 = np.empty((n, 4), np.float32)
+        d = np.empty((n, 128), np.uint16) if descriptor else None
         _check(lib().sift_hip_copy_to_host(self._h, _ptr(k3), _ptr(f4), _ptr(d) if d is not None else None, n), "copyToHost")
         self.final_kpts, self.final_features = k3, f4
         if d is not None:

@@ -557,7 +557,8 @@ def main():
     # is still one complete frame.
     B = max(a.batch, 1)
     nstreams = 1 if a.roofline_only else a.streams
-    dets = [sift.Detector(cfg, device=local, batch=B, exact_descriptors=a.exact_descriptors) for _ in range(nstreams)]
+    dets = [sift.Detector(cfg, device=local, batch=B, exact_descriptors=a.exact_descriptors, lanes=1)
+            for _ in range(nstreams)]
     for d in dets:
         d.gpuWarmUpAndAllocate()
     det = dets[0]
@@ -606,7 +607,7 @@ def main():
 
     # The same frames one at a time through ONE single-frame detector (frames
     # strictly serialised): latency-side reference numbers.
-    det = sift.Detector(cfg, device=local)
+    det = sift.Detector(cfg, device=local, lanes=1)
     det.gpuWarmUpAndAllocate()
     n1 = max(a.steps // 2, 1)
     barrier()
@@ -620,7 +621,7 @@ def main():
     # The C2 step with the exact descriptor mode (SIFT_HIP_DESC_EXACT: OpenCV's
     # sequential float histogram, descriptors bit-identical to the oracle):
     # its cost next to the default fixed-point mode (value above).
-    detx = [sift.Detector(cfg, device=local, batch=B, exact_descriptors=True) for _ in range(nstreams)]
+    detx = [sift.Detector(cfg, device=local, batch=B, exact_descriptors=True, lanes=1) for _ in range(nstreams)]
     for d in detx:
         d.gpuWarmUpAndAllocate()
 
@@ -652,7 +653,7 @@ def main():
     # ---- C4: 256 synthetic 1600x900 frames sharded per image over the ranks -------
     W4, H4, N4 = 1600, 900, 256
     mine4 = multi.frame_shard(N4, rank, world)
-    dets4 = [sift.Detector(make_config(col_width=W4, row_width=H4, numOctaves=0), device=local, batch=B)
+    dets4 = [sift.Detector(make_config(col_width=W4, row_width=H4, numOctaves=0), device=local, batch=B, lanes=1)
              for _ in range(a.streams)]
     for d in dets4:
         d.gpuWarmUpAndAllocate()
@@ -718,22 +719,52 @@ def main():
         det.detectAndCompute(host_f32[s % nframes])
         det.copyToHost(True)
     t_sync = max_over_ranks(time.perf_counter() - t)
-    tickets = []
-    t = time.perf_counter()
-    for s in range(nh):
-        tickets.append(det.submit(host_u8[s % nframes]))
-        if len(tickets) == 2:
-            det.wait(tickets.pop(0))
-            det.copyToHost(True)
-    det.wait(tickets.pop(0))
-    det.copyToHost(True)
-    t_pipe = max_over_ranks(time.perf_counter() - t)
+    # Frames in flight at the drop-in API: submit/wait with `depth` frames
+    # outstanding on a detector with that many compute lanes (one stream,
+    # frame arenas and graphs per lane; consecutive frames overlap).
+    PIPE_LANES = 3
+    detp = sift.Detector(cfg, device=local, lanes=PIPE_LANES)
+    detp.gpuWarmUpAndAllocate()
+
+    def pipelined(submit, fetch):
+        tickets = []
+        for s in range(nh + PIPE_LANES):  # the first PIPE_LANES frames create and warm the lanes
+            if s == PIPE_LANES:
+                while tickets:
+                    detp.wait(tickets.pop(0))
+                t = time.perf_counter()
+            tickets.append(submit(s))
+            if len(tickets) == PIPE_LANES:
+                detp.wait(tickets.pop(0))
+                if fetch:
+                    detp.copyToHost(True)
+        while tickets:
+            detp.wait(tickets.pop(0))
+            if fetch:
+                detp.copyToHost(True)
+        return max_over_ranks(time.perf_counter() - t)
+
+    t_pipe = pipelined(lambda s: detp.submit(host_u8[s % nframes]), True)
+    dev_u8 = [torch.from_numpy(f).to(dev) for f in host_u8]
+    torch.cuda.synchronize()
+    t_dev = pipelined(lambda s: detp.submitDevice(frames[s % nframes].data_ptr(), stride), False)
+    t_dev8 = pipelined(lambda s: detp.submitDevice(dev_u8[s % nframes].data_ptr(), W, u8=True), False)
     host_input = {
         "sync_f32": {"value": round(world * nh * W * H / 1e6 / t_sync, 2), "ms_per_frame": round(t_sync / nh * 1e3, 4)},
-        "pipelined_u8": {"value": round(world * nh * W * H / 1e6 / t_pipe, 2), "ms_per_frame": round(t_pipe / nh * 1e3, 4)},
+        "pipelined_u8": {"value": round(world * nh * W * H / 1e6 / t_pipe, 2), "ms_per_frame": round(t_pipe / nh * 1e3, 4),
+                         "lanes": PIPE_LANES, "in_flight": PIPE_LANES, "lanes_created": detp.lanes()[1]},
         "unit": "Mpix/s",
-        "note": "PCIe-inclusive, host frame -> results in host memory (copyToHost with descriptors), one detector",
+        "note": "PCIe-inclusive, host frame -> results in host memory (copyToHost with descriptors), one detector; "
+                f"pipelined: submit/wait with {PIPE_LANES} frames in flight on {PIPE_LANES} compute lanes",
     }
+    device_submit = {
+        "f32": {"value": round(world * nh * W * H / 1e6 / t_dev, 2), "ms_per_frame": round(t_dev / nh * 1e3, 4)},
+        "u8": {"value": round(world * nh * W * H / 1e6 / t_dev8, 2), "ms_per_frame": round(t_dev8 / nh * 1e3, 4)},
+        "unit": "Mpix/s", "lanes": PIPE_LANES, "in_flight": PIPE_LANES,
+        "note": "HBM-resident single frames through submitDevice/wait (sift_hip_submit_device), one detector, "
+                f"{PIPE_LANES} frames in flight on {PIPE_LANES} compute lanes; results stay on the device",
+    }
+    del detp, dev_u8
 
     # ---- per-kernel roofline: HIP events on the detector's own stream --------
     rl = measure_roofline(detb, frames, stride, a.traffic_summary, batch=fb if B > 1 else None)
@@ -927,6 +958,7 @@ def main():
             "single_stream": {"value": round(single_value, 2), "ms_per_frame": round(single / n1 * 1e3, 4)},
             "exact_descriptors": exact_leg,
             "host_input": host_input,
+            "device_submit": device_submit,
             "stage_us_per_frame_eager": stages,
             "stage_sum_us_eager": round(total_ms / nt * 1e3, 1),
             "dominant_stage": dom,

@@ -37,11 +37,20 @@ public:
     // Extra: pipelined input (sift_hip_submit / sift_hip_wait).  submit()
     // stages and uploads the frame while earlier frames compute and returns a
     // ticket; wait(ticket) makes that frame's results (and its predecessor's
-    // descriptors as prev_descriptor) current.  At most two frames in flight
-    // past the last waited one.
+    // descriptors as prev_descriptor) current.  Frames in flight compute
+    // concurrently on up to setLanes() compute lanes (default 2), at most two
+    // per lane past the last waited one.
     long long submit(const Imagef& image);
     long long submit(const Image8U& image);
+    // Extra: the same for a frame already in device memory (fp32 or 8-bit,
+    // row stride in bytes), read after `hip_stream` reaches the call; the
+    // buffer must stay unchanged until wait(ticket).
+    long long submitDevice(const void* device_image, size_t row_stride_bytes, bool u8 = false,
+                           void* hip_stream = nullptr);
     void wait(long long ticket);
+    // Extra: compute lanes for frames in flight (sift_hip_set_lanes, 1..4);
+    // before gpuWarmUpAndAllocate.  1 = every frame on one stream in order.
+    void setLanes(int lanes);
     // Extra: image already in device memory (fp32, row stride in bytes).
     void detectAndComputeDevice(const float* device_image, size_t row_stride_bytes, void* hip_stream = nullptr);
 

@@ -148,12 +148,32 @@ int sift_hip_batch_copy_to_host(sift_hip_t h, int i, float* kpts3, float* feats4
  * buffer is free again on return), uploads it on a copy stream while earlier
  * frames compute, enqueues the pipeline and returns a ticket without waiting.
  * sift_hip_wait(ticket) blocks until that frame is complete and makes it the
- * frame the result accessors address (prev_desc = frame ticket-1).  At most two
- * frames may be in flight past the last waited one (SIFT_HIP_ERR_STATE
- * otherwise); sift_hip_detect / sift_hip_detect_u8 = submit + wait. */
+ * frame the result accessors address (prev_desc = frame ticket-1).  At most
+ * 2 x lanes frames may be in flight past the last waited one
+ * (SIFT_HIP_ERR_STATE otherwise); sift_hip_detect / sift_hip_detect_u8 =
+ * submit + wait.
+ *
+ * Frames in flight compute concurrently: a handle has up to `lanes` compute
+ * lanes (a HIP stream with its own frame arenas, graphs and results ring
+ * each).  A frame goes to the first idle lane; when every lane is busy and
+ * fewer than `lanes` exist, a new one is created (its arenas and graphs, once:
+ * a synchronous caller never pays for a second lane).  Results are identical
+ * on every lane.  sift_hip_set_lanes(h, n), n = 1..4 (default 2), before
+ * sift_hip_warmup; n = 1 runs every frame of the handle in submission order
+ * on one stream.  sift_hip_lanes reports the limit and the lanes created. */
 int sift_hip_submit(sift_hip_t h, const void* host_img, size_t row_stride_bytes, int format,
                     long long* ticket);
 int sift_hip_wait(sift_hip_t h, long long ticket);
+int sift_hip_set_lanes(sift_hip_t h, int lanes);
+int sift_hip_lanes(sift_hip_t h, int* max_lanes, int* created);
+
+/* Pipelined device input: like sift_hip_submit for a frame already in device
+ * memory (f32 or u8, row stride in bytes), read on the frame's lane after
+ * `stream` (NULL: no ordering) reaches this call; the buffer must stay
+ * unchanged until sift_hip_wait(ticket) returns.  The results follow at
+ * sift_hip_wait, as for host frames. */
+int sift_hip_submit_device(sift_hip_t h, const void* dev_img, size_t row_stride_bytes, int format, void* stream,
+                           long long* ticket);
 
 /* Detector::total_size (Detector.hh:62, Detector.cu:584-604). */
 int sift_hip_num_keypoints(sift_hip_t h, int* n);

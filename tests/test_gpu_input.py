@@ -106,7 +106,7 @@ def test_pipelined_equals_sync(sift):
 def test_pipeline_limits(sift):
     w, h = 128, 96
     img = sift.synth_frame(1, w, h)
-    _, det = make_detector(sift, w, h)
+    _, det = make_detector(sift, w, h, lanes=1)  # one lane: two frames past the current one
     t0, t1 = det.submit(img), det.submit(img)
     with pytest.raises(sift.SiftHipError):  # a third frame past the current one
         det.submit(img)

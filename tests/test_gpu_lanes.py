@@ -1,0 +1,202 @@
+"""Frames in flight at the drop-in API ("Frames in flight").
+
+A handle runs frames submitted before their predecessors complete on up to
+`lanes` compute lanes (stream + frame arenas + graphs each).  Bar: every frame's
+keypoints, features and descriptors -- and prev_descriptor -- are bit for bit
+those of the synchronous one-frame-at-a-time path, whatever lane ran it; a
+synchronous caller never creates a second lane; the in-flight limits hold.
+Also (round-4 advisor): device frames from different buffers enqueued back to
+back without a host sync, results copied out stream-ordered, equal the
+synchronous results; device and host memory stay flat over a long loop.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_input import assert_identical, results
+from test_gpu_parity import make_detector
+
+pytestmark = pytest.mark.gpu
+
+W, H = 752, 480
+
+
+def sync_reference(sift, frames, **kw):
+    _, det = make_detector(sift, W, H, lanes=1, **kw)
+    out = []
+    for f in frames:
+        det.detectAndCompute(f)
+        out.append(results(det))
+    assert det.lanes() == (1, 1)
+    return out
+
+
+def prev_rows(sift, det, n):
+    prev = np.empty((n, 128), np.uint16)
+    if n:
+        sift._check(sift.lib().sift_hip_memcpy_d2h(prev.ctypes.data, det.prev_descriptor.data(), prev.nbytes), "d2h")
+    return prev
+
+
+def run_pipelined(sift, det, frames, ref, depth, submit):
+    """Keeps `depth` frames in flight; each waited frame must equal the synchronous path."""
+    queue, i = [], 0
+
+    def drain_one():
+        nonlocal i
+        t = queue.pop(0)
+        det.wait(t)
+        assert_identical(results(det), ref[i])
+        if i:
+            assert det.prev_size == len(ref[i - 1][0])
+            assert np.array_equal(prev_rows(sift, det, det.prev_size), ref[i - 1][2])
+        else:
+            assert det.prev_size == 0
+        i += 1
+
+    for s in range(len(frames)):
+        queue.append(submit(s))
+        if len(queue) == depth:
+            drain_one()
+    while queue:
+        drain_one()
+    assert i == len(frames)
+
+
+@pytest.mark.parametrize("lanes,depth", [(2, 2), (3, 3), (4, 4), (2, 4)])
+def test_host_submit_lanes_equal_sync(sift, lanes, depth):
+    frames = [sift.synth_frame(50 + i, W, H) for i in range(10)]
+    ref = sync_reference(sift, frames, numFeatures=2000)
+    _, det = make_detector(sift, W, H, numFeatures=2000, lanes=lanes)
+    run_pipelined(sift, det, frames, ref, depth,
+                  lambda s: det.submit(frames[s].astype(np.uint8) if s % 3 == 1 else frames[s]))
+    assert 1 <= det.lanes()[1] <= lanes
+
+
+def test_device_submit_lanes_equal_sync(sift):
+    frames = [sift.synth_frame(70 + i, W, H) for i in range(9)]
+    ref = sync_reference(sift, frames, numFeatures=2000)
+    dev = [torch.from_numpy(f).cuda() for f in frames]
+    u8 = [torch.from_numpy(f.astype(np.uint8)).cuda() for f in frames]
+    torch.cuda.synchronize()
+    _, det = make_detector(sift, W, H, numFeatures=2000, lanes=3)
+    run_pipelined(sift, det, frames, ref, 3,
+                  lambda s: det.submitDevice(u8[s].data_ptr(), W, u8=True) if s % 2
+                  else det.submitDevice(dev[s].data_ptr(), W * 4))
+
+
+def test_sync_caller_keeps_one_lane(sift):
+    _, det = make_detector(sift, W, H, numFeatures=2000)
+    img = sift.synth_frame(3, W, H)
+    for _ in range(4):
+        det.detectAndCompute(img)
+    dev = torch.from_numpy(img).cuda()
+    torch.cuda.synchronize()
+    for _ in range(3):
+        det.detectAndComputeDevice(dev.data_ptr(), W * 4, sync=True)
+    assert det.lanes() == (2, 1)
+
+
+def test_lane_limits(sift):
+    img = sift.synth_frame(1, 128, 96)
+    _, det = make_detector(sift, 128, 96, lanes=2)
+    t = [det.submit(img) for _ in range(4)]  # two per lane past the current frame
+    with pytest.raises(sift.SiftHipError):
+        det.submit(img)
+    det.wait(t[1])
+    det.wait(t[0])  # frames current-1 .. on stay readable
+    t.append(det.submit(img))
+    for x in t[2:]:
+        det.wait(x)
+    with pytest.raises(sift.SiftHipError):
+        sift.Detector(sift.CudaSiftConfig(col_width=128, row_width=96), lanes=5)
+
+
+class _Cai:
+    """A raw device pointer as a torch tensor (__cuda_array_interface__), no copy."""
+
+    def __init__(self, ptr, shape, typestr):
+        self.__cuda_array_interface__ = {"shape": shape, "typestr": typestr, "data": (ptr, False), "version": 2}
+
+
+def test_device_frames_back_to_back_stream_ordered(sift):
+    """Round-4 advisor: >= 5 device frames from different buffers enqueued
+    without a host sync (the frame graph's head node re-pointed per frame, or
+    the separate head launch while that graph is still in flight); each
+    frame's results copied out on the caller's stream right after it."""
+    frames = [sift.synth_frame(90 + i, W, H) for i in range(8)]
+    ref = sync_reference(sift, frames, numFeatures=2000)
+    bufs = [torch.from_numpy(f).cuda() for f in frames]
+    # a real stream: torch's default one is the null stream (no handle to order on)
+    stream = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    _, det = make_detector(sift, W, H, numFeatures=2000)
+    cap = det.capacities()["results"]
+    lib = sift.lib()
+    outs = []
+    ctx = torch.cuda.stream(stream)
+    ctx.__enter__()
+    for b in bufs:
+        det.detectAndComputeDevice(b.data_ptr(), W * 4, stream=stream.cuda_stream, sync=False)
+        k3, f4, d = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        sift._check(lib.sift_hip_results_device(det.handle, ctypes.byref(k3), ctypes.byref(f4), ctypes.byref(d),
+                                                None, None, None), "results_device")
+        outs.append((torch.as_tensor(_Cai(k3.value, (cap, 3), "<f4"), device="cuda").clone(),
+                     torch.as_tensor(_Cai(f4.value, (cap, 4), "<f4"), device="cuda").clone(),
+                     torch.as_tensor(_Cai(d.value, (cap, 128), "<i2"), device="cuda").clone()))
+    ctx.__exit__(None, None, None)
+    torch.cuda.synchronize()
+    det.sync()
+    assert det.total_size == len(ref[-1][0])
+    for (k, f, d), r in zip(outs, ref):
+        n = len(r[0])
+        got = (k[:n].cpu().numpy(), f[:n].cpu().numpy(), d[:n].cpu().numpy().view(np.uint16))
+        assert_identical(got, r)
+
+
+def test_long_loop_memory_flat(sift):
+    import os
+
+    import psutil
+
+    frames = [torch.from_numpy(sift.synth_frame(i, W, H)).cuda() for i in range(4)]
+    torch.cuda.synchronize()
+    _, det = make_detector(sift, W, H, numFeatures=2000)
+    proc = psutil.Process(os.getpid())
+
+    def run(n):
+        for s in range(n):
+            det.detectAndComputeDevice(frames[s % 4].data_ptr(), W * 4, sync=(s % 10 == 9))
+        det.sync()
+
+    run(50)  # both lanes created, graphs warm
+    free0, rss0 = torch.cuda.mem_get_info()[0], proc.memory_info().rss
+    run(400)
+    free1, rss1 = torch.cuda.mem_get_info()[0], proc.memory_info().rss
+    assert abs(free1 - free0) <= 4 << 20, f"device memory moved by {(free0 - free1) / 2**20:.1f} MiB"
+    assert rss1 - rss0 <= 32 << 20, f"host RSS grew by {(rss1 - rss0) / 2**20:.1f} MiB"
+
+
+@pytest.mark.parametrize("u8", [False, True])
+def test_strided_large_host_frames(sift, u8):
+    """Host frames of >= 1 MB are staged by the copy pool (row ranges split over
+    threads): contiguous and strided (a view into a wider buffer) frames give
+    the results of the same frame through the device path."""
+    w, h = 1920, 1200
+    img = sift.synth_frame(4, w, h)
+    src = img.astype(np.uint8) if u8 else img
+    _, det = make_detector(sift, w, h, numOctaves=3, lanes=1)
+    dev = torch.from_numpy(img).cuda()
+    torch.cuda.synchronize()
+    det.detectAndComputeDevice(dev.data_ptr(), w * 4, sync=True)
+    ref = results(det)
+    det.detectAndCompute(src)
+    assert_identical(results(det), ref)
+    wide = np.zeros((h, w + 29), src.dtype)
+    wide[:, 3:3 + w] = src
+    det.detectAndCompute(wide[:, 3:3 + w])
+    assert_identical(results(det), ref)
+    det.copyToHost(False)  # keypoints only, from the same host copy
+    assert np.array_equal(det.final_kpts.view(np.uint32), ref[0].view(np.uint32))
