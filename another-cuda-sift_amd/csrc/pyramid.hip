@@ -1210,8 +1210,15 @@ __device__ __forceinline__ void extrema_block(const OctGeom& g, int o, float thr
 #ifndef SIFT_EX_MASK_LOADS
 #define SIFT_EX_MASK_LOADS 1
 #endif
+#if defined(SIFT_EX_DIAG) && (SIFT_EX_DIAG == 1 || SIFT_EX_DIAG == 3)  // traffic variants (wrong results): no outer-column loads
+    const bool l4 = xl < W, le = false;
+#else
     const bool l4 = !SIFT_EX_MASK_LOADS || xl < W, le = !SIFT_EX_MASK_LOADS || lane == 0 || lane == 63;
+#endif
     auto issue_row = [&](int y, f4 (&v)[NG], float (&e)[NG]) {
+#if defined(SIFT_EX_DIAG) && (SIFT_EX_DIAG == 2 || SIFT_EX_DIAG == 3)  // traffic variants: halo rows -> the wave's own rows
+        y = min(max(y, y0), y0 + TR - 1);
+#endif
         const int yc = min(max(y, 0), H - 1);
         const unsigned off4 = l4 ? (unsigned)(yc * pitch + xl) * 4u : 0x80000000u;
         const unsigned offe = le ? (unsigned)(yc * pitch + xe) * 4u : 0x80000000u;
@@ -1300,23 +1307,37 @@ __device__ __forceinline__ void extrema_block(const OctGeom& g, int o, float thr
         // Strip row m = 0 .. TR + 1 (image row y0 - 1 + m) is loaded into raw
         // set m % NS; once formed, its set is reloaded with strip row m + NS
         // (rows past the image: clamped reads, never tested).
-        constexpr int NS = EX4_AHEAD + 1, NR = TR + 2;
+        constexpr int NS = EX4_AHEAD + 1;
         // Streams end at the image's last tested row (H - 6): no load or test
         // past it (uniform).
         const int nsteps = NB == 1 ? 1 : min(NB, (min(H - 5, y0 + TR) - y0 + EX4_TR - 1) / EX4_TR);
+        const int nr = nsteps * EX4_TR + 2, yb = y0 + nsteps * EX4_TR;
+        // Odd waves stream bottom to top.  Vertically adjacent waves share
+        // two rows (each one's halo row is the other's edge row), and a row
+        // a wave loads at the start of its stream was loaded by a same-way
+        // neighbour at the end of its stream: by then the XCD's L2 (4 MiB
+        // against ~20 MB streamed meanwhile) had dropped it, and the halo
+        // rows came back over the fabric -- 1.19x the algorithmic bytes (the
+        // Infinity Cache served them, FETCH_SIZE counted them).  With
+        // alternating directions every shared row is loaded by both waves at
+        // the same end of their streams.  The 3x3x3 test is symmetric in
+        // the rows (exact max / min), so candidates are unchanged.
+        const bool up = (wave & 1) != 0;
+        auto strip_row = [&](int m) { return up ? yb - m : y0 - 1 + m; };   // image row of strip row m
+        auto tested_row = [&](int k) { return up ? yb - 1 - k : y0 + k; };  // image row of tested row k
         auto form = [&](int m, int km, f4 (&d4)[ND], float (&de)[ND]) {  // km = m % NS (compile-time)
 #pragma unroll
             for (int d = 0; d < ND; d++) {
                 d4[d] = rv[km][d + 1] - rv[km][d];
                 de[d] = rev[km][d + 1] - rev[km][d];
             }
-            if (m + NS < NR) issue_row(y0 - 1 + m + NS, rv[km], rev[km]);
+            if (m + NS < nr) issue_row(strip_row(m + NS), rv[km], rev[km]);
         };
 #pragma unroll
-        for (int m = 0; m < NS && m < NR; m++) issue_row(y0 - 1 + m, rv[m], rev[m]);
+        for (int m = 0; m < NS; m++) issue_row(strip_row(m), rv[m], rev[m]);
         form(0, 0, rd[0], re[0]);
         form(1, 1 % NS, rd[1], re[1]);
-        // Row y0 + k + 1 (strip row k + 2) enters ring slot (k + 2) % 3, row y0 + k is tested.
+        // Strip row k + 2 enters ring slot (k + 2) % 3, tested row k is tested.
 #pragma unroll 1
         for (int kb = 0; kb < nsteps * EX4_TR; kb += EX4_TR) {
 #pragma unroll
@@ -1324,7 +1345,8 @@ __device__ __forceinline__ void extrema_block(const OctGeom& g, int o, float thr
                 const int k = kb + k6;
                 const int A = k6 % 3, B = (k6 + 1) % 3, C = (k6 + 2) % 3;
                 form(k + 2, (k6 + 2) % NS, rd[C], re[C]);
-                emit_row(y0 + k, test_row(y0 + k, A, B, C));
+                const int r = tested_row(k);
+                emit_row(r, test_row(r, A, B, C));
             }
         }
     }

@@ -286,28 +286,28 @@ def cpu_baseline(a, cfg, c3_sets):
                      f"oracle/sift_oracle.cpp OpenMP {threads} threads",
            "cpu_model": cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": aff, "omp_num_threads": env}
     cpu["value_per_thread"] = round(cpu["value"] / threads, 3)
-    # Whole host.  The box's OMP_NUM_THREADS (16) is this job's CPU share and
-    # its rules cap worker pools at that share, so the other CPUs of the
-    # affinity mask are not used.  Instead: one thread on the same workload,
-    # and the all-core rate extrapolated linearly from the better per-thread
-    # rate -- an upper bound on what the host's cores could do (OpenMP
-    # scaling is sublinear), so GPU / value_all_cores understates the GPU.
-    oracle.detect_and_compute(imgs[1], p, threads=1)
-    m, t = 0, time.perf_counter()
-    while True:
-        oracle.detect_and_compute(imgs[m % 4], p, threads=1)
-        m += 1
-        if time.perf_counter() - t > a.cpu_seconds / 3 and m >= 2:
-            break
-    dt1 = time.perf_counter() - t
-    one = m * W * H / 1e6 / dt1
-    best = max(one, cpu["value_per_thread"])
-    cpu["value_1_thread"] = round(one, 3)
-    cpu["scaling_1_to_%d_threads" % threads] = round(cpu["value"] / one, 2)
-    cpu["cores_all"] = aff
-    cpu["value_all_cores"] = round(best * aff, 2)
-    cpu["value_all_cores_kind"] = (f"extrapolated: max(per-thread rate at 1 and {threads} threads) x {aff} CPUs "
-                                   "(upper bound; not run on all CPUs: the box's job share is OMP_NUM_THREADS)")
+    cpu["stage_ms_per_frame"] = {str(threads): oracle.stage_ms()}
+    # Thread scaling on the same workload, measured (1, 4 and the job's CPU
+    # share; the box's OMP_NUM_THREADS is that share, and its rules cap worker
+    # pools at it, so no figure is given for the host's other CPUs), with the
+    # per-stage wall times that say where the threads stop helping.
+    curve = {str(threads): cpu["value"]}
+    for th in (1, 4):
+        if th >= threads:
+            continue
+        oracle.detect_and_compute(imgs[1], p, threads=th)
+        m, t = 0, time.perf_counter()
+        while True:
+            oracle.detect_and_compute(imgs[m % 4], p, threads=th)
+            m += 1
+            if time.perf_counter() - t > a.cpu_seconds / 4 and m >= 2:
+                break
+        curve[str(th)] = round(m * W * H / 1e6 / (time.perf_counter() - t), 3)
+        cpu["stage_ms_per_frame"][str(th)] = oracle.stage_ms()
+    cpu["scaling_curve_mpix_s"] = dict(sorted(curve.items(), key=lambda kv: int(kv[0])))
+    if "1" in curve:
+        cpu["value_1_thread"] = curve["1"]
+        cpu["scaling_1_to_%d_threads" % threads] = round(cpu["value"] / curve["1"], 2)
     # C1: 752x480, cv::SIFT defaults (firstOctave -1, nfeatures 0), frames 0 and 1, knn-2 + ratio 0.8.
     p1 = oracle.params(nfeatures=0, firstOctave=-1)
     f0, f1 = sift.synth_frame(0, 752, 480), sift.synth_frame(1, 752, 480)

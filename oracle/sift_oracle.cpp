@@ -45,9 +45,13 @@
 #include <climits>
 #include <cmath>
 #include <cstring>
+#include <memory>
+#include <utility>
 #include <vector>
 #ifdef _OPENMP
 #include <omp.h>
+
+#include <chrono>
 #endif
 
 #ifndef SIFT_ORACLE_VEC
@@ -90,10 +94,37 @@ inline int cvRoundF(float v) { return (int)lrintf(v); }
 inline int cvRoundD(double v) { return (int)lrint(v); }
 inline int cvFloorF(float v) { return (int)floorf(v); }
 
+// Planes are allocated without zero-filling: every producer writes each pixel
+// (in parallel loops, so the pages are first touched by the threads that fill
+// them -- a serial zero-fill of fresh pages bounded the oracle's thread
+// scaling).
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U>&) {}
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        if constexpr (sizeof...(A) == 0)
+            ::new ((void*)p) U;
+        else
+            ::new ((void*)p) U(std::forward<A>(a)...);
+    }
+};
+
 struct Plane {
     int w = 0, h = 0;
-    std::vector<float> d;
-    void create(int W, int H) { w = W; h = H; d.assign((size_t)W * H, 0.f); }
+    std::vector<float, NoInitAlloc<float>> d;
+    void create(int W, int H) {
+        w = W;
+        h = H;
+        d.clear();
+        d.resize((size_t)W * H);
+    }
     float at(int r, int c) const { return d[(size_t)r * w + c]; }
     float& at(int r, int c) { return d[(size_t)r * w + c]; }
 };
@@ -196,7 +227,7 @@ void gaussianBlur(const Plane& src, Plane& dst, double sigma, int threads) {
 // D = S0*b0 + S1*b1 (VResizeLinearVec_32f, v_muladd on the SSE baseline = mul+add).
 // Exact for integer-valued inputs.  Reference: Resize.cu:6-64 with the wrong
 // target size (SURVEY A-6).
-void upsample2x(const Plane& src, Plane& dst) {
+void upsample2x(const Plane& src, Plane& dst, int threads) {
     const int W = src.w, H = src.h, DW = W * 2, DH = H * 2;
     std::vector<int> xs(DW), ys(DH);
     std::vector<float> ax(DW * 2), ay(DH * 2);
@@ -214,6 +245,7 @@ void upsample2x(const Plane& src, Plane& dst) {
     for (int d = 0; d < DH; d++) coeffs(d, H, ys[d], &ay[2 * d]);
     Plane hrow;
     hrow.create(DW, H);
+#pragma omp parallel for num_threads(nthreadsOr(threads)) schedule(static)
     for (int y = 0; y < H; y++)
         for (int x = 0; x < DW; x++) {
             int sx = xs[x];
@@ -221,6 +253,7 @@ void upsample2x(const Plane& src, Plane& dst) {
             hrow.at(y, x) = src.at(y, sx) * ax[2 * x] + src.at(y, sx1) * ax[2 * x + 1];
         }
     dst.create(DW, DH);
+#pragma omp parallel for num_threads(nthreadsOr(threads)) schedule(static)
     for (int y = 0; y < DH; y++) {
         int sy = ys[y], sy1 = std::min(sy + 1, H - 1);
         for (int x = 0; x < DW; x++) dst.at(y, x) = hrow.at(sy, x) * ay[2 * y] + hrow.at(sy1, x) * ay[2 * y + 1];
@@ -393,6 +426,20 @@ int autoOctaves(int w, int h, const Params& P) {
     return cvRoundD(std::log((double)std::min(bw, bh)) / std::log(2.) - 2) - P.firstOctave;
 }
 
+// Wall time per stage of the last detect_and_compute call (bench.py's CPU
+// baseline reports where the threads go): initial image, Gaussian pyramid, DoG,
+// 3x3x3 candidates, keypoints (refine + orientation + dedupe + retainBest),
+// descriptors.
+double g_stage_ms[6];
+struct StageClock {
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void mark(int i) {
+        const auto n = std::chrono::steady_clock::now();
+        g_stage_ms[i] = std::chrono::duration<double, std::milli>(n - t).count();
+        t = n;
+    }
+};
+
 class Sift {
 public:
     Sift(const Params& P, int threads) : P_(P), threads_(threads) {}
@@ -404,7 +451,7 @@ public:
         if (P_.firstOctave < 0) {
             float sig_diff = sqrtf(std::max(sigma * sigma - SIFT_INIT_SIGMA * SIFT_INIT_SIGMA * 4, 0.01f));
             Plane dbl;
-            upsample2x(img, dbl);
+            upsample2x(img, dbl, threads_);
             gaussianBlur(dbl, base, sig_diff, threads_);
         } else {
             float sig_diff = sqrtf(std::max(sigma * sigma - SIFT_INIT_SIGMA * SIFT_INIT_SIGMA, 0.01f));
@@ -434,6 +481,7 @@ public:
                     // resize(src, dst, Size(cols/2, rows/2), 0, 0, INTER_NEAREST): pixel (2y, 2x).
                     const Plane& src = pyr[(o - 1) * (L + 3) + L];
                     dst.create(src.w / 2, src.h / 2);
+#pragma omp parallel for num_threads(nthreadsOr(threads_)) schedule(static)
                     for (int y = 0; y < dst.h; y++)
                         for (int x = 0; x < dst.w; x++) dst.at(y, x) = src.at(2 * y, 2 * x);
                 } else {
@@ -453,7 +501,9 @@ public:
                 const Plane& b = gpyr[o * (L + 3) + i + 1];
                 Plane& d = dogpyr[o * (L + 2) + i];
                 d.create(a.w, a.h);
-                for (size_t k = 0; k < a.d.size(); k++) d.d[k] = b.d[k] - a.d[k];
+                const long np = (long)a.d.size();
+#pragma omp parallel for num_threads(nthreadsOr(threads_)) schedule(static)
+                for (long k = 0; k < np; k++) d.d[k] = b.d[k] - a.d[k];
             }
     }
 
@@ -703,20 +753,23 @@ public:
         }
     }
 
+    // Rows of a plane are scanned in parallel (OpenCV's parallel_for_ over
+    // rows, findScaleSpaceExtremaComputer) and concatenated in row order, so
+    // the list is the sequential scan's.
     void candidates(const std::vector<Plane>& dog, int nOct, std::vector<int>& quads) const {
         const int L = P_.L, thr = threshold();
         for (int o = 0; o < nOct; o++)
             for (int i = 1; i <= L; i++) {
                 const int idx = o * (L + 2) + i;
                 const Plane& img = dog[idx];
-                for (int r = SIFT_IMG_BORDER; r < img.h - SIFT_IMG_BORDER; r++)
+                const int r0 = SIFT_IMG_BORDER, r1 = img.h - SIFT_IMG_BORDER;
+                if (r1 <= r0) continue;
+                std::vector<std::vector<int>> rows(r1 - r0);
+#pragma omp parallel for num_threads(nthreadsOr(threads_)) schedule(static)
+                for (int r = r0; r < r1; r++)
                     for (int c = SIFT_IMG_BORDER; c < img.w - SIFT_IMG_BORDER; c++)
-                        if (isExtremum(dog, idx, r, c, thr)) {
-                            quads.push_back(o);
-                            quads.push_back(i);
-                            quads.push_back(r);
-                            quads.push_back(c);
-                        }
+                        if (isExtremum(dog, idx, r, c, thr)) rows[r - r0].insert(rows[r - r0].end(), {o, i, r, c});
+                for (auto& v : rows) quads.insert(quads.end(), v.begin(), v.end());
             }
     }
 
@@ -898,14 +951,19 @@ public:
     // [OpenCV 4.x sift.dispatch.cpp: detectAndCompute], useProvidedKeypoints = false.
     std::vector<Keypoint> detect(const Plane& img, std::vector<Plane>& gpyr) const {
         const int L = P_.L;
+        StageClock clk;
         Plane base;
         initialImage(img, base);
+        clk.mark(0);
         const int nOct = autoOctaves(img.w, img.h, P_);
         gaussianPyramid(base, nOct, gpyr);
+        clk.mark(1);
         std::vector<Plane> dog;
         dogPyramid(gpyr, dog);
+        clk.mark(2);
         std::vector<int> quads;
         candidates(dog, nOct, quads);
+        clk.mark(3);
         const long nc = (long)quads.size() / 4;
         std::vector<std::vector<Keypoint>> per(nc);
 #pragma omp parallel for num_threads(nthreadsOr(threads_)) schedule(dynamic, 64)
@@ -946,6 +1004,7 @@ public:
                 kpt.size *= scale;
             }
         }
+        clk.mark(4);
         return kpts;
     }
 
@@ -1058,11 +1117,20 @@ long sift_oracle_detect_and_compute(const float* img, int w, int h, const sift_o
         for (long i = 0; i < m; i++)
             out[i] = sift_oracle_kpt{kpts[i].x, kpts[i].y, kpts[i].size, kpts[i].angle, kpts[i].response,
                                      kpts[i].octave};
+    StageClock clk;
+    g_stage_ms[5] = 0;
     if (desc && m > 0) {
         std::vector<Keypoint> head(kpts.begin(), kpts.begin() + m);
         s.descriptors(gpyr, head, desc);
+        clk.mark(5);
     }
     return n;
+}
+
+int sift_oracle_stage_ms(double* out, int cap) {
+    const int n = std::min(cap, 6);
+    for (int i = 0; i < n; i++) out[i] = g_stage_ms[i];
+    return 6;
 }
 
 int sift_oracle_compute_descriptors(const float* img, int w, int h, const sift_oracle_params* p,

@@ -81,6 +81,11 @@ long sift_oracle_detect_and_compute(const float* img, int w, int h,
 
 /* Descriptors for given keypoints (OpenCV's useProvidedKeypoints=false path
  * reuses this), computed on the pyramid of `img`. */
+/* Wall time (ms) of the stages of the last sift_oracle_detect_and_compute call:
+ * initial image, Gaussian pyramid, DoG, 3x3x3 candidates, keypoints (refine,
+ * orientation, dedupe, retainBest), descriptors.  Returns 6. */
+int sift_oracle_stage_ms(double* out, int cap);
+
 int sift_oracle_compute_descriptors(const float* img, int w, int h,
                                     const sift_oracle_params* p,
                                     const sift_oracle_kpt* kpts, long n, float* desc);

@@ -77,6 +77,9 @@ def lib(variant: str = "pinned") -> ctypes.CDLL:
         L.sift_oracle_extrema.restype = l
         L.sift_oracle_detect_and_compute.argtypes = [vp, i, i, P, i, vp, vp, l]
         L.sift_oracle_detect_and_compute.restype = l
+        if hasattr(L, "sift_oracle_stage_ms"):
+            L.sift_oracle_stage_ms.argtypes = [vp, i]
+            L.sift_oracle_stage_ms.restype = i
         L.sift_oracle_compute_descriptors.argtypes = [vp, i, i, P, vp, l, vp]
         L.sift_oracle_knn2.argtypes = [vp, l, vp, l, i, vp, vp]
         L.sift_oracle_variant.restype = ctypes.c_char_p
@@ -171,3 +174,13 @@ def knn2(query: np.ndarray, train: np.ndarray, threads: int = 0):
     dist = np.zeros((len(q), 2), np.float32)
     lib().sift_oracle_knn2(q.ctypes.data, len(q), t.ctypes.data, len(t), threads, idx.ctypes.data, dist.ctypes.data)
     return idx, dist
+
+
+STAGES = ("initial", "pyramid", "dog", "candidates", "keypoints", "descriptors")
+
+
+def stage_ms(variant: str = "pinned") -> dict:
+    """Wall time per stage (ms) of the last detect_and_compute call of this build."""
+    out = np.zeros(6, np.float64)
+    lib(variant).sift_oracle_stage_ms(out.ctypes.data, 6)
+    return dict(zip(STAGES, (round(float(x), 3) for x in out)))
