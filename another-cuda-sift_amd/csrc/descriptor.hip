@@ -162,8 +162,8 @@ constexpr int kDescWaves = 6;
 template <int kDT>
 __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* __restrict__ jobs, const Counters* __restrict__ ctr,
                                                    const unsigned* __restrict__ range_keys,
-                                                   uint16_t* __restrict__ desc, Counters* __restrict__ host_ctr,
-                                                   long fs, unsigned nf) {
+                                                   uint16_t* __restrict__ desc, Sidecar sidecar,
+                                                   Counters* __restrict__ host_ctr, long fs, unsigned nf) {
     // Two u32 fixed-point histograms so that each sample's orientation pair
     // (o0, o0+1) is one naturally aligned ds_add_u64 (low word o0, high word
     // o0+1): even o0 -> histE[cell*10 + o], odd o0 -> histO[cell*10 + 1 + o]
@@ -173,7 +173,9 @@ __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* _
     __shared__ __attribute__((aligned(16))) float sq[128];
     __shared__ int rowpre[kMaxRows + 4], rowlo[kMaxRows], rowln[kMaxRows];
     __shared__ float s_norm[12];
+    __shared__ int s_cn[2];  // |codes|^2 of the keypoint's two halves (sidecar key bias)
     constexpr int kPer = kDT >= 128 ? 1 : 128 / kDT;  // descriptor entries per thread in the epilogue
+    static_assert(kPer == 1, "the sidecar norm takes entries 0-63 / 64-127 from waves 0 / 1");
 
     const int tid = threadIdx.x, lane = tid & 63;
     // 1-D grid, frame = block % nf: consecutive workgroups are dispatched to
@@ -186,6 +188,8 @@ __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* _
     ctr = fptr(ctr, foff);
     range_keys = fptr(range_keys, foff);
     desc = fptr(desc, foff);
+    sidecar.codes = fptr(sidecar.codes, foff);
+    sidecar.keys = fptr(sidecar.keys, foff);
     host_ctr += frame;
     const unsigned n = ctr->final_n;
     // The frame's counters are final before this (last) kernel starts: hand
@@ -475,14 +479,26 @@ __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* _
         }
         lds_barrier();
         const float scale = s_norm[8];
+        const unsigned po = (unsigned)jb.out;  // output row (jobs run longest first, JobOrder)
+        int c2 = 0;  // this thread's share of |codes|^2
 #pragma unroll
         for (int h = 0; h < kPer; h++) {
             int v = cv_round(val[h] * scale);
             v = v < 0 ? 0 : (v > 255 ? 255 : v);
             const _Float16 hv = (_Float16)(float)v;
-            if (tid + kDT * h < 128) desc[(size_t)p * 128 + tid + kDT * h] = __builtin_bit_cast(uint16_t, hv);
+            if (tid + kDT * h < 128) {
+                desc[(size_t)po * 128 + tid + kDT * h] = __builtin_bit_cast(uint16_t, hv);
+                sidecar.codes[(size_t)po * 128 + tid + kDT * h] = (int8_t)(v - 128);
+                c2 += (v - 128) * (v - 128);
+            }
         }
+        // Sidecar key bias: each wave's sum (DPP scan, total in lane 63) to
+        // LDS before the barrier that ends the keypoint, thread 0 adds the
+        // two after it (s_cn is next written after several more barriers).
+        c2 = __builtin_amdgcn_readlane(wave_incl_scan(c2), 63);
+        if (lane == 0 && tid < 128) s_cn[tid >> 6] = c2;
         lds_barrier();  // sq / histograms are rewritten by the next keypoint
+        if (tid == 0) sidecar.keys[po] = -(256 * (s_cn[0] + s_cn[1]) + (int)(po & 255));
     }
 }
 
@@ -545,7 +561,7 @@ void upload_desc_exp_table(const float* tab64) {
 
 __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __restrict__ jobs,
                                                                const Counters* __restrict__ ctr,
-                                                               uint16_t* __restrict__ desc,
+                                                               uint16_t* __restrict__ desc, Sidecar sidecar,
                                                                Counters* __restrict__ host_ctr, long fs, unsigned nf) {
     __shared__ float s_tab[64];
     // Chunk sample s: per target cell (dr, dc) one float4 {P.x, P.y, S.x, S.y}
@@ -571,6 +587,8 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
     jobs = fptr(jobs, foff);
     ctr = fptr(ctr, foff);
     desc = fptr(desc, foff);
+    sidecar.codes = fptr(sidecar.codes, foff);
+    sidecar.keys = fptr(sidecar.keys, foff);
     host_ctr += frame;
     const unsigned n = ctr->final_n;
     static_assert(sizeof(Counters) <= 4 * kExactWG, "counters handed over by one workgroup");
@@ -845,19 +863,25 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
         b0 = b0 < 0 ? 0 : (b0 > 255 ? 255 : b0);
         b1 = b1 < 0 ? 0 : (b1 > 255 ? 255 : b1);
         const _Float16 h0 = (_Float16)(float)b0, h1 = (_Float16)(float)b1;
-        reinterpret_cast<unsigned*>(desc + (size_t)p * 128)[lane] =
+        const unsigned po = (unsigned)jb.out;  // output row (jobs run longest first, JobOrder)
+        reinterpret_cast<unsigned*>(desc + (size_t)po * 128)[lane] =
             (unsigned)__builtin_bit_cast(uint16_t, h0) | (unsigned)__builtin_bit_cast(uint16_t, h1) << 16;
+        // Matcher sidecar: int8 codes and the key bias (k_descriptor's epilogue).
+        reinterpret_cast<unsigned short*>(sidecar.codes + (size_t)po * 128)[lane] =
+            (unsigned short)((b0 - 128) & 255) | (unsigned short)(((b1 - 128) & 255) << 8);
+        const int c2 = __builtin_amdgcn_readlane(wave_incl_scan((b0 - 128) * (b0 - 128) + (b1 - 128) * (b1 - 128)), 63);
+        if (lane == 0) sidecar.keys[po] = -(256 * c2 + (int)(po & 255));
         wave_lds_sync();  // rowpre / raw / s_norm are rewritten by the next keypoint
     }
 }
 
 void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned* range_keys, uint16_t* desc,
-                       Counters* host_ctr, const KeypointParams& kp, const Frames& fr, hipStream_t s) {
+                       Sidecar sidecar, Counters* host_ctr, const KeypointParams& kp, const Frames& fr, hipStream_t s) {
     if (kp.descExact) {
         // One wave per keypoint; each workgroup loops over keypoints.
         const int per = fr.nf <= 1 ? 2048 : std::max(512, 8192 / fr.nf);
-        hipLaunchKernelGGL(k_descriptor_exact, dim3(per * fr.nf), dim3(kExactWG), 0, s, jobs, ctr, desc, host_ctr,
-                           fr.stride, (unsigned)fr.nf);
+        hipLaunchKernelGGL(k_descriptor_exact, dim3(per * fr.nf), dim3(kExactWG), 0, s, jobs, ctr, desc, sidecar,
+                           host_ctr, fr.stride, (unsigned)fr.nf);
         return;
     }
     // Threads per keypoint: 256 for a single frame (128: 34.6 us, 512: 47.6 vs
@@ -865,7 +889,7 @@ void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned*
     constexpr int kSingleDT = 256, kBatchDT = 128;
     if (fr.nf <= 1) {
         hipLaunchKernelGGL(k_descriptor<kSingleDT>, dim3(8192), dim3(kSingleDT), 0, s, jobs, ctr, range_keys, desc,
-                           host_ctr, fr.stride, 1u);
+                           sidecar, host_ctr, fr.stride, 1u);
     } else {
         // Workgroups per frame: 2048 at 8 frames (16384 in all).  The bigger
         // grids this kernel once had filled every CU slot and kept the other
@@ -874,7 +898,7 @@ void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned*
         // (tools/grid_sweep.sh).
         const int per = std::max(1024, 16384 / fr.nf);
         hipLaunchKernelGGL(k_descriptor<kBatchDT>, dim3(per * fr.nf), dim3(kBatchDT), 0, s, jobs, ctr, range_keys,
-                           desc, host_ctr, fr.stride, (unsigned)fr.nf);
+                           desc, sidecar, host_ctr, fr.stride, (unsigned)fr.nf);
     }
 }
 

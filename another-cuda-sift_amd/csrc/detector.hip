@@ -178,6 +178,43 @@ struct TimingAgg {
 
 void sift_amd::set_last_error(const std::string& msg) { g_err = msg; }
 
+namespace {
+
+// Matcher sidecars of the descriptor buffers the detector handles hand out
+// (one per results slot and frame of every lane): exact buffer base -> its
+// int8 codes and key biases (sift_kernels.h Sidecar).  sift_hip_match_* look
+// the query and train pointers up and, when both are detector buffers, match
+// their codes directly (k_match_direct) instead of converting the fp16 rows.
+struct SidecarReg {
+    const uint16_t* desc;
+    Sidecar side;
+    int cap;
+    const void* owner;
+};
+std::mutex g_side_mu;
+std::vector<SidecarReg> g_side;
+
+void register_sidecar(const void* owner, const uint16_t* desc, Sidecar side, int cap) {
+    std::lock_guard<std::mutex> g(g_side_mu);
+    g_side.push_back(SidecarReg{desc, side, cap, owner});
+}
+void unregister_sidecars(const void* owner) {
+    std::lock_guard<std::mutex> g(g_side_mu);
+    g_side.erase(std::remove_if(g_side.begin(), g_side.end(), [&](const SidecarReg& r) { return r.owner == owner; }),
+                 g_side.end());
+}
+bool find_sidecar(const uint16_t* desc, int n, Sidecar* out) {
+    std::lock_guard<std::mutex> g(g_side_mu);
+    for (const SidecarReg& r : g_side)
+        if (r.desc == desc && n <= r.cap) {
+            *out = r.side;
+            return true;
+        }
+    return false;
+}
+
+}  // namespace
+
 // Results slots per compute lane: frames f-1 .. f+2 of a lane never share one.
 constexpr int kResultSlots = 4;
 constexpr int kMaxLanes = 4;
@@ -219,8 +256,9 @@ struct Lane {
 // every arena of every lane).
 struct ArenaLayout {
     size_t input = 0, up = 0, pyr = 0, cand = 0, ref = 0, ori = 0, slot = 0, order = 0, jobs = 0, range = 0,
-           bcount = 0, boff = 0, bitmap = 0, ctr = 0;
+           bcount = 0, boff = 0, bitmap = 0, ctr = 0, jord = 0;
     size_t k3[kResultSlots] = {}, f4[kResultSlots] = {}, desc[kResultSlots] = {};
+    size_t codes[kResultSlots] = {}, ckeys[kResultSlots] = {};  // matcher sidecar of desc (Sidecar)
     size_t octave[kMaxOctaves] = {};  // float offset of each octave's planes inside the pyramid
 };
 
@@ -288,6 +326,7 @@ struct sift_hip_detector {
     int* dSlot = nullptr;
     int* dOrder = nullptr;
     DescJob* dJobs = nullptr;  // per final keypoint, written by k_bucket_rank
+    JobOrder* dJord = nullptr;  // descriptor job order (k_order -> k_rank_final)
     unsigned* dRange = nullptr;  // 2 * kRangeSlots pixel-range keys (initial blur -> descriptor)
     unsigned* dBcount = nullptr;
     unsigned* dBoff = nullptr;
@@ -299,6 +338,7 @@ struct sift_hip_detector {
     float* dKpts3[kSlots] = {};
     float* dFeats4[kSlots] = {};
     uint16_t* dDesc[kSlots] = {};
+    Sidecar dSide[kSlots] = {};
     int cur = 0, count = 0, prevCount = 0;  // frec(current).slot and the counts of current, current - 1
     bool countsValid = true;  // count / prevCount / the slot's host counters read after the frame completed
 
@@ -366,6 +406,7 @@ struct sift_hip_detector {
     }
 
     ~sift_hip_detector() {
+        unregister_sidecars(this);
         if (allocated) {
             (void)hipSetDevice(device);
             for (int k = 0; k < nLanes; k++) {
@@ -462,10 +503,9 @@ void setup_taps(sift_hip_detector* d) {
     }
     d->layerTaps.resize(L + 3);
     for (int i = 0; i < L + 3; i++) d->layerTaps[i] = gaussian_taps(sig[i]);
-#ifndef SIFT_TAIL
-#define SIFT_TAIL 1  // the pyramid tail for the small octaves (A/B builds: 0)
-#endif
-    d->tailOct = SIFT_TAIL && L + 3 <= kTailMaxPlanes ? tail_first_octave(d->pyr, d->layerTaps.data(), L) : d->nOct;
+    // The pyramid tail for the small octaves.  (Measured alternative, round
+    // 4: per-plane launches -- 752x480 sync 0.2177 vs 0.2094-0.2107 ms.)
+    d->tailOct = L + 3 <= kTailMaxPlanes ? tail_first_octave(d->pyr, d->layerTaps.data(), L) : d->nOct;
     d->threshold = (float)(int)std::floor(0.5 * d->cfg.contrastThreshould / L * 255 * 1.0);
     d->kp.contrastThreshold = (float)d->cfg.contrastThreshould;
     d->kp.edgeThreshold = (float)d->cfg.edgeThreshould;
@@ -534,6 +574,7 @@ void bind_lane(sift_hip_detector* d, int k) {
     d->dSlot = reinterpret_cast<int*>(A + a.slot);
     d->dOrder = reinterpret_cast<int*>(A + a.order);
     d->dJobs = reinterpret_cast<DescJob*>(A + a.jobs);
+    d->dJord = reinterpret_cast<JobOrder*>(A + a.jord);
     d->dRange = reinterpret_cast<unsigned*>(A + a.range);
     d->dBcount = reinterpret_cast<unsigned*>(A + a.bcount);
     d->dBoff = reinterpret_cast<unsigned*>(A + a.boff);
@@ -543,6 +584,7 @@ void bind_lane(sift_hip_detector* d, int k) {
         d->dKpts3[b] = reinterpret_cast<float*>(A + a.k3[b]);
         d->dFeats4[b] = reinterpret_cast<float*>(A + a.f4[b]);
         d->dDesc[b] = reinterpret_cast<uint16_t*>(A + a.desc[b]);
+        d->dSide[b] = Sidecar{reinterpret_cast<int8_t*>(A + a.codes[b]), reinterpret_cast<int*>(A + a.ckeys[b])};
     }
     d->hCtr = L.hCtr;
     d->hCtrDev = L.hCtrDev;
@@ -615,6 +657,7 @@ int allocate(sift_hip_detector* d) {
     a.slot = take(sizeof(int) * capO);
     a.order = take(sizeof(int) * capO);
     a.jobs = take(sizeof(DescJob) * capF);
+    a.jord = take(sizeof(JobOrder));
     a.range = take(sizeof(unsigned) * 2 * 2 * kRangeSlots);  // one set per frame parity
     a.bcount = take(sizeof(unsigned) * (size_t)d->kp.numBuckets);
     a.boff = take(sizeof(unsigned) * (size_t)d->kp.numBuckets);
@@ -624,6 +667,8 @@ int allocate(sift_hip_detector* d) {
         a.k3[b] = take(sizeof(float) * 3 * (size_t)capF);
         a.f4[b] = take(sizeof(float) * 4 * (size_t)capF);
         a.desc[b] = take(sizeof(uint16_t) * 128 * (size_t)capF);
+        a.codes[b] = take(128 * (size_t)capF);
+        a.ckeys[b] = take(sizeof(int) * (size_t)capF);
     }
     d->afs = (long)off;
     upload_exp_tab();
@@ -657,6 +702,11 @@ int add_lane(sift_hip_detector* d) {
             HIPCHK(hipEventRecord(d->evRead[i], L.stream));
         }
     bind_lane(d, k);
+    for (int i = 0; i < d->B; i++)
+        for (int b = 0; b < d->kSlots; b++)
+            register_sidecar(d, fptr(d->dDesc[b], (long)i * d->afs),
+                             Sidecar{fptr(d->dSide[b].codes, (long)i * d->afs), fptr(d->dSide[b].keys, (long)i * d->afs)},
+                             (int)d->kp.capFinal);
     return build_graphs(d);
 }
 
@@ -832,8 +882,8 @@ void enqueue_order(sift_hip_detector* d, int slot, int nf) {
     const Frames fr{nf, d->afs};
     if (d->kp.numBuckets <= kOrderMaxBuckets) {
         d->timed("order", 0, [&] {
-            launch_order(d->dOri, d->dCtr, range_keys(d, parity ^ 1), d->dBcount, d->dBoff, d->dSlot, d->dOrder, d->kp,
-                         fr, s);
+            launch_order(d->pyr, d->dOri, d->dCtr, range_keys(d, parity ^ 1), d->dBcount, d->dBoff, d->dSlot, d->dOrder,
+                         d->dJord, d->kp, fr, s);
         });
     } else {
         d->timed("select", 0, [&] { launch_select(d->dOri, d->dCtr, range_keys(d, parity ^ 1), d->kp, fr, s); });
@@ -845,7 +895,7 @@ void enqueue_order(sift_hip_detector* d, int slot, int nf) {
     }
     d->timed("bucket_rank", 0, [&] {
         if (d->kp.numBuckets <= kOrderMaxBuckets)
-            launch_rank_final(d->pyr, d->dOri, d->dBcount, d->dBoff, d->dOrder, d->dCtr, d->dJobs, d->dKpts3[slot],
+            launch_rank_final(d->pyr, d->dOri, d->dBcount, d->dBoff, d->dOrder, d->dCtr, d->dJord, d->dJobs, d->dKpts3[slot],
                               d->dFeats4[slot], d->kp, fr, s);
         else  // bucket_count needs zeroed counts: the bucket-parallel ranking re-zeroes them
             launch_bucket_rank(d->pyr, d->dOri, d->dBcount, d->dBoff, d->dOrder, d->dCtr, d->dJobs, d->dKpts3[slot],
@@ -856,7 +906,8 @@ void enqueue_order(sift_hip_detector* d, int slot, int nf) {
 void enqueue_descriptor(sift_hip_detector* d, int slot, int nf) {
     const Frames fr{nf, d->afs};
     d->timed("descriptor", 0, [&] {
-        launch_descriptor(d->dJobs, d->dCtr, range_keys(d, slot & 1), d->dDesc[slot], d->hCtrDev + (size_t)slot * d->B,
+        launch_descriptor(d->dJobs, d->dCtr, range_keys(d, slot & 1), d->dDesc[slot], d->dSide[slot],
+                          d->hCtrDev + (size_t)slot * d->B,
                           d->kp, fr, d->stream);
     });
 }
@@ -1343,7 +1394,7 @@ int dump_stage_files(sift_hip_detector* d) {
              "  \"oriented.rec\": \"OriKpt [slots] {f32 x, y, size, angle, response; i32 octave, bucket, sub}; "
              "bucket 0xffffffff = hole\",\n"
              "  \"jobs.rec\": \"DescJob [keypoints] 64 B {i64 plane o*(L+3)+layer; f32 cos_t, sin_t, angle, hist_width; "
-             "i32 ptx, pty, rows, cols, pitch, radius, pad[4]}\",\n"
+             "i32 ptx, pty, rows, cols, pitch, radius, out (the output row), pad[3]}; jobs run longest first\",\n"
              "  \"range.u32\": \"u32 [2][%d] pixel-range keys of the frame\",\n"
              "  \"counters.u32\": \"u32 [8] {cand, refined, oriented, final, overflow, retainBest threshold bits, "
              "order entries, 0}\"}\n}\n",
@@ -2030,6 +2081,7 @@ struct sift_hip_matcher {
     unsigned* dFlags = nullptr;           // per set slot: == epoch if the set is not all integers 0..255
     long codeRows = 0;
     unsigned epoch = 0;
+    bool sidecars = true;  // single pairs of detector buffers: match their sidecar codes (k_match_direct)
     ~sift_hip_matcher() {
         (void)hipSetDevice(device);
         for (void* p : {(void*)dKeys, (void*)dDone, (void*)dMatch, (void*)dCodes, (void*)dRowKeys, (void*)dFlags})
@@ -2076,6 +2128,12 @@ int sift_hip_matcher_create(int device, int max_query, int max_train, int max_pa
     return SIFT_HIP_OK;
 }
 
+int sift_hip_matcher_set_sidecars(sift_hip_matcher_t m, int enable) {
+    if (!m) return fail(SIFT_HIP_ERR_INVALID, "null matcher");
+    m->sidecars = enable != 0;
+    return SIFT_HIP_OK;
+}
+
 int sift_hip_matcher_destroy(sift_hip_matcher_t m) {
     delete m;
     return SIFT_HIP_OK;
@@ -2085,6 +2143,18 @@ int sift_hip_match_batched(sift_hip_matcher_t m, int P, const uint16_t* const* q
                            const uint16_t* const* t, const int* nt, float ratio, int ratio_on_squared, int* idx2,
                            float* d2, int* match, void* stream) {
     if (!m || P <= 0 || P > m->maxP || !q || !nq || !t || !nt) return fail(SIFT_HIP_ERR_INVALID, "bad batch");
+    Sidecar sq{}, st{};
+    if (P == 1 && m->sidecars && nq[0] > 0 && nt[0] > 0 && nq[0] <= m->maxQ && nt[0] <= m->maxT &&
+        find_sidecar(q[0], nq[0], &sq) && find_sidecar(t[0], nt[0], &st)) {
+        // Both sets are detector buffers: their codes are ready (no conversion).
+        HIPCHK(hipSetDevice(m->device));
+        const MatchPair pr{q[0], t[0], nq[0], nt[0], 0, 0, 0, 0, 0, 0};
+        launch_match_direct(pr, sq.codes, sq.keys, st.codes, st.keys, m->dCodes + (size_t)m->codeRows * 128,
+                            m->dRowKeys + m->codeRows, m->dKeys, m->dDone, ratio, ratio_on_squared, idx2, d2, match,
+                            (hipStream_t)stream);
+        HIPCHK(hipGetLastError());
+        return SIFT_HIP_OK;
+    }
     MatchBatch b{};
     MatchSets sets{};
     b.P = P;

@@ -314,14 +314,11 @@ __device__ __forceinline__ void write_match(int i1, float e1, int i2, float e2, 
 // its LDS slot is lane x 16 B).
 // ---------------------------------------------------------------------------
 constexpr int kTileBytes = kMatchTileRows * 128;
-#ifndef SIFT_MATCH_BATCH_NW
-#define SIFT_MATCH_BATCH_NW 8
-#endif
-#ifndef SIFT_MATCH_BATCH_QBW
-#define SIFT_MATCH_BATCH_QBW 2
-#endif
-constexpr int kMatchBatchNW = SIFT_MATCH_BATCH_NW;    // waves per k_match_batch workgroup
-constexpr int kMatchBatchQBW = SIFT_MATCH_BATCH_QBW;  // 32-query blocks per wave (512 queries per workgroup)
+// Waves per k_match_batch workgroup and 32-query blocks per wave (512 queries
+// per workgroup).  (Measured alternative, round 3: 16 waves x 1 block, 42.1
+// vs 39.1 us per C5 launch.)
+constexpr int kMatchBatchNW = 8;
+constexpr int kMatchBatchQBW = 2;
 constexpr int kMatchBatchQB = 32 * kMatchBatchQBW * kMatchBatchNW;
 constexpr int kMatchBatchWgPerCu = 2 * 8 / kMatchBatchNW > 0 ? 2 * 8 / kMatchBatchNW : 1;  // register budget: 16 waves per CU
 constexpr int kChunkRows = kChunkTiles * kMatchTileRows;
@@ -685,24 +682,112 @@ __global__ __launch_bounds__(64 * NW, (kMatchBatchWgPerCu * NW) / 4) void k_matc
                        1u, (unsigned)S, qv, o, ratio, ratio_on_squared, idx2, d2out, match);
 }
 
-#ifndef SIFT_MATCH_WG_TARGET_SINGLE
-#define SIFT_MATCH_WG_TARGET_SINGLE 256  // single pairs: workgroups a launch aims for when choosing train splits
-#endif
-#ifndef SIFT_MATCH_NW_SINGLE
-#define SIFT_MATCH_NW_SINGLE 4  // single pairs: waves per workgroup
-#endif
-#ifndef SIFT_MATCH_QBW_SINGLE
-#define SIFT_MATCH_QBW_SINGLE 2  // single pairs: 32-query blocks per wave (4 x 2: 256 queries per workgroup)
-#endif
-constexpr int kMatchSingleQB = 32 * SIFT_MATCH_QBW_SINGLE * SIFT_MATCH_NW_SINGLE;
-#ifndef SIFT_MATCH_FUSED_SINGLE
-#define SIFT_MATCH_FUSED_SINGLE 1  // single pairs: no prep launch (tools A/B builds set 0)
-#endif
+// ---------------------------------------------------------------------------
+// k_match_direct: one pair of detector-produced descriptor sets, read through
+// their sidecars (int8 codes + key bias, written by the descriptor kernels:
+// no conversion, no prep launch).  The integer path of k_match_batch with the
+// codes and keys addressed directly: query operands from the query sidecar,
+// the split's train key groups streamed through two LDS chunks by LDS-DMA.
+// grid = (query blocks of 32 QBW NW, splits S of whole key groups).
+// ---------------------------------------------------------------------------
+template <int NW, int QBW>
+__global__ __launch_bounds__(64 * NW) void k_match_direct(
+    MatchPair pr, const int8_t* __restrict__ qc, const int* __restrict__ qk, const int8_t* __restrict__ tc,
+    const int* __restrict__ tk, const int8_t* __restrict__ zc, const int* __restrict__ zk, int S,
+    unsigned long long* __restrict__ keys, unsigned* __restrict__ done, float ratio, int ratio_on_squared,
+    int* __restrict__ idx2, float* __restrict__ d2out, int* __restrict__ match) {
+    constexpr int QB = 32 * QBW * NW;
+    static_assert(QB <= 64 * NW, "the write-out gives each thread one query: at most 2 query blocks per wave");
+    __shared__ __attribute__((aligned(16))) int8_t s_codes[2][kChunkTiles * kTileBytes];
+    __shared__ __attribute__((aligned(16))) int s_key[2][kChunkRows];
+    __shared__ unsigned s_last;
+    static_assert(sizeof(Top2) * QB <= sizeof(s_codes), "results alias the code tiles");
+    Top2* const s_res = reinterpret_cast<Top2*>(&s_codes[0][0]);
+    const int q0 = blockIdx.x * QB;
+    if (q0 >= pr.nq) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, col = lane & 31, h = lane >> 5;
+    const int ntiles = (pr.nt + kMatchTileRows - 1) / kMatchTileRows;
+    const int tps = ((ntiles + S - 1) / S + kGroupTiles - 1) / kGroupTiles * kGroupTiles;  // whole key groups
+    const int tb = min(ntiles, (int)blockIdx.y * tps), te = min(ntiles, tb + tps);
+    const int q0w = q0 + 32 * QBW * w;
+    Top2 res[QBW];
+    {
+        if (tb < te)  // the first chunk's DMA before the query loads: both round trips overlap
+            stage_dma<NW>(tc, tk, pr.nt, tb * kMatchTileRows, min(kChunkTiles, te - tb), zc, zk, s_codes[0], s_key[0],
+                          w, lane);
+        i32x4 bq[QBW][4];
+        int qn[QBW];
+        load_queries<QBW>(qc, qk, pr.nq, q0w, col, h, bq, qn);
+        Best best[QBW];
+#pragma unroll
+        for (int qb = 0; qb < QBW; qb++) best[qb] = Best{kNone, kNone, kNone, kNone};
+        int buf = 0;
+        for (int c0 = tb; c0 < te; c0 += kChunkTiles, buf ^= 1) {
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            const int c1 = c0 + kChunkTiles;
+            if (c1 < te)
+                stage_dma<NW>(tc, tk, pr.nt, c1 * kMatchTileRows, min(kChunkTiles, te - c1), zc, zk, s_codes[buf ^ 1],
+                              s_key[buf ^ 1], w, lane);
+            chunk_top2(s_codes[buf], s_key[buf], min(kChunkTiles, te - c0), c0 * kMatchTileRows, col, h, bq, best);
+        }
+#pragma unroll
+        for (int qb = 0; qb < QBW; qb++) res[qb] = finish_best(best[qb], qn[qb]);
+    }
+    __syncthreads();  // s_res aliases the code tiles
+    if (h == 0) {
+#pragma unroll
+        for (int qb = 0; qb < QBW; qb++) s_res[32 * QBW * w + 32 * qb + col] = res[qb];
+    }
+    __syncthreads();
+    const int q = q0 + tid;
+    const bool qv = tid < QB && q < pr.nq;
+    const size_t o = (size_t)pr.out_off + q;
+    if (S == 1) {
+        if (qv) write_top2(s_res[tid], o, ratio, ratio_on_squared, idx2, d2out, match);
+        return;
+    }
+    merge_contribution(s_res, &s_last, keys + 2 * (size_t)q0, done + blockIdx.x, 1u, (unsigned)S, qv, o, ratio,
+                       ratio_on_squared, idx2, d2out, match);
+}
+
+// Direct single pairs: 4 waves x 1 query block (128 queries per workgroup, the
+// done-counter block), one key group (256 train rows) per split up to
+// kDirectWgTarget workgroups.
+constexpr int kDirectNW = 4, kDirectQBW = 1, kDirectQB = 32 * kDirectNW * kDirectQBW, kDirectWgTarget = 256;
+
+int match_direct_splits(int nq, int nt) {
+    const int ntiles = (nt + kMatchTileRows - 1) / kMatchTileRows, groups = (ntiles + kGroupTiles - 1) / kGroupTiles;
+    const int qblocks = (max(nq, 1) + kDirectQB - 1) / kDirectQB;
+    int S = max(1, min(groups, kDirectWgTarget / max(qblocks, 1)));
+    const int tps = ((ntiles + S - 1) / S + kGroupTiles - 1) / kGroupTiles * kGroupTiles;
+    return tps > 0 ? max(1, (ntiles + tps - 1) / tps) : 1;
+}
+
+void launch_match_direct(const MatchPair& pr, const int8_t* qc, const int* qk, const int8_t* tc, const int* tk,
+                         const int8_t* zc, const int* zk, unsigned long long* keys, unsigned* done, float ratio,
+                         int ratio_on_squared, int* idx2, float* d2, int* match, hipStream_t s) {
+    const int S = match_direct_splits(pr.nq, pr.nt);
+    dim3 g((max(pr.nq, 1) + kDirectQB - 1) / kDirectQB, S, 1);
+    hipLaunchKernelGGL((k_match_direct<kDirectNW, kDirectQBW>), g, dim3(64 * kDirectNW), 0, s, pr, qc, qk, tc, tk, zc,
+                       zk, S, keys, done, ratio, ratio_on_squared, idx2, d2, match);
+}
+
+// Single pairs of foreign buffers (k_match_single): workgroups a launch aims
+// for when choosing train splits (64-1024 measured equal, round 2), waves per
+// workgroup and 32-query blocks per wave (4 x 2: 256 queries per workgroup;
+// 128-query workgroups measured equal, round 4), and no prep launch (the
+// prep + batch kernel path: host-synchronous calls 32-42 vs 25-28 us, round 2).
+constexpr int kMatchWgTargetSingle = 256;
+constexpr int kMatchNWSingle = 4;
+constexpr int kMatchQBWSingle = 2;
+constexpr int kMatchSingleQB = 32 * kMatchQBWSingle * kMatchNWSingle;
 // The matcher's done counters are sized per (pair, kMatchQB-query block)
 // (sift_hip_matcher_create); a launch indexes them by its own block, which must
 // therefore hold at least kMatchQB queries.
 static_assert(kMatchSingleQB >= kMatchQB, "single-pair blocks smaller than the done-counter block");
 static_assert(kMatchBatchQB >= kMatchQB, "batched blocks smaller than the done-counter block");
+static_assert(kDirectQB >= kMatchQB, "direct blocks smaller than the done-counter block");
 
 static int device_cus() {
     static int cus = [] {
@@ -718,10 +803,10 @@ static int device_cus() {
 MatchPlan match_plan(int max_nq, int max_nt, int P) {
     MatchPlan pl;
     const int ntiles = (max_nt + kMatchTileRows - 1) / kMatchTileRows;
-    if (P == 1 && SIFT_MATCH_FUSED_SINGLE) {
-        pl.nw = SIFT_MATCH_NW_SINGLE;
+    if (P == 1) {
+        pl.nw = kMatchNWSingle;
         const int qblocks = (max_nq + kMatchSingleQB - 1) / kMatchSingleQB;
-        int S = (SIFT_MATCH_WG_TARGET_SINGLE + qblocks - 1) / qblocks;
+        int S = (kMatchWgTargetSingle + qblocks - 1) / qblocks;
         // >= 4 tiles per split: every split converts its workgroup's query rows
         // again (C3, 2000 x 2000: 4 tiles 11.5 us per call, 3 tiles 11.9, 2 12.4,
         // 1 15.8, 6 12.3, 8 13.4; tools/r3_c3_dma.sh).
@@ -767,10 +852,10 @@ MatchPlan match_plan(int max_nq, int max_nt, int P) {
 void launch_match(const MatchSets& sets, MatchBatch& batch, const MatchPlan& plan, int nq_stride, int8_t* codes,
                   int* rowkeys, int sentinel, unsigned* flags, unsigned epoch, unsigned long long* keys,
                   unsigned* done, float ratio, int ratio_on_squared, int* idx2, float* d2, int* match, hipStream_t s) {
-    if (batch.P == 1 && SIFT_MATCH_FUSED_SINGLE) {
+    if (batch.P == 1) {
         const MatchPair& pr = batch.pair[0];
         dim3 g((max(pr.nq, 1) + kMatchSingleQB - 1) / kMatchSingleQB, plan.S, 1);
-        hipLaunchKernelGGL((k_match_single<SIFT_MATCH_NW_SINGLE, SIFT_MATCH_QBW_SINGLE>), g, dim3(64 * SIFT_MATCH_NW_SINGLE),
+        hipLaunchKernelGGL((k_match_single<kMatchNWSingle, kMatchQBWSingle>), g, dim3(64 * kMatchNWSingle),
                            0, s, pr, plan.S, keys, done, ratio, ratio_on_squared, idx2, d2, match);
         return;
     }

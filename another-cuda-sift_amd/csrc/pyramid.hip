@@ -85,20 +85,15 @@ __device__ __forceinline__ f32x2 pk_mov_hi_lo(f32x2 a, f32x2 b) {
     return r;
 }
 constexpr int BLUR_TW = 64;
-#ifndef SIFT_BLUR_TH  // tile height: 64 (8 waves) beat 32 by 3-5 % of frame time (A/B builds: -DSIFT_BLUR_TH=32)
-#define SIFT_BLUR_TH 64
-#endif
-constexpr int BLUR_TH = SIFT_BLUR_TH;
+constexpr int BLUR_TH = 64;  // tile height: 64 (8 waves) beat 32 by 3-5 % of frame time (round 1)
 // Waves per workgroup NW (a template parameter): 4 for launches of >= 2048
 // tiles (octave-0 launches of frame batches: 2-8 % faster per launch, and a
 // workgroup pair holds half of a CU's wave slots, so the other stream's
 // keypoint kernels co-reside), 8 for the small launches (more waves per tile
 // hide their latency better).
-#ifndef SIFT_BLUR_BIG_TILES
-#define SIFT_BLUR_BIG_TILES 2048
-#endif
+constexpr int kBlurBigTiles = 2048;
 static_assert(BLUR_TH % 32 == 0, "blur tile height: 8-row column blocks for 4 or 8 waves");
-static int blur_waves(int tiles) { return tiles >= SIFT_BLUR_BIG_TILES ? 4 : 8; }
+static int blur_waves(int tiles) { return tiles >= kBlurBigTiles ? 4 : 8; }
 
 // One blur launch's job: plane src -> dst, optionally the next octave's base
 // plane (dec), the pixel range and the frame counters.
@@ -121,49 +116,38 @@ struct BlurJob {
 // R = 8: SQ_LDS_BANK_CONFLICT 16-21 % of the LDS cycles at R = 5, 6, 10, 13).
 // A multiple-of-16 pitch also lets the column pass fetch (y, y + 4) pairs with
 // one ds_read2st64_b32.
-#ifndef SIFT_BLUR_IW16
-#define SIFT_BLUR_IW16 1
-#endif
+constexpr bool kBlurIW16 = true;
 // Tiles with every input in the image read their staging rows as aligned
 // 16-byte loads of columns x0 - ORG .. x0 + 63 + ORG, ORG = 8 for radius <= 8
 // and R rounded up to a multiple of 4 above (12 at R = 10, 16 at R = 13): a
 // quarter of the load instructions of the per-column dword staging.  The LDS
 // tile starts at column x0 - ORG whichever staging ran.
-#ifndef SIFT_BLUR_X4LD
-#define SIFT_BLUR_X4LD 1
-#endif
-#ifndef SIFT_BLUR_X4LD_BIG
-#define SIFT_BLUR_X4LD_BIG 1  // the 16-byte staging for radii > 8 too
-#endif
-#ifndef SIFT_BLUR_X4LD_MAXR
-#define SIFT_BLUR_X4LD_MAXR 24
-#endif
+// (Measured alternative, round 3: the per-column dword staging for R > 8 --
+// the paired R = 13 launch 115.7 vs 113.0 us per 16 frames.)
+constexpr bool kBlurX4Ld = true;
+constexpr bool kBlurX4LdBig = true;  // the 16-byte staging for radii > 8 too
+constexpr int kBlurX4LdMaxR = 24;
 // Full tiles store their output rows as 16-byte stores (each wave's 8-row
 // blocks transposed through the freed LDS tile) instead of one dword per
 // lane and row: a quarter of the store instructions.
-#ifndef SIFT_BLUR_X4ST
-#define SIFT_BLUR_X4ST 1
-#endif
+constexpr bool kBlurX4St = true;
 // Interior-tile staging by LDS-DMA (global_load_lds_dwordx4) instead of
 // 16-byte loads into VGPRs + ds_write_b128.
-#ifndef SIFT_BLUR_DMA
-#define SIFT_BLUR_DMA 1
-#endif
+// (Measured alternative, round 2: VGPR staging -- the x4 launches 1-3 % slower.)
+constexpr bool kBlurDma = true;
 template <int R>
 constexpr int blur_org() {  // tile column 0 = image column x0 - ORG
-    return SIFT_BLUR_X4LD && R <= 8 ? 8 : SIFT_BLUR_X4LD && SIFT_BLUR_X4LD_BIG && R <= SIFT_BLUR_X4LD_MAXR ? (R + 3) & ~3 : R;
+    return kBlurX4Ld && R <= 8 ? 8 : kBlurX4Ld && kBlurX4LdBig && R <= kBlurX4LdMaxR ? (R + 3) & ~3 : R;
 }
 // Radius 11..24 with the dword staging: pitch 112 (16 mod 32, conflict-free
 // row-pass stores).  With the 16-byte staging (default) the rows stay unpadded
 // (R = 13: 96 floats) so the interior tiles stage by LDS-DMA: the paired
 // R = 13 launch 115.7 -> 113.0 us per 16 frames (tools/r3_blur_x4_ab.sh).
-#ifndef SIFT_BLUR_IW112
-#define SIFT_BLUR_IW112 0
-#endif
+constexpr bool kBlurIW112 = false;
 template <int R>
 constexpr int blur_iw() {  // radius 9, 10: the next 16-mod-32 pitch (112) costs a workgroup per CU -- kept at 64 + 2R
-    return SIFT_BLUR_IW16 && R <= 8 ? ((BLUR_TW + 2 * blur_org<R>() + 15) / 32) * 32 + 16
-           : SIFT_BLUR_IW112 && R >= 11 && R <= 24 ? 112
+    return kBlurIW16 && R <= 8 ? ((BLUR_TW + 2 * blur_org<R>() + 15) / 32) * 32 + 16
+           : kBlurIW112 && R >= 11 && R <= 24 ? 112
                                                    : (BLUR_TW + 2 * blur_org<R>() + 3) & ~3;
 }
 template <int R>
@@ -252,7 +236,7 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
             static_assert(!(ES == 4 && ORG % 4 == 0) || 4 * QW <= IW, "x4 staging row inside the LDS row");
             constexpr int NQ = QW * IH, NT = 64 * BLUR_NW, QPT = (NQ + NT - 1) / NT;
             const int rb0 = (y0 - R) * spitch + x0 - ORG;
-            if constexpr (SIFT_BLUR_DMA && IW == 4 * QW) {
+            if constexpr (kBlurDma && IW == 4 * QW) {
                 // LDS-DMA (the LDS rows are unpadded: float4 q of the tile goes
                 // to LDS float4 q; global_load_lds_dwordx4: a wave's 64 lanes
                 // fill 1 KiB at M0), no VGPR round trip and no ds_write_b128.
@@ -381,7 +365,7 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
     float mx = -FLT_MAX, nmn = -FLT_MAX;  // pixel range (range_keys only)
     const int gx = x0 + lane;
     const bool full = y0 + BLUR_TH <= H && x0 + BLUR_TW <= W;  // uniform
-    float outs[BLUR_CB][8];  // SIFT_BLUR_X4ST: full-tile rows kept for the widened stores
+    float outs[BLUR_CB][8];  // kBlurX4St: full-tile rows kept for the widened stores
 #pragma unroll
     for (int cbk = 0; cbk < BLUR_CB; cbk++) {
         const int lx = lane, yb = (wave + cbk * BLUR_NW) * 8;
@@ -404,7 +388,7 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
             out[q] = a[0];
             out[q + 4] = a[1];
         }
-        if (SIFT_BLUR_X4ST && full) {
+        if (kBlurX4St && full) {
 #pragma unroll
             for (int q = 0; q < 8; q++) outs[cbk][q] = out[q];
         } else if (full) {
@@ -423,7 +407,7 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
                 if (gy < H && gx < W) dst[(size_t)gy * dpitch + gx] = out[q];
             }
         }
-        if (dec_out && !(SIFT_BLUR_X4ST && full)) {
+        if (dec_out && !(kBlurX4St && full)) {
             // The next octave's base plane (edge tiles; full tiles store it
             // from the LDS image below): even rows and columns of this plane
             // (y0, yb even), stored by the even lanes; other lanes get an
@@ -448,7 +432,7 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
             }
         }
     }
-    if (SIFT_BLUR_X4ST && full) {
+    if (kBlurX4St && full) {
         // Widened stores: every wave's column pass has read `mid` (barrier);
         // each wave writes its 8-row blocks into the free LDS tile as a plain
         // 64-float-pitch image and reads back its own rows as float4s (the
@@ -948,9 +932,7 @@ __global__ __launch_bounds__(kTailThreads) void k_blur_tail(TailDesc T, long fs)
     }
 }
 
-#ifndef SIFT_TAIL_MAX_PX
-#define SIFT_TAIL_MAX_PX 6000  // largest octave the tail takes (one CU's VALU: 752x480 octave 3 = 94x60; 1920x1200 octave 4 (120x75) lost 10-20 us)
-#endif
+constexpr long kTailMaxPx = 6000;  // largest octave the tail takes (one CU's VALU: 752x480 octave 3 = 94x60; 1920x1200 octave 4 (120x75) lost 10-20 us)
 int tail_first_octave(const PyrDesc& pyr, const Taps* taps, int L) {
     for (int i = 1; i < L + 3; i++)
         if ((taps[i].n >> 1) > kTailRmax) return pyr.nOct;
@@ -959,7 +941,7 @@ int tail_first_octave(const PyrDesc& pyr, const Taps* taps, int L) {
         const OctGeom& g = pyr.oct[o];
         const long px = (long)tail_pitch(g.W) * g.H;
         const long nxt = o + 1 < pyr.nOct ? (long)tail_pitch(pyr.oct[o + 1].W) * pyr.oct[o + 1].H : 0;
-        if ((long)g.W * g.H > SIFT_TAIL_MAX_PX || 2 * px + nxt > kTailLdsFloats || g.W > kTailMaxDim ||
+        if ((long)g.W * g.H > kTailMaxPx || 2 * px + nxt > kTailLdsFloats || g.W > kTailMaxDim ||
             g.H > kTailMaxDim)
             break;
         T = o;
@@ -1152,10 +1134,11 @@ __global__ __launch_bounds__(256) void k_extrema(OctGeom g, int Lrt, int o, floa
 // ---------------------------------------------------------------------------
 constexpr int EX4_LIST = 2048;  // per-workgroup candidate list (LDS): a 256 x 32 x L block can hold
                                 // ~7 % extrema on textured frames; overflow spills to HBM
-#ifndef SIFT_EX_CPL
-#define SIFT_EX_CPL 4  // columns per lane of the extrema strips (2 or 4)
-#endif
-constexpr int EX4_COLS = 64 * SIFT_EX_CPL;  // columns per wave
+// Columns per lane of the extrema strips.  (Measured alternative, round 3: 2
+// columns per lane, 137 VGPRs / 3 waves per SIMD: 266-268 vs 252 us per
+// 16-frame launch.)
+constexpr int kExCpl = 4;
+constexpr int EX4_COLS = 64 * kExCpl;  // columns per wave
 
 __device__ __forceinline__ float dpp_left_or(float own, float v) {  // lane i <- lane i-1, lane 0 <- own
     return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own), __float_as_int(v), 0x138, 0xf, 0xf, false));
@@ -1171,7 +1154,7 @@ __device__ __forceinline__ float dpp_right_or(float own, float v) {  // lane i <
 // rows above and below are read once per NB * EX4_TR rows instead of once per
 // EX4_TR: strips of 6 rows read 8 (1.20x algorithmic HBM bytes measured at
 // 16 frames, round-3 verdict), 24-row streams read 26.
-template <int LT, int EX4_TR, int EX4_AHEAD, int NB = 1, int CPL = SIFT_EX_CPL>
+template <int LT, int EX4_TR, int EX4_AHEAD, int NB = 1, int CPL = kExCpl>
 __device__ __forceinline__ void extrema_block(const OctGeom& g, int o, float thr, uint2* __restrict__ cand,
                                               Counters* __restrict__ ctr, unsigned cap, int tile, int strips,
                                               uint2* s_list, unsigned& s_cnt, unsigned& s_base) {
@@ -1207,13 +1190,10 @@ __device__ __forceinline__ void extrema_block(const OctGeom& g, int o, float thr
     // row overhangs it: 1920 = 7.5 strips) and the lanes that do not use the
     // outer column (all but lanes 0 and 63) load from an offset past the
     // buffer: the hardware returns 0 without a memory request.
-#ifndef SIFT_EX_MASK_LOADS
-#define SIFT_EX_MASK_LOADS 1
-#endif
 #if defined(SIFT_EX_DIAG) && (SIFT_EX_DIAG == 1 || SIFT_EX_DIAG == 3)  // traffic variants (wrong results): no outer-column loads
     const bool l4 = xl < W, le = false;
 #else
-    const bool l4 = !SIFT_EX_MASK_LOADS || xl < W, le = !SIFT_EX_MASK_LOADS || lane == 0 || lane == 63;
+    const bool l4 = xl < W, le = lane == 0 || lane == 63;
 #endif
     auto issue_row = [&](int y, f4 (&v)[NG], float (&e)[NG]) {
 #if defined(SIFT_EX_DIAG) && (SIFT_EX_DIAG == 2 || SIFT_EX_DIAG == 3)  // traffic variants: halo rows -> the wave's own rows
@@ -1368,12 +1348,8 @@ __device__ __forceinline__ void extrema_block(const OctGeom& g, int o, float thr
 // still give >= 1024 waves, else 2 rows per wave (small octaves are
 // latency-bound and want waves; tools/kernel_bench: 1920x1200 16.7 us at 6
 // rows vs 19.8 at 2; 960x600 9.2 us at 2 rows vs 10.8 at 6).
-#ifndef SIFT_EX_TALL_MIN
-#define SIFT_EX_TALL_MIN 2048  // single frames: 6-row wave strips from this many strips per launch, else 2-row (1920x1200: 1600 -> 2-row, 26.4 -> 25.5 us); batches: 1024
-#endif
-#ifndef SIFT_EX_STREAM
-#define SIFT_EX_STREAM 2  // 6-row steps per tall wave stream (12 rows: 247 vs 251 us per 16-frame launch; 18, 24 rows slower)
-#endif
+constexpr int kExTallMin = 2048;  // single frames: 6-row wave strips from this many strips per launch, else 2-row (1920x1200: 1600 -> 2-row, 26.4 -> 25.5 us); batches: 1024
+constexpr int kExStream = 2;  // 6-row steps per tall wave stream (12 rows: 247 vs 251 us per 16-frame launch; 18, 24 rows slower)
 struct ExtremaPlan {
     int start[kMaxOctaves + 1];  // start[nOct] = blocks per frame
     int strips[kMaxOctaves];
@@ -1400,7 +1376,7 @@ __global__ __launch_bounds__(256) void k_extrema_all(PyrDesc pyr, ExtremaPlan pl
     ctr = fptr(ctr, f * fs);
     const int blk = b - plan.start[o];
     if (plan.tall[o])
-        extrema_block<LT, 6, 2, SIFT_EX_STREAM>(g, o, thr, cand, ctr, cap, blk, plan.strips[o], s_list, s_cnt, s_base);
+        extrema_block<LT, 6, 2, kExStream>(g, o, thr, cand, ctr, cap, blk, plan.strips[o], s_list, s_cnt, s_base);
     else
         extrema_block<LT, 2, 2>(g, o, thr, cand, ctr, cap, blk, plan.strips[o], s_list, s_cnt, s_base);
 }
@@ -1424,8 +1400,8 @@ bool launch_extrema_all(const PyrDesc& pyr, float threshold, uint2* cand, Counte
         const int strips = (g.W + EX4_COLS - 1) / EX4_COLS;
         // Frames of a batch count too: each brings its own strips.
         // (8, 12 or 20 rows per wave for batches: 147, 149, 582 us vs 131 at 6.)
-        const bool tall = strips * ((g.H + 5) / 6) * fr.nf >= (fr.nf > 1 ? 1024 : SIFT_EX_TALL_MIN);
-        const int tr = tall ? 6 * SIFT_EX_STREAM : 2;
+        const bool tall = strips * ((g.H + 5) / 6) * fr.nf >= (fr.nf > 1 ? 1024 : kExTallMin);
+        const int tr = tall ? 6 * kExStream : 2;
         plan.start[o] = total;
         plan.strips[o] = strips;
         plan.tall[o] = tall;

@@ -59,4 +59,12 @@ void launch_match(const MatchSets& sets, MatchBatch& batch, const MatchPlan& pla
                   unsigned* flags, unsigned epoch, unsigned long long* keys, unsigned* done, float ratio,
                   int ratio_on_squared, int* idx2, float* d2, int* match, hipStream_t s);
 
+// One pair of sets with matcher sidecars (detector-produced descriptor
+// buffers, sift_kernels.h Sidecar): codes qc/tc (128 B rows) and key biases
+// qk/tk; zc/zk the matcher's zero sentinel row and padding key.
+void launch_match_direct(const MatchPair& pr, const int8_t* qc, const int* qk, const int8_t* tc, const int* tk,
+                         const int8_t* zc, const int* zk, unsigned long long* keys, unsigned* done, float ratio,
+                         int ratio_on_squared, int* idx2, float* d2, int* match, hipStream_t s);
+int match_direct_splits(int nq, int nt);
+
 }  // namespace sift_amd

@@ -122,6 +122,7 @@ def lib() -> ctypes.CDLL:
         "sift_hip_debug_candidates": (i, [vp, vp, i, ip]),
         "sift_hip_matcher_create": (i, [i, i, i, i, ctypes.POINTER(vp)]),
         "sift_hip_matcher_destroy": (i, [vp]),
+        "sift_hip_matcher_set_sidecars": (i, [vp, i]),
         "sift_hip_match_device": (i, [vp, vp, i, vp, i, f, i, vp, vp, vp, vp]),
         "sift_hip_match_batched": (i, [vp, i, vp, vp, vp, vp, f, i, vp, vp, vp, vp]),
         "sift_hip_match_host": (i, [vp, vp, i, vp, i, f, i, vp]),
@@ -485,6 +486,10 @@ class Matcher:
         if m and m.value and _lib is not None:
             _lib.sift_hip_matcher_destroy(m)
             self._m = None
+
+    def set_sidecars(self, enable: bool) -> None:
+        """Single pairs of detector-produced buffers match their sidecar codes (default on; sift_hip_matcher_set_sidecars)."""
+        _check(lib().sift_hip_matcher_set_sidecars(self._m, int(bool(enable))), "matcher_set_sidecars")
 
     def match_device(self, q_ptr: int, nq: int, t_ptr: int, nt: int, ratio: float = 0.8, ratio_on_squared: bool = False,
                      idx2_ptr: int = 0, d2_ptr: int = 0, match_ptr: int = 0, stream: Optional[int] = None) -> None:

@@ -827,6 +827,36 @@ def main():
     flops = 2.0 * nq * nq * 128
     n_matches = int((out_m >= 0).sum().item())
 
+    # The reference's own pairing (tool/extract_and_match_example.cc:87):
+    # matchBruteForce(prev_descriptor, n0, device_descriptor, n1) on the
+    # detector's last two results, 2000 rows each; detector buffers carry
+    # their int8 codes (matcher sidecar), so no conversion runs.
+    n0d, n1d = min(det2.prev_size, nq), min(det2.total_size, nq)
+    qd, td = det2.prev_descriptor.data(), det2.device_descriptor.data()
+
+    def det_match():
+        matcher.match_device(qd, n0d, td, n1d, 0.8, False, out_idx.data_ptr(), out_d2.data_ptr(), out_m.data_ptr(),
+                             stream)
+
+    for _ in range(20):
+        det_match()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        det_match()
+    e1.record()
+    torch.cuda.synchronize()
+    match_det_ms = max_over_ranks(e0.elapsed_time(e1) / reps)
+    t = time.perf_counter()
+    for _ in range(20):
+        det_match()
+        torch.cuda.synchronize()
+    match_det_sync_ms = (time.perf_counter() - t) / 20 * 1e3
+    match_det = {"ms": round(match_det_ms, 4), "ms_sync_host": round(match_det_sync_ms, 4), "rows": [n0d, n1d],
+                 "tops": round(2.0 * n0d * n1d * 128 / (match_det_ms * 1e-3) / 1e12, 2),
+                 "path": "detector buffers (prev_descriptor x device_descriptor): sidecar int8 codes, k_match_direct",
+                 "matches": int((out_m[:n0d] >= 0).sum().item())}
+
     # ---- C5: 8-way (world-way) all-gather + pairwise match -------------------
     def run_c5_single_gpu(K=8):
         """world == 1: the 8 sets are already on this GPU (no exchange); all
@@ -965,7 +995,9 @@ def main():
             "match_2k": {"ms": round(match_ms, 4), "ms_sync_host": round(match_sync_ms, 4),
                          "tops": round(flops / match_ms / 1e9, 2), "mfma_frac": round(flops / match_ms / 1e9 / I8_MFMA_PEAK_TOPS, 5),
                          "dtype": "int8 codes (v - 128) on v_mfma_i32_32x32x32_i8, exact int32 d^2",
-                         "matches": n_matches, "ratio": 0.8},
+                         "matches": n_matches, "ratio": 0.8,
+                         "path": "foreign fp16 buffers (converted in the kernel, k_match_single)"},
+            "match_2k_detector": match_det,
             "c4_256_frames_1600x900": c4,
             "c5_allgather_match": c5,
             "c1_gpu": c1_gpu,

@@ -281,6 +281,16 @@ int sift_hip_match_batched(sift_hip_matcher_t m, int P, const uint16_t* const* q
                            float ratio, int ratio_on_squared, int* idx2, float* d2,
                            int* match, void* stream);
 
+/* Descriptor buffers handed out by a detector handle (sift_hip_results_device
+ * and the batch accessors: the base of a results slot) carry a matcher
+ * sidecar written by the same kernel -- int8 codes v - 128 and a per-row key
+ * bias.  A single-pair call whose query and train pointers are both such
+ * bases (e.g. matchBruteForce(prev_descriptor, n0, device_descriptor, n1))
+ * matches those codes directly: no fp16 conversion, no prep launch (results
+ * identical).  Treat detector buffers as read-only.  enable = 0 turns the
+ * lookup off for matcher m (every call converts the fp16 rows). */
+int sift_hip_matcher_set_sidecars(sift_hip_matcher_t m, int enable);
+
 /* matchBruteForce(des, num_des, src, num_src) (Match.cu:8-33): synchronous,
  * result to host memory out[nq]. */
 int sift_hip_match_host(sift_hip_matcher_t m, const uint16_t* query, int nq,
