@@ -250,13 +250,14 @@ struct Lane {
     char* hResDev = nullptr;
     hipEvent_t evHost[kResultSlots] = {};
     long long hostFrame[kResultSlots] = {-1, -1, -1, -1};  // the frame each host region holds
+    bool hostDesc[kResultSlots] = {};                       // ... with its descriptors
 };
 
 // Byte offsets of every per-frame buffer inside a frame arena (the same for
 // every arena of every lane).
 struct ArenaLayout {
     size_t input = 0, up = 0, pyr = 0, cand = 0, ref = 0, ori = 0, slot = 0, order = 0, jobs = 0, range = 0,
-           bcount = 0, boff = 0, bitmap = 0, ctr = 0, jord = 0;
+           bcount = 0, boff = 0, bitmap = 0, ctr = 0;
     size_t k3[kResultSlots] = {}, f4[kResultSlots] = {}, desc[kResultSlots] = {};
     size_t codes[kResultSlots] = {}, ckeys[kResultSlots] = {};  // matcher sidecar of desc (Sidecar)
     size_t octave[kMaxOctaves] = {};  // float offset of each octave's planes inside the pyramid
@@ -326,7 +327,6 @@ struct sift_hip_detector {
     int* dSlot = nullptr;
     int* dOrder = nullptr;
     DescJob* dJobs = nullptr;  // per final keypoint, written by k_bucket_rank
-    JobOrder* dJord = nullptr;  // descriptor job order (k_order -> k_rank_final)
     unsigned* dRange = nullptr;  // 2 * kRangeSlots pixel-range keys (initial blur -> descriptor)
     unsigned* dBcount = nullptr;
     unsigned* dBoff = nullptr;
@@ -346,6 +346,10 @@ struct sift_hip_detector {
     bool useGraph = true;
 
     CopyPool* pool = nullptr;  // staging copies of large host frames (created at the first one)
+    // What the caller's last sift_hip_copy_to_host took (0 nothing yet, 1
+    // keypoints, 2 keypoints + descriptors): host-input frames prefetch that
+    // much to pinned host memory (a caller that never copies back pays nothing).
+    int hostWant = 0;
 
     // Stage dumps (sift_hip_set_datagen): directory, and a device copy of the
     // frame's input as float (the caller's buffer may change before the dump).
@@ -574,7 +578,6 @@ void bind_lane(sift_hip_detector* d, int k) {
     d->dSlot = reinterpret_cast<int*>(A + a.slot);
     d->dOrder = reinterpret_cast<int*>(A + a.order);
     d->dJobs = reinterpret_cast<DescJob*>(A + a.jobs);
-    d->dJord = reinterpret_cast<JobOrder*>(A + a.jord);
     d->dRange = reinterpret_cast<unsigned*>(A + a.range);
     d->dBcount = reinterpret_cast<unsigned*>(A + a.bcount);
     d->dBoff = reinterpret_cast<unsigned*>(A + a.boff);
@@ -657,7 +660,6 @@ int allocate(sift_hip_detector* d) {
     a.slot = take(sizeof(int) * capO);
     a.order = take(sizeof(int) * capO);
     a.jobs = take(sizeof(DescJob) * capF);
-    a.jord = take(sizeof(JobOrder));
     a.range = take(sizeof(unsigned) * 2 * 2 * kRangeSlots);  // one set per frame parity
     a.bcount = take(sizeof(unsigned) * (size_t)d->kp.numBuckets);
     a.boff = take(sizeof(unsigned) * (size_t)d->kp.numBuckets);
@@ -882,8 +884,8 @@ void enqueue_order(sift_hip_detector* d, int slot, int nf) {
     const Frames fr{nf, d->afs};
     if (d->kp.numBuckets <= kOrderMaxBuckets) {
         d->timed("order", 0, [&] {
-            launch_order(d->pyr, d->dOri, d->dCtr, range_keys(d, parity ^ 1), d->dBcount, d->dBoff, d->dSlot, d->dOrder,
-                         d->dJord, d->kp, fr, s);
+            launch_order(d->dOri, d->dCtr, range_keys(d, parity ^ 1), d->dBcount, d->dBoff, d->dSlot, d->dOrder, d->kp,
+                         fr, s);
         });
     } else {
         d->timed("select", 0, [&] { launch_select(d->dOri, d->dCtr, range_keys(d, parity ^ 1), d->kp, fr, s); });
@@ -895,7 +897,7 @@ void enqueue_order(sift_hip_detector* d, int slot, int nf) {
     }
     d->timed("bucket_rank", 0, [&] {
         if (d->kp.numBuckets <= kOrderMaxBuckets)
-            launch_rank_final(d->pyr, d->dOri, d->dBcount, d->dBoff, d->dOrder, d->dCtr, d->dJord, d->dJobs, d->dKpts3[slot],
+            launch_rank_final(d->pyr, d->dOri, d->dBcount, d->dBoff, d->dOrder, d->dCtr, d->dJobs, d->dKpts3[slot],
                               d->dFeats4[slot], d->kp, fr, s);
         else  // bucket_count needs zeroed counts: the bucket-parallel ranking re-zeroes them
             launch_bucket_rank(d->pyr, d->dOri, d->dBcount, d->dBoff, d->dOrder, d->dCtr, d->dJobs, d->dKpts3[slot],
@@ -1181,6 +1183,7 @@ void host_res(const sift_hip_detector* d, char* base, int slot, float** k3, floa
 // region on the lane's stream (the next frame of the lane follows it; other
 // lanes keep computing), evHost[slot] once they are there.
 int prefetch_results(sift_hip_detector* d, long long f) {
+    if (!d->hostWant) return SIFT_HIP_OK;
     Lane& L = d->lane();
     const int slot = d->frec(f).slot;
     if (!L.hRes) {
@@ -1192,10 +1195,12 @@ int prefetch_results(sift_hip_detector* d, long long f) {
     float *k3, *f4;
     uint16_t* desc;
     host_res(d, L.hResDev, slot, &k3, &f4, &desc);
-    launch_results_to_host(d->dKpts3[slot], d->dFeats4[slot], d->dDesc[slot], d->dCtr, d->kp.capFinal, k3, f4, desc,
-                           d->stream);
+    const bool withDesc = d->hostWant > 1;
+    launch_results_to_host(d->dKpts3[slot], d->dFeats4[slot], d->dDesc[slot], d->dCtr, d->kp.capFinal, k3, f4,
+                           withDesc ? desc : nullptr, d->stream);
     HIPCHK(hipEventRecord(L.evHost[slot], d->stream));
     L.hostFrame[slot] = f;
+    L.hostDesc[slot] = withDesc;
     return SIFT_HIP_OK;
 }
 
@@ -1394,7 +1399,7 @@ int dump_stage_files(sift_hip_detector* d) {
              "  \"oriented.rec\": \"OriKpt [slots] {f32 x, y, size, angle, response; i32 octave, bucket, sub}; "
              "bucket 0xffffffff = hole\",\n"
              "  \"jobs.rec\": \"DescJob [keypoints] 64 B {i64 plane o*(L+3)+layer; f32 cos_t, sin_t, angle, hist_width; "
-             "i32 ptx, pty, rows, cols, pitch, radius, out (the output row), pad[3]}; jobs run longest first\",\n"
+             "i32 ptx, pty, rows, cols, pitch, radius, pad[4]}\",\n"
              "  \"range.u32\": \"u32 [2][%d] pixel-range keys of the frame\",\n"
              "  \"counters.u32\": \"u32 [8] {cand, refined, oriented, final, overflow, retainBest threshold bits, "
              "order entries, 0}\"}\n}\n",
@@ -1956,7 +1961,8 @@ int sift_hip_copy_to_host(sift_hip_t d, float* k3, float* f4, uint16_t* desc, in
     if (int rc = ensure_counts(d)) return rc;
     const int n = std::min(d->count, cap);
     Lane& L = d->lane();
-    if (L.hRes && L.hostFrame[d->cur] == d->current && d->current >= d->firstFrame) {
+    d->hostWant = std::max(d->hostWant, desc ? 2 : 1);
+    if (L.hRes && L.hostFrame[d->cur] == d->current && d->current >= d->firstFrame && (!desc || L.hostDesc[d->cur])) {
         // A host-input frame: its results already went to pinned host memory.
         HIPCHK(hipEventSynchronize(L.evHost[d->cur]));
         float *hk3, *hf4;

@@ -336,20 +336,22 @@ constexpr int kOriAhead = 1;
 // XCD-aware keypoint mapping (a 1-D grid of nf * per one-wave workgroups;
 // the dispatcher hands workgroup w to XCD w % 8, and each XCD has its own L2).
 // Frame = w % nf, so with nf a multiple of 8 every frame lives on one XCD (its
-// windows are fetched into one L2); with nf dividing 8 a frame's q = 8 / nf
-// XCDs each take a contiguous range of its keypoints (the refined list is in
-// scan order, so neighbouring keypoints -- overlapping windows -- share an
-// L2).  The round-4 mapping (frame = blockIdx.y, keypoint round-robin over
-// blockIdx.x) put every frame's neighbouring keypoints on all 8 XCDs: 2.2x the
-// window bytes fetched from HBM.
+// windows are fetched into one L2): 16-frame launches fetch 209.9 MB instead
+// of 270.4 (the round-4 mapping, frame = blockIdx.y with keypoints
+// round-robin over blockIdx.x, put every frame's neighbouring keypoints on all
+// 8 XCDs), against 192.1 MB for a perfect cache at 128-byte lines
+// (tools/window_line_model.py).
 __global__ __launch_bounds__(64) void k_orientation(PyrDesc pyr, const RefKpt* __restrict__ in,
                                                     Counters* __restrict__ ctr, OriKpt* __restrict__ out,
                                                     uint32_t* __restrict__ bitmap, KeypointParams kp, long fs,
                                                     unsigned nf) {
     __shared__ __attribute__((aligned(16))) float chunk[64 + 3 * kOriBins];  // bin runs padded to 4
+    // Below 8 frames a frame's keypoints stay round-robin over its XCDs
+    // (q = 1): single frames are latency-bound and contiguous per-XCD ranges
+    // unbalance the XCDs (C2 single frame 26.7 -> 29.8 us with ranges).
     const unsigned w = blockIdx.x, per = gridDim.x / nf;
     const unsigned frame = w % nf, l = w / nf;
-    const unsigned q = (nf < 8 && 8 % nf == 0) ? 8 / nf : 1;  // XCDs sharing this frame
+    const unsigned q = 1;
     const unsigned range = l % q, j = l / q, step = per / q;
     const long foff = (long)frame * fs;
     in = fptr(in, foff);
@@ -594,24 +596,13 @@ void launch_bucket_scatter(const OriKpt* kpts, const Counters* ctr, const unsign
 // the counts), and order[].  Used when the buckets fit in LDS
 // (kOrderMaxBuckets); the four kernels above remain for larger pyramids.
 // ---------------------------------------------------------------------------
-// Segment (octave, layer) of a final keypoint in the bucket order (k_order's
-// job-order segments; JobOrder).
-__device__ __forceinline__ int lpt_seg(int packed_octave, int fo, int L) {
-    const int o = (int)(signed char)(packed_octave & 255) - fo, layer = (packed_octave >> 8) & 255;
-    return o * L + layer - 1;
-}
-
-__global__ __launch_bounds__(1024) void k_order(PyrDesc pyr, const OriKpt* __restrict__ kpts, Counters* __restrict__ ctr,
+__global__ __launch_bounds__(1024) void k_order(const OriKpt* __restrict__ kpts, Counters* __restrict__ ctr,
                                                 unsigned* __restrict__ zero_range, unsigned* __restrict__ bcount,
                                                 unsigned* __restrict__ boff, int* __restrict__ slot,
-                                                int* __restrict__ order, JobOrder* __restrict__ jord,
-                                                KeypointParams kp, long fs) {
+                                                int* __restrict__ order, KeypointParams kp, long fs) {
     extern __shared__ unsigned s_bucket[];  // counts, then exclusive offsets
     __shared__ unsigned hist[256], wsum[16];
     __shared__ unsigned s_prefix, s_k;
-    __shared__ unsigned s_seg[kLptSegs];  // kept keypoints per (octave, layer) segment
-    const int L = pyr.L, fo = pyr.firstOctave;
-    const bool lpt = L <= 8 && pyr.nOct * L <= kLptSegs;
     const long foff = blockIdx.y * fs;  // frame blockIdx.y
     kpts = fptr(kpts, foff);
     ctr = fptr(ctr, foff);
@@ -620,13 +611,11 @@ __global__ __launch_bounds__(1024) void k_order(PyrDesc pyr, const OriKpt* __res
     boff = fptr(boff, foff);
     slot = fptr(slot, foff);
     order = fptr(order, foff);
-    jord = fptr(jord, foff);
     const unsigned n = oriented_count(ctr, kp);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nb = kp.numBuckets;
     for (int i = tid; i < 2 * kRangeSlots; i += 1024) zero_range[i] = 0u;  // next frame's range keys
     for (int i = tid; i < nb; i += 1024) s_bucket[i] = 0u;
-    if (tid < kLptSegs) s_seg[tid] = 0u;
     if (tid == 0) {
         s_prefix = 0;
         s_k = (unsigned)kp.numFeatures;
@@ -680,29 +669,24 @@ __global__ __launch_bounds__(1024) void k_order(PyrDesc pyr, const OriKpt* __res
         for (int u = 0; u < kOrderRegs; u++) {
             const unsigned i = tid + 1024u * u;
             rbk[u] = __float_as_int(q[u].z);
-            const bool keep = i < n && (unsigned)rbk[u] != kHoleBucket && q[u].x >= thr;
-            rsl[u] = keep ? (int)atomicAdd(&s_bucket[rbk[u]], 1u) : -1;
-            if (keep && lpt) atomicAdd(&s_seg[lpt_seg(__float_as_int(q[u].y), fo, L)], 1u);
+            rsl[u] = i < n && (unsigned)rbk[u] != kHoleBucket && q[u].x >= thr ? (int)atomicAdd(&s_bucket[rbk[u]], 1u)
+                                                                               : -1;
         }
     } else {
         for (unsigned i0 = tid; i0 < n; i0 += 4 * 1024) {
-            int bk[4], oc[4];
+            int bk[4];
             float rs[4];
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const unsigned i = min(i0 + 1024u * u, n - 1);
                 bk[u] = kpts[i].bucket;
                 rs[u] = kpts[i].response;
-                oc[u] = kpts[i].octave;
             }
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const unsigned i = i0 + 1024u * u;
-                if (i < n) {
-                    const bool keep = (unsigned)bk[u] != kHoleBucket && rs[u] >= thr;
-                    slot[i] = keep ? (int)atomicAdd(&s_bucket[bk[u]], 1u) : -1;
-                    if (keep && lpt) atomicAdd(&s_seg[lpt_seg(oc[u], fo, L)], 1u);
-                }
+                if (i < n)
+                    slot[i] = (unsigned)bk[u] != kHoleBucket && rs[u] >= thr ? (int)atomicAdd(&s_bucket[bk[u]], 1u) : -1;
             }
         }
     }
@@ -736,24 +720,6 @@ __global__ __launch_bounds__(1024) void k_order(PyrDesc pyr, const OriKpt* __res
             ctr->final_n = min(total, kp.capFinal);
             ctr->pad[0] = total;  // entries of `order` (k_rank_final)
             if (total > kp.capFinal) atomicOr(&ctr->overflow, 8u);
-            // Job order, longest first (JobOrder): segments in bucket order
-            // give the final positions, layers high to low the job positions.
-            const bool use = lpt && total <= kp.capFinal;
-            jord->valid = use;
-            if (use) {
-                const int ns = pyr.nOct * L;
-                unsigned start = 0;
-                for (int sg = 0; sg < ns; sg++) {
-                    jord->segStart[sg] = (int)start;
-                    start += s_seg[sg];
-                }
-                unsigned job = 0;
-                for (int l = L; l >= 1; l--)
-                    for (int o = 0; o < pyr.nOct; o++) {
-                        jord->jobBase[o * L + l - 1] = (int)job;
-                        job += s_seg[o * L + l - 1];
-                    }
-            }
         }
     }
     __syncthreads();
@@ -770,12 +736,11 @@ __global__ __launch_bounds__(1024) void k_order(PyrDesc pyr, const OriKpt* __res
     }
 }
 
-bool launch_order(const PyrDesc& pyr, const OriKpt* kpts, Counters* ctr, unsigned* zero_range, unsigned* bcount,
-                  unsigned* boff, int* slot, int* order, JobOrder* jord, const KeypointParams& kp, const Frames& fr,
-                  hipStream_t s) {
+bool launch_order(const OriKpt* kpts, Counters* ctr, unsigned* zero_range, unsigned* bcount, unsigned* boff, int* slot,
+                  int* order, const KeypointParams& kp, const Frames& fr, hipStream_t s) {
     if (kp.numBuckets > kOrderMaxBuckets) return false;
-    hipLaunchKernelGGL(k_order, dim3(1, fr.nf), dim3(1024), sizeof(unsigned) * (size_t)kp.numBuckets, s, pyr, kpts,
-                       ctr, zero_range, bcount, boff, slot, order, jord, kp, fr.stride);
+    hipLaunchKernelGGL(k_order, dim3(1, fr.nf), dim3(1024), sizeof(unsigned) * (size_t)kp.numBuckets, s, kpts, ctr,
+                       zero_range, bcount, boff, slot, order, kp, fr.stride);
     return true;
 }
 
@@ -809,8 +774,7 @@ __device__ DescJob make_desc_job(const PyrDesc& pyr, const OriKpt& kpt, long fof
     const float arg = angle * (float)(M_PI / 180);  // cosf/sinf via double
     j.cos_t = (float)cos((double)arg) / j.hist_width;
     j.sin_t = (float)sin((double)arg) / j.hist_width;
-    j.out = 0;
-    j.pad[0] = j.pad[1] = j.pad[2] = 0;
+    j.pad[0] = j.pad[1] = j.pad[2] = j.pad[3] = 0;
     return j;
 }
 
@@ -857,9 +821,7 @@ __global__ __launch_bounds__(256) void k_bucket_rank(PyrDesc pyr, const OriKpt* 
             const unsigned pos = base + rank;
             if (e < cnt && pos < cap) {
                 const OriKpt k = kpts[idx];
-                DescJob j = make_desc_job(pyr, k, foff);
-                j.out = (int)pos;
-                jobs[pos] = j;
+                jobs[pos] = make_desc_job(pyr, k, foff);
                 kpts3[3 * (size_t)pos + 0] = k.x;
                 kpts3[3 * (size_t)pos + 1] = k.y;
                 kpts3[3 * (size_t)pos + 2] = (float)((k.octave >> 8) & 255);
@@ -879,16 +841,15 @@ __global__ __launch_bounds__(256) void k_bucket_rank(PyrDesc pyr, const OriKpt* 
 __global__ __launch_bounds__(256) void k_rank_final(PyrDesc pyr, const OriKpt* __restrict__ kpts,
                                                     const unsigned* __restrict__ bcount,
                                                     const unsigned* __restrict__ boff, const int* __restrict__ order,
-                                                    const Counters* __restrict__ ctr, const JobOrder* __restrict__ jord,
-                                                    DescJob* __restrict__ jobs, float* __restrict__ kpts3,
-                                                    float* __restrict__ feats4, KeypointParams kp, long fs) {
+                                                    const Counters* __restrict__ ctr, DescJob* __restrict__ jobs,
+                                                    float* __restrict__ kpts3, float* __restrict__ feats4,
+                                                    KeypointParams kp, long fs) {
     const long foff = blockIdx.y * fs;  // frame blockIdx.y
     kpts = fptr(kpts, foff);
     bcount = fptr(bcount, foff);
     boff = fptr(boff, foff);
     order = fptr(order, foff);
     ctr = fptr(ctr, foff);
-    jord = fptr(jord, foff);
     jobs = fptr(jobs, foff);
     kpts3 = fptr(kpts3, foff);
     feats4 = fptr(feats4, foff);
@@ -896,7 +857,6 @@ __global__ __launch_bounds__(256) void k_rank_final(PyrDesc pyr, const OriKpt* _
     // positions below it); positions >= capFinal are dropped.
     const unsigned n = ctr->pad[0];
     const unsigned cap = kp.capFinal;
-    const bool lpt = jord->valid != 0;
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const OriKpt k = kpts[order[i]];
         const unsigned base = boff[k.bucket], cnt = bcount[k.bucket];
@@ -904,14 +864,7 @@ __global__ __launch_bounds__(256) void k_rank_final(PyrDesc pyr, const OriKpt* _
         for (unsigned f = 0; f < cnt; f++) rank += (unsigned)(kpts[order[base + f]].sub < k.sub);
         const unsigned pos = base + rank;
         if (pos < cap) {
-            DescJob j = make_desc_job(pyr, k, foff);
-            j.out = (int)pos;
-            int q = (int)pos;
-            if (lpt) {
-                const int sg = lpt_seg(k.octave, pyr.firstOctave, pyr.L);
-                q = jord->jobBase[sg] + ((int)pos - jord->segStart[sg]);
-            }
-            jobs[q] = j;
+            jobs[pos] = make_desc_job(pyr, k, foff);
             kpts3[3 * (size_t)pos + 0] = k.x;
             kpts3[3 * (size_t)pos + 1] = k.y;
             kpts3[3 * (size_t)pos + 2] = (float)((k.octave >> 8) & 255);
@@ -921,10 +874,10 @@ __global__ __launch_bounds__(256) void k_rank_final(PyrDesc pyr, const OriKpt* _
 }
 
 void launch_rank_final(const PyrDesc& pyr, const OriKpt* kpts, const unsigned* bcount, const unsigned* boff,
-                       const int* order, const Counters* ctr, const JobOrder* jord, DescJob* jobs, float* kpts3,
-                       float* feats4, const KeypointParams& kp, const Frames& fr, hipStream_t s) {
-    hipLaunchKernelGGL(k_rank_final, dim3(64, fr.nf), dim3(256), 0, s, pyr, kpts, bcount, boff, order, ctr, jord, jobs,
-                       kpts3, feats4, kp, fr.stride);
+                       const int* order, const Counters* ctr, DescJob* jobs, float* kpts3, float* feats4,
+                       const KeypointParams& kp, const Frames& fr, hipStream_t s) {
+    hipLaunchKernelGGL(k_rank_final, dim3(64, fr.nf), dim3(256), 0, s, pyr, kpts, bcount, boff, order, ctr, jobs, kpts3,
+                       feats4, kp, fr.stride);
 }
 
 void launch_bucket_rank(const PyrDesc& pyr, const OriKpt* kpts, unsigned* bcount, const unsigned* boff,
@@ -936,10 +889,11 @@ void launch_bucket_rank(const PyrDesc& pyr, const OriKpt* kpts, unsigned* bcount
 
 // ---------------------------------------------------------------------------
 // Results of a host-input frame copied into mapped pinned host memory right
-// after the frame (sift_hip_submit): the caller's copyToHost then reads host
-// memory instead of a pageable device-to-host copy (Detector.cu:606-634 copies
-// after the frame, synchronously).  n = min(final_n, cap) rows, the count read
-// on the device; 16-byte stores where the layouts allow.
+// after the frame (sift_hip_submit, when the caller copies its results to the
+// host): copyToHost then reads host memory instead of a pageable
+// device-to-host copy (Detector.cu:606-634 copies after the frame,
+// synchronously).  n = min(final_n, cap) rows, the count read on the device;
+// 16-byte stores where the layouts allow; hdesc null: keypoints only.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_results_to_host(const float* __restrict__ k3, const float* __restrict__ f4,
                                                          const uint16_t* __restrict__ desc,
@@ -950,7 +904,8 @@ __global__ __launch_bounds__(256) void k_results_to_host(const float* __restrict
     const unsigned tid = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
     const uint4* __restrict__ sd = reinterpret_cast<const uint4*>(desc);
     uint4* __restrict__ dd = reinterpret_cast<uint4*>(hdesc);
-    for (unsigned i = tid; i < n * 16; i += nt) dd[i] = sd[i];
+    if (hdesc)
+        for (unsigned i = tid; i < n * 16; i += nt) dd[i] = sd[i];
     const float4* __restrict__ sf = reinterpret_cast<const float4*>(f4);
     float4* __restrict__ df = reinterpret_cast<float4*>(hf4);
     for (unsigned i = tid; i < n; i += nt) df[i] = sf[i];

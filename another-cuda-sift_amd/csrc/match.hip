@@ -751,10 +751,13 @@ __global__ __launch_bounds__(64 * NW) void k_match_direct(
                        ratio_on_squared, idx2, d2out, match);
 }
 
-// Direct single pairs: 4 waves x 1 query block (128 queries per workgroup, the
-// done-counter block), one key group (256 train rows) per split up to
-// kDirectWgTarget workgroups.
-constexpr int kDirectNW = 4, kDirectQBW = 1, kDirectQB = 32 * kDirectNW * kDirectQBW, kDirectWgTarget = 256;
+// Direct single pairs: 8 waves x 1 query block (256 queries per workgroup),
+// one key group (256 train rows) per split up to kDirectWgTarget workgroups.
+// 2000 x 2000 on detector buffers (tools/match_direct_time.py, two passes):
+// 7.71 / 7.78 us; 4 waves 8.06 / 7.90; 4 waves x 2 blocks 8.97 / 8.98; two key
+// groups per split (target 64) 9.65 / 9.72; the converting k_match_single
+// on the same pair 11.2-11.4 (profiles/round5/match_direct_ab.jsonl).
+constexpr int kDirectNW = 8, kDirectQBW = 1, kDirectQB = 32 * kDirectNW * kDirectQBW, kDirectWgTarget = 256;
 
 int match_direct_splits(int nq, int nt) {
     const int ntiles = (nt + kMatchTileRows - 1) / kMatchTileRows, groups = (ntiles + kGroupTiles - 1) / kGroupTiles;
