@@ -43,7 +43,7 @@ CXX_SRCS := $(SRC)/detector_cxx.cpp $(SRC)/multi_cxx.cpp
 $(OUT)/libsift_cuda.so: $(CXX_SRCS) $(wildcard include/sift_cuda/*.hh) include/sift_hip.h $(OUT)/libsift_hip.so
 	$(CXX) $(CXXFLAGS) -pthread -shared -o $@ $(CXX_SRCS) -L$(OUT) -lsift_hip -Wl,-rpath,'$$ORIGIN'
 
-tools: $(OUT)/detection_example $(OUT)/extract_and_match_example $(OUT)/multi_gpu_example
+tools: $(OUT)/detection_example $(OUT)/extract_and_match_example $(OUT)/multi_gpu_example $(OUT)/host_pipeline_bench
 
 $(OUT)/%: tools/%.cpp $(OUT)/libsift_cuda.so
 	$(CXX) $(CXXFLAGS) -pthread -o $@ $< -L$(OUT) -lsift_cuda -lsift_hip -Wl,-rpath,'$$ORIGIN'

@@ -248,6 +248,18 @@ struct Lane {
     // lane's first host-input frame).
     char* hRes = nullptr;
     char* hResDev = nullptr;
+    // Host-input staging of this lane: two pinned (coarse-grained, so the
+    // GPU's L2 caches the halo re-reads) host buffers that the frame's first
+    // kernel reads over PCIe itself -- no upload copy: a separate H2D copy
+    // (60 us for a 2.3 MB frame) sat between a lane finishing one frame and
+    // starting the next, and host-input frames ran at 0.17 ms/frame where
+    // the same frames from device memory ran at 0.113 (3 lanes).  A slot is
+    // rewritten for the lane's frame after next, once evRead[slot] (recorded
+    // after the first kernel) has passed.
+    static constexpr int kInSlots = 2;
+    void* hStage[kInSlots] = {};
+    hipEvent_t evRead[kInSlots] = {};
+    long long uploads = 0;
     hipEvent_t evHost[kResultSlots] = {};
     long long hostFrame[kResultSlots] = {-1, -1, -1, -1};  // the frame each host region holds
     bool hostDesc[kResultSlots] = {};                       // ... with its descriptors
@@ -295,11 +307,6 @@ struct sift_hip_detector {
     FrameRec& frec(long long f) { return frecs[f & (kFrameRing - 1)]; }
     Lane& lane() { return lanes[ln]; }
     long long submitted = 0, current = -1, firstFrame = 0, uploads = 0;
-    static constexpr int kMaxInSlots = kMaxLanes + 1;
-    int nIn = 2;                                            // upload ring slots: lanes + 1
-    void* dIn[kMaxInSlots] = {};                            // uploaded frames (f32 or u8)
-    void* hStage[kMaxInSlots] = {};                         // pinned staging
-    hipEvent_t evUp[kMaxInSlots] = {}, evRead[kMaxInSlots] = {};  // upload done / first kernel done
 
     // Frame batches: up to B frames per launch (sift_hip_set_batch).  Every
     // per-frame buffer below lives in frame 0's arena of the bound lane; frame
@@ -426,15 +433,13 @@ struct sift_hip_detector {
                 if (L.arena) (void)hipFree(L.arena);
                 if (L.hCtr) (void)hipHostFree(L.hCtr);
                 if (L.hRes) (void)hipHostFree(L.hRes);
+                for (int k = 0; k < Lane::kInSlots; k++) {
+                    if (L.hStage[k]) (void)hipHostFree(L.hStage[k]);
+                    if (L.evRead[k]) (void)hipEventDestroy(L.evRead[k]);
+                }
                 for (hipEvent_t e : L.evHost)
                     if (e) (void)hipEventDestroy(e);
                 if (L.stream) (void)hipStreamDestroy(L.stream);
-            }
-            for (int k = 0; k < kMaxInSlots; k++) {
-                if (dIn[k]) (void)hipFree(dIn[k]);
-                if (hStage[k]) (void)hipHostFree(hStage[k]);
-                if (evUp[k]) (void)hipEventDestroy(evUp[k]);
-                if (evRead[k]) (void)hipEventDestroy(evRead[k]);
             }
             if (dDg) (void)hipFree(dDg);
             for (auto e : evPool) (void)hipEventDestroy(e);
@@ -623,17 +628,6 @@ int allocate(sift_hip_detector* d) {
     HIPCHK(hipEventCreateWithFlags(&d->evOut, hipEventDisableTiming));
     const int W = d->cfg.col_width, H = d->cfg.row_width;
     d->inPitch = (W + 63) / 64 * 64;
-    // Upload ring (host input path): one slot per lane + 1, sized for f32
-    // rows of pitch inPitch (an 8-bit frame uses the first quarter with a
-    // byte pitch of inPitch).
-    d->nIn = d->maxLanes + 1;
-    const size_t inBytes = sizeof(float) * (size_t)d->inPitch * H;
-    for (int k = 0; k < d->nIn; k++) {
-        if (hipMalloc(&d->dIn[k], inBytes) != hipSuccess) return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc failed");
-        HIPCHK(hipHostMalloc(&d->hStage[k], inBytes, hipHostMallocDefault));
-        HIPCHK(hipEventCreateWithFlags(&d->evUp[k], hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&d->evRead[k], hipEventDisableTiming));
-    }
     if (d->firstOctave < 0) d->upPitch = (2 * W + 63) / 64 * 64;
     size_t pyrFloats = 0;
     for (int o = 0; o < d->nOct; o++) pyrFloats += (size_t)d->pyr.oct[o].planeStride * (d->L + 3);
@@ -698,11 +692,15 @@ int add_lane(sift_hip_detector* d) {
         HIPCHK(hipEventCreateWithFlags(&L.evFrame[b], hipEventDisableTiming));
         HIPCHK(hipEventRecord(L.evFrame[b], L.stream));
     }
-    if (k == 0)  // upload-ring events start complete (recorded on the first lane)
-        for (int i = 0; i < d->nIn; i++) {
-            HIPCHK(hipEventRecord(d->evUp[i], L.stream));
-            HIPCHK(hipEventRecord(d->evRead[i], L.stream));
-        }
+    // The lane's host-input staging, sized for f32 rows of pitch inPitch (an
+    // 8-bit frame uses the first quarter with a byte pitch of inPitch); its
+    // events start complete.
+    const size_t inBytes = sizeof(float) * (size_t)d->inPitch * d->cfg.row_width;
+    for (int i = 0; i < Lane::kInSlots; i++) {
+        HIPCHK(hipHostMalloc(&L.hStage[i], inBytes, hipHostMallocMapped | hipHostMallocNonCoherent));
+        HIPCHK(hipEventCreateWithFlags(&L.evRead[i], hipEventDisableTiming));
+        HIPCHK(hipEventRecord(L.evRead[i], L.stream));
+    }
     bind_lane(d, k);
     for (int i = 0; i < d->B; i++)
         for (int b = 0; b < d->kSlots; b++)
@@ -1053,7 +1051,7 @@ int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEven
             launch_u8_to_f32((const uint8_t*)img, pitch, W, H, d->dDg, W, Frames{1, 0}, 0, d->stream);
         else
             HIPCHK(hipMemcpy2DAsync(d->dDg, sizeof(float) * W, img, sizeof(float) * (size_t)pitch, sizeof(float) * W,
-                                    H, hipMemcpyDeviceToDevice, d->stream));
+                                    H, hipMemcpyDefault, d->stream));
     }
     const bool graphs = d->useGraph && !d->timing;
     hipGraphExec_t gh = !graphs || consumed || fmt != SIFT_HIP_F32 ? nullptr
@@ -1216,20 +1214,18 @@ int submit_host(sift_hip_detector* d, const void* img, size_t stride, int fmt, l
     if (stride == 0) stride = rowB;
     if (stride < rowB) return fail(SIFT_HIP_ERR_INVALID, "row stride smaller than width");
     if (int rc = check_in_flight(d)) return rc;
-    hipStream_t cs;
-    if (int rc = copy_stream(d, &cs)) return rc;
     if (int rc = pick_lane(d)) return rc;
-    const int k = (int)(d->uploads % d->nIn);
-    HIPCHK(hipEventSynchronize(d->evUp[k]));  // staging slot k no longer being read
+    Lane& L = d->lane();
+    const int k = (int)(L.uploads & 1);
+    HIPCHK(hipEventSynchronize(L.evRead[k]));  // staging slot k no longer being read (the lane's frame before last)
     if (!d->pool && rowB * H >= (1u << 20)) d->pool = new CopyPool(3);
-    copy_rows(d->pool, (char*)d->hStage[k], pitchB, (const char*)img, stride, rowB, H);
-    HIPCHK(hipStreamWaitEvent(cs, d->evRead[k], 0));  // device slot k read by its last frame
-    HIPCHK(hipMemcpyAsync(d->dIn[k], d->hStage[k], pitchB * H, hipMemcpyHostToDevice, cs));
-    HIPCHK(hipEventRecord(d->evUp[k], cs));
-    HIPCHK(hipStreamWaitEvent(d->stream, d->evUp[k], 0));
+    copy_rows(d->pool, (char*)L.hStage[k], pitchB, (const char*)img, stride, rowB, H);
+    void* src = nullptr;
+    HIPCHK(hipHostGetDevicePointer(&src, L.hStage[k], 0));
+    L.uploads++;
     d->uploads++;
     const long long f = d->submitted;
-    int rc = run_frame(d, d->dIn[k], d->inPitch, fmt, d->evRead[k]);
+    int rc = run_frame(d, src, d->inPitch, fmt, L.evRead[k]);
     if (rc) return rc;
     if (d->dgDir.empty() && (rc = prefetch_results(d, f))) return rc;
     if (ticket) *ticket = f;
