@@ -479,6 +479,7 @@ __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* _
         }
         lds_barrier();
         const float scale = s_norm[8];
+        const unsigned po = (unsigned)jb.out;  // output row (the job order may differ: JobOrder)
         int c2 = 0;  // this thread's share of |codes|^2
 #pragma unroll
         for (int h = 0; h < kPer; h++) {
@@ -486,8 +487,8 @@ __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* _
             v = v < 0 ? 0 : (v > 255 ? 255 : v);
             const _Float16 hv = (_Float16)(float)v;
             if (tid + kDT * h < 128) {
-                desc[(size_t)p * 128 + tid + kDT * h] = __builtin_bit_cast(uint16_t, hv);
-                sidecar.codes[(size_t)p * 128 + tid + kDT * h] = (int8_t)(v - 128);
+                desc[(size_t)po * 128 + tid + kDT * h] = __builtin_bit_cast(uint16_t, hv);
+                sidecar.codes[(size_t)po * 128 + tid + kDT * h] = (int8_t)(v - 128);
                 c2 += (v - 128) * (v - 128);
             }
         }
@@ -497,7 +498,7 @@ __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* _
         c2 = __builtin_amdgcn_readlane(wave_incl_scan(c2), 63);
         if (lane == 0 && tid < 128) s_cn[tid >> 6] = c2;
         lds_barrier();  // sq / histograms are rewritten by the next keypoint
-        if (tid == 0) sidecar.keys[p] = -(256 * (s_cn[0] + s_cn[1]) + (int)(p & 255));
+        if (tid == 0) sidecar.keys[po] = -(256 * (s_cn[0] + s_cn[1]) + (int)(po & 255));
     }
 }
 
@@ -862,13 +863,14 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
         b0 = b0 < 0 ? 0 : (b0 > 255 ? 255 : b0);
         b1 = b1 < 0 ? 0 : (b1 > 255 ? 255 : b1);
         const _Float16 h0 = (_Float16)(float)b0, h1 = (_Float16)(float)b1;
-        reinterpret_cast<unsigned*>(desc + (size_t)p * 128)[lane] =
+        const unsigned po = (unsigned)jb.out;  // output row (jobs run longest first, JobOrder)
+        reinterpret_cast<unsigned*>(desc + (size_t)po * 128)[lane] =
             (unsigned)__builtin_bit_cast(uint16_t, h0) | (unsigned)__builtin_bit_cast(uint16_t, h1) << 16;
         // Matcher sidecar: int8 codes and the key bias (k_descriptor's epilogue).
-        reinterpret_cast<unsigned short*>(sidecar.codes + (size_t)p * 128)[lane] =
+        reinterpret_cast<unsigned short*>(sidecar.codes + (size_t)po * 128)[lane] =
             (unsigned short)((b0 - 128) & 255) | (unsigned short)(((b1 - 128) & 255) << 8);
         const int c2 = __builtin_amdgcn_readlane(wave_incl_scan((b0 - 128) * (b0 - 128) + (b1 - 128) * (b1 - 128)), 63);
-        if (lane == 0) sidecar.keys[p] = -(256 * c2 + (int)(p & 255));
+        if (lane == 0) sidecar.keys[po] = -(256 * c2 + (int)(po & 255));
         wave_lds_sync();  // rowpre / raw / s_norm are rewritten by the next keypoint
     }
 }

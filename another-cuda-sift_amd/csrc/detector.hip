@@ -269,7 +269,7 @@ struct Lane {
 // every arena of every lane).
 struct ArenaLayout {
     size_t input = 0, up = 0, pyr = 0, cand = 0, ref = 0, ori = 0, slot = 0, order = 0, jobs = 0, range = 0,
-           bcount = 0, boff = 0, bitmap = 0, ctr = 0;
+           bcount = 0, boff = 0, bitmap = 0, ctr = 0, jord = 0;
     size_t k3[kResultSlots] = {}, f4[kResultSlots] = {}, desc[kResultSlots] = {};
     size_t codes[kResultSlots] = {}, ckeys[kResultSlots] = {};  // matcher sidecar of desc (Sidecar)
     size_t octave[kMaxOctaves] = {};  // float offset of each octave's planes inside the pyramid
@@ -334,6 +334,7 @@ struct sift_hip_detector {
     int* dSlot = nullptr;
     int* dOrder = nullptr;
     DescJob* dJobs = nullptr;  // per final keypoint, written by k_bucket_rank
+    JobOrder* dJord = nullptr;  // descriptor job order (k_order -> k_rank_final)
     unsigned* dRange = nullptr;  // 2 * kRangeSlots pixel-range keys (initial blur -> descriptor)
     unsigned* dBcount = nullptr;
     unsigned* dBoff = nullptr;
@@ -583,6 +584,7 @@ void bind_lane(sift_hip_detector* d, int k) {
     d->dSlot = reinterpret_cast<int*>(A + a.slot);
     d->dOrder = reinterpret_cast<int*>(A + a.order);
     d->dJobs = reinterpret_cast<DescJob*>(A + a.jobs);
+    d->dJord = reinterpret_cast<JobOrder*>(A + a.jord);
     d->dRange = reinterpret_cast<unsigned*>(A + a.range);
     d->dBcount = reinterpret_cast<unsigned*>(A + a.bcount);
     d->dBoff = reinterpret_cast<unsigned*>(A + a.boff);
@@ -654,6 +656,7 @@ int allocate(sift_hip_detector* d) {
     a.slot = take(sizeof(int) * capO);
     a.order = take(sizeof(int) * capO);
     a.jobs = take(sizeof(DescJob) * capF);
+    a.jord = take(sizeof(JobOrder));
     a.range = take(sizeof(unsigned) * 2 * 2 * kRangeSlots);  // one set per frame parity
     a.bcount = take(sizeof(unsigned) * (size_t)d->kp.numBuckets);
     a.boff = take(sizeof(unsigned) * (size_t)d->kp.numBuckets);
@@ -882,8 +885,8 @@ void enqueue_order(sift_hip_detector* d, int slot, int nf) {
     const Frames fr{nf, d->afs};
     if (d->kp.numBuckets <= kOrderMaxBuckets) {
         d->timed("order", 0, [&] {
-            launch_order(d->dOri, d->dCtr, range_keys(d, parity ^ 1), d->dBcount, d->dBoff, d->dSlot, d->dOrder, d->kp,
-                         fr, s);
+            launch_order(d->pyr, d->dOri, d->dCtr, range_keys(d, parity ^ 1), d->dBcount, d->dBoff, d->dSlot, d->dOrder,
+                         d->dJord, d->kp, fr, s);
         });
     } else {
         d->timed("select", 0, [&] { launch_select(d->dOri, d->dCtr, range_keys(d, parity ^ 1), d->kp, fr, s); });
@@ -895,7 +898,7 @@ void enqueue_order(sift_hip_detector* d, int slot, int nf) {
     }
     d->timed("bucket_rank", 0, [&] {
         if (d->kp.numBuckets <= kOrderMaxBuckets)
-            launch_rank_final(d->pyr, d->dOri, d->dBcount, d->dBoff, d->dOrder, d->dCtr, d->dJobs, d->dKpts3[slot],
+            launch_rank_final(d->pyr, d->dOri, d->dBcount, d->dBoff, d->dOrder, d->dCtr, d->dJord, d->dJobs, d->dKpts3[slot],
                               d->dFeats4[slot], d->kp, fr, s);
         else  // bucket_count needs zeroed counts: the bucket-parallel ranking re-zeroes them
             launch_bucket_rank(d->pyr, d->dOri, d->dBcount, d->dBoff, d->dOrder, d->dCtr, d->dJobs, d->dKpts3[slot],
@@ -1395,7 +1398,7 @@ int dump_stage_files(sift_hip_detector* d) {
              "  \"oriented.rec\": \"OriKpt [slots] {f32 x, y, size, angle, response; i32 octave, bucket, sub}; "
              "bucket 0xffffffff = hole\",\n"
              "  \"jobs.rec\": \"DescJob [keypoints] 64 B {i64 plane o*(L+3)+layer; f32 cos_t, sin_t, angle, hist_width; "
-             "i32 ptx, pty, rows, cols, pitch, radius, pad[4]}\",\n"
+             "i32 ptx, pty, rows, cols, pitch, radius, out (the output row), pad[3]}; exact mode: largest windows first\",\n"
              "  \"range.u32\": \"u32 [2][%d] pixel-range keys of the frame\",\n"
              "  \"counters.u32\": \"u32 [8] {cand, refined, oriented, final, overflow, retainBest threshold bits, "
              "order entries, 0}\"}\n}\n",

@@ -596,13 +596,24 @@ void launch_bucket_scatter(const OriKpt* kpts, const Counters* ctr, const unsign
 // the counts), and order[].  Used when the buckets fit in LDS
 // (kOrderMaxBuckets); the four kernels above remain for larger pyramids.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_order(const OriKpt* __restrict__ kpts, Counters* __restrict__ ctr,
+// Segment (octave, layer) of a final keypoint in the bucket order (k_order's
+// job-order segments; JobOrder).
+__device__ __forceinline__ int lpt_seg(int packed_octave, int fo, int L) {
+    const int o = (int)(signed char)(packed_octave & 255) - fo, layer = (packed_octave >> 8) & 255;
+    return o * L + layer - 1;
+}
+
+__global__ __launch_bounds__(1024) void k_order(PyrDesc pyr, const OriKpt* __restrict__ kpts, Counters* __restrict__ ctr,
                                                 unsigned* __restrict__ zero_range, unsigned* __restrict__ bcount,
                                                 unsigned* __restrict__ boff, int* __restrict__ slot,
-                                                int* __restrict__ order, KeypointParams kp, long fs) {
+                                                int* __restrict__ order, JobOrder* __restrict__ jord,
+                                                KeypointParams kp, long fs) {
     extern __shared__ unsigned s_bucket[];  // counts, then exclusive offsets
     __shared__ unsigned hist[256], wsum[16];
     __shared__ unsigned s_prefix, s_k;
+    __shared__ unsigned s_seg[kLptSegs];  // kept keypoints per (octave, layer) segment
+    const int L = pyr.L, fo = pyr.firstOctave;
+    const bool lpt = kp.descExact && L <= 8 && pyr.nOct * L <= kLptSegs;  // exact mode only (JobOrder)
     const long foff = blockIdx.y * fs;  // frame blockIdx.y
     kpts = fptr(kpts, foff);
     ctr = fptr(ctr, foff);
@@ -611,11 +622,13 @@ __global__ __launch_bounds__(1024) void k_order(const OriKpt* __restrict__ kpts,
     boff = fptr(boff, foff);
     slot = fptr(slot, foff);
     order = fptr(order, foff);
+    jord = fptr(jord, foff);
     const unsigned n = oriented_count(ctr, kp);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nb = kp.numBuckets;
     for (int i = tid; i < 2 * kRangeSlots; i += 1024) zero_range[i] = 0u;  // next frame's range keys
     for (int i = tid; i < nb; i += 1024) s_bucket[i] = 0u;
+    if (tid < kLptSegs) s_seg[tid] = 0u;
     if (tid == 0) {
         s_prefix = 0;
         s_k = (unsigned)kp.numFeatures;
@@ -669,24 +682,29 @@ __global__ __launch_bounds__(1024) void k_order(const OriKpt* __restrict__ kpts,
         for (int u = 0; u < kOrderRegs; u++) {
             const unsigned i = tid + 1024u * u;
             rbk[u] = __float_as_int(q[u].z);
-            rsl[u] = i < n && (unsigned)rbk[u] != kHoleBucket && q[u].x >= thr ? (int)atomicAdd(&s_bucket[rbk[u]], 1u)
-                                                                               : -1;
+            const bool keep = i < n && (unsigned)rbk[u] != kHoleBucket && q[u].x >= thr;
+            rsl[u] = keep ? (int)atomicAdd(&s_bucket[rbk[u]], 1u) : -1;
+            if (keep && lpt) atomicAdd(&s_seg[lpt_seg(__float_as_int(q[u].y), fo, L)], 1u);
         }
     } else {
         for (unsigned i0 = tid; i0 < n; i0 += 4 * 1024) {
-            int bk[4];
+            int bk[4], oc[4];
             float rs[4];
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const unsigned i = min(i0 + 1024u * u, n - 1);
                 bk[u] = kpts[i].bucket;
                 rs[u] = kpts[i].response;
+                oc[u] = kpts[i].octave;
             }
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const unsigned i = i0 + 1024u * u;
-                if (i < n)
-                    slot[i] = (unsigned)bk[u] != kHoleBucket && rs[u] >= thr ? (int)atomicAdd(&s_bucket[bk[u]], 1u) : -1;
+                if (i < n) {
+                    const bool keep = (unsigned)bk[u] != kHoleBucket && rs[u] >= thr;
+                    slot[i] = keep ? (int)atomicAdd(&s_bucket[bk[u]], 1u) : -1;
+                    if (keep && lpt) atomicAdd(&s_seg[lpt_seg(oc[u], fo, L)], 1u);
+                }
             }
         }
     }
@@ -720,6 +738,24 @@ __global__ __launch_bounds__(1024) void k_order(const OriKpt* __restrict__ kpts,
             ctr->final_n = min(total, kp.capFinal);
             ctr->pad[0] = total;  // entries of `order` (k_rank_final)
             if (total > kp.capFinal) atomicOr(&ctr->overflow, 8u);
+            // Job order, longest first (JobOrder): segments in bucket order
+            // give the final positions, layers high to low the job positions.
+            const bool use = lpt && total <= kp.capFinal;
+            jord->valid = use;
+            if (use) {
+                const int ns = pyr.nOct * L;
+                unsigned start = 0;
+                for (int sg = 0; sg < ns; sg++) {
+                    jord->segStart[sg] = (int)start;
+                    start += s_seg[sg];
+                }
+                unsigned job = 0;
+                for (int l = L; l >= 1; l--)
+                    for (int o = 0; o < pyr.nOct; o++) {
+                        jord->jobBase[o * L + l - 1] = (int)job;
+                        job += s_seg[o * L + l - 1];
+                    }
+            }
         }
     }
     __syncthreads();
@@ -736,11 +772,12 @@ __global__ __launch_bounds__(1024) void k_order(const OriKpt* __restrict__ kpts,
     }
 }
 
-bool launch_order(const OriKpt* kpts, Counters* ctr, unsigned* zero_range, unsigned* bcount, unsigned* boff, int* slot,
-                  int* order, const KeypointParams& kp, const Frames& fr, hipStream_t s) {
+bool launch_order(const PyrDesc& pyr, const OriKpt* kpts, Counters* ctr, unsigned* zero_range, unsigned* bcount,
+                  unsigned* boff, int* slot, int* order, JobOrder* jord, const KeypointParams& kp, const Frames& fr,
+                  hipStream_t s) {
     if (kp.numBuckets > kOrderMaxBuckets) return false;
-    hipLaunchKernelGGL(k_order, dim3(1, fr.nf), dim3(1024), sizeof(unsigned) * (size_t)kp.numBuckets, s, kpts, ctr,
-                       zero_range, bcount, boff, slot, order, kp, fr.stride);
+    hipLaunchKernelGGL(k_order, dim3(1, fr.nf), dim3(1024), sizeof(unsigned) * (size_t)kp.numBuckets, s, pyr, kpts,
+                       ctr, zero_range, bcount, boff, slot, order, jord, kp, fr.stride);
     return true;
 }
 
@@ -774,7 +811,8 @@ __device__ DescJob make_desc_job(const PyrDesc& pyr, const OriKpt& kpt, long fof
     const float arg = angle * (float)(M_PI / 180);  // cosf/sinf via double
     j.cos_t = (float)cos((double)arg) / j.hist_width;
     j.sin_t = (float)sin((double)arg) / j.hist_width;
-    j.pad[0] = j.pad[1] = j.pad[2] = j.pad[3] = 0;
+    j.out = 0;
+    j.pad[0] = j.pad[1] = j.pad[2] = 0;
     return j;
 }
 
@@ -821,7 +859,9 @@ __global__ __launch_bounds__(256) void k_bucket_rank(PyrDesc pyr, const OriKpt* 
             const unsigned pos = base + rank;
             if (e < cnt && pos < cap) {
                 const OriKpt k = kpts[idx];
-                jobs[pos] = make_desc_job(pyr, k, foff);
+                DescJob j = make_desc_job(pyr, k, foff);
+                j.out = (int)pos;
+                jobs[pos] = j;
                 kpts3[3 * (size_t)pos + 0] = k.x;
                 kpts3[3 * (size_t)pos + 1] = k.y;
                 kpts3[3 * (size_t)pos + 2] = (float)((k.octave >> 8) & 255);
@@ -841,15 +881,16 @@ __global__ __launch_bounds__(256) void k_bucket_rank(PyrDesc pyr, const OriKpt* 
 __global__ __launch_bounds__(256) void k_rank_final(PyrDesc pyr, const OriKpt* __restrict__ kpts,
                                                     const unsigned* __restrict__ bcount,
                                                     const unsigned* __restrict__ boff, const int* __restrict__ order,
-                                                    const Counters* __restrict__ ctr, DescJob* __restrict__ jobs,
-                                                    float* __restrict__ kpts3, float* __restrict__ feats4,
-                                                    KeypointParams kp, long fs) {
+                                                    const Counters* __restrict__ ctr, const JobOrder* __restrict__ jord,
+                                                    DescJob* __restrict__ jobs, float* __restrict__ kpts3,
+                                                    float* __restrict__ feats4, KeypointParams kp, long fs) {
     const long foff = blockIdx.y * fs;  // frame blockIdx.y
     kpts = fptr(kpts, foff);
     bcount = fptr(bcount, foff);
     boff = fptr(boff, foff);
     order = fptr(order, foff);
     ctr = fptr(ctr, foff);
+    jord = fptr(jord, foff);
     jobs = fptr(jobs, foff);
     kpts3 = fptr(kpts3, foff);
     feats4 = fptr(feats4, foff);
@@ -857,6 +898,7 @@ __global__ __launch_bounds__(256) void k_rank_final(PyrDesc pyr, const OriKpt* _
     // positions below it); positions >= capFinal are dropped.
     const unsigned n = ctr->pad[0];
     const unsigned cap = kp.capFinal;
+    const bool lpt = jord->valid != 0;
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const OriKpt k = kpts[order[i]];
         const unsigned base = boff[k.bucket], cnt = bcount[k.bucket];
@@ -864,7 +906,14 @@ __global__ __launch_bounds__(256) void k_rank_final(PyrDesc pyr, const OriKpt* _
         for (unsigned f = 0; f < cnt; f++) rank += (unsigned)(kpts[order[base + f]].sub < k.sub);
         const unsigned pos = base + rank;
         if (pos < cap) {
-            jobs[pos] = make_desc_job(pyr, k, foff);
+            DescJob j = make_desc_job(pyr, k, foff);
+            j.out = (int)pos;
+            int q = (int)pos;
+            if (lpt) {
+                const int sg = lpt_seg(k.octave, pyr.firstOctave, pyr.L);
+                q = jord->jobBase[sg] + ((int)pos - jord->segStart[sg]);
+            }
+            jobs[q] = j;
             kpts3[3 * (size_t)pos + 0] = k.x;
             kpts3[3 * (size_t)pos + 1] = k.y;
             kpts3[3 * (size_t)pos + 2] = (float)((k.octave >> 8) & 255);
@@ -874,10 +923,10 @@ __global__ __launch_bounds__(256) void k_rank_final(PyrDesc pyr, const OriKpt* _
 }
 
 void launch_rank_final(const PyrDesc& pyr, const OriKpt* kpts, const unsigned* bcount, const unsigned* boff,
-                       const int* order, const Counters* ctr, DescJob* jobs, float* kpts3, float* feats4,
-                       const KeypointParams& kp, const Frames& fr, hipStream_t s) {
-    hipLaunchKernelGGL(k_rank_final, dim3(64, fr.nf), dim3(256), 0, s, pyr, kpts, bcount, boff, order, ctr, jobs, kpts3,
-                       feats4, kp, fr.stride);
+                       const int* order, const Counters* ctr, const JobOrder* jord, DescJob* jobs, float* kpts3,
+                       float* feats4, const KeypointParams& kp, const Frames& fr, hipStream_t s) {
+    hipLaunchKernelGGL(k_rank_final, dim3(64, fr.nf), dim3(256), 0, s, pyr, kpts, bcount, boff, order, ctr, jord, jobs,
+                       kpts3, feats4, kp, fr.stride);
 }
 
 void launch_bucket_rank(const PyrDesc& pyr, const OriKpt* kpts, unsigned* bcount, const unsigned* boff,

@@ -179,8 +179,25 @@ void launch_select(const OriKpt* kpts, Counters* ctr, unsigned* zero_range, cons
 // false (nothing launched) when the row buckets exceed kOrderMaxBuckets.
 constexpr int kOrderMaxBuckets = 16384;  // 64 KiB of LDS
 
-bool launch_order(const OriKpt* kpts, Counters* ctr, unsigned* zero_range, unsigned* bcount, unsigned* boff, int* slot,
-                  int* order, const KeypointParams& kp, const Frames& fr, hipStream_t s);
+// Descriptor job order, longest first (exact descriptor mode): jobs are
+// stored grouped by layer, highest layer (largest windows) first, octave and
+// final order inside, so the descriptor grid starts its largest keypoints in
+// its first residency round (a job's `out` keeps the output order).  Per
+// frame, written by k_order and read by k_rank_final: per (octave, layer)
+// segment its first final position and its first job index, and whether the
+// order is in use.  Measured (tools/desc_mode_bench.py, two passes): exact
+// mode 0.153 vs 0.156-0.157 ms per frame, single-frame sync 0.378-0.382 vs
+// 0.408-0.409 ms; the default mode 0.092-0.093 vs 0.090-0.091 ms per frame
+// (its per-keypoint cost varies less), so only the exact mode uses it.
+constexpr int kLptSegs = kMaxOctaves * 8;  // octaves x (L <= 8) layers
+struct JobOrder {
+    int valid;
+    int segStart[kLptSegs];
+    int jobBase[kLptSegs];
+};
+
+bool launch_order(const PyrDesc& pyr, const OriKpt* kpts, Counters* ctr, unsigned* zero_range, unsigned* bcount, unsigned* boff, int* slot,
+                  int* order, JobOrder* jord, const KeypointParams& kp, const Frames& fr, hipStream_t s);
 void launch_bucket_count(const OriKpt* kpts, const Counters* ctr, unsigned* bcount, int* slot,
                          const KeypointParams& kp, const Frames& fr, hipStream_t s);
 void launch_bucket_scan(unsigned* bcount, unsigned* boff, Counters* ctr, const KeypointParams& kp, const Frames& fr,
@@ -198,13 +215,14 @@ struct DescJob {
     int ptx, pty;            // rounded keypoint position in the octave
     int rows, cols, pitch;   // plane geometry
     int radius;              // window radius (clamped to the plane diagonal)
-    int pad[4];
+    int out;                 // output slot (descriptor row) of this job's keypoint
+    int pad[3];
 };
 
 static_assert(sizeof(DescJob) == 64, "DescJob is one 64-byte scalar load");
 
 void launch_rank_final(const PyrDesc& pyr, const OriKpt* kpts, const unsigned* bcount, const unsigned* boff,
-                       const int* order, const Counters* ctr, DescJob* jobs, float* kpts3, float* feats4,
+                       const int* order, const Counters* ctr, const JobOrder* jord, DescJob* jobs, float* kpts3, float* feats4,
                        const KeypointParams& kp, const Frames& fr, hipStream_t s);
 // Results of a finished frame -> mapped pinned host buffers (host-input frames).
 void launch_results_to_host(const float* k3, const float* f4, const uint16_t* desc, const Counters* ctr, unsigned cap,

@@ -101,7 +101,7 @@ def test_stage_replay_uses_the_dumped_input(sift, tmp_path):
     got = np.fromfile(os.path.join(out, "desc.f16"), np.uint16).reshape(-1, 128)
     ref = np.fromfile(os.path.join(dump, "desc.f16"), np.uint16).reshape(-1, 128)
     rows = np.nonzero(np.any(got != ref, 1))[0]
-    assert list(rows) == [3]
+    assert list(rows) == [int(jobs[3, 12])]  # the job's output row (DescJob.out)
     with pytest.raises(sift.SiftHipError):
         det.replayStage(dump, "no-such-stage", out)
 
