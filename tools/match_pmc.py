@@ -21,6 +21,15 @@ idx2 = sift.DeviceArray(K * (K - 1) * n * 8)
 m = sift.Matcher(n, n, max_pairs=K * (K - 1))
 for _ in range(10 * REPS):
     m.match_device(sets[0].value, n, sets[1].value, n, 0.8, False, idx2.value, 0, 0)
+# C3 on detector buffers (the reference's prev_descriptor x device_descriptor
+# call): the sidecar path, k_match_direct.
+W, H = 1920, 1200
+det = sift.Detector(sift.CudaSiftConfig(col_width=W, row_width=H, numOctaves=3, numFeatures=5000), device=0)
+det.gpuWarmUpAndAllocate()
+det.detectAndCompute(sift.synth_frame(77, W, H))
+det.detectAndCompute(sift.synth_frame(78, W, H))
+for _ in range(10 * REPS):
+    m.match_device(det.prev_descriptor.data(), n, det.device_descriptor.data(), n, 0.8, False, idx2.value, 0, 0)
 pairs = [(i, j) for i in range(K) for j in range(K) if i != j]
 for _ in range(5 * REPS):
     m.match_batched([sets[i].value for i, _ in pairs], [n] * len(pairs), [sets[j].value for _, j in pairs],

@@ -2,7 +2,7 @@
 
 Usage: python3 tools/mfma_summary.py TAG > profiles/roundN/mfma_counters.json
 Reads gpurun_out/mpmc_TAG_p{1,2}/run_counter_collection.csv; averages each
-counter over the dispatches of a matcher kernel with the same grid size.
+counter over the dispatches of a matcher kernel with the same (name, grid size).
 
 MFMA busy fraction = SQ_VALU_MFMA_BUSY_CYCLES / (kernel duration x 2.4 GHz x
 1024 SIMDs), the duration from the same pass's kernel trace: the fraction of
@@ -14,11 +14,18 @@ only as a raw counter.
 """
 import csv
 import json
+import re
 import sys
 from collections import defaultdict
 
 KEEP = ["SQ_INSTS_MFMA", "SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "SQ_INSTS_VALU", "SQ_LDS_BANK_CONFLICT",
         "SQ_ACTIVE_INST_LDS"]
+
+
+def kname(row):
+    """Short kernel name: k_match_single / k_match_direct / k_match_batch ..."""
+    m = re.search(r"(k_match\w*)", row["Kernel_Name"])
+    return m.group(1) if m else row["Kernel_Name"]
 
 
 def main(tag):
@@ -29,7 +36,7 @@ def main(tag):
             for row in csv.DictReader(f):
                 if "k_match" not in row["Kernel_Name"] or "prep" in row["Kernel_Name"]:
                     continue
-                per[(int(row["Grid_Size"]), row["Dispatch_Id"])][row["Counter_Name"]] += float(row["Counter_Value"])
+                per[((kname(row), int(row["Grid_Size"])), row["Dispatch_Id"])][row["Counter_Name"]] += float(row["Counter_Value"])
         for (grid, _), cs in per.items():
             for c, v in cs.items():
                 if c in KEEP and not (p == 2 and c == "GRBM_GUI_ACTIVE"):
@@ -38,20 +45,20 @@ def main(tag):
     with open(f"gpurun_out/mpmc_{tag}_p1/run_kernel_trace.csv") as f:
         for row in csv.DictReader(f):
             if "k_match" in row["Kernel_Name"] and "prep" not in row["Kernel_Name"]:
-                grid = int(row["Grid_Size_X"]) * int(row["Grid_Size_Y"]) * int(row["Grid_Size_Z"])
+                grid = (kname(row), int(row["Grid_Size_X"]) * int(row["Grid_Size_Y"]) * int(row["Grid_Size_Z"]))
                 dur[grid].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e3)
     dur_kt = defaultdict(list)  # unprofiled durations (kernel-trace-only run), if present
     try:
         with open(f"gpurun_out/mpmc_{tag}_kt/run_kernel_trace.csv") as f:
             for row in csv.DictReader(f):
                 if "k_match" in row["Kernel_Name"] and "prep" not in row["Kernel_Name"]:
-                    grid = int(row["Grid_Size_X"]) * int(row["Grid_Size_Y"]) * int(row["Grid_Size_Z"])
+                    grid = (kname(row), int(row["Grid_Size_X"]) * int(row["Grid_Size_Y"]) * int(row["Grid_Size_Z"]))
                     dur_kt[grid].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e3)
     except FileNotFoundError:
         pass
     out = []
     for grid in sorted(vals):
-        d = {"grid_size": grid, "dispatches": len(vals[grid]["SQ_INSTS_MFMA"])}
+        d = {"kernel": grid[0], "grid_size": grid[1], "dispatches": len(vals[grid]["SQ_INSTS_MFMA"])}
         for c in KEEP:
             xs = vals[grid][c]
             if xs:
