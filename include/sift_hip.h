@@ -144,9 +144,10 @@ int sift_hip_batch_copy_to_host(sift_hip_t h, int i, float* kpts3, float* feats4
 
 /* Pipelined host input (replaces the synchronous upload of CudaImage.cu:97-105
  * and the per-frame loop of extract_and_match_example.cc:69-101).
- * sift_hip_submit copies the frame into a pinned staging ring (the caller's
- * buffer is free again on return), uploads it on a copy stream while earlier
- * frames compute, enqueues the pipeline and returns a ticket without waiting.
+ * sift_hip_submit copies the frame into one of its lane's two mapped pinned
+ * staging buffers (the caller's buffer is free again on return), enqueues the
+ * pipeline -- whose first kernel reads the staging buffer over PCIe, no
+ * separate upload -- and returns a ticket without waiting.
  * sift_hip_wait(ticket) blocks until that frame is complete and makes it the
  * frame the result accessors address (prev_desc = frame ticket-1).  At most
  * 2 x lanes frames may be in flight past the last waited one
