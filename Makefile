@@ -48,6 +48,11 @@ tools: $(OUT)/detection_example $(OUT)/extract_and_match_example $(OUT)/multi_gp
 $(OUT)/%: tools/%.cpp $(OUT)/libsift_cuda.so
 	$(CXX) $(CXXFLAGS) -pthread -o $@ $< -L$(OUT) -lsift_cuda -lsift_hip -Wl,-rpath,'$$ORIGIN'
 
+# The host pipeline microbenchmark also calls the HIP runtime (pinned frames, a copy stream).
+$(OUT)/host_pipeline_bench: tools/host_pipeline_bench.cpp $(OUT)/libsift_cuda.so
+	$(CXX) $(CXXFLAGS) -pthread -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -o $@ $< -L$(OUT) -lsift_cuda -lsift_hip \
+	    -L$(ROCM_LIB) -lamdhip64 -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(ROCM_LIB)
+
 oracle:
 	$(MAKE) -C oracle
 

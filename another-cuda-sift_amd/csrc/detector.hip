@@ -250,12 +250,17 @@ struct Lane {
     char* hResDev = nullptr;
     // Host-input staging of this lane: two pinned (coarse-grained, so the
     // GPU's L2 caches the halo re-reads) host buffers that the frame's first
-    // kernel reads over PCIe itself -- no upload copy: a separate H2D copy
-    // (60 us for a 2.3 MB frame) sat between a lane finishing one frame and
-    // starting the next, and host-input frames ran at 0.17 ms/frame where
-    // the same frames from device memory ran at 0.113 (3 lanes).  A slot is
-    // rewritten for the lane's frame after next, once evRead[slot] (recorded
-    // after the first kernel) has passed.
+    // kernel reads over PCIe itself.  Measured alternatives
+    // (tools/host_pipeline_bench.cpp, 3 lanes x 6 frames, C2 u8 frames,
+    // profiles/round5/upload_ab.jsonl): DMA on a separate upload stream
+    // 0.169 ms/frame at HIP's default 4 hardware queues per process (two
+    // active streams then share a queue: device frames ordered after a
+    // 4 KiB copy on a 4th stream run at 0.160 instead of 0.112), 0.119-0.126
+    // at GPU_MAX_HW_QUEUES=8 -- but 8 queues slowed the bench process's
+    // device-frame lanes to 0.160; DMA on the lane's own stream 0.21-0.23
+    // (the submit waits behind the lane); this zero-copy read 0.165-0.170.  A
+    // slot is rewritten for the lane's frame after next, once evRead[slot]
+    // (recorded after the first kernel) has passed.
     static constexpr int kInSlots = 2;
     void* hStage[kInSlots] = {};
     hipEvent_t evRead[kInSlots] = {};
@@ -1970,7 +1975,10 @@ int sift_hip_copy_to_host(sift_hip_t d, float* k3, float* f4, uint16_t* desc, in
         if (n > 0) {
             if (k3) memcpy(k3, hk3, sizeof(float) * 3 * n);
             if (f4) memcpy(f4, hf4, sizeof(float) * 4 * n);
-            if (desc) memcpy(desc, hdesc, sizeof(uint16_t) * 128 * n);
+            if (desc) {  // 2.2 MB at C2: split over the copy pool (one thread: 0.100 -> 0.047 ms, C++ loop)
+                if (!d->pool && 256u * n >= (1u << 20)) d->pool = new CopyPool(3);
+                copy_rows(d->pool, (char*)desc, 256, (const char*)hdesc, 256, 256, n);
+            }
         }
         return SIFT_HIP_OK;
     }

@@ -17,8 +17,8 @@ W, H, N = 1920, 1200, 150
 cfg = sift.CudaSiftConfig(col_width=W, row_width=H, numFeatures=5000, numOctaves=3)
 dev = [torch.from_numpy(sift.synth_frame(i, W, H)).cuda() for i in range(4)]
 torch.cuda.synchronize()
-out = {"lib": os.environ.get("SIFT_HIP_LIB", "default")}
-for lanes, depth in ((3, 3), (3, 6), (2, 4)):
+out = {"lib": os.environ.get("SIFT_HIP_LIB", "default"), "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "")}
+for lanes, depth in ((3, 3), (3, 6), (2, 4), (4, 8)):
     det = sift.Detector(cfg, lanes=lanes)
     det.gpuWarmUpAndAllocate()
     q = []

@@ -5,12 +5,23 @@
 // ms per frame, and the mean wall time of each call.
 //   host_pipeline_bench [lanes] [depth] [frames] [desc 0|1|2] [dev 0|1]
 // desc 2: no copyToHost at all; dev 1: the frames already in device memory
-// (submitDevice) instead of host frames (submit).
+// (submitDevice) instead of host frames (submit); dev 2: the frames in pinned
+// host memory, read by the frame's first kernel over PCIe (submitDevice with
+// the mapped pointer: no staging copy on the calling thread); dev 3: the same
+// pinned frames moved by DMA (hipMemcpyAsync on a copy stream into a device
+// ring of `depth` + 1 slots) and submitted ordered after the copy.  Timing
+// diagnostics: dev 4 = device frames ordered after a 4 KiB copy on the copy
+// stream (the cross-stream wait alone); dev 5 = dev 3's DMA with the frame
+// submitted unordered (the copy's concurrency alone; the frame reads the slot's
+// previous contents, a valid older frame).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <deque>
 #include <vector>
+
+#include <hip/hip_runtime_api.h>
 
 #include "sift_cuda/Detector.hh"
 #include "sift_hip.h"
@@ -20,7 +31,7 @@ int main(int argc, char** argv) {
     const int frames = argc > 3 ? std::atoi(argv[3]) : 200;
     const int descMode = argc > 4 ? std::atoi(argv[4]) : 1;
     const bool desc = descMode == 1, copy = descMode != 2;
-    const bool dev = argc > 5 && std::atoi(argv[5]) != 0;
+    const int dev = argc > 5 ? std::atoi(argv[5]) : 0;
     const int W = 1920, H = 1200;
     std::vector<Image8U> imgs;
     for (int i = 0; i < 4; i++) {
@@ -39,12 +50,43 @@ int main(int argc, char** argv) {
     sift_cuda::Detector det(cfg);
     det.setLanes(lanes);
     det.gpuWarmUpAndAllocate();
-    std::vector<void*> dframes(4, nullptr);
-    if (dev)
+    std::vector<void*> dframes(4, nullptr), pinned(4, nullptr), ring(depth + 1, nullptr);
+    hipStream_t cs = nullptr;
+    if (dev == 1 || dev == 4)
         for (int i = 0; i < 4; i++) {
             sift_hip_malloc(&dframes[i], (size_t)W * H);
             sift_hip_memcpy_h2d(dframes[i], imgs[i].m_data->data(), (size_t)W * H);
         }
+    if (dev == 2 || dev == 3 || dev == 5)
+        for (int i = 0; i < 4; i++) {
+            if (hipHostMalloc(&pinned[i], (size_t)W * H, hipHostMallocMapped) != hipSuccess) return 1;
+            std::memcpy(pinned[i], imgs[i].m_data->data(), (size_t)W * H);
+            if (dev == 2 && hipHostGetDevicePointer(&dframes[i], pinned[i], 0) != hipSuccess) return 1;
+        }
+    void *small = nullptr, *smallDev = nullptr;
+    if (dev >= 3) {
+        if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) return 1;
+        for (auto& r : ring) {
+            sift_hip_malloc(&r, (size_t)W * H);
+            sift_hip_memcpy_h2d(r, imgs[0].m_data->data(), (size_t)W * H);
+        }
+        if (hipHostMalloc(&small, 4096, 0) != hipSuccess) return 1;
+        sift_hip_malloc(&smallDev, 4096);
+    }
+    long long nsub = 0;
+    auto submit = [&](int s) -> long long {
+        if (dev == 0) return det.submit(imgs[s % 4]);
+        if (dev == 4) {
+            (void)hipMemcpyAsync(smallDev, small, 4096, hipMemcpyHostToDevice, cs);
+            return det.submitDevice(dframes[s % 4], W, true, cs);
+        }
+        if (dev != 3 && dev != 5) return det.submitDevice(dframes[s % 4], W, true);
+        // ring slot nsub % (depth + 1) was last read by a frame already waited
+        // for (at most `depth` frames in flight)
+        void* dst = ring[nsub++ % ring.size()];
+        (void)hipMemcpyAsync(dst, pinned[s % 4], (size_t)W * H, hipMemcpyHostToDevice, cs);
+        return det.submitDevice(dst, W, true, dev == 3 ? cs : nullptr);
+    };
     using clk = std::chrono::steady_clock;
     double tSub = 0, tWait = 0, tCopy = 0;
     auto run = [&](int n, bool timed) {
@@ -63,7 +105,7 @@ int main(int argc, char** argv) {
         };
         for (int s = 0; s < n; s++) {
             auto a = clk::now();
-            q.push_back(dev ? det.submitDevice(dframes[s % 4], W, true) : det.submit(imgs[s % 4]));
+            q.push_back(submit(s));
             if (timed) tSub += std::chrono::duration<double, std::milli>(clk::now() - a).count();
             if ((int)q.size() == depth) drain();
         }

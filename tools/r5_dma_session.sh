@@ -1,0 +1,23 @@
+#!/bin/bash
+# Host frames by DMA on the lane's stream: GPU tests, the C++ host pipeline
+# and a short bench run (HIP's default hardware queues).
+set -o pipefail
+export TMPDIR=/tmp
+B=another-cuda-sift_amd/lib/host_pipeline_bench
+timeout -k 10 600 python -u -m pytest tests/ -q -m gpu -x --timeout 120 --timeout-method thread > gpurun_out/pytest_dma.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_dma.log; [ $rc -eq 0 ] || exit 1
+: > gpurun_out/dma_modes.jsonl
+run() { timeout -k 10 120 "$@" >> gpurun_out/dma_modes.jsonl 2> gpurun_out/dma_modes.err || { tail -5 gpurun_out/dma_modes.err; exit 1; }; }
+run $B 3 6 300 2 0
+run $B 3 6 300 1 0
+run $B 3 6 300 0 0
+run $B 2 4 300 1 0
+run $B 4 8 300 1 0
+run $B 1 2 150 1 0
+run $B 1 1 150 1 0
+run $B 3 6 300 2 1
+grep dev gpurun_out/dma_modes.jsonl
+timeout -k 10 400 python bench.py --steps 50 --warmup 10 --no-cpu-baseline > gpurun_out/bench_dma.json 2> gpurun_out/bench_dma.err || { tail -5 gpurun_out/bench_dma.err; exit 1; }
+python3 -c "
+import json; d=json.loads(open('gpurun_out/bench_dma.json').read().strip().splitlines()[-1])
+print(d['value'], d['sync_ms_per_frame'], json.dumps(d['host_input']), json.dumps(d['device_submit']))"
