@@ -240,9 +240,11 @@ struct Lane {
     hipGraph_t graphH[kResultSlots] = {}, graphH1[kResultSlots] = {};
     hipGraphNode_t headH[kResultSlots] = {}, headH1[kResultSlots] = {};
     int nfOf[kResultSlots] = {};  // frames of the launch group that wrote each slot
-    long long slotFrame[kResultSlots] = {-1, -1, -1, -1};  // the frame whose results each slot holds
+    long long slotFrame[kResultSlots] = {-1, -1, -1, -1};  // the (first) frame whose results each slot holds
+    int slotNum[kResultSlots] = {};  // frame numbers in that slot (> 1: a micro-batch, frame slotFrame + i in arena i)
     long long launched = 0;  // launch groups run on this lane; the next takes slot launched % kResultSlots
     long long last = -1;     // the last frame launched here (-1: none since warm-up)
+    char* mbIn = nullptr;    // micro-batch input copies: mb frames of f32 rows (created at the first micro-batch)
     // Host-input frames: results copied to mapped pinned host memory right
     // after the frame (k_results_to_host), one region per slot (created at the
     // lane's first host-input frame).
@@ -305,8 +307,25 @@ struct sift_hip_detector {
     int maxLanes = 2;  // sift_hip_set_lanes
     int ln = 0;        // the lane the pointer views below are bound to (bind_lane)
     int curLane = 0;   // lane of `current`
+    int curIdx = 0;    // arena of `current` in its lane (micro-batches)
+    // Micro-batching (sift_hip_set_micro_batch): device frames submitted with
+    // sift_hip_submit_device queue here until mb of them run as one launch
+    // group on a lane (the B-frame graphs, frame i in arena i), or until a
+    // wait / sync / other submit needs them.  Tickets run ahead of `submitted`
+    // by the frames pending.
+    static constexpr int kMaxMicroBatch = 16;
+    int mb = 1;
+    struct PendingFrame {
+        const void* img;
+        size_t stride;
+        int fmt;
+        bool ordered;  // the lane waits for evPend[i] (the caller's stream)
+    };
+    PendingFrame pend[kMaxMicroBatch] = {};
+    hipEvent_t evPend[kMaxMicroBatch] = {};
+    int npend = 0;
     struct FrameRec {
-        int lane = 0, slot = 0;
+        int lane = 0, slot = 0, idx = 0;  // idx: the frame's arena in a micro-batch
     };
     FrameRec frecs[kFrameRing];
     FrameRec& frec(long long f) { return frecs[f & (kFrameRing - 1)]; }
@@ -437,6 +456,7 @@ struct sift_hip_detector {
                     if (L.evFrame[b]) (void)hipEventDestroy(L.evFrame[b]);
                 }
                 if (L.arena) (void)hipFree(L.arena);
+                if (L.mbIn) (void)hipFree(L.mbIn);
                 if (L.hCtr) (void)hipHostFree(L.hCtr);
                 if (L.hRes) (void)hipHostFree(L.hRes);
                 for (int k = 0; k < Lane::kInSlots; k++) {
@@ -450,6 +470,8 @@ struct sift_hip_detector {
             if (dDg) (void)hipFree(dDg);
             for (auto e : evPool) (void)hipEventDestroy(e);
             if (evIn) (void)hipEventDestroy(evIn);
+            for (hipEvent_t e : evPend)
+                if (e) (void)hipEventDestroy(e);
             if (evOut) (void)hipEventDestroy(evOut);
             if (copyStream) (void)hipStreamDestroy(copyStream);
         }
@@ -572,8 +594,10 @@ int dalloc(T** p, size_t count) {
 
 // Points the handle's buffer views (stream, frame-0 arena pointers, host
 // counters) at lane k.  Every entry point binds the lane it works on: the
-// submitting lane for a new frame, the current frame's lane for accessors.
-void bind_lane(sift_hip_detector* d, int k) {
+// submitting lane for a new frame (idx 0: launches address frame 0's arena),
+// the current frame's lane and arena for accessors (idx: its arena in a
+// micro-batch, which offsets the results views and host counters).
+void bind_lane(sift_hip_detector* d, int k, int idx = 0) {
     Lane& L = d->lanes[k];
     const ArenaLayout& a = d->lay;
     char* A = L.arena;
@@ -595,24 +619,25 @@ void bind_lane(sift_hip_detector* d, int k) {
     d->dBoff = reinterpret_cast<unsigned*>(A + a.boff);
     d->dBitmap = reinterpret_cast<uint32_t*>(A + a.bitmap);
     d->dCtr = reinterpret_cast<Counters*>(A + a.ctr);
+    char* R = A + (size_t)idx * d->afs;
     for (int b = 0; b < d->kSlots; b++) {
-        d->dKpts3[b] = reinterpret_cast<float*>(A + a.k3[b]);
-        d->dFeats4[b] = reinterpret_cast<float*>(A + a.f4[b]);
-        d->dDesc[b] = reinterpret_cast<uint16_t*>(A + a.desc[b]);
-        d->dSide[b] = Sidecar{reinterpret_cast<int8_t*>(A + a.codes[b]), reinterpret_cast<int*>(A + a.ckeys[b])};
+        d->dKpts3[b] = reinterpret_cast<float*>(R + a.k3[b]);
+        d->dFeats4[b] = reinterpret_cast<float*>(R + a.f4[b]);
+        d->dDesc[b] = reinterpret_cast<uint16_t*>(R + a.desc[b]);
+        d->dSide[b] = Sidecar{reinterpret_cast<int8_t*>(R + a.codes[b]), reinterpret_cast<int*>(R + a.ckeys[b])};
     }
-    d->hCtr = L.hCtr;
-    d->hCtrDev = L.hCtrDev;
+    d->hCtr = L.hCtr + idx;
+    d->hCtrDev = L.hCtrDev + idx;
 }
 
 // Results of frame f (lane and slot from its record), without binding.
 const uint16_t* frame_desc(const sift_hip_detector* d, long long f) {
     const auto& r = d->frecs[f & (kFrameRing - 1)];
-    return reinterpret_cast<const uint16_t*>(d->lanes[r.lane].arena + d->lay.desc[r.slot]);
+    return reinterpret_cast<const uint16_t*>(d->lanes[r.lane].arena + (size_t)r.idx * d->afs + d->lay.desc[r.slot]);
 }
 const Counters& frame_counters(const sift_hip_detector* d, long long f, int i = 0) {
     const auto& r = d->frecs[f & (kFrameRing - 1)];
-    return d->lanes[r.lane].hCtr[(size_t)r.slot * d->B + i];
+    return d->lanes[r.lane].hCtr[(size_t)r.slot * d->B + r.idx + i];
 }
 
 // Per-handle allocations shared by the lanes: the upload ring and the frame
@@ -1018,7 +1043,8 @@ int warm_lane(sift_hip_detector* d) {
 int pick_lane(sift_hip_detector* d) {
     auto slot_free = [&](int k) {
         const Lane& L = d->lanes[k];
-        const long long occ = L.slotFrame[L.launched % d->kSlots];
+        const int s = (int)(L.launched % d->kSlots);
+        const long long occ = L.slotFrame[s] < 0 ? -1 : L.slotFrame[s] + std::max(L.slotNum[s], 1) - 1;  // its last frame
         return occ < 0 || occ < d->firstFrame || occ < d->current - 1;
     };
     int busy = -1;
@@ -1043,10 +1069,11 @@ int pick_lane(sift_hip_detector* d) {
 
 // Enqueues launch group d->submitted (nf frames at byte stride sfs) on the
 // bound lane (pick_lane); `consumed` (nullable) is recorded once the input has
-// been read.  With stage dumps on (single frames after warm-up) the frame's
+// been read.  A batch (sift_hip_detect_batch_device) is one frame number; a
+// micro-batch (`numbered`) takes nf numbers, frame d->submitted + i in arena i.  With stage dumps on (single frames after warm-up) the frame's
 // input is kept as float, the frame is completed synchronously and dumped.
 int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEvent_t consumed, int nf = 1,
-              long sfs = 0) {
+              long sfs = 0, bool numbered = false) {
     const long long f = d->submitted;
     Lane& L = d->lane();
     const int slot = (int)(L.launched % d->kSlots);
@@ -1087,17 +1114,20 @@ int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEven
         }
     }
     HIPCHK(hipEventRecord(L.evFrame[slot], d->stream));
+    const int nums = numbered ? nf : 1;
     L.nfOf[slot] = nf;
     L.slotFrame[slot] = f;
+    L.slotNum[slot] = nums;
     L.launched++;
-    L.last = f;
-    d->frec(f) = sift_hip_detector::FrameRec{d->ln, slot};
-    d->submitted = f + 1;
+    L.last = f + nums - 1;
+    for (int i = 0; i < nums; i++) d->frec(f + i) = sift_hip_detector::FrameRec{d->ln, slot, i};
+    d->submitted = f + nums;
     if (dump) {
         HIPCHK(hipStreamSynchronize(d->stream));
         if (d->timing) d->collect_timing();
         d->current = f;
         d->curLane = d->ln;
+        d->curIdx = 0;
         d->cur = slot;
         complete_counts(d);
         return dump_stage_files(d);
@@ -1110,9 +1140,10 @@ int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEven
 void make_current(sift_hip_detector* d, long long f) {
     d->current = f;
     d->curLane = d->frec(f).lane;
+    d->curIdx = d->frec(f).idx;
     d->cur = d->frec(f).slot;
     d->countsValid = false;
-    bind_lane(d, d->curLane);
+    bind_lane(d, d->curLane, d->curIdx);
 }
 
 void complete_counts(sift_hip_detector* d) {
@@ -1146,7 +1177,10 @@ int sync_lanes(sift_hip_detector* d) {
     return SIFT_HIP_OK;
 }
 
+int run_group(sift_hip_detector* d);
+
 int finish_frame(sift_hip_detector* d) {
+    if (int rc = run_group(d)) return rc;
     if (int rc = sync_lanes(d)) return rc;
     if (d->submitted > 0) {
         make_current(d, d->submitted - 1);
@@ -1166,8 +1200,8 @@ int format_size(int fmt) { return fmt == SIFT_HIP_U8 ? 1 : (fmt == SIFT_HIP_F32 
 // Frames in flight past `current` (host-input and device submits): at most 2
 // per lane the handle may use.
 int check_in_flight(sift_hip_detector* d) {
-    if (d->submitted > d->current + 2LL * d->maxLanes)
-        return fail(SIFT_HIP_ERR_STATE, "every lane already has two frames in flight past the current one: sift_hip_wait first");
+    if (d->submitted + d->npend > d->current + 2LL * d->maxLanes * d->mb)
+        return fail(SIFT_HIP_ERR_STATE, "every lane already has two launch groups in flight past the current frame: sift_hip_wait first");
     return SIFT_HIP_OK;
 }
 
@@ -1222,6 +1256,7 @@ int submit_host(sift_hip_detector* d, const void* img, size_t stride, int fmt, l
     if (stride == 0) stride = rowB;
     if (stride < rowB) return fail(SIFT_HIP_ERR_INVALID, "row stride smaller than width");
     if (int rc = check_in_flight(d)) return rc;
+    if (int rc = run_group(d)) return rc;  // pending micro-batch frames keep their submission order
     if (int rc = pick_lane(d)) return rc;
     Lane& L = d->lane();
     const int k = (int)(L.uploads & 1);
@@ -1240,11 +1275,52 @@ int submit_host(sift_hip_detector* d, const void* img, size_t stride, int fmt, l
     return SIFT_HIP_OK;
 }
 
+// The pending micro-batch frames as one launch group on a lane: each frame's
+// rows are copied (device to device, on the lane's stream after the caller's
+// stream event) into the lane's micro-batch input at a fixed frame stride, and
+// the group runs the B-frame graphs (a partial group: the 1-frame graphs, or
+// the same launches eagerly), frame d->submitted + i in arena i.
+int run_group(sift_hip_detector* d) {
+    const int n = d->npend;
+    if (!n) return SIFT_HIP_OK;
+    if (int rc = pick_lane(d)) return rc;
+    Lane& L = d->lane();
+    const int W = d->cfg.col_width, H = d->cfg.row_width;
+    const size_t fb = sizeof(float) * (size_t)d->inPitch * H;  // one frame of f32 rows (an 8-bit frame uses a quarter)
+    if (!L.mbIn && hipMalloc((void**)&L.mbIn, fb * d->mb) != hipSuccess)
+        return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc of the micro-batch input failed");
+    const int fmt = d->pend[0].fmt, es = format_size(fmt);
+    for (int i = 0; i < n; i++) {
+        const auto& p = d->pend[i];
+        if (p.ordered) HIPCHK(hipStreamWaitEvent(d->stream, d->evPend[i], 0));
+        HIPCHK(hipMemcpy2DAsync(L.mbIn + fb * i, (size_t)es * d->inPitch, p.img, p.stride, (size_t)es * W, H,
+                                hipMemcpyDeviceToDevice, d->stream));
+    }
+    d->npend = 0;
+    return run_frame(d, L.mbIn, d->inPitch, fmt, nullptr, n, (long)fb, true);
+}
+
 // Device frame (HBM-resident, fp32 or u8) -> the frame's lane; the lane waits
-// for `stream` (the caller's producer) before reading it.
+// for `stream` (the caller's producer) before reading it.  `queue`: a single
+// frame of sift_hip_submit_device on a micro-batching handle joins the pending
+// group instead (one format per group: a frame of the other format flushes it).
 int submit_device(sift_hip_detector* d, const void* img, size_t stride, int fmt, void* stream, int nf, size_t fstride,
-                  long long* ticket) {
+                  long long* ticket, bool queue = false) {
     hipStream_t ext = (hipStream_t)stream;
+    if (queue && d->mb > 1 && nf == 1 && d->dgDir.empty() && !d->timing) {
+        if (d->npend && d->pend[0].fmt != fmt)
+            if (int rc = run_group(d)) return rc;
+        const int i = d->npend;
+        if (ext) {
+            if (!d->evPend[i]) HIPCHK(hipEventCreateWithFlags(&d->evPend[i], hipEventDisableTiming));
+            HIPCHK(hipEventRecord(d->evPend[i], ext));
+        }
+        d->pend[i] = sift_hip_detector::PendingFrame{img, stride, fmt, ext != nullptr};
+        d->npend = i + 1;
+        if (ticket) *ticket = d->submitted + i;
+        return d->npend == d->mb ? run_group(d) : SIFT_HIP_OK;
+    }
+    if (int rc = run_group(d)) return rc;  // frames are numbered (and launched) in submission order
     if (int rc = pick_lane(d)) return rc;
     if (ext) {
         HIPCHK(hipEventRecord(d->evIn, ext));
@@ -1257,11 +1333,14 @@ int submit_device(sift_hip_detector* d, const void* img, size_t stride, int fmt,
 }
 
 int wait_frame(sift_hip_detector* d, long long f) {
+    if (f >= d->submitted && f < d->submitted + d->npend)
+        if (int rc = run_group(d)) return rc;  // a pending micro-batch frame: launch the partial group now
     if (f < d->firstFrame || f >= d->submitted || f < d->submitted - kFrameRing)
         return fail(SIFT_HIP_ERR_INVALID, "unknown frame ticket");
     const auto& r = d->frec(f);
     Lane& L = d->lanes[r.lane];
-    if (L.slotFrame[r.slot] != f) return fail(SIFT_HIP_ERR_STATE, "frame results already recycled");
+    if (L.slotFrame[r.slot] < 0 || f < L.slotFrame[r.slot] || f >= L.slotFrame[r.slot] + std::max(L.slotNum[r.slot], 1))
+        return fail(SIFT_HIP_ERR_STATE, "frame results already recycled");
     if (d->timing) {
         if (int rc = sync_lanes(d)) return rc;
     } else {
@@ -1478,6 +1557,7 @@ int replay_reset(sift_hip_detector* d) {
     d->firstFrame = d->submitted;
     d->current = d->submitted - 1;
     d->curLane = 0;
+    d->curIdx = 0;
     d->cur = 0;
     d->count = d->prevCount = 0;
     d->countsValid = true;
@@ -1641,7 +1721,7 @@ int replay_stage(sift_hip_detector* d, const std::string& in, const std::string&
         if (!(h)->allocated || !(h)->nLanes)                                                  \
             return fail(SIFT_HIP_ERR_STATE, "sift_hip_warmup not called");                    \
         HIPCHK(hipSetDevice((h)->device));                                                    \
-        bind_lane((h), (h)->curLane);                                                         \
+        bind_lane((h), (h)->curLane, (h)->curIdx);                                            \
     } while (0)
 
 }  // namespace
@@ -1707,6 +1787,11 @@ int sift_hip_destroy(sift_hip_t h) {
 int sift_hip_warmup(sift_hip_t d) {
     if (!d) return fail(SIFT_HIP_ERR_INVALID, "null handle");
     if (d->allocated) return d->nLanes ? SIFT_HIP_OK : fail(SIFT_HIP_ERR_STATE, "an earlier warm-up failed");
+    if (d->mb > 1) {  // a micro-batch runs the lane's B-frame graphs
+        if (d->B > 1 && d->B != d->mb)
+            return fail(SIFT_HIP_ERR_INVALID, "micro-batch and batch size differ (set one, or both equal)");
+        d->B = d->mb;
+    }
     int rc = allocate(d);
     if (rc) return rc;
     rc = add_lane(d);  // lane 0; more lanes on demand (pick_lane)
@@ -1792,7 +1877,7 @@ int sift_hip_submit_device(sift_hip_t d, const void* img, size_t stride, int for
     if (stride % es || stride < (size_t)es * W)
         return fail(SIFT_HIP_ERR_INVALID, "row stride must be a multiple of the pixel size and >= width");
     if (int rc = check_in_flight(d)) return rc;
-    return submit_device(d, img, stride, format, stream, 1, 0, ticket);
+    return submit_device(d, img, stride, format, stream, 1, 0, ticket, true);
 }
 
 int sift_hip_detect_device(sift_hip_t d, const float* img, size_t stride, void* stream) {
@@ -1812,6 +1897,21 @@ int sift_hip_set_lanes(sift_hip_t d, int lanes) {
     if (lanes < 1 || lanes > kMaxLanes) return fail(SIFT_HIP_ERR_INVALID, "lanes out of range (1..4)");
     if (d->allocated) return fail(SIFT_HIP_ERR_STATE, "sift_hip_set_lanes after sift_hip_warmup");
     d->maxLanes = lanes;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_set_micro_batch(sift_hip_t d, int frames) {
+    if (!d) return fail(SIFT_HIP_ERR_INVALID, "null handle");
+    if (frames < 1 || frames > sift_hip_detector::kMaxMicroBatch)
+        return fail(SIFT_HIP_ERR_INVALID, "micro-batch out of range (1..16)");
+    if (d->allocated) return fail(SIFT_HIP_ERR_STATE, "sift_hip_set_micro_batch after sift_hip_warmup");
+    d->mb = frames;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_micro_batch(sift_hip_t d, int* frames) {
+    if (!d || !frames) return fail(SIFT_HIP_ERR_INVALID, "null argument");
+    *frames = d->mb;
     return SIFT_HIP_OK;
 }
 
@@ -1919,7 +2019,7 @@ int sift_hip_num_keypoints(sift_hip_t d, int* n) {
     if (!d || !n) return fail(SIFT_HIP_ERR_INVALID, "null argument");
     if (d->allocated && d->nLanes) {
         HIPCHK(hipSetDevice(d->device));
-        bind_lane(d, d->curLane);
+        bind_lane(d, d->curLane, d->curIdx);
         if (int rc = ensure_counts(d)) return rc;
     }
     *n = d->count;
@@ -1930,7 +2030,7 @@ int sift_hip_overflow_flags(sift_hip_t d, int* flags) {
     if (!d || !flags) return fail(SIFT_HIP_ERR_INVALID, "null argument");
     if (d->allocated && d->nLanes) {
         HIPCHK(hipSetDevice(d->device));
-        bind_lane(d, d->curLane);
+        bind_lane(d, d->curLane, d->curIdx);
         if (int rc = ensure_counts(d)) return rc;
     }
     *flags = d->hCtr ? (int)d->hCtr[(size_t)d->cur * d->B].overflow : 0;

@@ -158,6 +158,10 @@ void Detector::setLanes(int lanes) {
     if (m_handle) check(sift_hip_set_lanes(m_handle, lanes), "setLanes");
 }
 
+void Detector::setMicroBatch(int frames) {
+    if (m_handle) check(sift_hip_set_micro_batch(m_handle, frames), "setMicroBatch");
+}
+
 void Detector::wait(long long ticket) {
     check(sift_hip_wait(m_handle, ticket), "wait");
     refreshViews();

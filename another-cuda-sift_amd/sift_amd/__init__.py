@@ -97,6 +97,8 @@ def lib() -> ctypes.CDLL:
         "sift_hip_submit_device": (i, [vp, vp, sz, i, vp, ctypes.POINTER(ctypes.c_longlong)]),
         "sift_hip_set_lanes": (i, [vp, i]),
         "sift_hip_lanes": (i, [vp, ip, ip]),
+        "sift_hip_set_micro_batch": (i, [vp, i]),
+        "sift_hip_micro_batch": (i, [vp, ip]),
         "sift_hip_sync": (i, [vp]),
         "sift_hip_set_batch": (i, [vp, i]),
         "sift_hip_batch_capacity": (i, [vp, ip]),
@@ -224,13 +226,15 @@ class Detector:
     """sift_cuda::Detector (Detector.hh:24-96) over the C ABI."""
 
     def __init__(self, config: CudaSiftConfig, device: int = -1, batch: int = 1, exact_descriptors: bool = False,
-                 lanes: Optional[int] = None):
+                 lanes: Optional[int] = None, micro_batch: int = 1):
         """batch > 1: frame-batch handle (sift_hip_set_batch): detectBatchDevice runs up to `batch`
         frames per launch; the single-frame methods keep working (frame 0's arena).
         exact_descriptors: OpenCV's sequential float histogram (SIFT_HIP_DESC_EXACT), descriptors
         bit-identical to the oracle; default the fixed-point histogram (+-1 on a byte).
         lanes: compute lanes for frames in flight (sift_hip_set_lanes, 1..4, library default 2):
-        frames submitted before the previous one completes run concurrently on another lane."""
+        frames submitted before the previous one completes run concurrently on another lane.
+        micro_batch > 1: frames of submitDevice queue until that many run as one launch group on a
+        lane (sift_hip_set_micro_batch; a wait on a queued frame launches the partial group)."""
         self.config = config
         self.batch = int(batch)
         self.exact_descriptors = bool(exact_descriptors)
@@ -240,6 +244,8 @@ class Detector:
             _check(lib().sift_hip_set_batch(self._h, self.batch), "set_batch")
         if lanes is not None:
             _check(lib().sift_hip_set_lanes(self._h, int(lanes)), "set_lanes")
+        if micro_batch != 1:
+            _check(lib().sift_hip_set_micro_batch(self._h, int(micro_batch)), "set_micro_batch")
         if self.exact_descriptors:
             _check(lib().sift_hip_set_descriptor_mode(self._h, SIFT_HIP_DESC_EXACT), "set_descriptor_mode")
         n = ctypes.c_int()
@@ -342,6 +348,12 @@ class Detector:
         m, c = ctypes.c_int(), ctypes.c_int()
         _check(lib().sift_hip_lanes(self._h, ctypes.byref(m), ctypes.byref(c)), "lanes")
         return m.value, c.value
+
+    def micro_batch(self) -> int:
+        """Frames per submitDevice launch group (sift_hip_micro_batch)."""
+        m = ctypes.c_int()
+        _check(lib().sift_hip_micro_batch(self._h, ctypes.byref(m)), "micro_batch")
+        return m.value
 
     def wait(self, ticket: int) -> None:
         """Block until frame `ticket` is complete and expose its results (prev = frame ticket-1)."""

@@ -757,12 +757,28 @@ def main():
         "note": "PCIe-inclusive, host frame -> results in host memory (copyToHost with descriptors), one detector; "
                 f"pipelined: submit/wait with {PIPE_DEPTH} frames in flight on {PIPE_LANES} compute lanes",
     }
+    del detp
+    # The same loop on a micro-batching handle (sift_hip_set_micro_batch):
+    # submitted frames run MB at a time as one launch group per lane.
+    MB_LANES, MB, MB_DEPTH = 3, 4, 12  # (2 lanes x 8 in flight: 0.0998 ms/frame, 3 x 12: 0.0942; 2-frame groups 0.110)
+    detp = sift.Detector(cfg, device=local, lanes=MB_LANES, micro_batch=MB)
+    detp.gpuWarmUpAndAllocate()
+    PIPE_DEPTH_SAVED, PIPE_DEPTH = PIPE_DEPTH, MB_DEPTH
+    t_mb = pipelined(lambda s: detp.submitDevice(frames[s % nframes].data_ptr(), stride), False)
+    t_mb8 = pipelined(lambda s: detp.submitDevice(dev_u8[s % nframes].data_ptr(), W, u8=True), False)
+    PIPE_DEPTH = PIPE_DEPTH_SAVED
     device_submit = {
         "f32": {"value": round(world * nh * W * H / 1e6 / t_dev, 2), "ms_per_frame": round(t_dev / nh * 1e3, 4)},
         "u8": {"value": round(world * nh * W * H / 1e6 / t_dev8, 2), "ms_per_frame": round(t_dev8 / nh * 1e3, 4)},
         "unit": "Mpix/s", "lanes": PIPE_LANES, "in_flight": PIPE_DEPTH,
         "note": "HBM-resident single frames through submitDevice/wait (sift_hip_submit_device), one detector, "
                 f"{PIPE_DEPTH} frames in flight on {PIPE_LANES} compute lanes; results stay on the device",
+        "micro_batch": {
+            "f32": {"value": round(world * nh * W * H / 1e6 / t_mb, 2), "ms_per_frame": round(t_mb / nh * 1e3, 4)},
+            "u8": {"value": round(world * nh * W * H / 1e6 / t_mb8, 2), "ms_per_frame": round(t_mb8 / nh * 1e3, 4)},
+            "lanes": MB_LANES, "frames_per_group": MB, "in_flight": MB_DEPTH,
+            "note": "the same submitDevice/wait loop on a handle with sift_hip_set_micro_batch(4): frames run as "
+                    "4-frame launch groups (per-frame results identical, tests/test_gpu_lanes.py)"},
     }
     del detp, dev_u8
 

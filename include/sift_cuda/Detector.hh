@@ -51,6 +51,9 @@ public:
     // Extra: compute lanes for frames in flight (sift_hip_set_lanes, 1..4);
     // before gpuWarmUpAndAllocate.  1 = every frame on one stream in order.
     void setLanes(int lanes);
+    // Extra: submitDevice frames run in launch groups of `frames`
+    // (sift_hip_set_micro_batch, 1..16); before gpuWarmUpAndAllocate.
+    void setMicroBatch(int frames);
     // Extra: image already in device memory (fp32, row stride in bytes).
     void detectAndComputeDevice(const float* device_image, size_t row_stride_bytes, void* hip_stream = nullptr);
 

@@ -176,6 +176,20 @@ int sift_hip_lanes(sift_hip_t h, int* max_lanes, int* created);
 int sift_hip_submit_device(sift_hip_t h, const void* dev_img, size_t row_stride_bytes, int format, void* stream,
                            long long* ticket);
 
+/* Micro-batching of pipelined device frames: with frames = M > 1 (before
+ * sift_hip_warmup; the handle's batch size becomes M), frames submitted by
+ * sift_hip_submit_device queue until M of them run as ONE launch group on a
+ * lane (each frame's rows copied device-to-device into the lane's group input
+ * after its `stream` event; one launch per pipeline stage for the group, as
+ * sift_hip_detect_batch_device).  Tickets, results and prev_descriptor are per
+ * frame and identical to unbatched submission.  A frame still queued is
+ * launched (with the frames before it, as a partial group) by sift_hip_wait
+ * on it, sift_hip_sync, or any other detect / submit call; its `dev_img` must
+ * stay unchanged until then.  At most 2 x lanes x M frames may be in flight
+ * past the last waited one.  Default 1 (every frame launched at submit). */
+int sift_hip_set_micro_batch(sift_hip_t h, int frames);
+int sift_hip_micro_batch(sift_hip_t h, int* frames);
+
 /* Detector::total_size (Detector.hh:62, Detector.cu:584-604). */
 int sift_hip_num_keypoints(sift_hip_t h, int* n);
 /* Capacities of the handle's per-frame buffers (host-only, valid right after

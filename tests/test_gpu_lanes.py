@@ -87,6 +87,54 @@ def test_device_submit_lanes_equal_sync(sift):
                   else det.submitDevice(dev[s].data_ptr(), W * 4))
 
 
+@pytest.mark.parametrize("mb,lanes,depth", [(4, 2, 8), (4, 2, 3), (3, 3, 9), (2, 1, 4)])
+def test_device_submit_micro_batch_equal_sync(sift, mb, lanes, depth):
+    """Micro-batching (sift_hip_set_micro_batch): frames queue into launch
+    groups of mb; full groups, partial groups launched by a wait on a queued
+    frame (depth < mb), format changes inside a group, and frames ordered after
+    the caller's stream all give the synchronous path's results and
+    prev_descriptor."""
+    frames = [sift.synth_frame(110 + i, W, H) for i in range(13)]
+    ref = sync_reference(sift, frames, numFeatures=2000)
+    dev = [torch.from_numpy(f).cuda() for f in frames]
+    u8 = [torch.from_numpy(f.astype(np.uint8)).cuda() for f in frames]
+    stream = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    _, det = make_detector(sift, W, H, numFeatures=2000, lanes=lanes, micro_batch=mb)
+    assert det.micro_batch() == mb
+
+    def submit(s):
+        if s % 5 == 3:  # a u8 frame inside a group of f32 frames: the group is flushed first
+            return det.submitDevice(u8[s].data_ptr(), W, u8=True)
+        if s % 4 == 1:
+            return det.submitDevice(dev[s].data_ptr(), W * 4, stream=stream.cuda_stream)
+        return det.submitDevice(dev[s].data_ptr(), W * 4)
+
+    run_pipelined(sift, det, frames, ref, depth, submit)
+    # a synchronous detect between queued frames launches them first, in order
+    t0 = det.submitDevice(dev[0].data_ptr(), W * 4)
+    det.detectAndComputeDevice(dev[1].data_ptr(), W * 4, sync=True)
+    assert_identical(results(det), ref[1])
+    det.wait(t0)
+    assert_identical(results(det), ref[0])
+
+
+def test_micro_batch_limits(sift):
+    img = torch.from_numpy(sift.synth_frame(1, 128, 96)).cuda()
+    torch.cuda.synchronize()
+    _, det = make_detector(sift, 128, 96, lanes=1, micro_batch=2)
+    t = [det.submitDevice(img.data_ptr(), 128 * 4) for _ in range(4)]  # two groups of 2 on the one lane
+    with pytest.raises(sift.SiftHipError):
+        det.submitDevice(img.data_ptr(), 128 * 4)
+    for x in t:
+        det.wait(x)
+    with pytest.raises(sift.SiftHipError):
+        sift.Detector(sift.CudaSiftConfig(col_width=128, row_width=96), micro_batch=17)
+    with pytest.raises(sift.SiftHipError):  # batch and micro-batch must agree
+        d2 = sift.Detector(sift.CudaSiftConfig(col_width=128, row_width=96), batch=4, micro_batch=2)
+        d2.gpuWarmUpAndAllocate()
+
+
 def test_sync_caller_keeps_one_lane(sift):
     _, det = make_detector(sift, W, H, numFeatures=2000)
     img = sift.synth_frame(3, W, H)

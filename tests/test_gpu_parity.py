@@ -19,9 +19,9 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def make_detector(sift, w, h, exact_descriptors=False, lanes=None, **kw):
+def make_detector(sift, w, h, exact_descriptors=False, lanes=None, micro_batch=1, **kw):
     cfg = sift.CudaSiftConfig(col_width=w, row_width=h, **kw)
-    det = sift.Detector(cfg, exact_descriptors=exact_descriptors, lanes=lanes)
+    det = sift.Detector(cfg, exact_descriptors=exact_descriptors, lanes=lanes, micro_batch=micro_batch)
     det.gpuWarmUpAndAllocate()
     return cfg, det
 

@@ -18,8 +18,12 @@ cfg = sift.CudaSiftConfig(col_width=W, row_width=H, numFeatures=5000, numOctaves
 dev = [torch.from_numpy(sift.synth_frame(i, W, H)).cuda() for i in range(4)]
 torch.cuda.synchronize()
 out = {"lib": os.environ.get("SIFT_HIP_LIB", "default"), "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "")}
-for lanes, depth in ((3, 3), (3, 6), (2, 4), (4, 8)):
-    det = sift.Detector(cfg, lanes=lanes)
+# (lanes, depth, micro-batch); DEV_CONFIGS="l:d:m,..." overrides
+CONFIGS = [(3, 3, 1), (3, 6, 1), (2, 4, 1), (4, 8, 1)]
+if os.environ.get("DEV_CONFIGS"):
+    CONFIGS = [tuple(int(x) for x in c.split(":")) for c in os.environ["DEV_CONFIGS"].split(",")]
+for lanes, depth, mb in CONFIGS:
+    det = sift.Detector(cfg, lanes=lanes, micro_batch=mb)
     det.gpuWarmUpAndAllocate()
     q = []
     for s in range(N + 2 * depth):
@@ -32,8 +36,8 @@ for lanes, depth in ((3, 3), (3, 6), (2, 4), (4, 8)):
             det.wait(q.pop(0))
     while q:
         det.wait(q.pop(0))
-    out[f"l{lanes}d{depth}_ms"] = round((time.perf_counter() - t) / N * 1e3, 4)
-    if lanes == 3 and depth == 3:
+    out[f"l{lanes}d{depth}" + (f"m{mb}" if mb > 1 else "") + "_ms"] = round((time.perf_counter() - t) / N * 1e3, 4)
+    if lanes == 3 and depth == 3 and mb == 1:
         lat = []
         for s in range(40):
             t = time.perf_counter()
