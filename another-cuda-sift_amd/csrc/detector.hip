@@ -144,6 +144,11 @@ private:
     bool stop_ = false;
 };
 
+// Pool threads besides the caller (a copy >= 1 MB runs in kCopyWorkers + 1
+// parts).  (Measured alternative: 7 workers, the C++ host loop at 3 lanes
+// 0.174-0.176 vs 0.170-0.171 ms/frame, profiles/round5/stage_modes.jsonl.)
+constexpr int kCopyWorkers = 3;
+
 // Row copy (dst pitch / src stride in bytes), split over the pool when large.
 void copy_rows(CopyPool* pool, char* dst, size_t dpitch, const char* src, size_t sstride, size_t rowB, int rows) {
     auto part = [&](int lo, int hi) {
@@ -218,7 +223,7 @@ bool find_sidecar(const uint16_t* desc, int n, Sidecar* out) {
 // Results slots per compute lane: frames f-1 .. f+2 of a lane never share one.
 constexpr int kResultSlots = 4;
 constexpr int kMaxLanes = 4;
-constexpr int kFrameRing = 64;  // per-frame (lane, slot) records; far more than can be alive at once
+constexpr int kFrameRing = 256;  // per-frame (lane, slot, arena) records: > 2 x kMaxLanes x kMaxMicroBatch (frames in flight) + the two readable
 
 // A compute lane: one HIP stream, its B frame arenas (every per-frame buffer of
 // the pipeline, sift_kernels.h Frames), the graphs captured on them and a ring
@@ -265,11 +270,14 @@ struct Lane {
     // (recorded after the first kernel) has passed.
     static constexpr int kInSlots = 2;
     void* hStage[kInSlots] = {};
+    void* dStage[kInSlots] = {};  // device copies (k_stage_to_device), allocated at the lane's first host frame
     hipEvent_t evRead[kInSlots] = {};
     long long uploads = 0;
+    // Host results regions: one per (results slot, arena) -- region slot * B + arena.
+    static constexpr int kHostRegions = kResultSlots * 16;  // 16 = sift_hip_detector::kMaxMicroBatch
     hipEvent_t evHost[kResultSlots] = {};
-    long long hostFrame[kResultSlots] = {-1, -1, -1, -1};  // the frame each host region holds
-    bool hostDesc[kResultSlots] = {};                       // ... with its descriptors
+    long long hostFrame[kHostRegions];  // the frame each host region holds (-1: none; set in add_lane)
+    bool hostDesc[kHostRegions] = {};   // ... with its descriptors
 };
 
 // Byte offsets of every per-frame buffer inside a frame arena (the same for
@@ -316,11 +324,22 @@ struct sift_hip_detector {
     static constexpr int kMaxMicroBatch = 16;
     int mb = 1;
     struct PendingFrame {
-        const void* img;
+        const void* img;  // device frame, or the device address of a host frame's pinned staging
         size_t stride;
         int fmt;
         bool ordered;  // the lane waits for evPend[i] (the caller's stream)
+        int hslot;     // host frames: their staging slot (-1: a device frame)
     };
+    // Pinned staging of micro-batched host frames: one block of hstSlots
+    // slots (one per frame that can be pending or queued on a lane; a slot is
+    // refilled once the copy kernel that read it, event hstRead[i], has run),
+    // allocated in one piece at the first such frame (per-slot allocations
+    // inside the submits of a running loop stalled it for milliseconds).
+    char* hstBlock = nullptr;
+    size_t hstSlotBytes = 0;
+    int hstSlots = 0;
+    std::vector<hipEvent_t> hstRead;
+    long long hstNext = 0;
     PendingFrame pend[kMaxMicroBatch] = {};
     hipEvent_t evPend[kMaxMicroBatch] = {};
     int npend = 0;
@@ -461,6 +480,7 @@ struct sift_hip_detector {
                 if (L.hRes) (void)hipHostFree(L.hRes);
                 for (int k = 0; k < Lane::kInSlots; k++) {
                     if (L.hStage[k]) (void)hipHostFree(L.hStage[k]);
+                    if (L.dStage[k]) (void)hipFree(L.dStage[k]);
                     if (L.evRead[k]) (void)hipEventDestroy(L.evRead[k]);
                 }
                 for (hipEvent_t e : L.evHost)
@@ -469,6 +489,8 @@ struct sift_hip_detector {
             }
             if (dDg) (void)hipFree(dDg);
             for (auto e : evPool) (void)hipEventDestroy(e);
+            if (hstBlock) (void)hipHostFree(hstBlock);
+            for (hipEvent_t e : hstRead) (void)hipEventDestroy(e);
             if (evIn) (void)hipEventDestroy(evIn);
             for (hipEvent_t e : evPend)
                 if (e) (void)hipEventDestroy(e);
@@ -478,6 +500,9 @@ struct sift_hip_detector {
         delete pool;
     }
 };
+
+static_assert(kFrameRing > 2 * kMaxLanes * sift_hip_detector::kMaxMicroBatch + 2 && (kFrameRing & (kFrameRing - 1)) == 0,
+              "frame records outlive every frame in flight");
 
 namespace {
 
@@ -705,6 +730,7 @@ int allocate(sift_hip_detector* d) {
 }
 
 int build_graphs(sift_hip_detector* d);
+int ensure_host_res(sift_hip_detector* d, Lane& L);
 
 // A new compute lane: stream, zeroed arenas, host counters, events and the
 // captured graphs (bound on return).
@@ -725,6 +751,7 @@ int add_lane(sift_hip_detector* d) {
         HIPCHK(hipEventCreateWithFlags(&L.evFrame[b], hipEventDisableTiming));
         HIPCHK(hipEventRecord(L.evFrame[b], L.stream));
     }
+    std::fill(std::begin(L.hostFrame), std::end(L.hostFrame), -1LL);
     // The lane's host-input staging, sized for f32 rows of pitch inPitch (an
     // 8-bit frame uses the first quarter with a byte pitch of inPitch); its
     // events start complete.
@@ -740,6 +767,8 @@ int add_lane(sift_hip_detector* d) {
             register_sidecar(d, fptr(d->dDesc[b], (long)i * d->afs),
                              Sidecar{fptr(d->dSide[b].codes, (long)i * d->afs), fptr(d->dSide[b].keys, (long)i * d->afs)},
                              (int)d->kp.capFinal);
+    if (d->hostWant)
+        if (int rc = ensure_host_res(d, L)) return rc;
     return build_graphs(d);
 }
 
@@ -1210,43 +1239,98 @@ size_t host_res_bytes(const sift_hip_detector* d) {
     const size_t c = d->kp.capFinal;
     return ((12 * c + 255) & ~(size_t)255) + 16 * c + 256 * c;
 }
-void host_res(const sift_hip_detector* d, char* base, int slot, float** k3, float** f4, uint16_t** desc) {
+void host_res(const sift_hip_detector* d, char* base, int region, float** k3, float** f4, uint16_t** desc) {
     const size_t c = d->kp.capFinal;
-    char* p = base + host_res_bytes(d) * slot;
+    char* p = base + host_res_bytes(d) * region;
     *k3 = reinterpret_cast<float*>(p);
     p += (12 * c + 255) & ~(size_t)255;
     *f4 = reinterpret_cast<float*>(p);
     *desc = reinterpret_cast<uint16_t*>(p + 16 * c);
 }
 
-// After a host-input frame: its results into the lane slot's pinned host
-// region on the lane's stream (the next frame of the lane follows it; other
-// lanes keep computing), evHost[slot] once they are there.
-int prefetch_results(sift_hip_detector* d, long long f) {
-    if (!d->hostWant) return SIFT_HIP_OK;
-    Lane& L = d->lane();
-    const int slot = d->frec(f).slot;
-    if (!L.hRes) {
-        const size_t bytes = host_res_bytes(d) * d->kSlots;
-        HIPCHK(hipHostMalloc((void**)&L.hRes, bytes, hipHostMallocMapped | hipHostMallocCoherent));
-        HIPCHK(hipHostGetDevicePointer((void**)&L.hResDev, L.hRes, 0));
-        for (hipEvent_t& e : L.evHost) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    }
-    float *k3, *f4;
-    uint16_t* desc;
-    host_res(d, L.hResDev, slot, &k3, &f4, &desc);
-    const bool withDesc = d->hostWant > 1;
-    launch_results_to_host(d->dKpts3[slot], d->dFeats4[slot], d->dDesc[slot], d->dCtr, d->kp.capFinal, k3, f4,
-                           withDesc ? desc : nullptr, d->stream);
-    HIPCHK(hipEventRecord(L.evHost[slot], d->stream));
-    L.hostFrame[slot] = f;
-    L.hostDesc[slot] = withDesc;
+// After host-input frames f .. f + n - 1 (one launch group, frame f + i in
+// arena i): their results into the lane's pinned host regions (slot * B + i)
+// on the lane's stream (the lane's next group follows; other lanes keep
+// computing), evHost[slot] once they are there.
+// The lane's pinned results regions (kSlots x B), allocated for every lane
+// once a caller reads results back (sift_hip_copy_to_host turns hostWant on)
+// and for lanes created after that: a lazy allocation inside a submit stalled
+// it for ~14 ms.
+int ensure_host_res(sift_hip_detector* d, Lane& L) {
+    if (L.hRes) return SIFT_HIP_OK;
+    const size_t bytes = host_res_bytes(d) * d->kSlots * d->B;
+    HIPCHK(hipHostMalloc((void**)&L.hRes, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer((void**)&L.hResDev, L.hRes, 0));
+    for (hipEvent_t& e : L.evHost) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     return SIFT_HIP_OK;
 }
 
-// Host frame -> pinned staging (the caller's buffer is free on return) ->
-// device upload ring on copyStream (overlapping the frames in flight) ->
-// pipeline on the frame's lane -> results to pinned host memory.
+int prefetch_results(sift_hip_detector* d, long long f, int n = 1) {
+    if (!d->hostWant) return SIFT_HIP_OK;
+    Lane& L = d->lane();
+    const int slot = d->frec(f).slot;
+    if (int rc = ensure_host_res(d, L)) return rc;
+    const bool withDesc = d->hostWant > 1;
+    for (int i = 0; i < n; i++) {
+        const int region = slot * d->B + i;
+        const long o = (long)i * d->afs;
+        float *k3, *f4;
+        uint16_t* desc;
+        host_res(d, L.hResDev, region, &k3, &f4, &desc);
+        launch_results_to_host(fptr(d->dKpts3[slot], o), fptr(d->dFeats4[slot], o), fptr(d->dDesc[slot], o),
+                               fptr(d->dCtr, o), d->kp.capFinal, k3, f4, withDesc ? desc : nullptr, d->stream);
+        L.hostFrame[region] = f + i;
+        L.hostDesc[region] = withDesc;
+    }
+    HIPCHK(hipEventRecord(L.evHost[slot], d->stream));
+    return SIFT_HIP_OK;
+}
+
+int run_group(sift_hip_detector* d);
+
+// A host frame on a micro-batching handle: into the next pinned staging slot
+// of the handle's ring (the caller's buffer is free on return), pending until
+// its group runs (run_group copies it to the lane's group input).
+int queue_host(sift_hip_detector* d, const void* img, size_t stride, int fmt, long long* ticket) {
+    const int es = format_size(fmt), H = d->cfg.row_width;
+    const size_t rowB = (size_t)es * d->cfg.col_width, pitchB = (size_t)es * d->inPitch;
+    if (d->npend && d->pend[0].fmt != fmt)
+        if (int rc = run_group(d)) return rc;
+    if (d->hstSlotBytes < pitchB * H) {  // first host frame, or a larger format: (re)allocate the block
+        if (int rc = run_group(d)) return rc;
+        if (int rc = sync_lanes(d)) return rc;  // no copy kernel still reads the old block
+        if (d->hstBlock) HIPCHK(hipHostFree(d->hstBlock));
+        d->hstBlock = nullptr;
+        d->hstSlotBytes = 0;
+        d->hstSlots = (2 * d->maxLanes + 1) * d->mb;  // frames pending or queued on the lanes
+        if (hipHostMalloc((void**)&d->hstBlock, pitchB * H * d->hstSlots, hipHostMallocMapped | hipHostMallocNonCoherent) !=
+            hipSuccess)
+            return fail(SIFT_HIP_ERR_NOMEM, "hipHostMalloc of the micro-batch host staging failed");
+        d->hstSlotBytes = pitchB * H;
+        while ((int)d->hstRead.size() < d->hstSlots) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            d->hstRead.push_back(e);
+        }
+    }
+    const int hs = (int)(d->hstNext++ % d->hstSlots);
+    HIPCHK(hipEventSynchronize(d->hstRead[hs]));  // the copy kernel that last read the slot has run
+    char* slot = d->hstBlock + d->hstSlotBytes * hs;
+    if (!d->pool && rowB * H >= (1u << 20)) d->pool = new CopyPool(kCopyWorkers);
+    copy_rows(d->pool, slot, pitchB, (const char*)img, stride, rowB, H);
+    void* dev = nullptr;
+    HIPCHK(hipHostGetDevicePointer(&dev, slot, 0));
+    const int i = d->npend;
+    d->pend[i] = sift_hip_detector::PendingFrame{dev, pitchB, fmt, false, hs};
+    d->npend = i + 1;
+    if (ticket) *ticket = d->submitted + i;
+    return d->npend == d->mb ? run_group(d) : SIFT_HIP_OK;
+}
+
+// Host frame -> the lane's pinned staging (the caller's buffer is free on
+// return) -> device staging by a small-grid copy kernel on the lane's stream
+// -> pipeline on the frame's lane -> results to pinned host memory.  On a
+// micro-batching handle the frame joins the pending group (queue_host).
 int submit_host(sift_hip_detector* d, const void* img, size_t stride, int fmt, long long* ticket) {
     const int es = format_size(fmt);
     if (!es) return fail(SIFT_HIP_ERR_INVALID, "unknown pixel format");
@@ -1256,19 +1340,25 @@ int submit_host(sift_hip_detector* d, const void* img, size_t stride, int fmt, l
     if (stride == 0) stride = rowB;
     if (stride < rowB) return fail(SIFT_HIP_ERR_INVALID, "row stride smaller than width");
     if (int rc = check_in_flight(d)) return rc;
+    if (d->mb > 1 && d->dgDir.empty() && !d->timing) return queue_host(d, img, stride, fmt, ticket);
     if (int rc = run_group(d)) return rc;  // pending micro-batch frames keep their submission order
     if (int rc = pick_lane(d)) return rc;
     Lane& L = d->lane();
     const int k = (int)(L.uploads & 1);
     HIPCHK(hipEventSynchronize(L.evRead[k]));  // staging slot k no longer being read (the lane's frame before last)
-    if (!d->pool && rowB * H >= (1u << 20)) d->pool = new CopyPool(3);
+    if (!d->pool && rowB * H >= (1u << 20)) d->pool = new CopyPool(kCopyWorkers);
     copy_rows(d->pool, (char*)L.hStage[k], pitchB, (const char*)img, stride, rowB, H);
     void* src = nullptr;
     HIPCHK(hipHostGetDevicePointer(&src, L.hStage[k], 0));
+    const size_t inBytes = sizeof(float) * (size_t)d->inPitch * H;
+    if (!L.dStage[k] && hipMalloc(&L.dStage[k], inBytes) != hipSuccess)
+        return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc of the device staging failed");
+    launch_copy_rows(src, pitchB, L.dStage[k], pitchB, pitchB, H, kStageWg, d->stream);
+    HIPCHK(hipEventRecord(L.evRead[k], d->stream));  // host slot k read; device slot k is stream-ordered
     L.uploads++;
     d->uploads++;
     const long long f = d->submitted;
-    int rc = run_frame(d, src, d->inPitch, fmt, L.evRead[k]);
+    int rc = run_frame(d, L.dStage[k], d->inPitch, fmt, nullptr);
     if (rc) return rc;
     if (d->dgDir.empty() && (rc = prefetch_results(d, f))) return rc;
     if (ticket) *ticket = f;
@@ -1276,7 +1366,7 @@ int submit_host(sift_hip_detector* d, const void* img, size_t stride, int fmt, l
 }
 
 // The pending micro-batch frames as one launch group on a lane: each frame's
-// rows are copied (device to device, on the lane's stream after the caller's
+// rows are copied (device to device by launch_copy_rows, on the lane's stream after the caller's
 // stream event) into the lane's micro-batch input at a fixed frame stride, and
 // the group runs the B-frame graphs (a partial group: the 1-frame graphs, or
 // the same launches eagerly), frame d->submitted + i in arena i.
@@ -1290,14 +1380,23 @@ int run_group(sift_hip_detector* d) {
     if (!L.mbIn && hipMalloc((void**)&L.mbIn, fb * d->mb) != hipSuccess)
         return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc of the micro-batch input failed");
     const int fmt = d->pend[0].fmt, es = format_size(fmt);
+    bool host = false;
     for (int i = 0; i < n; i++) {
         const auto& p = d->pend[i];
         if (p.ordered) HIPCHK(hipStreamWaitEvent(d->stream, d->evPend[i], 0));
-        HIPCHK(hipMemcpy2DAsync(L.mbIn + fb * i, (size_t)es * d->inPitch, p.img, p.stride, (size_t)es * W, H,
-                                hipMemcpyDeviceToDevice, d->stream));
+        if (p.hslot >= 0) {  // pinned staging: whole pitch rows over PCIe by a small grid
+            launch_copy_rows(p.img, p.stride, L.mbIn + fb * i, p.stride, p.stride, H, kStageWg, d->stream);
+            HIPCHK(hipEventRecord(d->hstRead[p.hslot], d->stream));
+            host = true;
+        } else {
+            launch_copy_rows(p.img, p.stride, L.mbIn + fb * i, (size_t)es * d->inPitch, (size_t)es * W, H,
+                             kGroupCopyWg, d->stream);
+        }
     }
     d->npend = 0;
-    return run_frame(d, L.mbIn, d->inPitch, fmt, nullptr, n, (long)fb, true);
+    const long long f = d->submitted;
+    if (int rc = run_frame(d, L.mbIn, d->inPitch, fmt, nullptr, n, (long)fb, true)) return rc;
+    return host ? prefetch_results(d, f, n) : SIFT_HIP_OK;
 }
 
 // Device frame (HBM-resident, fp32 or u8) -> the frame's lane; the lane waits
@@ -1315,7 +1414,7 @@ int submit_device(sift_hip_detector* d, const void* img, size_t stride, int fmt,
             if (!d->evPend[i]) HIPCHK(hipEventCreateWithFlags(&d->evPend[i], hipEventDisableTiming));
             HIPCHK(hipEventRecord(d->evPend[i], ext));
         }
-        d->pend[i] = sift_hip_detector::PendingFrame{img, stride, fmt, ext != nullptr};
+        d->pend[i] = sift_hip_detector::PendingFrame{img, stride, fmt, ext != nullptr, -1};
         d->npend = i + 1;
         if (ticket) *ticket = d->submitted + i;
         return d->npend == d->mb ? run_group(d) : SIFT_HIP_OK;
@@ -2065,18 +2164,22 @@ int sift_hip_copy_to_host(sift_hip_t d, float* k3, float* f4, uint16_t* desc, in
     if (int rc = ensure_counts(d)) return rc;
     const int n = std::min(d->count, cap);
     Lane& L = d->lane();
+    if (!d->hostWant)
+        for (int k = 0; k < d->nLanes; k++)
+            if (int rc = ensure_host_res(d, d->lanes[k])) return rc;
     d->hostWant = std::max(d->hostWant, desc ? 2 : 1);
-    if (L.hRes && L.hostFrame[d->cur] == d->current && d->current >= d->firstFrame && (!desc || L.hostDesc[d->cur])) {
+    const int region = d->cur * d->B + d->curIdx;
+    if (L.hRes && L.hostFrame[region] == d->current && d->current >= d->firstFrame && (!desc || L.hostDesc[region])) {
         // A host-input frame: its results already went to pinned host memory.
         HIPCHK(hipEventSynchronize(L.evHost[d->cur]));
         float *hk3, *hf4;
         uint16_t* hdesc;
-        host_res(d, L.hRes, d->cur, &hk3, &hf4, &hdesc);
+        host_res(d, L.hRes, region, &hk3, &hf4, &hdesc);
         if (n > 0) {
             if (k3) memcpy(k3, hk3, sizeof(float) * 3 * n);
             if (f4) memcpy(f4, hf4, sizeof(float) * 4 * n);
             if (desc) {  // 2.2 MB at C2: split over the copy pool (one thread: 0.100 -> 0.047 ms, C++ loop)
-                if (!d->pool && 256u * n >= (1u << 20)) d->pool = new CopyPool(3);
+                if (!d->pool && 256u * n >= (1u << 20)) d->pool = new CopyPool(kCopyWorkers);
                 copy_rows(d->pool, (char*)desc, 256, (const char*)hdesc, 256, 256, n);
             }
         }

@@ -966,4 +966,49 @@ void launch_results_to_host(const float* k3, const float* f4, const uint16_t* de
     hipLaunchKernelGGL(k_results_to_host, dim3(128), dim3(256), 0, s, k3, f4, desc, ctr, cap, hk3, hf4, hdesc);
 }
 
+// ---------------------------------------------------------------------------
+// Frame rows copied by a small grid on the frame's lane stream: a host-input
+// frame's staging (mapped pinned host memory) into device memory before the
+// frame's first kernel, and a micro-batch's frames into the lane's group
+// input.  kStageWg workgroups with four 16-byte loads in flight per thread
+// (1 MiB in flight, the PCIe link's rate) hold a few CUs for the transfer,
+// where the first blur reading the pinned buffer itself held every tile's
+// workgroup for it and slowed the other lanes;
+// a runtime 2-D copy of a device frame took a slow path (0.165 vs 0.093
+// ms/frame for f32 vs u8 micro-batches).  16-byte units when the rows and
+// pitches allow, bytes otherwise.
+// ---------------------------------------------------------------------------
+constexpr int kStageUnroll = 4;
+__global__ __launch_bounds__(256) void k_copy_rows16(const char* __restrict__ src, size_t spitch, char* __restrict__ dst,
+                                                     size_t dpitch, unsigned row16, unsigned n16) {
+    const unsigned nt = gridDim.x * blockDim.x;
+    auto at = [&](unsigned i, size_t pitch) { return (size_t)(i / row16) * pitch + (size_t)(i % row16) * 16; };
+    unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + (kStageUnroll - 1) * nt < n16; i += kStageUnroll * nt) {
+        uint4 v[kStageUnroll];
+#pragma unroll
+        for (int u = 0; u < kStageUnroll; u++) v[u] = *reinterpret_cast<const uint4*>(src + at(i + u * nt, spitch));
+#pragma unroll
+        for (int u = 0; u < kStageUnroll; u++) *reinterpret_cast<uint4*>(dst + at(i + u * nt, dpitch)) = v[u];
+    }
+    for (; i < n16; i += nt) *reinterpret_cast<uint4*>(dst + at(i, dpitch)) = *reinterpret_cast<const uint4*>(src + at(i, spitch));
+}
+__global__ __launch_bounds__(256) void k_copy_rows1(const unsigned char* __restrict__ src, size_t spitch,
+                                                    unsigned char* __restrict__ dst, size_t dpitch, unsigned rowB,
+                                                    unsigned n) {
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        dst[(size_t)(i / rowB) * dpitch + i % rowB] = src[(size_t)(i / rowB) * spitch + i % rowB];
+}
+
+void launch_copy_rows(const void* src, size_t spitch, void* dst, size_t dpitch, size_t rowB, int rows, int wgs,
+                      hipStream_t s) {
+    const bool v16 = ((uintptr_t)src | (uintptr_t)dst | spitch | dpitch | rowB) % 16 == 0;
+    if (v16)
+        hipLaunchKernelGGL(k_copy_rows16, dim3(wgs), dim3(256), 0, s, static_cast<const char*>(src), spitch,
+                           static_cast<char*>(dst), dpitch, (unsigned)(rowB / 16), (unsigned)(rowB / 16 * rows));
+    else
+        hipLaunchKernelGGL(k_copy_rows1, dim3(wgs), dim3(256), 0, s, static_cast<const unsigned char*>(src), spitch,
+                           static_cast<unsigned char*>(dst), dpitch, (unsigned)rowB, (unsigned)(rowB * rows));
+}
+
 }  // namespace sift_amd

@@ -227,6 +227,13 @@ void launch_rank_final(const PyrDesc& pyr, const OriKpt* kpts, const unsigned* b
 // Results of a finished frame -> mapped pinned host buffers (host-input frames).
 void launch_results_to_host(const float* k3, const float* f4, const uint16_t* desc, const Counters* ctr, unsigned cap,
                             float* hk3, float* hf4, uint16_t* hdesc, hipStream_t s);
+// Frame rows (rowB bytes, `rows` of them, pitches in bytes) copied by `wgs`
+// 256-thread workgroups on the lane stream: host staging -> device, and
+// micro-batch frames -> the group input (keypoints.hip).
+constexpr int kStageWg = 64;      // host staging (PCIe-bound)
+constexpr int kGroupCopyWg = 512; // device-to-device (HBM)
+void launch_copy_rows(const void* src, size_t spitch, void* dst, size_t dpitch, size_t rowB, int rows, int wgs,
+                      hipStream_t s);
 void launch_bucket_rank(const PyrDesc& pyr, const OriKpt* kpts, unsigned* bcount, const unsigned* boff,
                         const int* order, const Counters* ctr, DescJob* jobs, float* kpts3, float* feats4,
                         const KeypointParams& kp, const Frames& fr, hipStream_t s);

@@ -727,11 +727,15 @@ def main():
     detp.gpuWarmUpAndAllocate()
 
     def pipelined(submit, fetch):
-        tickets = []
-        for s in range(nh + PIPE_DEPTH):  # the first PIPE_DEPTH frames create and warm the lanes
-            if s == PIPE_DEPTH:
+        # The first `warm` frames (the same loop) create and warm the lanes,
+        # their staging and results regions; then nh frames are timed.
+        tickets, warm = [], max(3 * PIPE_DEPTH, 24)
+        for s in range(nh + warm):
+            if s == warm:
                 while tickets:
                     detp.wait(tickets.pop(0))
+                    if fetch:
+                        detp.copyToHost(True)
                 t = time.perf_counter()
             tickets.append(submit(s))
             if len(tickets) == PIPE_DEPTH:
@@ -764,6 +768,10 @@ def main():
     detp = sift.Detector(cfg, device=local, lanes=MB_LANES, micro_batch=MB)
     detp.gpuWarmUpAndAllocate()
     PIPE_DEPTH_SAVED, PIPE_DEPTH = PIPE_DEPTH, MB_DEPTH
+    t_mbh = pipelined(lambda s: detp.submit(host_u8[s % nframes]), True)
+    host_input["pipelined_u8_micro_batch"] = {
+        "value": round(world * nh * W * H / 1e6 / t_mbh, 2), "ms_per_frame": round(t_mbh / nh * 1e3, 4),
+        "lanes": MB_LANES, "frames_per_group": MB, "in_flight": MB_DEPTH}
     t_mb = pipelined(lambda s: detp.submitDevice(frames[s % nframes].data_ptr(), stride), False)
     t_mb8 = pipelined(lambda s: detp.submitDevice(dev_u8[s % nframes].data_ptr(), W, u8=True), False)
     PIPE_DEPTH = PIPE_DEPTH_SAVED

@@ -119,6 +119,28 @@ def test_device_submit_micro_batch_equal_sync(sift, mb, lanes, depth):
     assert_identical(results(det), ref[0])
 
 
+@pytest.mark.parametrize("mb,lanes,depth", [(4, 2, 8), (3, 3, 2)])
+def test_host_submit_micro_batch_equal_sync(sift, mb, lanes, depth):
+    """Host frames on a micro-batching handle: staged into the handle's pinned
+    ring, copied into the group input by the group's lane, results prefetched
+    per frame to pinned host memory (copyToHost after every wait); host and
+    device frames share groups."""
+    frames = [sift.synth_frame(130 + i, W, H) for i in range(11)]
+    ref = sync_reference(sift, frames, numFeatures=2000)
+    dev = [torch.from_numpy(f).cuda() for f in frames]
+    torch.cuda.synchronize()
+    _, det = make_detector(sift, W, H, numFeatures=2000, lanes=lanes, micro_batch=mb)
+
+    def submit(s):
+        if s % 4 == 2:
+            return det.submitDevice(dev[s].data_ptr(), W * 4)
+        return det.submit(frames[s].astype(np.uint8) if s % 3 == 1 else frames[s])
+
+    run_pipelined(sift, det, frames, ref, depth, submit)
+    det.detectAndCompute(frames[5])  # a synchronous host frame: a group of one
+    assert_identical(results(det), ref[5])
+
+
 def test_micro_batch_limits(sift):
     img = torch.from_numpy(sift.synth_frame(1, 128, 96)).cuda()
     torch.cuda.synchronize()

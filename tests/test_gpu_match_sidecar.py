@@ -79,3 +79,29 @@ def test_sidecar_batch_frames_and_foreign_buffers(sift, oracle):
         foreign = sift.DeviceArray.from_numpy(np.ascontiguousarray(d1.astype(np.float16)).view(np.uint16))
         fi, fd, _ = run(sift, m, p0, n0, foreign.value, n1)
         assert np.array_equal(fi, oi) and np.array_equal(fd.view(np.uint32), gd.view(np.uint32)), i
+
+
+def test_sidecar_micro_batch_frames(sift):
+    """Micro-batched device frames (frame i of a launch group in arena i):
+    prev_descriptor x device_descriptor inside a group and across groups match
+    from the sidecars exactly as the converting path does."""
+    import torch
+
+    w, h = 752, 480
+    cfg = sift.CudaSiftConfig(col_width=w, row_width=h, numFeatures=2000)
+    det = sift.Detector(cfg, lanes=2, micro_batch=3)
+    det.gpuWarmUpAndAllocate()
+    dev = [torch.from_numpy(sift.synth_frame(120 + i, w, h)).cuda() for i in range(7)]
+    torch.cuda.synchronize()
+    tickets = [det.submitDevice(d.data_ptr(), w * 4) for d in dev]
+    m = sift.Matcher(4096, 4096)
+    mc = sift.Matcher(4096, 4096)
+    mc.set_sidecars(False)
+    for t in tickets[1:]:  # frames 1, 2 share a group with their predecessor; 3 and 6 start groups
+        det.wait(t)
+        n0, n1 = det.prev_size, det.total_size
+        assert n0 > 100 and n1 > 100
+        a = run(sift, m, det.prev_descriptor.data(), n0, det.device_descriptor.data(), n1)
+        b = run(sift, mc, det.prev_descriptor.data(), n0, det.device_descriptor.data(), n1)
+        for x, y in zip(a, b):
+            assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), t

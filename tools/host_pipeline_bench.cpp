@@ -3,7 +3,7 @@
 // with `depth` frames in flight on `lanes` compute lanes (setLanes), as
 // bench.py's host_input.pipelined_u8 runs them.  Prints one JSON line:
 // ms per frame, and the mean wall time of each call.
-//   host_pipeline_bench [lanes] [depth] [frames] [desc 0|1|2] [dev 0|1]
+//   host_pipeline_bench [lanes] [depth] [frames] [desc 0|1|2] [dev 0..5] [micro-batch]
 // desc 2: no copyToHost at all; dev 1: the frames already in device memory
 // (submitDevice) instead of host frames (submit); dev 2: the frames in pinned
 // host memory, read by the frame's first kernel over PCIe (submitDevice with
@@ -14,6 +14,7 @@
 // stream (the cross-stream wait alone); dev 5 = dev 3's DMA with the frame
 // submitted unordered (the copy's concurrency alone; the frame reads the slot's
 // previous contents, a valid older frame).
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -32,6 +33,7 @@ int main(int argc, char** argv) {
     const int descMode = argc > 4 ? std::atoi(argv[4]) : 1;
     const bool desc = descMode == 1, copy = descMode != 2;
     const int dev = argc > 5 ? std::atoi(argv[5]) : 0;
+    const int mb = argc > 6 ? std::atoi(argv[6]) : 1;  // micro-batch (setMicroBatch)
     const int W = 1920, H = 1200;
     std::vector<Image8U> imgs;
     for (int i = 0; i < 4; i++) {
@@ -49,6 +51,7 @@ int main(int argc, char** argv) {
     cfg.numOctaves = 3;
     sift_cuda::Detector det(cfg);
     det.setLanes(lanes);
+    if (mb > 1) det.setMicroBatch(mb);
     det.gpuWarmUpAndAllocate();
     std::vector<void*> dframes(4, nullptr), pinned(4, nullptr), ring(depth + 1, nullptr);
     hipStream_t cs = nullptr;
@@ -89,6 +92,7 @@ int main(int argc, char** argv) {
     };
     using clk = std::chrono::steady_clock;
     double tSub = 0, tWait = 0, tCopy = 0;
+    std::vector<double> subs;  // per-submit wall times of the timed run (ms)
     auto run = [&](int n, bool timed) {
         std::deque<long long> q;
         auto drain = [&] {
@@ -106,7 +110,11 @@ int main(int argc, char** argv) {
         for (int s = 0; s < n; s++) {
             auto a = clk::now();
             q.push_back(submit(s));
-            if (timed) tSub += std::chrono::duration<double, std::milli>(clk::now() - a).count();
+            if (timed) {
+                const double ms = std::chrono::duration<double, std::milli>(clk::now() - a).count();
+                tSub += ms;
+                subs.push_back(ms);
+            }
             if ((int)q.size() == depth) drain();
         }
         while (!q.empty()) drain();
@@ -115,8 +123,12 @@ int main(int argc, char** argv) {
     const auto t0 = clk::now();
     run(frames, true);
     const double ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
-    std::printf("{\"dev\": %d, \"lanes\": %d, \"depth\": %d, \"desc\": %d, \"ms_per_frame\": %.4f, \"submit_ms\": %.4f, "
-                "\"wait_ms\": %.4f, \"copy_ms\": %.4f, \"keypoints\": %d}\n",
-                (int)dev, lanes, depth, descMode, ms / frames, tSub / frames, tWait / frames, tCopy / frames, det.total_size);
+    std::sort(subs.begin(), subs.end());
+    auto pct = [&](double q) { return subs.empty() ? 0.0 : subs[std::min(subs.size() - 1, (size_t)(q * subs.size()))]; };
+    std::printf("{\"dev\": %d, \"lanes\": %d, \"depth\": %d, \"micro_batch\": %d, \"desc\": %d, \"ms_per_frame\": %.4f, "
+                "\"submit_ms\": %.4f, \"submit_p50_p90_max\": [%.4f, %.4f, %.4f], \"wait_ms\": %.4f, \"copy_ms\": %.4f, "
+                "\"keypoints\": %d}\n",
+                (int)dev, lanes, depth, mb, descMode, ms / frames, tSub / frames, pct(0.5), pct(0.9), pct(1.0),
+                tWait / frames, tCopy / frames, det.total_size);
     return 0;
 }
