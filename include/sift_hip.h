@@ -145,9 +145,9 @@ int sift_hip_batch_copy_to_host(sift_hip_t h, int i, float* kpts3, float* feats4
 /* Pipelined host input (replaces the synchronous upload of CudaImage.cu:97-105
  * and the per-frame loop of extract_and_match_example.cc:69-101).
  * sift_hip_submit copies the frame into one of its lane's two mapped pinned
- * staging buffers (the caller's buffer is free again on return), enqueues the
- * pipeline -- whose first kernel reads the staging buffer over PCIe, no
- * separate upload -- and returns a ticket without waiting.
+ * staging buffers (the caller's buffer is free again on return), enqueues a
+ * small copy kernel (staging -> device, over PCIe) and the pipeline on the
+ * lane's stream and returns a ticket without waiting.
  * sift_hip_wait(ticket) blocks until that frame is complete and makes it the
  * frame the result accessors address (prev_desc = frame ticket-1).  At most
  * 2 x lanes frames may be in flight past the last waited one
@@ -176,12 +176,13 @@ int sift_hip_lanes(sift_hip_t h, int* max_lanes, int* created);
 int sift_hip_submit_device(sift_hip_t h, const void* dev_img, size_t row_stride_bytes, int format, void* stream,
                            long long* ticket);
 
-/* Micro-batching of pipelined device frames: with frames = M > 1 (before
+/* Micro-batching of pipelined frames: with frames = M > 1 (before
  * sift_hip_warmup; the handle's batch size becomes M), frames submitted by
- * sift_hip_submit_device queue until M of them run as ONE launch group on a
- * lane (each frame's rows copied device-to-device into the lane's group input
- * after its `stream` event; one launch per pipeline stage for the group, as
- * sift_hip_detect_batch_device).  Tickets, results and prev_descriptor are per
+ * sift_hip_submit_device or sift_hip_submit queue until M of them run as ONE
+ * launch group on a lane (each frame's rows copied into the lane's group
+ * input -- device frames after their `stream` event, host frames from the
+ * pinned staging block they were copied into at submit; one launch per
+ * pipeline stage for the group, as sift_hip_detect_batch_device).  Tickets, results and prev_descriptor are per
  * frame and identical to unbatched submission.  A frame still queued is
  * launched (with the frames before it, as a partial group) by sift_hip_wait
  * on it, sift_hip_sync, or any other detect / submit call; its `dev_img` must
