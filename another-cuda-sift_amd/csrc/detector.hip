@@ -255,19 +255,21 @@ struct Lane {
     // lane's first host-input frame).
     char* hRes = nullptr;
     char* hResDev = nullptr;
-    // Host-input staging of this lane: two pinned (coarse-grained, so the
-    // GPU's L2 caches the halo re-reads) host buffers that the frame's first
-    // kernel reads over PCIe itself.  Measured alternatives
+    // Host-input staging of this lane: two pinned host buffers, moved into
+    // the lane's device staging by a 64-workgroup copy kernel on the lane's
+    // stream ahead of the frame (launch_copy_rows).  Measured alternatives
     // (tools/host_pipeline_bench.cpp, 3 lanes x 6 frames, C2 u8 frames,
-    // profiles/round5/upload_ab.jsonl): DMA on a separate upload stream
-    // 0.169 ms/frame at HIP's default 4 hardware queues per process (two
-    // active streams then share a queue: device frames ordered after a
-    // 4 KiB copy on a 4th stream run at 0.160 instead of 0.112), 0.119-0.126
-    // at GPU_MAX_HW_QUEUES=8 -- but 8 queues slowed the bench process's
-    // device-frame lanes to 0.160; DMA on the lane's own stream 0.21-0.23
-    // (the submit waits behind the lane); this zero-copy read 0.165-0.170.  A
-    // slot is rewritten for the lane's frame after next, once evRead[slot]
-    // (recorded after the first kernel) has passed.
+    // profiles/round5/): the first blur reading the pinned buffer itself
+    // 0.165-0.170 ms/frame against 0.154 (its tiles' workgroups wait out the
+    // PCIe transfer and crowd the other lanes); DMA on a separate upload
+    // stream 0.169 at HIP's default 4 hardware queues per process (two active
+    // streams then share a queue: device frames ordered after a 4 KiB copy on
+    // a 4th stream ran at 0.160 instead of 0.112), 0.119-0.126 at
+    // GPU_MAX_HW_QUEUES=8 -- but 8 queues slowed the bench process's other
+    // legs; DMA on the lane's own stream 0.21-0.23 (the submit waited behind
+    // the lane).  Host slot k is rewritten for the lane's frame after next,
+    // once evRead[k] (recorded after the copy kernel) has passed; the device
+    // slot is stream-ordered.
     static constexpr int kInSlots = 2;
     void* hStage[kInSlots] = {};
     void* dStage[kInSlots] = {};  // device copies (k_stage_to_device), allocated at the lane's first host frame
