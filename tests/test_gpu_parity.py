@@ -435,6 +435,13 @@ def test_cpp_tools(sift):
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
     assert p.stdout == r.stdout
+    # ... and in 3-frame micro-batches (Detector::setMicroBatch): the same lines again
+    m = subprocess.run([os.path.join(lib, "extract_and_match_example"), "--frames", "7", "--pipelined", "--micro-batch", "3"],
+                       capture_output=True, text=True, timeout=300)
+    r7 = subprocess.run([os.path.join(lib, "extract_and_match_example"), "--frames", "7"], capture_output=True, text=True,
+                        timeout=300)
+    assert m.returncode == 0 and r7.returncode == 0, m.stdout + m.stderr + r7.stderr
+    assert m.stdout == r7.stdout
     # the exact descriptor mode through the C++ surface (setExactDescriptors)
     x = subprocess.run([os.path.join(lib, "extract_and_match_example"), "--frames", "3", "--exact"],
                        capture_output=True, text=True, timeout=300)

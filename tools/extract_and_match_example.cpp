@@ -5,7 +5,9 @@
 // --pipelined: 8-bit frames through Detector::submit / wait, frame f+1 staged
 // and uploaded while frame f computes; prints the same lines as the default
 // synchronous Imagef loop.  --exact: Detector::setExactDescriptors(true)
-// (OpenCV's descriptor bytes, sift_hip_set_descriptor_mode).
+// (OpenCV's descriptor bytes, sift_hip_set_descriptor_mode).  --micro-batch N
+// (with --pipelined): Detector::setMicroBatch(N) on 2 lanes, 2N frames
+// submitted ahead, so frames run in N-frame launch groups; same lines.
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -17,6 +19,7 @@
 int main(int argc, char** argv) {
     int W = 752, H = 480, frames = 4, dx = 3, dy = 2;
     bool pipelined = false, exact = false;
+    int micro = 1;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         if (a == "--pipelined") pipelined = true;
@@ -24,6 +27,7 @@ int main(int argc, char** argv) {
         else if (a == "--width" && i + 1 < argc) W = std::atoi(argv[++i]);
         else if (a == "--height" && i + 1 < argc) H = std::atoi(argv[++i]);
         else if (a == "--frames" && i + 1 < argc) frames = std::atoi(argv[++i]);
+        else if (a == "--micro-batch" && i + 1 < argc) micro = std::atoi(argv[++i]);
     }
     const int PW = W + frames * dx, PH = H + frames * dy;
     std::vector<float> big((size_t)PW * PH);
@@ -36,6 +40,10 @@ int main(int argc, char** argv) {
     config.row_width = H;
     sift_cuda::Detector detector(config);
     if (exact) detector.setExactDescriptors(true);  // before the warm-up: part of the captured graphs
+    if (micro > 1) {
+        detector.setLanes(2);
+        detector.setMicroBatch(micro);
+    }
     detector.gpuWarmUpAndAllocate();
     int prev_size = 0;
     std::vector<sift_cuda::Float3> prev_kpts;
@@ -50,10 +58,12 @@ int main(int argc, char** argv) {
         frame(f, img);
         ticket[f] = detector.submit(img);
     };
-    if (pipelined) submit(0);
+    const int ahead = micro > 1 ? 2 * micro : 1;  // frames submitted past the one being waited for
+    if (pipelined)
+        for (int f = 0; f < ahead && f < frames; f++) submit(f);
     for (int f = 0; f < frames; f++) {
         if (pipelined) {
-            if (f + 1 < frames) submit(f + 1);
+            if (f + ahead < frames) submit(f + ahead);
             detector.wait(ticket[f]);
         } else {
             Imagef img(H, W);
