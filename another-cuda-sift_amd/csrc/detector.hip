@@ -276,7 +276,7 @@ struct Lane {
     hipEvent_t evRead[kInSlots] = {};
     long long uploads = 0;
     // Host results regions: one per (results slot, arena) -- region slot * B + arena.
-    static constexpr int kHostRegions = kResultSlots * 16;  // 16 = sift_hip_detector::kMaxMicroBatch
+    static constexpr int kHostRegions = kResultSlots * kMaxBatch;  // B <= kMaxBatch arenas per lane
     hipEvent_t evHost[kResultSlots] = {};
     long long hostFrame[kHostRegions];  // the frame each host region holds (-1: none; set in add_lane)
     bool hostDesc[kHostRegions] = {};   // ... with its descriptors
