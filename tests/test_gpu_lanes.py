@@ -270,3 +270,19 @@ def test_strided_large_host_frames(sift, u8):
     assert_identical(results(det), ref)
     det.copyToHost(False)  # keypoints only, from the same host copy
     assert np.array_equal(det.final_kpts.view(np.uint32), ref[0].view(np.uint32))
+
+
+def test_host_frames_on_large_batch_handle(sift):
+    """A 32-frame batch handle taking host frames with results read back
+    (per-(slot, arena) host regions up to slot 3 x 32): the synchronous path's results."""
+    frames = [sift.synth_frame(150 + i, W, H) for i in range(6)]
+    ref = sync_reference(sift, frames, numFeatures=2000)
+    det = sift.Detector(sift.CudaSiftConfig(col_width=W, row_width=H, numFeatures=2000), batch=32, lanes=1)
+    det.gpuWarmUpAndAllocate()
+    for f, r in zip(frames, ref):
+        det.detectAndCompute(f)
+        assert_identical(results(det), r)
+    q = [det.submit(f) for f in frames[:2]]
+    for t, r in zip(q, ref[:2]):
+        det.wait(t)
+        assert_identical(results(det), r)
