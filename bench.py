@@ -703,92 +703,100 @@ def main():
         lat.append(time.perf_counter() - t)
     sync_ms = float(np.median(lat) * 1e3)
 
-    # ---- Host input path, PCIe-inclusive (reported beside `value`, never as it) ----
-    # Host frame in -> keypoints, features and descriptors back in host memory,
-    # one detector.  (a) the reference's sequence: synchronous fp32 upload,
-    # detectAndCompute, copyToHost(true); (b) 8-bit frames through submit/wait
-    # with the next frame staged and uploaded while the current one computes.
-    host_f32 = [sift.synth_frame(1000 * rank + i, W, H) for i in range(nframes)]
-    host_u8 = [f.astype(np.uint8) for f in host_f32]
-    nh = max(min(a.steps, 60), 4)
-    for s in range(3):
-        det.detectAndCompute(host_f32[s % nframes])
-        det.copyToHost(True)
-    t = time.perf_counter()
-    for s in range(nh):
-        det.detectAndCompute(host_f32[s % nframes])
-        det.copyToHost(True)
-    t_sync = max_over_ranks(time.perf_counter() - t)
-    # Frames in flight at the drop-in API: submit/wait with `depth` frames
-    # outstanding on a detector with that many compute lanes (one stream,
-    # frame arenas and graphs per lane; consecutive frames overlap).
-    PIPE_LANES, PIPE_DEPTH = 3, 6  # (3 x 3: 0.118-0.122 ms/frame for device frames, 3 x 6: 0.114-0.117)
-    detp = sift.Detector(cfg, device=local, lanes=PIPE_LANES)
-    detp.gpuWarmUpAndAllocate()
+    def pipelined_legs():
+        # ---- Host input path, PCIe-inclusive (reported beside `value`, never as it) ----
+        # Host frame in -> keypoints, features and descriptors back in host memory,
+        # one detector.  (a) the reference's sequence: synchronous fp32 upload,
+        # detectAndCompute, copyToHost(true); (b) 8-bit frames through submit/wait
+        # with the next frame staged and uploaded while the current one computes.
+        host_f32 = [sift.synth_frame(1000 * rank + i, W, H) for i in range(nframes)]
+        host_u8 = [f.astype(np.uint8) for f in host_f32]
+        nh = max(min(a.steps, 60), 4)
+        for s in range(3):
+            det.detectAndCompute(host_f32[s % nframes])
+            det.copyToHost(True)
+        t = time.perf_counter()
+        for s in range(nh):
+            det.detectAndCompute(host_f32[s % nframes])
+            det.copyToHost(True)
+        t_sync = max_over_ranks(time.perf_counter() - t)
+        # Frames in flight at the drop-in API: submit/wait with `depth` frames
+        # outstanding on a detector with that many compute lanes (one stream,
+        # frame arenas and graphs per lane; consecutive frames overlap).
+        PIPE_LANES, PIPE_DEPTH = 3, 6  # (3 x 3: 0.118-0.122 ms/frame for device frames, 3 x 6: 0.114-0.117)
+        detp = sift.Detector(cfg, device=local, lanes=PIPE_LANES)
+        detp.gpuWarmUpAndAllocate()
 
-    def pipelined(submit, fetch):
-        # The first `warm` frames (the same loop) create and warm the lanes,
-        # their staging and results regions; then nh frames are timed.
-        tickets, warm = [], max(3 * PIPE_DEPTH, 24)
-        for s in range(nh + warm):
-            if s == warm:
-                while tickets:
+        def pipelined(submit, fetch):
+            # The first `warm` frames (the same loop) create and warm the lanes,
+            # their staging and results regions; then nh frames are timed.
+            tickets, warm = [], max(3 * PIPE_DEPTH, 24)
+            for s in range(nh + warm):
+                if s == warm:
+                    while tickets:
+                        detp.wait(tickets.pop(0))
+                        if fetch:
+                            detp.copyToHost(True)
+                    t = time.perf_counter()
+                tickets.append(submit(s))
+                if len(tickets) == PIPE_DEPTH:
                     detp.wait(tickets.pop(0))
                     if fetch:
                         detp.copyToHost(True)
-                t = time.perf_counter()
-            tickets.append(submit(s))
-            if len(tickets) == PIPE_DEPTH:
+            while tickets:
                 detp.wait(tickets.pop(0))
                 if fetch:
                     detp.copyToHost(True)
-        while tickets:
-            detp.wait(tickets.pop(0))
-            if fetch:
-                detp.copyToHost(True)
-        return max_over_ranks(time.perf_counter() - t)
+            return max_over_ranks(time.perf_counter() - t)
 
-    t_pipe = pipelined(lambda s: detp.submit(host_u8[s % nframes]), True)
-    dev_u8 = [torch.from_numpy(f).to(dev) for f in host_u8]
-    torch.cuda.synchronize()
-    t_dev = pipelined(lambda s: detp.submitDevice(frames[s % nframes].data_ptr(), stride), False)
-    t_dev8 = pipelined(lambda s: detp.submitDevice(dev_u8[s % nframes].data_ptr(), W, u8=True), False)
-    host_input = {
-        "sync_f32": {"value": round(world * nh * W * H / 1e6 / t_sync, 2), "ms_per_frame": round(t_sync / nh * 1e3, 4)},
-        "pipelined_u8": {"value": round(world * nh * W * H / 1e6 / t_pipe, 2), "ms_per_frame": round(t_pipe / nh * 1e3, 4),
-                         "lanes": PIPE_LANES, "in_flight": PIPE_DEPTH, "lanes_created": detp.lanes()[1]},
-        "unit": "Mpix/s",
-        "note": "PCIe-inclusive, host frame -> results in host memory (copyToHost with descriptors), one detector; "
-                f"pipelined: submit/wait with {PIPE_DEPTH} frames in flight on {PIPE_LANES} compute lanes",
-    }
-    del detp
-    # The same loop on a micro-batching handle (sift_hip_set_micro_batch):
-    # submitted frames run MB at a time as one launch group per lane.
-    MB_LANES, MB, MB_DEPTH = 3, 4, 12  # (2 lanes x 8 in flight: 0.0998 ms/frame, 3 x 12: 0.0942; 2-frame groups 0.110)
-    detp = sift.Detector(cfg, device=local, lanes=MB_LANES, micro_batch=MB)
-    detp.gpuWarmUpAndAllocate()
-    PIPE_DEPTH_SAVED, PIPE_DEPTH = PIPE_DEPTH, MB_DEPTH
-    t_mbh = pipelined(lambda s: detp.submit(host_u8[s % nframes]), True)
-    host_input["pipelined_u8_micro_batch"] = {
-        "value": round(world * nh * W * H / 1e6 / t_mbh, 2), "ms_per_frame": round(t_mbh / nh * 1e3, 4),
-        "lanes": MB_LANES, "frames_per_group": MB, "in_flight": MB_DEPTH}
-    t_mb = pipelined(lambda s: detp.submitDevice(frames[s % nframes].data_ptr(), stride), False)
-    t_mb8 = pipelined(lambda s: detp.submitDevice(dev_u8[s % nframes].data_ptr(), W, u8=True), False)
-    PIPE_DEPTH = PIPE_DEPTH_SAVED
-    device_submit = {
-        "f32": {"value": round(world * nh * W * H / 1e6 / t_dev, 2), "ms_per_frame": round(t_dev / nh * 1e3, 4)},
-        "u8": {"value": round(world * nh * W * H / 1e6 / t_dev8, 2), "ms_per_frame": round(t_dev8 / nh * 1e3, 4)},
-        "unit": "Mpix/s", "lanes": PIPE_LANES, "in_flight": PIPE_DEPTH,
-        "note": "HBM-resident single frames through submitDevice/wait (sift_hip_submit_device), one detector, "
-                f"{PIPE_DEPTH} frames in flight on {PIPE_LANES} compute lanes; results stay on the device",
-        "micro_batch": {
-            "f32": {"value": round(world * nh * W * H / 1e6 / t_mb, 2), "ms_per_frame": round(t_mb / nh * 1e3, 4)},
-            "u8": {"value": round(world * nh * W * H / 1e6 / t_mb8, 2), "ms_per_frame": round(t_mb8 / nh * 1e3, 4)},
-            "lanes": MB_LANES, "frames_per_group": MB, "in_flight": MB_DEPTH,
-            "note": "the same submitDevice/wait loop on a handle with sift_hip_set_micro_batch(4): frames run as "
-                    "4-frame launch groups (per-frame results identical, tests/test_gpu_lanes.py)"},
-    }
-    del detp, dev_u8
+        t_pipe = pipelined(lambda s: detp.submit(host_u8[s % nframes]), True)
+        dev_u8 = [torch.from_numpy(f).to(dev) for f in host_u8]
+        torch.cuda.synchronize()
+        t_dev = pipelined(lambda s: detp.submitDevice(frames[s % nframes].data_ptr(), stride), False)
+        t_dev8 = pipelined(lambda s: detp.submitDevice(dev_u8[s % nframes].data_ptr(), W, u8=True), False)
+        host_input = {
+            "sync_f32": {"value": round(world * nh * W * H / 1e6 / t_sync, 2), "ms_per_frame": round(t_sync / nh * 1e3, 4)},
+            "pipelined_u8": {"value": round(world * nh * W * H / 1e6 / t_pipe, 2), "ms_per_frame": round(t_pipe / nh * 1e3, 4),
+                             "lanes": PIPE_LANES, "in_flight": PIPE_DEPTH, "lanes_created": detp.lanes()[1]},
+            "unit": "Mpix/s",
+            "note": "PCIe-inclusive, host frame -> results in host memory (copyToHost with descriptors), one detector; "
+                    f"pipelined: submit/wait with {PIPE_DEPTH} frames in flight on {PIPE_LANES} compute lanes",
+        }
+        del detp
+        # The same loop on a micro-batching handle (sift_hip_set_micro_batch):
+        # submitted frames run MB at a time as one launch group per lane.
+        MB_LANES, MB, MB_DEPTH = 3, 4, 12  # (2 lanes x 8 in flight: 0.0998 ms/frame, 3 x 12: 0.0942; 2-frame groups 0.110)
+        detp = sift.Detector(cfg, device=local, lanes=MB_LANES, micro_batch=MB)
+        detp.gpuWarmUpAndAllocate()
+        PIPE_DEPTH_SAVED, PIPE_DEPTH = PIPE_DEPTH, MB_DEPTH
+        t_mbh = pipelined(lambda s: detp.submit(host_u8[s % nframes]), True)
+        host_input["pipelined_u8_micro_batch"] = {
+            "value": round(world * nh * W * H / 1e6 / t_mbh, 2), "ms_per_frame": round(t_mbh / nh * 1e3, 4),
+            "lanes": MB_LANES, "frames_per_group": MB, "in_flight": MB_DEPTH}
+        t_mb = pipelined(lambda s: detp.submitDevice(frames[s % nframes].data_ptr(), stride), False)
+        t_mb8 = pipelined(lambda s: detp.submitDevice(dev_u8[s % nframes].data_ptr(), W, u8=True), False)
+        PIPE_DEPTH = PIPE_DEPTH_SAVED
+        device_submit = {
+            "f32": {"value": round(world * nh * W * H / 1e6 / t_dev, 2), "ms_per_frame": round(t_dev / nh * 1e3, 4)},
+            "u8": {"value": round(world * nh * W * H / 1e6 / t_dev8, 2), "ms_per_frame": round(t_dev8 / nh * 1e3, 4)},
+            "unit": "Mpix/s", "lanes": PIPE_LANES, "in_flight": PIPE_DEPTH,
+            "note": "HBM-resident single frames through submitDevice/wait (sift_hip_submit_device), one detector, "
+                    f"{PIPE_DEPTH} frames in flight on {PIPE_LANES} compute lanes; results stay on the device",
+            "micro_batch": {
+                "f32": {"value": round(world * nh * W * H / 1e6 / t_mb, 2), "ms_per_frame": round(t_mb / nh * 1e3, 4)},
+                "u8": {"value": round(world * nh * W * H / 1e6 / t_mb8, 2), "ms_per_frame": round(t_mb8 / nh * 1e3, 4)},
+                "lanes": MB_LANES, "frames_per_group": MB, "in_flight": MB_DEPTH,
+                "note": "the same submitDevice/wait loop on a handle with sift_hip_set_micro_batch(4): frames run as "
+                        "4-frame launch groups (per-frame results identical, tests/test_gpu_lanes.py)"},
+        }
+        del detp, dev_u8
+        return host_input, device_submit
+
+    # Side legs: a failure here keeps the C2 line (recorded as an error).
+    try:
+        host_input, device_submit = pipelined_legs()
+    except Exception as e:  # noqa: BLE001
+        host_input = device_submit = {"error": repr(e)[:300]}
 
     # ---- per-kernel roofline: HIP events on the detector's own stream --------
     rl = measure_roofline(detb, frames, stride, a.traffic_summary, batch=fb if B > 1 else None)
