@@ -2202,6 +2202,46 @@ int sift_hip_copy_to_host(sift_hip_t d, float* k3, float* f4, uint16_t* desc, in
     return SIFT_HIP_OK;
 }
 
+// The current frame's results in the handle's pinned host region (the lane's
+// region slot * B + idx): a host-input frame's were written there by its last
+// kernel (prefetch_results), any other frame's are copied there now over the
+// copy stream.  No copy into caller memory.
+int sift_hip_results_host(sift_hip_t d, const float** k3, const float** f4, const uint16_t** desc, int* count) {
+    CHECK_HANDLE(d);
+    if (int rc = ensure_counts(d)) return rc;
+    const int n = std::min(d->count, (int)d->kp.capFinal);
+    Lane& L = d->lane();
+    if (!d->hostWant)
+        for (int k = 0; k < d->nLanes; k++)
+            if (int rc = ensure_host_res(d, d->lanes[k])) return rc;
+    d->hostWant = std::max(d->hostWant, desc ? 2 : 1);
+    const int region = d->cur * d->B + d->curIdx;
+    float *hk3, *hf4;
+    uint16_t* hdesc;
+    host_res(d, L.hRes, region, &hk3, &hf4, &hdesc);
+    if (L.hostFrame[region] == d->current && d->current >= d->firstFrame && (!desc || L.hostDesc[region])) {
+        HIPCHK(hipEventSynchronize(L.evHost[d->cur]));
+    } else {
+        hipStream_t s;
+        if (int rc = copy_stream(d, &s)) return rc;
+        HIPCHK(hipStreamWaitEvent(s, L.evFrame[d->cur], 0));
+        if (n > 0) {
+            HIPCHK(hipMemcpyAsync(hk3, d->dKpts3[d->cur], sizeof(float) * 3 * n, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(hf4, d->dFeats4[d->cur], sizeof(float) * 4 * n, hipMemcpyDeviceToHost, s));
+            if (desc)
+                HIPCHK(hipMemcpyAsync(hdesc, d->dDesc[d->cur], sizeof(uint16_t) * 128 * n, hipMemcpyDeviceToHost, s));
+        }
+        HIPCHK(hipStreamSynchronize(s));
+        L.hostFrame[region] = d->current;
+        L.hostDesc[region] = desc != nullptr;
+    }
+    if (k3) *k3 = hk3;
+    if (f4) *f4 = hf4;
+    if (desc) *desc = hdesc;
+    if (count) *count = n;
+    return SIFT_HIP_OK;
+}
+
 int sift_hip_copy_descriptors_device(sift_hip_t d, uint16_t* dst, int cap, void* stream) {
     CHECK_HANDLE(d);
     if (int rc = ensure_counts(d)) return rc;

@@ -202,6 +202,18 @@ void Detector::copyToHost(bool descriptor) {
           "copyToHost");
 }
 
+Detector::HostResults Detector::hostResults(bool descriptor) {
+    HostResults r;
+    if (!m_initialized) return r;
+    const float *k3 = nullptr, *f4 = nullptr;
+    const uint16_t* desc = nullptr;
+    check(sift_hip_results_host(m_handle, &k3, &f4, descriptor ? &desc : nullptr, &r.count), "hostResults");
+    r.kpts = reinterpret_cast<const Float3*>(k3);
+    r.features = reinterpret_cast<const Float4*>(f4);
+    r.descriptors = reinterpret_cast<const Half*>(desc);
+    return r;
+}
+
 namespace {
 
 struct MatcherDeleter {

@@ -113,6 +113,7 @@ def lib() -> ctypes.CDLL:
         "sift_hip_overflow_flags": (i, [vp, ip]),
         "sift_hip_results_device": (i, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), ip, ip]),
         "sift_hip_copy_to_host": (i, [vp, vp, vp, vp, i]),
+        "sift_hip_results_host": (i, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), ip]),
         "sift_hip_copy_descriptors_device": (i, [vp, vp, i, vp]),
         "sift_hip_set_datagen": (i, [vp, ctypes.c_char_p]),
         "sift_hip_replay_stage": (i, [vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]),
@@ -417,6 +418,28 @@ class Detector:
         self.final_kpts, self.final_features = k3, f4
         if d is not None:
             self.descriptors = d.view(np.float16)
+
+    def results_host(self, descriptor: bool = True):
+        """(kpts3 (n,3), feats4 (n,4), descriptors (n,128) fp16 or None) of the
+        current frame as read-only views of the handle's pinned host results
+        (sift_hip_results_host: no copy into Python memory).  They stay valid
+        while the frame is the current or the previous one; copy what must
+        outlive that."""
+        k3, f4, d, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int()
+        _check(lib().sift_hip_results_host(self._h, ctypes.byref(k3), ctypes.byref(f4),
+                                           ctypes.byref(d) if descriptor else None, ctypes.byref(n)), "results_host")
+
+        def view(ptr, ctype, cols, dtype):
+            if n.value == 0:
+                return np.zeros((0, cols), dtype)
+            a = np.ctypeslib.as_array((ctype * (n.value * cols)).from_address(ptr)).reshape(n.value, cols)
+            a.flags.writeable = False
+            return a
+
+        kp = view(k3.value, ctypes.c_float, 3, np.float32)
+        ft = view(f4.value, ctypes.c_float, 4, np.float32)
+        ds = view(d.value, ctypes.c_uint16, 128, np.uint16).view(np.float16) if descriptor else None
+        return kp, ft, ds
 
     def capacities(self) -> dict:
         """Per-frame buffer capacities (sift_hip_capacities; host-only)."""

@@ -727,6 +727,14 @@ def main():
         detp = sift.Detector(cfg, device=local, lanes=PIPE_LANES)
         detp.gpuWarmUpAndAllocate()
 
+        def copy_out():
+            detp.copyToHost(True)
+
+        def view_out():  # the detector's pinned host rows, no copy (sift_hip_results_host)
+            k3, _, d = detp.results_host(True)
+            if len(k3):
+                float(k3[-1, 0]) + float(d[-1, -1])
+
         def pipelined(submit, fetch):
             # The first `warm` frames (the same loop) create and warm the lanes,
             # their staging and results regions; then nh frames are timed.
@@ -736,24 +744,24 @@ def main():
                     while tickets:
                         detp.wait(tickets.pop(0))
                         if fetch:
-                            detp.copyToHost(True)
+                            fetch()
                     t = time.perf_counter()
                 tickets.append(submit(s))
                 if len(tickets) == PIPE_DEPTH:
                     detp.wait(tickets.pop(0))
                     if fetch:
-                        detp.copyToHost(True)
+                        fetch()
             while tickets:
                 detp.wait(tickets.pop(0))
                 if fetch:
-                    detp.copyToHost(True)
+                    fetch()
             return max_over_ranks(time.perf_counter() - t)
 
-        t_pipe = pipelined(lambda s: detp.submit(host_u8[s % nframes]), True)
+        t_pipe = pipelined(lambda s: detp.submit(host_u8[s % nframes]), copy_out)
         dev_u8 = [torch.from_numpy(f).to(dev) for f in host_u8]
         torch.cuda.synchronize()
-        t_dev = pipelined(lambda s: detp.submitDevice(frames[s % nframes].data_ptr(), stride), False)
-        t_dev8 = pipelined(lambda s: detp.submitDevice(dev_u8[s % nframes].data_ptr(), W, u8=True), False)
+        t_dev = pipelined(lambda s: detp.submitDevice(frames[s % nframes].data_ptr(), stride), None)
+        t_dev8 = pipelined(lambda s: detp.submitDevice(dev_u8[s % nframes].data_ptr(), W, u8=True), None)
         host_input = {
             "sync_f32": {"value": round(world * nh * W * H / 1e6 / t_sync, 2), "ms_per_frame": round(t_sync / nh * 1e3, 4)},
             "pipelined_u8": {"value": round(world * nh * W * H / 1e6 / t_pipe, 2), "ms_per_frame": round(t_pipe / nh * 1e3, 4),
@@ -769,12 +777,21 @@ def main():
         detp = sift.Detector(cfg, device=local, lanes=MB_LANES, micro_batch=MB)
         detp.gpuWarmUpAndAllocate()
         PIPE_DEPTH_SAVED, PIPE_DEPTH = PIPE_DEPTH, MB_DEPTH
-        t_mbh = pipelined(lambda s: detp.submit(host_u8[s % nframes]), True)
+        t_mbh = pipelined(lambda s: detp.submit(host_u8[s % nframes]), copy_out)
         host_input["pipelined_u8_micro_batch"] = {
             "value": round(world * nh * W * H / 1e6 / t_mbh, 2), "ms_per_frame": round(t_mbh / nh * 1e3, 4),
             "lanes": MB_LANES, "frames_per_group": MB, "in_flight": MB_DEPTH}
-        t_mb = pipelined(lambda s: detp.submitDevice(frames[s % nframes].data_ptr(), stride), False)
-        t_mb8 = pipelined(lambda s: detp.submitDevice(dev_u8[s % nframes].data_ptr(), W, u8=True), False)
+        # The same, reading the results where the frame's last kernel put them
+        # (results_host: views of the detector's pinned rows, as the
+        # reference's final_kpts / descriptors host vectors) instead of copying
+        # them into new arrays.
+        t_mbv = pipelined(lambda s: detp.submit(host_u8[s % nframes]), view_out)
+        host_input["pipelined_u8_micro_batch_views"] = {
+            "value": round(world * nh * W * H / 1e6 / t_mbv, 2), "ms_per_frame": round(t_mbv / nh * 1e3, 4),
+            "lanes": MB_LANES, "frames_per_group": MB, "in_flight": MB_DEPTH,
+            "note": "results_host(True) after every wait instead of copyToHost(True)"}
+        t_mb = pipelined(lambda s: detp.submitDevice(frames[s % nframes].data_ptr(), stride), None)
+        t_mb8 = pipelined(lambda s: detp.submitDevice(dev_u8[s % nframes].data_ptr(), W, u8=True), None)
         PIPE_DEPTH = PIPE_DEPTH_SAVED
         device_submit = {
             "f32": {"value": round(world * nh * W * H / 1e6 / t_dev, 2), "ms_per_frame": round(t_dev / nh * 1e3, 4)},

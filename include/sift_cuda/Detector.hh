@@ -59,6 +59,17 @@ public:
 
     // Detector.cu:606-634: copies total_size results (+ descriptors) to host.
     void copyToHost(bool descriptor);
+    // Extra: the same rows without the copy into final_kpts / final_features /
+    // descriptors -- views of the detector's pinned host results of the
+    // current frame (sift_hip_results_host), valid while that frame is the
+    // current or the previous one.
+    struct HostResults {
+        const Float3* kpts = nullptr;
+        const Float4* features = nullptr;
+        const Half* descriptors = nullptr;  // 128 per keypoint; null unless requested
+        int count = 0;
+    };
+    HostResults hostResults(bool descriptor);
 
     // Detector.hh:48-51 debug snapshot switch: every following detectAndCompute
     // writes its stage dumps into `path` (sift_hip_set_datagen: meta.json,

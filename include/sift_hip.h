@@ -216,6 +216,18 @@ int sift_hip_results_device(sift_hip_t h, const float** kpts3, const float** fea
  * min(count, cap) results; desc may be NULL. */
 int sift_hip_copy_to_host(sift_hip_t h, float* kpts3, float* feats4, uint16_t* desc, int cap);
 
+/* The same results without a copy into caller memory: the reference's
+ * detector-owned host vectors final_kpts / final_features / descriptors
+ * (Detector.hh:58-60, filled by copyToHost).  Returns pointers into the
+ * handle's pinned results region of the current frame (*count rows; desc may
+ * be NULL).  A frame submitted from host memory already had its results
+ * written there by its last kernel; any other frame's are copied there by
+ * this call.  The rows stay valid while the frame is the current or the
+ * previous one (the lifetime of prev_descriptor): until a second later frame
+ * has been made current by wait / detect.  Read-only for the caller. */
+int sift_hip_results_host(sift_hip_t h, const float** kpts3, const float** feats4, const uint16_t** desc,
+                          int* count);
+
 /* Device-to-device copy of this frame's descriptors (e.g. into a torch tensor
  * for an RCCL all-gather).  Copies min(count, cap) rows, pads nothing.  The
  * row count is needed on the host, so this call (like sift_hip_results_device

@@ -141,6 +141,53 @@ def test_host_submit_micro_batch_equal_sync(sift, mb, lanes, depth):
     assert_identical(results(det), ref[5])
 
 
+def view_results(det):
+    k3, f4, d = det.results_host(True)
+    return k3, f4, d.view(np.uint16)
+
+
+@pytest.mark.parametrize("mb,lanes,depth", [(1, 3, 6), (4, 3, 12), (3, 2, 4)])
+def test_results_host_views_equal_sync(sift, mb, lanes, depth):
+    """sift_hip_results_host: the current frame's rows as views of the handle's
+    pinned results (no copy into caller memory) equal the synchronous path's
+    for host frames (written there by the frame's last kernel) and device
+    frames (copied there by the call), and a frame's views stay intact while
+    it is the previous frame (the next frame waited, later frames in flight)."""
+    frames = [sift.synth_frame(150 + i, W, H) for i in range(12)]
+    ref = sync_reference(sift, frames, numFeatures=2000)
+    dev = [torch.from_numpy(f).cuda() for f in frames]
+    torch.cuda.synchronize()
+    _, det = make_detector(sift, W, H, numFeatures=2000, lanes=lanes, micro_batch=mb)
+    queue, i, prev = [], 0, None
+
+    def drain_one():
+        nonlocal i, prev
+        det.wait(queue.pop(0))
+        if i % 5 == 4:  # keypoints only first: the descriptor rows come on the next request
+            k3, f4, d = det.results_host(False)
+            assert d is None
+            assert_identical((k3, f4), ref[i][:2])
+        cur = view_results(det)
+        assert_identical(cur, ref[i])
+        if prev is not None:
+            assert_identical(prev, ref[i - 1])
+        prev = cur
+        i += 1
+
+    for s in range(len(frames)):
+        queue.append(det.submitDevice(dev[s].data_ptr(), W * 4) if s % 3 == 2
+                     else det.submit(frames[s].astype(np.uint8) if s % 2 else frames[s]))
+        if len(queue) == depth:
+            drain_one()
+    while queue:
+        drain_one()
+    det.detectAndCompute(frames[3])  # synchronous: copied by the call
+    assert_identical(view_results(det), ref[3])
+    _, det0 = make_detector(sift, W, H, numFeatures=2000)
+    det0.detectAndCompute(frames[0])
+    assert_identical(view_results(det0), ref[0])  # first call on a handle (regions allocated by it)
+
+
 def test_micro_batch_limits(sift):
     img = torch.from_numpy(sift.synth_frame(1, 128, 96)).cuda()
     torch.cuda.synchronize()

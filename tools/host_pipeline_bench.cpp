@@ -3,8 +3,9 @@
 // with `depth` frames in flight on `lanes` compute lanes (setLanes), as
 // bench.py's host_input.pipelined_u8 runs them.  Prints one JSON line:
 // ms per frame, and the mean wall time of each call.
-//   host_pipeline_bench [lanes] [depth] [frames] [desc 0|1|2] [dev 0..5] [micro-batch]
-// desc 2: no copyToHost at all; dev 1: the frames already in device memory
+//   host_pipeline_bench [lanes] [depth] [frames] [desc 0|1|2|3] [dev 0..5] [micro-batch]
+// desc 2: no copyToHost at all; desc 3: hostResults(true) (views of the
+// detector's pinned results with descriptors, no copy); dev 1: the frames already in device memory
 // (submitDevice) instead of host frames (submit); dev 2: the frames in pinned
 // host memory, read by the frame's first kernel over PCIe (submitDevice with
 // the mapped pointer: no staging copy on the calling thread); dev 3: the same
@@ -31,7 +32,7 @@ int main(int argc, char** argv) {
     const int lanes = argc > 1 ? std::atoi(argv[1]) : 3, depth = argc > 2 ? std::atoi(argv[2]) : 3;
     const int frames = argc > 3 ? std::atoi(argv[3]) : 200;
     const int descMode = argc > 4 ? std::atoi(argv[4]) : 1;
-    const bool desc = descMode == 1, copy = descMode != 2;
+    const bool desc = descMode == 1, copy = descMode == 0 || descMode == 1, view = descMode == 3;
     const int dev = argc > 5 ? std::atoi(argv[5]) : 0;
     const int mb = argc > 6 ? std::atoi(argv[6]) : 1;  // micro-batch (setMicroBatch)
     const int W = 1920, H = 1200;
@@ -92,6 +93,7 @@ int main(int argc, char** argv) {
     };
     using clk = std::chrono::steady_clock;
     double tSub = 0, tWait = 0, tCopy = 0;
+    volatile float sink = 0;
     std::vector<double> subs;  // per-submit wall times of the timed run (ms)
     auto run = [&](int n, bool timed) {
         std::deque<long long> q;
@@ -101,6 +103,10 @@ int main(int argc, char** argv) {
             q.pop_front();
             auto b = clk::now();
             if (copy) det.copyToHost(desc);
+            if (view) {
+                const auto r = det.hostResults(true);
+                if (r.count > 0) sink += r.kpts[r.count - 1].x + (float)r.descriptors[128 * r.count - 1].bits;
+            }
             auto c = clk::now();
             if (timed) {
                 tWait += std::chrono::duration<double, std::milli>(b - a).count();
