@@ -60,6 +60,33 @@ constexpr int kHistWords = 2 * kCells * kCellW;  // one copy: the even- and the 
 // worse); the oracle's correctly rounded division / sqrt / exp32f in the
 // sample loop (+16 % time, flip counts unchanged).)
 
+// This frame's host rows (HostOut): null pointers unless the frame asked
+// for them (Counters.pad[1] level, set by k_order / k_select) and the handle
+// has a host region for it.
+struct HostRows {
+    float* k3;
+    float* f4;
+    uint16_t* desc;
+};
+// (Also moves h's device result pointers to the frame.)
+__device__ __forceinline__ HostRows host_rows(HostOut& h, const Counters* ctr, unsigned frame, long foff) {
+    h.k3 = fptr(h.k3, foff);
+    h.f4 = fptr(h.f4, foff);
+    const unsigned level = ctr->pad[1] & ((1u << kHostReqShift) - 1);
+    char* r = level ? h.tab[frame] : nullptr;
+    if (!r) return HostRows{nullptr, nullptr, nullptr};
+    float* f4 = reinterpret_cast<float*>(r + ((12 * (size_t)h.cap + 255) & ~(size_t)255));
+    return HostRows{reinterpret_cast<float*>(r), f4,
+                    level > 1 ? reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(f4) + 16 * (size_t)h.cap) : nullptr};
+}
+// Output row po's keypoint (lanes 0-2) and features (lanes 3-6) to the host rows.
+__device__ __forceinline__ void host_row(const HostRows& hr, const HostOut& h, unsigned po, int t) {
+    if (t < 3)
+        hr.k3[(size_t)po * 3 + t] = h.k3[(size_t)po * 3 + t];
+    else
+        hr.f4[(size_t)po * 4 + t - 3] = h.f4[(size_t)po * 4 + t - 3];
+}
+
 struct DescGeom {
     float cos_t, sin_t, exp_scale;
     int ptx, pty, rows, cols;
@@ -163,7 +190,8 @@ template <int kDT>
 __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* __restrict__ jobs, const Counters* __restrict__ ctr,
                                                    const unsigned* __restrict__ range_keys,
                                                    uint16_t* __restrict__ desc, Sidecar sidecar,
-                                                   Counters* __restrict__ host_ctr, long fs, unsigned nf) {
+                                                   Counters* __restrict__ host_ctr, HostOut host, long fs,
+                                                   unsigned nf) {
     // Two u32 fixed-point histograms so that each sample's orientation pair
     // (o0, o0+1) is one naturally aligned ds_add_u64 (low word o0, high word
     // o0+1): even o0 -> histE[cell*10 + o], odd o0 -> histO[cell*10 + 1 + o]
@@ -196,6 +224,7 @@ __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* _
     // them to the host's pinned copy directly (no D2H copy node in the graph).
     if (wg == 0 && tid < (int)(sizeof(Counters) / 4))
         reinterpret_cast<unsigned*>(host_ctr)[tid] = reinterpret_cast<const unsigned*>(ctr)[tid];
+    const HostRows hr = host_rows(host, ctr, frame, foff);
     // A single frame's grid (8192) exceeds its keypoint count: the surplus
     // workgroups leave before the pixel-range reduction below.
     if (wg >= n) return;
@@ -488,6 +517,7 @@ __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* _
             const _Float16 hv = (_Float16)(float)v;
             if (tid + kDT * h < 128) {
                 desc[(size_t)po * 128 + tid + kDT * h] = __builtin_bit_cast(uint16_t, hv);
+                if (hr.desc) hr.desc[(size_t)po * 128 + tid + kDT * h] = __builtin_bit_cast(uint16_t, hv);
                 sidecar.codes[(size_t)po * 128 + tid + kDT * h] = (int8_t)(v - 128);
                 c2 += (v - 128) * (v - 128);
             }
@@ -497,6 +527,7 @@ __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* _
         // two after it (s_cn is next written after several more barriers).
         c2 = __builtin_amdgcn_readlane(wave_incl_scan(c2), 63);
         if (lane == 0 && tid < 128) s_cn[tid >> 6] = c2;
+        if (hr.k3 && tid < 7) host_row(hr, host, po, tid);
         lds_barrier();  // sq / histograms are rewritten by the next keypoint
         if (tid == 0) sidecar.keys[po] = -(256 * (s_cn[0] + s_cn[1]) + (int)(po & 255));
     }
@@ -562,7 +593,8 @@ void upload_desc_exp_table(const float* tab64) {
 __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __restrict__ jobs,
                                                                const Counters* __restrict__ ctr,
                                                                uint16_t* __restrict__ desc, Sidecar sidecar,
-                                                               Counters* __restrict__ host_ctr, long fs, unsigned nf) {
+                                                               Counters* __restrict__ host_ctr, HostOut host, long fs,
+                                                               unsigned nf) {
     __shared__ float s_tab[64];
     // Chunk sample s: per target cell (dr, dc) one float4 {P.x, P.y, S.x, S.y}
     // (below), at s*16 + (dr*2 + dc)*4; then a zero record for absent hits.
@@ -864,8 +896,14 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
         b1 = b1 < 0 ? 0 : (b1 > 255 ? 255 : b1);
         const _Float16 h0 = (_Float16)(float)b0, h1 = (_Float16)(float)b1;
         const unsigned po = (unsigned)jb.out;  // output row (jobs run longest first, JobOrder)
-        reinterpret_cast<unsigned*>(desc + (size_t)po * 128)[lane] =
-            (unsigned)__builtin_bit_cast(uint16_t, h0) | (unsigned)__builtin_bit_cast(uint16_t, h1) << 16;
+        const unsigned pair = (unsigned)__builtin_bit_cast(uint16_t, h0) | (unsigned)__builtin_bit_cast(uint16_t, h1) << 16;
+        reinterpret_cast<unsigned*>(desc + (size_t)po * 128)[lane] = pair;
+        // Host rows looked up here, not kept across the keypoint loop (VGPRs:
+        // 73 vs 62, one wave per SIMD less).
+        HostOut hf = host;
+        const HostRows hr = host_rows(hf, ctr, frame, foff);
+        if (hr.desc) reinterpret_cast<unsigned*>(hr.desc + (size_t)po * 128)[lane] = pair;
+        if (hr.k3 && lane < 7) host_row(hr, hf, po, lane);
         // Matcher sidecar: int8 codes and the key bias (k_descriptor's epilogue).
         reinterpret_cast<unsigned short*>(sidecar.codes + (size_t)po * 128)[lane] =
             (unsigned short)((b0 - 128) & 255) | (unsigned short)(((b1 - 128) & 255) << 8);
@@ -876,12 +914,13 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
 }
 
 void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned* range_keys, uint16_t* desc,
-                       Sidecar sidecar, Counters* host_ctr, const KeypointParams& kp, const Frames& fr, hipStream_t s) {
+                       Sidecar sidecar, Counters* host_ctr, HostOut host, const KeypointParams& kp, const Frames& fr,
+                       hipStream_t s) {
     if (kp.descExact) {
         // One wave per keypoint; each workgroup loops over keypoints.
         const int per = fr.nf <= 1 ? 2048 : std::max(512, 8192 / fr.nf);
         hipLaunchKernelGGL(k_descriptor_exact, dim3(per * fr.nf), dim3(kExactWG), 0, s, jobs, ctr, desc, sidecar,
-                           host_ctr, fr.stride, (unsigned)fr.nf);
+                           host_ctr, host, fr.stride, (unsigned)fr.nf);
         return;
     }
     // Threads per keypoint: 256 for a single frame (128: 34.6 us, 512: 47.6 vs
@@ -889,7 +928,7 @@ void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned*
     constexpr int kSingleDT = 256, kBatchDT = 128;
     if (fr.nf <= 1) {
         hipLaunchKernelGGL(k_descriptor<kSingleDT>, dim3(8192), dim3(kSingleDT), 0, s, jobs, ctr, range_keys, desc,
-                           sidecar, host_ctr, fr.stride, 1u);
+                           sidecar, host_ctr, host, fr.stride, 1u);
     } else {
         // Workgroups per frame: 2048 at 8 frames (16384 in all).  The bigger
         // grids this kernel once had filled every CU slot and kept the other
@@ -898,7 +937,7 @@ void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned*
         // (tools/grid_sweep.sh).
         const int per = std::max(1024, 16384 / fr.nf);
         hipLaunchKernelGGL(k_descriptor<kBatchDT>, dim3(per * fr.nf), dim3(kBatchDT), 0, s, jobs, ctr, range_keys,
-                           desc, sidecar, host_ctr, fr.stride, (unsigned)fr.nf);
+                           desc, sidecar, host_ctr, host, fr.stride, (unsigned)fr.nf);
     }
 }
 

@@ -250,11 +250,14 @@ struct Lane {
     long long launched = 0;  // launch groups run on this lane; the next takes slot launched % kResultSlots
     long long last = -1;     // the last frame launched here (-1: none since warm-up)
     char* mbIn = nullptr;    // micro-batch input copies: mb frames of f32 rows (created at the first micro-batch)
-    // Host-input frames: results copied to mapped pinned host memory right
-    // after the frame (k_results_to_host), one region per slot (created at the
-    // lane's first host-input frame).
+    // Host-input frames: results written to mapped pinned host memory by the
+    // frame's descriptor kernel (HostOut), one region per (slot, arena)
+    // (created once a caller reads results back); dHostTab (device, kSlots x
+    // B region pointers, null until then) tells the kernel where.
     char* hRes = nullptr;
     char* hResDev = nullptr;
+    char** dHostTab = nullptr;
+    std::vector<char*> hostTab;  // its host copy (the source of the async upload)
     // Host-input staging of this lane: two pinned host buffers, moved into
     // the lane's device staging by a 64-workgroup copy kernel on the lane's
     // stream ahead of the frame (launch_copy_rows).  Measured alternatives
@@ -277,7 +280,6 @@ struct Lane {
     long long uploads = 0;
     // Host results regions: one per (results slot, arena) -- region slot * B + arena.
     static constexpr int kHostRegions = kResultSlots * kMaxBatch;  // B <= kMaxBatch arenas per lane
-    hipEvent_t evHost[kResultSlots] = {};
     long long hostFrame[kHostRegions];  // the frame each host region holds (-1: none; set in add_lane)
     bool hostDesc[kHostRegions] = {};   // ... with its descriptors
 };
@@ -480,13 +482,12 @@ struct sift_hip_detector {
                 if (L.mbIn) (void)hipFree(L.mbIn);
                 if (L.hCtr) (void)hipHostFree(L.hCtr);
                 if (L.hRes) (void)hipHostFree(L.hRes);
+                if (L.dHostTab) (void)hipFree(L.dHostTab);
                 for (int k = 0; k < Lane::kInSlots; k++) {
                     if (L.hStage[k]) (void)hipHostFree(L.hStage[k]);
                     if (L.dStage[k]) (void)hipFree(L.dStage[k]);
                     if (L.evRead[k]) (void)hipEventDestroy(L.evRead[k]);
                 }
-                for (hipEvent_t e : L.evHost)
-                    if (e) (void)hipEventDestroy(e);
                 if (L.stream) (void)hipStreamDestroy(L.stream);
             }
             if (dDg) (void)hipFree(dDg);
@@ -749,6 +750,9 @@ int add_lane(sift_hip_detector* d) {
     HIPCHK(hipHostMalloc((void**)&L.hCtr, sizeof(Counters) * nh, hipHostMallocMapped | hipHostMallocCoherent));
     memset(L.hCtr, 0, sizeof(Counters) * nh);
     HIPCHK(hipHostGetDevicePointer((void**)&L.hCtrDev, L.hCtr, 0));
+    if (hipMalloc((void**)&L.dHostTab, sizeof(char*) * nh) != hipSuccess)
+        return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc of the host results table failed");
+    HIPCHK(hipMemsetAsync(L.dHostTab, 0, sizeof(char*) * nh, L.stream));
     for (int b = 0; b < d->kSlots; b++) {
         HIPCHK(hipEventCreateWithFlags(&L.evFrame[b], hipEventDisableTiming));
         HIPCHK(hipEventRecord(L.evFrame[b], L.stream));
@@ -972,6 +976,8 @@ void enqueue_descriptor(sift_hip_detector* d, int slot, int nf) {
     d->timed("descriptor", 0, [&] {
         launch_descriptor(d->dJobs, d->dCtr, range_keys(d, slot & 1), d->dDesc[slot], d->dSide[slot],
                           d->hCtrDev + (size_t)slot * d->B,
+                          HostOut{d->lanes[d->ln].dHostTab + (size_t)slot * d->B, d->dKpts3[slot], d->dFeats4[slot],
+                                  d->kp.capFinal},
                           d->kp, fr, d->stream);
     });
 }
@@ -1250,42 +1256,39 @@ void host_res(const sift_hip_detector* d, char* base, int region, float** k3, fl
     *desc = reinterpret_cast<uint16_t*>(p + 16 * c);
 }
 
-// After host-input frames f .. f + n - 1 (one launch group, frame f + i in
-// arena i): their results into the lane's pinned host regions (slot * B + i)
-// on the lane's stream (the lane's next group follows; other lanes keep
-// computing), evHost[slot] once they are there.
-// The lane's pinned results regions (kSlots x B), allocated for every lane
-// once a caller reads results back (sift_hip_copy_to_host turns hostWant on)
-// and for lanes created after that: a lazy allocation inside a submit stalled
-// it for ~14 ms.
+// The lane's pinned results regions (kSlots x B) and the device table that
+// points the descriptor kernel at them (HostOut), set up for every lane once a
+// caller reads results back (sift_hip_copy_to_host / sift_hip_results_host
+// turn hostWant on) and for lanes created after that: a lazy allocation
+// inside a submit stalled it for ~14 ms.  The table goes in on the lane's
+// stream (after its zeroing; frames launched earlier keep a null table).
 int ensure_host_res(sift_hip_detector* d, Lane& L) {
     if (L.hRes) return SIFT_HIP_OK;
-    const size_t bytes = host_res_bytes(d) * d->kSlots * d->B;
-    HIPCHK(hipHostMalloc((void**)&L.hRes, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+    const size_t nr = (size_t)d->kSlots * d->B, rb = host_res_bytes(d);
+    HIPCHK(hipHostMalloc((void**)&L.hRes, rb * nr, hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(hipHostGetDevicePointer((void**)&L.hResDev, L.hRes, 0));
-    for (hipEvent_t& e : L.evHost) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    L.hostTab.resize(nr);
+    for (size_t r = 0; r < nr; r++) L.hostTab[r] = L.hResDev + rb * r;
+    HIPCHK(hipMemcpyAsync(L.dHostTab, L.hostTab.data(), sizeof(char*) * nr, hipMemcpyHostToDevice, L.stream));
     return SIFT_HIP_OK;
 }
 
-int prefetch_results(sift_hip_detector* d, long long f, int n = 1) {
-    if (!d->hostWant) return SIFT_HIP_OK;
-    Lane& L = d->lane();
-    const int slot = d->frec(f).slot;
-    if (int rc = ensure_host_res(d, L)) return rc;
-    const bool withDesc = d->hostWant > 1;
-    for (int i = 0; i < n; i++) {
-        const int region = slot * d->B + i;
-        const long o = (long)i * d->afs;
-        float *k3, *f4;
-        uint16_t* desc;
-        host_res(d, L.hResDev, region, &k3, &f4, &desc);
-        launch_results_to_host(fptr(d->dKpts3[slot], o), fptr(d->dFeats4[slot], o), fptr(d->dDesc[slot], o),
-                               fptr(d->dCtr, o), d->kp.capFinal, k3, f4, withDesc ? desc : nullptr, d->stream);
-        L.hostFrame[region] = f + i;
-        L.hostDesc[region] = withDesc;
-    }
-    HIPCHK(hipEventRecord(L.evHost[slot], d->stream));
-    return SIFT_HIP_OK;
+// A host-input frame's results request (the word its staging copy sets:
+// arena i's Counters.pad[1], HostOut): null unless a caller reads results back.
+unsigned* host_request(sift_hip_detector* d, int i, unsigned* val) {
+    *val = (unsigned)d->hostWant << kHostReqShift;
+    return d->hostWant ? &fptr(d->dCtr, (long)i * d->afs)->pad[1] : nullptr;
+}
+
+// After host-input frame f (arena i of its launch group) was launched with a
+// request: its results land in the lane's region slot * B + i.
+void mark_host_results(sift_hip_detector* d, long long f) {
+    if (!d->hostWant) return;
+    const auto& r = d->frec(f);
+    Lane& L = d->lanes[r.lane];
+    const int region = r.slot * d->B + r.idx;
+    L.hostFrame[region] = f;
+    L.hostDesc[region] = d->hostWant > 1;
 }
 
 int run_group(sift_hip_detector* d);
@@ -1355,14 +1358,15 @@ int submit_host(sift_hip_detector* d, const void* img, size_t stride, int fmt, l
     const size_t inBytes = sizeof(float) * (size_t)d->inPitch * H;
     if (!L.dStage[k] && hipMalloc(&L.dStage[k], inBytes) != hipSuccess)
         return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc of the device staging failed");
-    launch_copy_rows(src, pitchB, L.dStage[k], pitchB, pitchB, H, kStageWg, d->stream);
+    unsigned req = 0;
+    unsigned* reqAt = d->dgDir.empty() ? host_request(d, 0, &req) : nullptr;
+    launch_copy_rows(src, pitchB, L.dStage[k], pitchB, pitchB, H, kStageWg, d->stream, reqAt, req);
     HIPCHK(hipEventRecord(L.evRead[k], d->stream));  // host slot k read; device slot k is stream-ordered
     L.uploads++;
     d->uploads++;
     const long long f = d->submitted;
-    int rc = run_frame(d, L.dStage[k], d->inPitch, fmt, nullptr);
-    if (rc) return rc;
-    if (d->dgDir.empty() && (rc = prefetch_results(d, f))) return rc;
+    if (int rc = run_frame(d, L.dStage[k], d->inPitch, fmt, nullptr)) return rc;
+    if (reqAt) mark_host_results(d, f);
     if (ticket) *ticket = f;
     return SIFT_HIP_OK;
 }
@@ -1382,14 +1386,16 @@ int run_group(sift_hip_detector* d) {
     if (!L.mbIn && hipMalloc((void**)&L.mbIn, fb * d->mb) != hipSuccess)
         return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc of the micro-batch input failed");
     const int fmt = d->pend[0].fmt, es = format_size(fmt);
-    bool host = false;
+    bool host[sift_hip_detector::kMaxMicroBatch] = {};
     for (int i = 0; i < n; i++) {
         const auto& p = d->pend[i];
         if (p.ordered) HIPCHK(hipStreamWaitEvent(d->stream, d->evPend[i], 0));
         if (p.hslot >= 0) {  // pinned staging: whole pitch rows over PCIe by a small grid
-            launch_copy_rows(p.img, p.stride, L.mbIn + fb * i, p.stride, p.stride, H, kStageWg, d->stream);
+            unsigned req;
+            unsigned* reqAt = host_request(d, i, &req);
+            launch_copy_rows(p.img, p.stride, L.mbIn + fb * i, p.stride, p.stride, H, kStageWg, d->stream, reqAt, req);
             HIPCHK(hipEventRecord(d->hstRead[p.hslot], d->stream));
-            host = true;
+            host[i] = reqAt != nullptr;
         } else {
             launch_copy_rows(p.img, p.stride, L.mbIn + fb * i, (size_t)es * d->inPitch, (size_t)es * W, H,
                              kGroupCopyWg, d->stream);
@@ -1398,7 +1404,9 @@ int run_group(sift_hip_detector* d) {
     d->npend = 0;
     const long long f = d->submitted;
     if (int rc = run_frame(d, L.mbIn, d->inPitch, fmt, nullptr, n, (long)fb, true)) return rc;
-    return host ? prefetch_results(d, f, n) : SIFT_HIP_OK;
+    for (int i = 0; i < n; i++)
+        if (host[i]) mark_host_results(d, f + i);
+    return SIFT_HIP_OK;
 }
 
 // Device frame (HBM-resident, fp32 or u8) -> the frame's lane; the lane waits
@@ -1783,6 +1791,7 @@ int replay_stage_body(sift_hip_detector* d, const std::string& in, const std::st
         HIPCHK(hipMemcpy(range_keys(d, 0), range.data(), sizeof(unsigned) * range.size(), hipMemcpyHostToDevice));
         c = dumped[0];
         c.final_n = (unsigned)jobs.size();
+        c.pad[1] = 0;  // no host results request (HostOut)
         HIPCHK(hipMemcpy(d->dCtr, &c, sizeof c, hipMemcpyHostToDevice));
         enqueue_descriptor(d, 0, 1);
         HIPCHK(hipStreamSynchronize(s));
@@ -2172,8 +2181,8 @@ int sift_hip_copy_to_host(sift_hip_t d, float* k3, float* f4, uint16_t* desc, in
     d->hostWant = std::max(d->hostWant, desc ? 2 : 1);
     const int region = d->cur * d->B + d->curIdx;
     if (L.hRes && L.hostFrame[region] == d->current && d->current >= d->firstFrame && (!desc || L.hostDesc[region])) {
-        // A host-input frame: its results already went to pinned host memory.
-        HIPCHK(hipEventSynchronize(L.evHost[d->cur]));
+        // A host-input frame: its descriptor kernel wrote them to pinned host memory.
+        HIPCHK(hipEventSynchronize(L.evFrame[d->cur]));
         float *hk3, *hf4;
         uint16_t* hdesc;
         host_res(d, L.hRes, region, &hk3, &hf4, &hdesc);
@@ -2203,8 +2212,8 @@ int sift_hip_copy_to_host(sift_hip_t d, float* k3, float* f4, uint16_t* desc, in
 }
 
 // The current frame's results in the handle's pinned host region (the lane's
-// region slot * B + idx): a host-input frame's were written there by its last
-// kernel (prefetch_results), any other frame's are copied there now over the
+// region slot * B + idx): a host-input frame's were written there by its
+// descriptor kernel (HostOut), any other frame's are copied there now over the
 // copy stream.  No copy into caller memory.
 int sift_hip_results_host(sift_hip_t d, const float** k3, const float** f4, const uint16_t** desc, int* count) {
     CHECK_HANDLE(d);
@@ -2220,7 +2229,7 @@ int sift_hip_results_host(sift_hip_t d, const float** k3, const float** f4, cons
     uint16_t* hdesc;
     host_res(d, L.hRes, region, &hk3, &hf4, &hdesc);
     if (L.hostFrame[region] == d->current && d->current >= d->firstFrame && (!desc || L.hostDesc[region])) {
-        HIPCHK(hipEventSynchronize(L.evHost[d->cur]));
+        HIPCHK(hipEventSynchronize(L.evFrame[d->cur]));
     } else {
         hipStream_t s;
         if (int rc = copy_stream(d, &s)) return rc;

@@ -459,6 +459,7 @@ __global__ __launch_bounds__(1024) void k_select(const OriKpt* __restrict__ kpts
     const unsigned n = oriented_count(ctr, kp);
     const int tid = threadIdx.x, lane = tid & 63;
     for (int i = tid; i < 2 * kRangeSlots; i += 1024) zero_range[i] = 0u;  // next frame's range keys
+    if (tid == 0) ctr->pad[1] >>= kHostReqShift;  // host results request -> level (HostOut)
     if (kp.numFeatures <= 0 || n <= (unsigned)kp.numFeatures) {
         if (tid == 0) ctr->thr_bits = 0u;
         return;
@@ -628,6 +629,7 @@ __global__ __launch_bounds__(1024) void k_order(PyrDesc pyr, const OriKpt* __res
     const int nb = kp.numBuckets;
     for (int i = tid; i < 2 * kRangeSlots; i += 1024) zero_range[i] = 0u;  // next frame's range keys
     for (int i = tid; i < nb; i += 1024) s_bucket[i] = 0u;
+    if (tid == 0) ctr->pad[1] >>= kHostReqShift;  // host results request -> level (HostOut)
     if (tid < kLptSegs) s_seg[tid] = 0u;
     if (tid == 0) {
         s_prefix = 0;
@@ -937,36 +939,6 @@ void launch_bucket_rank(const PyrDesc& pyr, const OriKpt* kpts, unsigned* bcount
 }
 
 // ---------------------------------------------------------------------------
-// Results of a host-input frame copied into mapped pinned host memory right
-// after the frame (sift_hip_submit, when the caller copies its results to the
-// host): copyToHost then reads host memory instead of a pageable
-// device-to-host copy (Detector.cu:606-634 copies after the frame,
-// synchronously).  n = min(final_n, cap) rows, the count read on the device;
-// 16-byte stores where the layouts allow; hdesc null: keypoints only.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_results_to_host(const float* __restrict__ k3, const float* __restrict__ f4,
-                                                         const uint16_t* __restrict__ desc,
-                                                         const Counters* __restrict__ ctr, unsigned cap,
-                                                         float* __restrict__ hk3, float* __restrict__ hf4,
-                                                         uint16_t* __restrict__ hdesc) {
-    const unsigned n = min(ctr->final_n, cap);
-    const unsigned tid = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
-    const uint4* __restrict__ sd = reinterpret_cast<const uint4*>(desc);
-    uint4* __restrict__ dd = reinterpret_cast<uint4*>(hdesc);
-    if (hdesc)
-        for (unsigned i = tid; i < n * 16; i += nt) dd[i] = sd[i];
-    const float4* __restrict__ sf = reinterpret_cast<const float4*>(f4);
-    float4* __restrict__ df = reinterpret_cast<float4*>(hf4);
-    for (unsigned i = tid; i < n; i += nt) df[i] = sf[i];
-    for (unsigned i = tid; i < n * 3; i += nt) hk3[i] = k3[i];
-}
-
-void launch_results_to_host(const float* k3, const float* f4, const uint16_t* desc, const Counters* ctr, unsigned cap,
-                            float* hk3, float* hf4, uint16_t* hdesc, hipStream_t s) {
-    hipLaunchKernelGGL(k_results_to_host, dim3(128), dim3(256), 0, s, k3, f4, desc, ctr, cap, hk3, hf4, hdesc);
-}
-
-// ---------------------------------------------------------------------------
 // Frame rows copied by a small grid on the frame's lane stream: a host-input
 // frame's staging (mapped pinned host memory) into device memory before the
 // frame's first kernel, and a micro-batch's frames into the lane's group
@@ -976,12 +948,16 @@ void launch_results_to_host(const float* k3, const float* f4, const uint16_t* de
 // workgroup for it and slowed the other lanes;
 // a runtime 2-D copy of a device frame took a slow path (0.165 vs 0.093
 // ms/frame for f32 vs u8 micro-batches).  16-byte units when the rows and
-// pitches allow, bytes otherwise.
+// pitches allow, bytes otherwise.  `flag` (nullable): thread 0 of
+// workgroup 0 stores flag_val there (a host frame's results request in its
+// Counters, HostOut).
 // ---------------------------------------------------------------------------
 constexpr int kStageUnroll = 4;
 __global__ __launch_bounds__(256) void k_copy_rows16(const char* __restrict__ src, size_t spitch, char* __restrict__ dst,
-                                                     size_t dpitch, unsigned row16, unsigned n16) {
+                                                     size_t dpitch, unsigned row16, unsigned n16,
+                                                     unsigned* __restrict__ flag, unsigned flag_val) {
     const unsigned nt = gridDim.x * blockDim.x;
+    if (flag && blockIdx.x == 0 && threadIdx.x == 0) *flag = flag_val;
     auto at = [&](unsigned i, size_t pitch) { return (size_t)(i / row16) * pitch + (size_t)(i % row16) * 16; };
     unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
     for (; i + (kStageUnroll - 1) * nt < n16; i += kStageUnroll * nt) {
@@ -995,20 +971,21 @@ __global__ __launch_bounds__(256) void k_copy_rows16(const char* __restrict__ sr
 }
 __global__ __launch_bounds__(256) void k_copy_rows1(const unsigned char* __restrict__ src, size_t spitch,
                                                     unsigned char* __restrict__ dst, size_t dpitch, unsigned rowB,
-                                                    unsigned n) {
+                                                    unsigned n, unsigned* __restrict__ flag, unsigned flag_val) {
+    if (flag && blockIdx.x == 0 && threadIdx.x == 0) *flag = flag_val;
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
         dst[(size_t)(i / rowB) * dpitch + i % rowB] = src[(size_t)(i / rowB) * spitch + i % rowB];
 }
 
 void launch_copy_rows(const void* src, size_t spitch, void* dst, size_t dpitch, size_t rowB, int rows, int wgs,
-                      hipStream_t s) {
+                      hipStream_t s, unsigned* flag, unsigned flag_val) {
     const bool v16 = ((uintptr_t)src | (uintptr_t)dst | spitch | dpitch | rowB) % 16 == 0;
     if (v16)
         hipLaunchKernelGGL(k_copy_rows16, dim3(wgs), dim3(256), 0, s, static_cast<const char*>(src), spitch,
-                           static_cast<char*>(dst), dpitch, (unsigned)(rowB / 16), (unsigned)(rowB / 16 * rows));
+                           static_cast<char*>(dst), dpitch, (unsigned)(rowB / 16), (unsigned)(rowB / 16 * rows), flag, flag_val);
     else
         hipLaunchKernelGGL(k_copy_rows1, dim3(wgs), dim3(256), 0, s, static_cast<const unsigned char*>(src), spitch,
-                           static_cast<unsigned char*>(dst), dpitch, (unsigned)rowB, (unsigned)(rowB * rows));
+                           static_cast<unsigned char*>(dst), dpitch, (unsigned)rowB, (unsigned)(rowB * rows), flag, flag_val);
 }
 
 }  // namespace sift_amd

@@ -188,7 +188,11 @@ __device__ __forceinline__ void blur_tile(const BlurJob& J, int blk, float* __re
     const int x0 = (tile % J.tilesX) * BLUR_TW, y0 = (tile / J.tilesX) * BLUR_TH;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // The frame's first blur also zeroes the frame counters (no memset node).
-    if (zero_ctr && tile == 0 && tid < (int)(sizeof(Counters) / 4)) reinterpret_cast<unsigned*>(zero_ctr)[tid] = 0u;
+    // (Counters.pad[1] keeps its host-results request half: set by a host
+    // frame's staging copy before this kernel, HostOut.)
+    if (zero_ctr && tile == 0 && tid < (int)(sizeof(Counters) / 4))
+        reinterpret_cast<unsigned*>(zero_ctr)[tid] =
+            tid == offsetof(Counters, pad[1]) / 4 ? zero_ctr->pad[1] & ~((1u << kHostReqShift) - 1) : 0u;
 
     // Stage the input tile row by row: wave w takes rows w, w+4, ...; lane l
     // columns l and 64+l.  A row's source offset is wave-uniform (SGPR,

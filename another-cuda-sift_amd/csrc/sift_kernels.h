@@ -75,7 +75,7 @@ struct Counters {
     unsigned final_n;    // after retainBest (written by the bucket scan)
     unsigned overflow;   // bit 0 cand, 1 refined, 2 oriented, 3 final
     unsigned thr_bits;   // retainBest response threshold (float bits)
-    unsigned pad[2];     // pad[0]: entries of the order list (k_order path)
+    unsigned pad[2];     // pad[0]: entries of the order list (k_order path); pad[1]: host results (HostOut)
 };
 
 // Oriented keypoint list: refined keypoint k's first peak sits in slot k (no
@@ -225,15 +225,15 @@ void launch_rank_final(const PyrDesc& pyr, const OriKpt* kpts, const unsigned* b
                        const int* order, const Counters* ctr, const JobOrder* jord, DescJob* jobs, float* kpts3, float* feats4,
                        const KeypointParams& kp, const Frames& fr, hipStream_t s);
 // Results of a finished frame -> mapped pinned host buffers (host-input frames).
-void launch_results_to_host(const float* k3, const float* f4, const uint16_t* desc, const Counters* ctr, unsigned cap,
-                            float* hk3, float* hf4, uint16_t* hdesc, hipStream_t s);
 // Frame rows (rowB bytes, `rows` of them, pitches in bytes) copied by `wgs`
 // 256-thread workgroups on the lane stream: host staging -> device, and
 // micro-batch frames -> the group input (keypoints.hip).
 constexpr int kStageWg = 64;      // host staging (PCIe-bound)
 constexpr int kGroupCopyWg = 512; // device-to-device (HBM)
+// flag (nullable): a word set to flag_val by the copy (a host frame's
+// results request, Counters.pad[1]).
 void launch_copy_rows(const void* src, size_t spitch, void* dst, size_t dpitch, size_t rowB, int rows, int wgs,
-                      hipStream_t s);
+                      hipStream_t s, unsigned* flag = nullptr, unsigned flag_val = 0);
 void launch_bucket_rank(const PyrDesc& pyr, const OriKpt* kpts, unsigned* bcount, const unsigned* boff,
                         const int* order, const Counters* ctr, DescJob* jobs, float* kpts3, float* feats4,
                         const KeypointParams& kp, const Frames& fr, hipStream_t s);
@@ -248,8 +248,24 @@ struct Sidecar {
     int8_t* codes;
     int* keys;
 };
+// Host results written by the descriptor kernel itself (host-input frames of a
+// handle whose caller reads results back): Counters.pad[1] carries the
+// request -- high half set by the frame's staging copy (kHostReqShift), moved
+// into the low half (the level: 1 keypoints + features, 2 also descriptors)
+// by k_order / k_select, which clear the request; the frame's first blur keeps
+// only the request half.  tab[frame] = the frame's pinned host region (null:
+// none), laid out as the detector's host results (k3 | f4 at 256-aligned
+// 12 cap | descriptors at + 16 cap); k3 / f4 = the slot's device results.
+constexpr int kHostReqShift = 16;
+struct HostOut {
+    char* const* tab;
+    const float* k3;
+    const float* f4;
+    unsigned cap;
+};
 void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned* range_keys, uint16_t* desc,
-                       Sidecar side, Counters* host_ctr, const KeypointParams& kp, const Frames& fr, hipStream_t s);
+                       Sidecar side, Counters* host_ctr, HostOut host, const KeypointParams& kp, const Frames& fr,
+                       hipStream_t s);
 
 // Order-preserving unsigned key of a float (0 is below every key), so that
 // atomicMax over keys is a float max with a zeroed counter as the identity.
