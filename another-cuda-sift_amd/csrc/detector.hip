@@ -401,9 +401,10 @@ struct sift_hip_detector {
     bool useGraph = true;
 
     CopyPool* pool = nullptr;  // staging copies of large host frames (created at the first one)
-    // What the caller's last sift_hip_copy_to_host took (0 nothing yet, 1
-    // keypoints, 2 keypoints + descriptors): host-input frames prefetch that
-    // much to pinned host memory (a caller that never copies back pays nothing).
+    // The most the caller's sift_hip_copy_to_host / sift_hip_results_host
+    // calls took (0 nothing yet, 1 keypoints, 2 keypoints + descriptors):
+    // host-input frames have their descriptor kernel write that much to
+    // pinned host memory (HostOut; a caller that never reads back pays nothing).
     int hostWant = 0;
 
     // Stage dumps (sift_hip_set_datagen): directory, and a device copy of the
