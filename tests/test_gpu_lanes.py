@@ -188,6 +188,34 @@ def test_results_host_views_equal_sync(sift, mb, lanes, depth):
     assert_identical(view_results(det0), ref[0])  # first call on a handle (regions allocated by it)
 
 
+@pytest.mark.parametrize("kw,mb", [({"upscale": True}, 2), ({"exact_descriptors": True}, 3),
+                                   ({"upscale": True, "exact_descriptors": True}, 1)])
+def test_host_rows_other_heads_and_exact_kernel(sift, kw, mb):
+    """The host rows written by the descriptor kernel (HostOut) on the other
+    paths that carry the request: a doubled base (the request crosses the
+    upsample head and survives the body's first blur) and the exact
+    descriptor kernel; results_host and copyToHost both equal the sync path."""
+    w, h = 320, 240
+    frames = [sift.synth_frame(170 + i, w, h) for i in range(7)]
+    _, ref_det = make_detector(sift, w, h, numFeatures=1500, lanes=1, **kw)
+    ref = []
+    for f in frames:
+        ref_det.detectAndCompute(f)
+        ref.append(results(ref_det))
+    _, det = make_detector(sift, w, h, numFeatures=1500, lanes=2, micro_batch=mb, **kw)
+    queue, i = [], 0
+    for s in range(len(frames)):
+        queue.append(det.submit(frames[s].astype(np.uint8) if s % 2 else frames[s]))
+        if len(queue) == 3:
+            det.wait(queue.pop(0))
+            assert_identical(view_results(det) if i % 2 else results(det), ref[i])
+            i += 1
+    while queue:
+        det.wait(queue.pop(0))
+        assert_identical(view_results(det), ref[i])
+        i += 1
+
+
 def test_micro_batch_limits(sift):
     img = torch.from_numpy(sift.synth_frame(1, 128, 96)).cuda()
     torch.cuda.synchronize()
