@@ -737,9 +737,13 @@ def main():
 
         def pipelined(submit, fetch):
             # The first `warm` frames (the same loop) create and warm the lanes,
-            # their staging and results regions; then nh frames are timed.
+            # their staging and results regions; then npipe frames are timed
+            # (at least 8 x the frames in flight, so the pipeline's fill and
+            # drain stay a small part of the run).  Returns the time of nh
+            # frames at the measured rate (the legs below divide by nh).
             tickets, warm = [], max(3 * PIPE_DEPTH, 24)
-            for s in range(nh + warm):
+            npipe = max(nh, 8 * PIPE_DEPTH)
+            for s in range(npipe + warm):
                 if s == warm:
                     while tickets:
                         detp.wait(tickets.pop(0))
@@ -755,7 +759,7 @@ def main():
                 detp.wait(tickets.pop(0))
                 if fetch:
                     fetch()
-            return max_over_ranks(time.perf_counter() - t)
+            return max_over_ranks(time.perf_counter() - t) * nh / npipe
 
         t_pipe = pipelined(lambda s: detp.submit(host_u8[s % nframes]), copy_out)
         dev_u8 = [torch.from_numpy(f).to(dev) for f in host_u8]
@@ -773,7 +777,10 @@ def main():
         del detp
         # The same loop on a micro-batching handle (sift_hip_set_micro_batch):
         # submitted frames run MB at a time as one launch group per lane.
-        MB_LANES, MB, MB_DEPTH = 3, 4, 12  # (2 lanes x 8 in flight: 0.0998 ms/frame, 3 x 12: 0.0942; 2-frame groups 0.110)
+        # (device frames: 2 lanes x 8 in flight 0.0998 ms/frame, 3 x 12 in 4-frame groups 0.0942, 2-frame
+        # groups 0.110; host frames read back with views, C++ loop: 4-frame groups x 12 in flight 0.129-0.143,
+        # 8-frame groups x 24 0.113-0.119, 12-frame 0.126, 4 lanes x 16 0.140; profiles/round5/host_mb8.jsonl)
+        MB_LANES, MB, MB_DEPTH = 3, 8, 24
         detp = sift.Detector(cfg, device=local, lanes=MB_LANES, micro_batch=MB)
         detp.gpuWarmUpAndAllocate()
         PIPE_DEPTH_SAVED, PIPE_DEPTH = PIPE_DEPTH, MB_DEPTH
@@ -803,8 +810,8 @@ def main():
                 "f32": {"value": round(world * nh * W * H / 1e6 / t_mb, 2), "ms_per_frame": round(t_mb / nh * 1e3, 4)},
                 "u8": {"value": round(world * nh * W * H / 1e6 / t_mb8, 2), "ms_per_frame": round(t_mb8 / nh * 1e3, 4)},
                 "lanes": MB_LANES, "frames_per_group": MB, "in_flight": MB_DEPTH,
-                "note": "the same submitDevice/wait loop on a handle with sift_hip_set_micro_batch(4): frames run as "
-                        "4-frame launch groups (per-frame results identical, tests/test_gpu_lanes.py)"},
+                "note": f"the same submitDevice/wait loop on a handle with sift_hip_set_micro_batch({MB}): frames run as "
+                        f"{MB}-frame launch groups (per-frame results identical, tests/test_gpu_lanes.py)"},
         }
         del detp, dev_u8
         return host_input, device_submit

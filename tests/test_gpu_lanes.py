@@ -146,7 +146,7 @@ def view_results(det):
     return k3, f4, d.view(np.uint16)
 
 
-@pytest.mark.parametrize("mb,lanes,depth", [(1, 3, 6), (4, 3, 12), (3, 2, 4)])
+@pytest.mark.parametrize("mb,lanes,depth", [(1, 3, 6), (4, 3, 12), (3, 2, 4), (8, 3, 24)])
 def test_results_host_views_equal_sync(sift, mb, lanes, depth):
     """sift_hip_results_host: the current frame's rows as views of the handle's
     pinned results (no copy into caller memory) equal the synchronous path's
