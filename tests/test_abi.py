@@ -116,6 +116,8 @@ def test_invalid_arguments_fail_with_status(sift):
     assert L.sift_hip_create(ctypes.byref(c), 0, ctypes.byref(h)) == -1
     assert L.sift_hip_create(None, 0, ctypes.byref(h)) == -1
     assert L.sift_hip_destroy(None) == 0  # like free(NULL): a no-op
+    k3 = ctypes.c_void_p()
+    assert L.sift_hip_results_host(None, ctypes.byref(k3), None, None, None) != 0  # null handle: a status, no crash
 
 
 def test_no_gpu_fails_loudly(sift):
