@@ -244,6 +244,16 @@ struct Lane {
     hipGraphExec_t execH[kResultSlots] = {}, execH1[kResultSlots] = {};
     hipGraph_t graphH[kResultSlots] = {}, graphH1[kResultSlots] = {};
     hipGraphNode_t headH[kResultSlots] = {}, headH1[kResultSlots] = {};
+    // The input each exec's head node reads now (image, pitch, frame stride;
+    // [slot][0]: execH, [1]: execH1): a frame from the same buffer as that
+    // exec's last one launches without re-pointing the node.
+    struct HeadIn {
+        const void* img = nullptr;
+        int pitch = 0;
+        long sfs = 0;
+        bool operator==(const HeadIn& o) const { return img == o.img && pitch == o.pitch && sfs == o.sfs; }
+    };
+    HeadIn headIn[kResultSlots][2];
     int nfOf[kResultSlots] = {};  // frames of the launch group that wrote each slot
     long long slotFrame[kResultSlots] = {-1, -1, -1, -1};  // the (first) frame whose results each slot holds
     int slotNum[kResultSlots] = {};  // frame numbers in that slot (> 1: a micro-batch, frame slotFrame + i in arena i)
@@ -1039,9 +1049,11 @@ int build_graphs(sift_hip_detector* d) {
     for (int b = 0; b < d->kSlots; b++) {
         if (int rc = capture(d, b, d->B, &L.exec[b])) return rc;
         if (int rc = capture_with_head(d, b, d->B, &L.execH[b], &L.graphH[b], &L.headH[b])) return rc;
+        L.headIn[b][0] = Lane::HeadIn{d->dInput, d->inPitch, d->afs};
         if (d->B > 1) {
             if (int rc = capture(d, b, 1, &L.exec1[b])) return rc;
             if (int rc = capture_with_head(d, b, 1, &L.execH1[b], &L.graphH1[b], &L.headH1[b])) return rc;
+            L.headIn[b][1] = Lane::HeadIn{d->dInput, d->inPitch, d->afs};
         }
     }
     return SIFT_HIP_OK;
@@ -1137,9 +1149,14 @@ int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEven
     // frame takes the separate head launch and the plain exec.
     if (gh && !event_done(L.evFrame[slot])) gh = nullptr;
     if (gh) {  // device f32 input: one launch for the whole frame, the head re-pointed at img
-        HeadNode& h = d->headNode;
-        head_node(d, h, static_cast<const float*>(img), pitch, slot & 1, nf, sfs);
-        HIPCHK(hipGraphExecKernelNodeSetParams(gh, nf == d->B ? L.headH[slot] : L.headH1[slot], &h.p));
+        const Lane::HeadIn in{img, pitch, sfs};
+        Lane::HeadIn& cur = L.headIn[slot][nf == d->B ? 0 : 1];
+        if (!(cur == in)) {
+            HeadNode& h = d->headNode;
+            head_node(d, h, static_cast<const float*>(img), pitch, slot & 1, nf, sfs);
+            HIPCHK(hipGraphExecKernelNodeSetParams(gh, nf == d->B ? L.headH[slot] : L.headH1[slot], &h.p));
+            cur = in;
+        }
         HIPCHK(hipGraphLaunch(gh, d->stream));
     } else {
         enqueue_head(d, img, pitch, fmt, slot & 1, nf, sfs);
