@@ -779,7 +779,8 @@ def main():
         # submitted frames run MB at a time as one launch group per lane.
         # (device frames: 2 lanes x 8 in flight 0.0998 ms/frame, 3 x 12 in 4-frame groups 0.0942, 2-frame
         # groups 0.110; host frames read back with views, C++ loop: 4-frame groups x 12 in flight 0.129-0.143,
-        # 8-frame groups x 24 0.113-0.119, 12-frame 0.126, 4 lanes x 16 0.140; profiles/round5/host_mb8.jsonl)
+        # 8-frame groups x 24 0.112-0.119, 12-frame 0.126-0.129, 16-frame x 48 0.113, 4 lanes x 16 0.140;
+        # profiles/round5/host_mb8.jsonl, host_mb16.jsonl)
         MB_LANES, MB, MB_DEPTH = 3, 8, 24
         detp = sift.Detector(cfg, device=local, lanes=MB_LANES, micro_batch=MB)
         detp.gpuWarmUpAndAllocate()
