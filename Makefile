@@ -20,13 +20,13 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
             $(if $(strip $(EXTRA_HIPFLAGS)),-DSIFT_AB_FLAGS='"$(strip $(EXTRA_HIPFLAGS))"')
 CXXFLAGS := -O2 -std=c++17 -fPIC -Iinclude -Wall -Wextra
 
-HIP_SRCS := $(SRC)/detector.hip $(SRC)/pyramid.hip $(SRC)/keypoints.hip $(SRC)/descriptor.hip $(SRC)/match.hip \
+HIP_SRCS := $(SRC)/detector.hip $(SRC)/lanes.hip $(SRC)/datagen.hip $(SRC)/matcher_api.hip $(SRC)/pyramid.hip $(SRC)/keypoints.hip $(SRC)/descriptor.hip $(SRC)/match.hip \
             $(SRC)/multi.hip
 HIP_OBJS := $(patsubst $(SRC)/%.hip,$(OUT)/obj/%.o,$(HIP_SRCS)) $(OUT)/obj/synth_frame.o
 
 all: $(OUT)/libsift_hip.so $(OUT)/libsift_cuda.so tools
 
-$(OUT)/obj/%.o: $(SRC)/%.hip $(SRC)/sift_kernels.h $(SRC)/sift_math.h $(SRC)/sift_match.h $(SRC)/sift_refine.h include/sift_hip.h
+$(OUT)/obj/%.o: $(SRC)/%.hip $(SRC)/detector_state.h $(SRC)/sift_kernels.h $(SRC)/sift_math.h $(SRC)/sift_match.h $(SRC)/sift_refine.h include/sift_hip.h
 	@mkdir -p $(OUT)/obj
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -913,14 +913,390 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
     }
 }
 
+// ---------------------------------------------------------------------------
+// Exact mode, packed owner runs (round 6).  Same owners and the same
+// per-bin raster order as k_descriptor_exact above, but a chunk's hits are
+// pushed to their owners instead of pulled: each owner lane (cell, pair g)
+// counts its hits (popcount of its ballot mask), a wave scan of the counts
+// gives every owner a contiguous run in LDS, and each sample writes, for every
+// owner it touches, the two floats that owner adds at position run start +
+// rank, rank = the number of earlier samples of the chunk in the owner's mask
+// (v_mbcnt).  The walk is then a straight read of the owner's run, four
+// entries per step with no bit scans, record decoding or selects; its length
+// is still the busiest owner's hit count (a 64-sample chunk is a thin band of
+// the window), but each hit costs ~2.5 instructions instead of ~15.
+//   * owners: lane = (cell 0..15, orientation pair g 0..3) adds bins 2g, 2g+1;
+//     bin 8 (o0 = 7's upper bin) has its own run per cell (row g = 4), walked
+//     by the cell's g = 0 lane into its third accumulator;
+//   * entries are float2 {into bin 2g, into bin 2g + 1}: even o0 writes
+//     (v_o0, v_o0+1) to pair o0 / 2; odd o0 writes (+0, v_o0) to pair
+//     (o0 - 1) / 2 and (v_o0+1, +0) to pair (o0 + 1) / 2 (bin 8's run for
+//     o0 = 7, whose walk reads the x halves only).  Runs are padded to four
+//     entries with zeros; every contribution is >= +0, so x + 0 = x exactly;
+//   * a sample's targets outside the 4x4 interior read a null row (mask 0,
+//     start = a trash entry).
+// ---------------------------------------------------------------------------
+#ifndef SIFT_DBG_BFI
+#define SIFT_DBG_BFI 0
+#endif
+#ifndef SIFT_DBG_DPP
+#define SIFT_DBG_DPP 0
+#endif
+#ifndef SIFT_DBG_PADS
+#define SIFT_DBG_PADS 0
+#endif
+constexpr int kRunRows = 16 * 5;               // (cell, g): g = 0..3 pairs, g = 4 bin 8
+constexpr int kNullRow = kRunRows;             // invalid targets
+constexpr int kPoolEntries = 64 * 8 + 80 * 3;  // <= 8 entries per sample + padding of 80 runs to multiples of 4
+constexpr int kTrash = kPoolEntries;           // 4 entries: invalid targets, and the zeroing of empty runs
+// Bitfield select d = (sel & s) | (~sel & v) with the SGPR operand in place:
+// one v_bfi_b32 (the compiler's form of the pick moved every ballot half to a
+// VGPR and used two instructions per step).
+__device__ __forceinline__ unsigned bfi_sv(unsigned sel, unsigned s, unsigned v) {
+    unsigned d;
+    asm volatile("v_bfi_b32 %0, %1, %2, %3" : "=v"(d) : "v"(sel), "s"(s), "v"(v));
+    return d;
+}
+// Inclusive wave prefix sum with the DPP row shifts / broadcasts applied to
+// the adds themselves (no zero-initialised copies): wave_incl_scan's result.
+// Rows outside row_mask are not written and keep their sum.
+__device__ __forceinline__ int wave_incl_scan_dpp(int x) {
+    asm volatile(
+        "s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"
+        "s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+        "s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+        "s_nop 1"
+        : "+v"(x));
+    return x;
+}
+__global__ __launch_bounds__(kExactWG) void k_descriptor_exact_runs(const DescJob* __restrict__ jobs,
+                                                                    const Counters* __restrict__ ctr,
+                                                                    uint16_t* __restrict__ desc, Sidecar sidecar,
+                                                                    Counters* __restrict__ host_ctr, HostOut host,
+                                                                    long fs, unsigned nf) {
+    __shared__ float s_tab[64];
+    __shared__ __attribute__((aligned(16))) float2 s_pool[kExactWaves][kPoolEntries + 4];  // + the trash entries
+    __shared__ __attribute__((aligned(16))) uint4 s_tbl[kExactWaves][kRunRows + 1];        // {mask lo, hi, start, -}
+    __shared__ unsigned short s_rowpre[kExactWaves][kMaxRows + 1];
+    __shared__ signed char s_rowlo[kExactWaves][kMaxRows];
+    __shared__ float s_nrm[kExactWaves][12];
+
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float2* pool = s_pool[w];
+    uint4* tbl = s_tbl[w];
+    unsigned short* rowpre = s_rowpre[w];
+    signed char* rowlo = s_rowlo[w];
+    float* raw = reinterpret_cast<float*>(pool);     // after the chunk loop
+    float* s_norm = s_nrm[w];
+    int* rowmap = reinterpret_cast<int*>(pool);      // inside fetch(), before a chunk's runs are written
+    const unsigned frame = blockIdx.x % nf, wg = blockIdx.x / nf, nwg = gridDim.x / nf;
+    const long foff = frame * fs;
+    jobs = fptr(jobs, foff);
+    ctr = fptr(ctr, foff);
+    desc = fptr(desc, foff);
+    sidecar.codes = fptr(sidecar.codes, foff);
+    sidecar.keys = fptr(sidecar.keys, foff);
+    host_ctr += frame;
+    const unsigned n = ctr->final_n;
+    static_assert(sizeof(Counters) <= 4 * kExactWG, "counters handed over by one workgroup");
+    if (wg == 0 && threadIdx.x < sizeof(Counters) / 4)
+        reinterpret_cast<unsigned*>(host_ctr)[threadIdx.x] = reinterpret_cast<const unsigned*>(ctr)[threadIdx.x];
+    if (wg * kExactWaves >= n) return;  // workgroup-uniform
+    if (w == 0) s_tab[lane] = c_desc_exptab[lane];
+    if (lane == 0) tbl[kNullRow] = make_uint4(0u, 0u, (unsigned)kTrash, 0u);
+    lds_barrier();
+    const float bins_per_rad = kN / 360.f;
+    const float exp_scale = -1.f / (kD * kD * 0.5f);
+    // This lane's bins: interior cell (ci, cj), orientations 2g and 2g + 1.
+    const int cell = lane >> 2, g = lane & 3, ci = cell >> 2, cj = cell & 3;
+
+    for (unsigned p = wg * kExactWaves + w; p < n; p += nwg * kExactWaves) {
+        JobWords jwd;
+        const unsigned* __restrict__ jw = reinterpret_cast<const unsigned*>(jobs + p);
+#pragma unroll
+        for (int q = 0; q < 16; q++) jwd.w[q >> 2][q & 3] = __builtin_amdgcn_readfirstlane(jw[q]);
+        const DescJob jb = __builtin_bit_cast(DescJob, jwd);
+        DescGeom G;
+        G.cos_t = jb.cos_t;
+        G.sin_t = jb.sin_t;
+        G.exp_scale = exp_scale;
+        G.ptx = jb.ptx;
+        G.pty = jb.pty;
+        G.rows = jb.rows;
+        G.cols = jb.cols;
+        const int radius = jb.radius, side = 2 * radius + 1;
+        const bool enumerated = side <= kMaxRows;
+        const __amdgpu_buffer_rsrc_t rsrc =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(jb.img), 0, jb.rows * jb.pitch * 4, 0x00020000);
+        int N;
+        if (enumerated) {
+            const float inv_sin = __builtin_amdgcn_rcpf(G.sin_t), inv_cos = __builtin_amdgcn_rcpf(G.cos_t);
+            int len2[2];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int t = 2 * lane + h, i = t - radius, r = G.pty + i;
+                int lo = max(-radius, 1 - G.ptx), hi = min(radius, G.cols - 2 - G.ptx);
+                if (r <= 0 || r >= G.rows - 1 || t >= side) hi = lo - 1;
+                clip_interval(lo, hi, G.sin_t, inv_sin, (float)i * G.cos_t + (kD / 2 - 0.5f), radius);
+                clip_interval(lo, hi, G.cos_t, inv_cos, -(float)i * G.sin_t + (kD / 2 - 0.5f), radius);
+                len2[h] = max(hi - lo + 1, 0);
+                if (t < side) rowlo[t] = lo;
+            }
+            const int sum = wave_incl_scan(len2[0] + len2[1]);
+            if (2 * lane + 1 <= side) rowpre[2 * lane + 1] = sum - len2[1];
+            if (2 * lane + 2 <= side) rowpre[2 * lane + 2] = sum;
+            if (lane == 0) rowpre[0] = 0;
+            N = __builtin_amdgcn_readlane(sum, 63);
+        } else {
+            N = side * side;  // huge window: the full raster, the oracle's test per sample
+        }
+        wave_lds_sync();
+
+        auto row_search = [&](int k) {
+            int lo = 0, hi = side - 1;  // last row with rowpre[row] <= k
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (rowpre[mid] <= k) lo = mid;
+                else hi = mid - 1;
+            }
+            return lo;
+        };
+        auto gload = [&](unsigned o) {
+            return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o, 0, 0));
+        };
+        const unsigned pitch4 = 4u * jb.pitch;
+        struct Fetch {
+            int i, j;
+            float l, r, u, d;
+        };
+        // As k_descriptor_exact's fetch: gradient loads two chunks ahead, rows
+        // of a chunk by a ds_max scatter of row starts + a DPP prefix maximum.
+        int frb = N > 0 ? __builtin_amdgcn_readfirstlane(enumerated ? row_search(0) : 0) : 0;
+        auto fetch = [&](int kf) {
+            Fetch f;
+            if (enumerated) {
+                int row;
+                const bool covered = rowpre[min(frb + 65, side)] >= min(kf + 64, N);  // uniform
+                if (covered) {
+                    rowmap[lane] = frb;
+                    wave_lds_sync();
+                    const int r = frb + 1 + lane;
+                    if (r < side) {
+                        const int st = rowpre[r] - kf;
+                        if (st >= 0 && st < 64) atomicMax(&rowmap[st], r);
+                    }
+                    wave_lds_sync();
+                    row = wave_incl_max(rowmap[lane]);
+                    wave_lds_sync();
+                } else {
+                    row = row_search(min(kf + lane, N - 1));
+                }
+                frb = __builtin_amdgcn_readlane(row, 63);
+                f.i = row - radius;
+                f.j = rowlo[row] + (kf + lane - rowpre[row]);
+            } else {
+                const int k = min(kf + lane, N - 1);
+                f.i = k / side - radius;
+                f.j = k % side - radius;
+            }
+            const unsigned o = (unsigned)((G.pty + f.i) * jb.pitch + G.ptx + f.j) * 4u;
+            f.l = gload(o - 4u);
+            f.r = gload(o + 4u);
+            f.u = gload(o - pitch4);
+            f.d = gload(o + pitch4);
+            return f;
+        };
+        Fetch f1 = fetch(0), f2 = fetch(64);
+        unsigned sel_ci[kD], sel_cj[kD], sel_g[kD];  // all ones where this lane's index is q
+#pragma unroll
+        for (int q = 0; q < kD; q++) {
+            sel_ci[q] = ci == q ? ~0u : 0u;
+            sel_cj[q] = cj == q ? ~0u : 0u;
+            sel_g[q] = g == q ? ~0u : 0u;
+        }
+        float accA = 0.f, accB = 0.f, accW = 0.f;  // bins 2g, 2g + 1, and 8 (g = 0)
+        for (int k0 = 0; k0 < N; k0 += 64) {
+            // ---- sample k0 + lane: the oracle's math (as k_descriptor_exact) ----
+            const int i = f1.i, j = f1.j;
+            const float l = f1.l, r = f1.r, u = f1.u, d = f1.d;
+            f1 = f2;
+            f2 = fetch(k0 + 128);
+            float rbin, cbin, c_rot, r_rot;
+            const bool valid = desc_sample(G, i, j, rbin, cbin, c_rot, r_rot) && k0 + lane < N;
+            const float dx = r - l, dy = u - d;
+            const float wgt = cv_exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, s_tab);
+            const float gori = cv_fast_atan2(dy, dx);
+            const float gmag = cv_magnitude(dx, dy);
+            float obin = (gori - jb.angle) * bins_per_rad;
+            const float mag = gmag * wgt;
+            const int r0 = cv_floor(rbin), c0 = cv_floor(cbin);
+            int o0 = cv_floor(obin);
+            rbin -= (float)r0;
+            cbin -= (float)c0;
+            obin -= (float)o0;
+            if (o0 < 0) o0 += kN;
+            if (o0 >= kN) o0 -= kN;
+            float v[8];
+            trilinear(mag, rbin, cbin, obin, v);
+            // ---- owners: masks, counts, runs ----
+            // Samples touching interior cell row / column q (r0 in {q - 1, q}),
+            // orientation pair q (o0 in {2q - 1, 2q, 2q + 1}; pair 0 without
+            // o0 = 7, whose upper bin is bin 8) and bin 8 (o0 = 7).
+            const int r0v = valid ? r0 : 64;
+            unsigned long long RR[kD], CC[kD], OO[kD];
+#pragma unroll
+            for (int q = 0; q < kD; q++) {
+                RR[q] = __builtin_amdgcn_ballot_w64((unsigned)(r0v - q + 1) < 2u);
+                CC[q] = __builtin_amdgcn_ballot_w64((unsigned)(c0 - q + 1) < 2u);
+                OO[q] = __builtin_amdgcn_ballot_w64(q == 0 ? (unsigned)o0 < 2u : (unsigned)(o0 - 2 * q + 1) < 3u);
+            }
+            const unsigned long long O7 = __builtin_amdgcn_ballot_w64(o0 == kN - 1);
+            auto pick = [](const unsigned long long (&X)[kD], const unsigned (&sel)[kD]) {
+                unsigned lo = (unsigned)X[0], hi = (unsigned)(X[0] >> 32);
+#pragma unroll
+                for (int q = 1; q < kD; q++) {
+#if SIFT_DBG_BFI
+                    lo = bfi_sv(sel[q], (unsigned)X[q], lo);
+                    hi = bfi_sv(sel[q], (unsigned)(X[q] >> 32), hi);
+#else
+                    lo = ((unsigned)X[q] & sel[q]) | (lo & ~sel[q]);
+                    hi = ((unsigned)(X[q] >> 32) & sel[q]) | (hi & ~sel[q]);
+#endif
+                }
+                return (unsigned long long)hi << 32 | lo;
+            };
+            const unsigned long long RC = pick(RR, sel_ci) & pick(CC, sel_cj);
+            const unsigned long long M = RC & pick(OO, sel_g);
+            const unsigned long long Mw = g == 0 ? RC & O7 : 0ull;
+            const int cnt = __builtin_popcountll(M), cntw = __builtin_popcountll(Mw);
+            const int c4 = (cnt + 3) & ~3, w4 = (cntw + 3) & ~3;
+            // Runs: every pair run, then every bin-8 run (16-bit halves of one scan).
+            const int packed = c4 | w4 << 16;
+#if SIFT_DBG_DPP
+            const int incl = wave_incl_scan_dpp(packed), excl = incl - packed;
+#else
+            const int incl = wave_incl_scan(packed), excl = incl - packed;
+#endif
+            const int start = excl & 0xffff, startw = (__builtin_amdgcn_readlane(incl, 63) & 0xffff) + (excl >> 16);
+            tbl[cell * 5 + g] = make_uint4((unsigned)M, (unsigned)(M >> 32), (unsigned)start, 0u);
+            if (g == 0) tbl[cell * 5 + 4] = make_uint4((unsigned)Mw, (unsigned)(Mw >> 32), (unsigned)startw, 0u);
+            // Padding: the run's last four entries are zeroed unconditionally
+            // (the samples' writes below land on the real ones afterwards); an
+            // empty run zeroes the trash entries instead.
+#if !SIFT_DBG_PADS
+#pragma unroll
+            for (int t = 1; t < 4; t++) {  // zero padding up to four entries
+                if (cnt + t <= c4 && (cnt & 3)) pool[start + c4 - t] = make_float2(0.f, 0.f);
+                if (cntw + t <= w4 && (cntw & 3)) pool[startw + w4 - t] = make_float2(0.f, 0.f);
+            }
+#else
+            {
+                float4* zp = reinterpret_cast<float4*>(pool + (c4 ? start + c4 - 4 : kTrash));
+                zp[0] = zp[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+                float4* zw = reinterpret_cast<float4*>(pool + (w4 ? startw + w4 - 4 : kTrash));
+                zw[0] = zw[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#endif
+            wave_lds_sync();
+            // ---- samples: push each contribution pair to its owner's run ----
+            const bool odd = o0 & 1;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int tci = r0 + (q >> 1), tcj = c0 + (q & 1);
+                const bool ok = valid && (unsigned)tci < (unsigned)kD && (unsigned)tcj < (unsigned)kD;
+                const int rp = ok ? (tci * kD + tcj) * 5 + (o0 >> 1) : kNullRow;
+                const int rs = ok && odd ? rp + 1 : kNullRow;
+                const uint4 tp = tbl[rp], ts = tbl[rs];
+                const unsigned ip = __builtin_amdgcn_mbcnt_hi(tp.y, __builtin_amdgcn_mbcnt_lo(tp.x, tp.z));
+                const unsigned is = __builtin_amdgcn_mbcnt_hi(ts.y, __builtin_amdgcn_mbcnt_lo(ts.x, ts.z));
+                const float lo = v[2 * q], hi = v[2 * q + 1];
+                pool[ip] = make_float2(odd ? 0.f : lo, odd ? lo : hi);
+                pool[is] = make_float2(hi, 0.f);
+            }
+            wave_lds_sync();
+            // ---- owners: add the runs in order ----
+            const float4* run = reinterpret_cast<const float4*>(pool + start);
+            for (int k = 0; k < c4 / 2; k += 2) {
+                const float4 e0 = run[k], e1 = run[k + 1];
+                accA = accA + e0.x;
+                accB = accB + e0.y;
+                accA = accA + e0.z;
+                accB = accB + e0.w;
+                accA = accA + e1.x;
+                accB = accB + e1.y;
+                accA = accA + e1.z;
+                accB = accB + e1.w;
+            }
+            const float4* runw = reinterpret_cast<const float4*>(pool + startw);
+            for (int k = 0; k < w4 / 2; k += 2) {  // g = 0 lanes (w4 = 0 elsewhere)
+                const float4 e0 = runw[k], e1 = runw[k + 1];
+                accW = accW + e0.x;
+                accW = accW + e0.z;
+                accW = accW + e1.x;
+                accW = accW + e1.z;
+            }
+            wave_lds_sync();
+        }
+        // OpenCV's wrap: hist[0] += hist[8] (hist[1] += hist[9] adds +0).
+        raw[cell * kN + 2 * g] = g == 0 ? accA + accW : accA;
+        raw[cell * kN + 2 * g + 1] = accB;
+        wave_lds_sync();
+        if (lane < 8) {
+            float a = 0.f;
+#pragma unroll
+            for (int q = 0; q < 16; q++) a = __fmaf_rn(raw[lane + 8 * q], raw[lane + 8 * q], a);
+            s_norm[lane] = a;
+        }
+        wave_lds_sync();
+        const float t0 = s_norm[0] + s_norm[4], t1 = s_norm[1] + s_norm[5], t2 = s_norm[2] + s_norm[6],
+                    t3 = s_norm[3] + s_norm[7];
+        const float thr = __builtin_sqrtf((t0 + t2) + (t1 + t3)) * 0.2f;
+        const float v0 = fminf(raw[2 * lane], thr), v1 = fminf(raw[2 * lane + 1], thr);
+        wave_lds_sync();
+        raw[2 * lane] = v0;
+        raw[2 * lane + 1] = v1;
+        wave_lds_sync();
+        if (lane == 0) {
+            float nrm2 = 0.f;
+            for (int q = 0; q < 128; q++) nrm2 = nrm2 + raw[q] * raw[q];
+            s_norm[8] = 512.f / fmaxf(__builtin_sqrtf(nrm2), FLT_EPSILON);
+        }
+        wave_lds_sync();
+        const float scale = s_norm[8];
+        int b0 = cv_round(v0 * scale), b1 = cv_round(v1 * scale);
+        b0 = b0 < 0 ? 0 : (b0 > 255 ? 255 : b0);
+        b1 = b1 < 0 ? 0 : (b1 > 255 ? 255 : b1);
+        const _Float16 h0 = (_Float16)(float)b0, h1 = (_Float16)(float)b1;
+        const unsigned po = (unsigned)jb.out;
+        const unsigned pair = (unsigned)__builtin_bit_cast(uint16_t, h0) | (unsigned)__builtin_bit_cast(uint16_t, h1) << 16;
+        reinterpret_cast<unsigned*>(desc + (size_t)po * 128)[lane] = pair;
+        HostOut hf = host;
+        const HostRows hr = host_rows(hf, ctr, frame, foff);
+        if (hr.desc) reinterpret_cast<unsigned*>(hr.desc + (size_t)po * 128)[lane] = pair;
+        if (hr.k3 && lane < 7) host_row(hr, hf, po, lane);
+        reinterpret_cast<unsigned short*>(sidecar.codes + (size_t)po * 128)[lane] =
+            (unsigned short)((b0 - 128) & 255) | (unsigned short)(((b1 - 128) & 255) << 8);
+        const int c2 = __builtin_amdgcn_readlane(wave_incl_scan((b0 - 128) * (b0 - 128) + (b1 - 128) * (b1 - 128)), 63);
+        if (lane == 0) sidecar.keys[po] = -(256 * c2 + (int)(po & 255));
+        wave_lds_sync();  // rowpre / raw / s_norm are rewritten by the next keypoint
+    }
+}
+
+#ifndef SIFT_EXACT_RUNS
+#define SIFT_EXACT_RUNS 1  // A/B: 0 = the mask walk (k_descriptor_exact)
+#endif
+
 void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned* range_keys, uint16_t* desc,
                        Sidecar sidecar, Counters* host_ctr, HostOut host, const KeypointParams& kp, const Frames& fr,
                        hipStream_t s) {
     if (kp.descExact) {
         // One wave per keypoint; each workgroup loops over keypoints.
         const int per = fr.nf <= 1 ? 2048 : std::max(512, 8192 / fr.nf);
-        hipLaunchKernelGGL(k_descriptor_exact, dim3(per * fr.nf), dim3(kExactWG), 0, s, jobs, ctr, desc, sidecar,
-                           host_ctr, host, fr.stride, (unsigned)fr.nf);
+        hipLaunchKernelGGL(SIFT_EXACT_RUNS ? k_descriptor_exact_runs : k_descriptor_exact, dim3(per * fr.nf),
+                           dim3(kExactWG), 0, s, jobs, ctr, desc, sidecar, host_ctr, host, fr.stride, (unsigned)fr.nf);
         return;
     }
     // Threads per keypoint: 256 for a single frame (128: 34.6 us, 512: 47.6 vs

@@ -6,30 +6,20 @@
 // pool) with ONE graph per descriptor buffer: every data-dependent size lives
 // in device counters, every launch has a fixed grid, and the only host sync
 // per frame is the final 32-byte counter readback.
+//
+// The handle's state and the orchestration split over four translation units
+// (detector_state.h): this one holds geometry, arenas, graph capture, the frame
+// launch and the detector entry points.
 #include <hip/hip_runtime.h>
-#include <rocprofiler-sdk-roctx/roctx.h>
-
-#include <sys/stat.h>
 
 #include <algorithm>
-#include <cerrno>
 #include <cmath>
-#include <condition_variable>
 #include <cstdio>
-#include <cstring>
-#include <functional>
-#include <mutex>
-#include <string>
-#include <thread>
-#include <vector>
 
-#include "sift_hip.h"
-#include "sift_kernels.h"
-#include "sift_match.h"
+#include "detector_state.h"
 
-using namespace sift_amd;
-
-namespace {
+namespace sift_amd {
+namespace det {
 
 thread_local std::string g_err;
 
@@ -38,12 +28,7 @@ int fail(int code, const std::string& msg) {
     return code;
 }
 
-#define HIPCHK(expr)                                                                                    \
-    do {                                                                                                \
-        hipError_t e_ = (expr);                                                                         \
-        if (e_ != hipSuccess)                                                                           \
-            return fail(SIFT_HIP_ERR_RUNTIME, std::string(#expr) + ": " + hipGetErrorString(e_));      \
-    } while (0)
+namespace {
 
 // OpenCV getGaussianKernelBitExact (same arithmetic as oracle gaussianTaps).
 Taps gaussian_taps(double sigma) {
@@ -86,439 +71,7 @@ const char* build_flags() {
 #endif
 }
 
-// Host copies of large frames split over a few persistent threads (the
-// staging copy of a host frame: one thread moves ~10 GB/s, a 1920x1200 f32
-// frame is 9.2 MB).  run(parts, fn) calls fn(0..parts-1), part 0 on the
-// calling thread, and returns when every part is done.
-class CopyPool {
-public:
-    explicit CopyPool(int workers) {
-        for (int i = 0; i < workers; i++) th_.emplace_back([this, i] { loop(i + 1); });
-    }
-    ~CopyPool() {
-        {
-            std::lock_guard<std::mutex> g(m_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (auto& t : th_) t.join();
-    }
-    int parts() const { return (int)th_.size() + 1; }
-    void run(const std::function<void(int)>& fn) {
-        {
-            std::lock_guard<std::mutex> g(m_);
-            fn_ = &fn;
-            pending_ = (int)th_.size();
-            gen_++;
-        }
-        cv_.notify_all();
-        fn(0);
-        std::unique_lock<std::mutex> g(m_);
-        done_.wait(g, [this] { return pending_ == 0; });
-        fn_ = nullptr;
-    }
-
-private:
-    void loop(int part) {
-        unsigned long long seen = 0;
-        for (;;) {
-            const std::function<void(int)>* fn;
-            {
-                std::unique_lock<std::mutex> g(m_);
-                cv_.wait(g, [&] { return stop_ || gen_ != seen; });
-                if (stop_) return;
-                seen = gen_;
-                fn = fn_;
-            }
-            (*fn)(part);
-            std::lock_guard<std::mutex> g(m_);
-            if (--pending_ == 0) done_.notify_one();
-        }
-    }
-    std::vector<std::thread> th_;
-    std::mutex m_;
-    std::condition_variable cv_, done_;
-    const std::function<void(int)>* fn_ = nullptr;
-    int pending_ = 0;
-    unsigned long long gen_ = 0;
-    bool stop_ = false;
-};
-
-// Pool threads besides the caller (a copy >= 1 MB runs in kCopyWorkers + 1
-// parts).  (Measured alternative: 7 workers, the C++ host loop at 3 lanes
-// 0.174-0.176 vs 0.170-0.171 ms/frame, profiles/round5/stage_modes.jsonl.)
-constexpr int kCopyWorkers = 3;
-
-// Row copy (dst pitch / src stride in bytes), split over the pool when large.
-void copy_rows(CopyPool* pool, char* dst, size_t dpitch, const char* src, size_t sstride, size_t rowB, int rows) {
-    auto part = [&](int lo, int hi) {
-        if (dpitch == sstride && dpitch == rowB) {
-            if (hi > lo) memcpy(dst + dpitch * lo, src + sstride * lo, rowB * (hi - lo));
-        } else {
-            for (int y = lo; y < hi; y++) memcpy(dst + dpitch * y, src + sstride * y, rowB);
-        }
-    };
-    if (!pool || rowB * rows < (1u << 20)) {
-        part(0, rows);
-        return;
-    }
-    const int P = pool->parts();
-    pool->run([&](int k) { part((int)((long)rows * k / P), (int)((long)rows * (k + 1) / P)); });
-}
-
-struct TimingRec {
-    int name;
-    hipEvent_t e0, e1;
-    double bytes;
-    int launches;
-};
-
-struct TimingAgg {
-    std::string name;
-    double ms = 0, bytes = 0;
-    int launches = 0;
-};
-
 }  // namespace
-
-void sift_amd::set_last_error(const std::string& msg) { g_err = msg; }
-
-namespace {
-
-// Matcher sidecars of the descriptor buffers the detector handles hand out
-// (one per results slot and frame of every lane): exact buffer base -> its
-// int8 codes and key biases (sift_kernels.h Sidecar).  sift_hip_match_* look
-// the query and train pointers up and, when both are detector buffers, match
-// their codes directly (k_match_direct) instead of converting the fp16 rows.
-struct SidecarReg {
-    const uint16_t* desc;
-    Sidecar side;
-    int cap;
-    const void* owner;
-};
-std::mutex g_side_mu;
-std::vector<SidecarReg> g_side;
-
-void register_sidecar(const void* owner, const uint16_t* desc, Sidecar side, int cap) {
-    std::lock_guard<std::mutex> g(g_side_mu);
-    g_side.push_back(SidecarReg{desc, side, cap, owner});
-}
-void unregister_sidecars(const void* owner) {
-    std::lock_guard<std::mutex> g(g_side_mu);
-    g_side.erase(std::remove_if(g_side.begin(), g_side.end(), [&](const SidecarReg& r) { return r.owner == owner; }),
-                 g_side.end());
-}
-bool find_sidecar(const uint16_t* desc, int n, Sidecar* out) {
-    std::lock_guard<std::mutex> g(g_side_mu);
-    for (const SidecarReg& r : g_side)
-        if (r.desc == desc && n <= r.cap) {
-            *out = r.side;
-            return true;
-        }
-    return false;
-}
-
-}  // namespace
-
-// Results slots per compute lane: frames f-1 .. f+2 of a lane never share one.
-constexpr int kResultSlots = 4;
-constexpr int kMaxLanes = 4;
-constexpr int kFrameRing = 256;  // per-frame (lane, slot, arena) records: > 2 x kMaxLanes x kMaxMicroBatch (frames in flight) + the two readable
-
-// A compute lane: one HIP stream, its B frame arenas (every per-frame buffer of
-// the pipeline, sift_kernels.h Frames), the graphs captured on them and a ring
-// of kResultSlots results slots.  A lane runs its frames in order; frames on
-// different lanes run concurrently ("Frames in flight").
-struct Lane {
-    hipStream_t stream = nullptr;
-    char* arena = nullptr;
-    Counters* hCtr = nullptr;     // kResultSlots x B pinned host copies of the counters (written by k_descriptor)
-    Counters* hCtrDev = nullptr;  // their device-side address
-    hipEvent_t evFrame[kResultSlots] = {};  // recorded after each slot's last frame
-    hipGraphExec_t exec[kResultSlots] = {};   // B frames per launch
-    hipGraphExec_t exec1[kResultSlots] = {};  // one frame (B > 1 only; exec when B = 1)
-    // The same graphs with the f32 head captured in (device input): the head
-    // node is re-pointed at each frame's image (hipGraphExecKernelNodeSetParams),
-    // so the frame is ONE graph launch -- a separate head launch left ~6 us
-    // between the head and the graph's first kernel on every single frame.
-    hipGraphExec_t execH[kResultSlots] = {}, execH1[kResultSlots] = {};
-    hipGraph_t graphH[kResultSlots] = {}, graphH1[kResultSlots] = {};
-    hipGraphNode_t headH[kResultSlots] = {}, headH1[kResultSlots] = {};
-    // The input each exec's head node reads now (image, pitch, frame stride;
-    // [slot][0]: execH, [1]: execH1): a frame from the same buffer as that
-    // exec's last one launches without re-pointing the node.
-    struct HeadIn {
-        const void* img = nullptr;
-        int pitch = 0;
-        long sfs = 0;
-        bool operator==(const HeadIn& o) const { return img == o.img && pitch == o.pitch && sfs == o.sfs; }
-    };
-    HeadIn headIn[kResultSlots][2];
-    int nfOf[kResultSlots] = {};  // frames of the launch group that wrote each slot
-    long long slotFrame[kResultSlots] = {-1, -1, -1, -1};  // the (first) frame whose results each slot holds
-    int slotNum[kResultSlots] = {};  // frame numbers in that slot (> 1: a micro-batch, frame slotFrame + i in arena i)
-    long long launched = 0;  // launch groups run on this lane; the next takes slot launched % kResultSlots
-    long long last = -1;     // the last frame launched here (-1: none since warm-up)
-    char* mbIn = nullptr;    // micro-batch input copies: mb frames of f32 rows (created at the first micro-batch)
-    // Host-input frames: results written to mapped pinned host memory by the
-    // frame's descriptor kernel (HostOut), one region per (slot, arena)
-    // (created once a caller reads results back); dHostTab (device, kSlots x
-    // B region pointers, null until then) tells the kernel where.
-    char* hRes = nullptr;
-    char* hResDev = nullptr;
-    char** dHostTab = nullptr;
-    std::vector<char*> hostTab;  // its host copy (the source of the async upload)
-    // Host-input staging of this lane: two pinned host buffers, moved into
-    // the lane's device staging by a 64-workgroup copy kernel on the lane's
-    // stream ahead of the frame (launch_copy_rows).  Measured alternatives
-    // (tools/host_pipeline_bench.cpp, 3 lanes x 6 frames, C2 u8 frames,
-    // profiles/round5/): the first blur reading the pinned buffer itself
-    // 0.165-0.170 ms/frame against 0.154 (its tiles' workgroups wait out the
-    // PCIe transfer and crowd the other lanes); DMA on a separate upload
-    // stream 0.169 at HIP's default 4 hardware queues per process (two active
-    // streams then share a queue: device frames ordered after a 4 KiB copy on
-    // a 4th stream ran at 0.160 instead of 0.112), 0.119-0.126 at
-    // GPU_MAX_HW_QUEUES=8 -- but 8 queues slowed the bench process's other
-    // legs; DMA on the lane's own stream 0.21-0.23 (the submit waited behind
-    // the lane).  Host slot k is rewritten for the lane's frame after next,
-    // once evRead[k] (recorded after the copy kernel) has passed; the device
-    // slot is stream-ordered.
-    static constexpr int kInSlots = 2;
-    void* hStage[kInSlots] = {};
-    void* dStage[kInSlots] = {};  // device copies (k_stage_to_device), allocated at the lane's first host frame
-    hipEvent_t evRead[kInSlots] = {};
-    long long uploads = 0;
-    // Host results regions: one per (results slot, arena) -- region slot * B + arena.
-    static constexpr int kHostRegions = kResultSlots * kMaxBatch;  // B <= kMaxBatch arenas per lane
-    long long hostFrame[kHostRegions];  // the frame each host region holds (-1: none; set in add_lane)
-    bool hostDesc[kHostRegions] = {};   // ... with its descriptors
-};
-
-// Byte offsets of every per-frame buffer inside a frame arena (the same for
-// every arena of every lane).
-struct ArenaLayout {
-    size_t input = 0, up = 0, pyr = 0, cand = 0, ref = 0, ori = 0, slot = 0, order = 0, jobs = 0, range = 0,
-           bcount = 0, boff = 0, bitmap = 0, ctr = 0, jord = 0;
-    size_t k3[kResultSlots] = {}, f4[kResultSlots] = {}, desc[kResultSlots] = {};
-    size_t codes[kResultSlots] = {}, ckeys[kResultSlots] = {};  // matcher sidecar of desc (Sidecar)
-    size_t octave[kMaxOctaves] = {};  // float offset of each octave's planes inside the pyramid
-};
-
-struct sift_hip_detector {
-    sift_hip_config cfg{};
-    int device = 0;
-    int L = 3, nOct = 0, firstOctave = 0;
-    int tailOct = 0;  // first octave of the pyramid-tail launch (nOct: none)
-    int baseW = 0, baseH = 0;
-    // Frame uploads and result downloads.  Created on first use: a stream
-    // holds a hardware queue, and device-input callers (several detectors per
-    // GPU, one stream each) need none.
-    hipStream_t copyStream = nullptr;
-    hipEvent_t evIn = nullptr, evOut = nullptr;
-    bool allocated = false;
-
-    // Frames are numbered in submission order.  Frame f runs on lane
-    // frec(f).lane and writes that lane's results slot frec(f).slot; `current`
-    // is the frame the result accessors expose (its predecessor's descriptors
-    // are prev_descriptor).  A frame may take a lane's slot only if the slot
-    // holds no frame from current - 1 on, and at most 2 frames per lane may be
-    // in flight past `current`.
-    static constexpr int kSlots = kResultSlots;
-    Lane lanes[kMaxLanes];
-    int nLanes = 0;    // lanes created (lane 0 at warm-up, more on demand)
-    int maxLanes = 2;  // sift_hip_set_lanes
-    int ln = 0;        // the lane the pointer views below are bound to (bind_lane)
-    int curLane = 0;   // lane of `current`
-    int curIdx = 0;    // arena of `current` in its lane (micro-batches)
-    // Micro-batching (sift_hip_set_micro_batch): device frames submitted with
-    // sift_hip_submit_device queue here until mb of them run as one launch
-    // group on a lane (the B-frame graphs, frame i in arena i), or until a
-    // wait / sync / other submit needs them.  Tickets run ahead of `submitted`
-    // by the frames pending.
-    static constexpr int kMaxMicroBatch = 16;
-    int mb = 1;
-    struct PendingFrame {
-        const void* img;  // device frame, or the device address of a host frame's pinned staging
-        size_t stride;
-        int fmt;
-        bool ordered;  // the lane waits for evPend[i] (the caller's stream)
-        int hslot;     // host frames: their staging slot (-1: a device frame)
-    };
-    // Pinned staging of micro-batched host frames: one block of hstSlots
-    // slots (one per frame that can be pending or queued on a lane; a slot is
-    // refilled once the copy kernel that read it, event hstRead[i], has run),
-    // allocated in one piece at the first such frame (per-slot allocations
-    // inside the submits of a running loop stalled it for milliseconds).
-    char* hstBlock = nullptr;
-    size_t hstSlotBytes = 0;
-    int hstSlots = 0;
-    std::vector<hipEvent_t> hstRead;
-    long long hstNext = 0;
-    PendingFrame pend[kMaxMicroBatch] = {};
-    hipEvent_t evPend[kMaxMicroBatch] = {};
-    int npend = 0;
-    struct FrameRec {
-        int lane = 0, slot = 0, idx = 0;  // idx: the frame's arena in a micro-batch
-    };
-    FrameRec frecs[kFrameRing];
-    FrameRec& frec(long long f) { return frecs[f & (kFrameRing - 1)]; }
-    Lane& lane() { return lanes[ln]; }
-    long long submitted = 0, current = -1, firstFrame = 0, uploads = 0;
-
-    // Frame batches: up to B frames per launch (sift_hip_set_batch).  Every
-    // per-frame buffer below lives in frame 0's arena of the bound lane; frame
-    // f's copy is at + f * afs bytes (Frames, sift_kernels.h).
-    int B = 1;
-    long afs = 0;
-    ArenaLayout lay;
-
-    PyrDesc pyr{};
-    Taps initTaps{};
-    std::vector<Taps> layerTaps;
-    float threshold = 1.f;
-    KeypointParams kp{};
-
-    // Views of the bound lane (bind_lane): its stream and frame-0 arena pointers.
-    hipStream_t stream = nullptr;
-    int inPitch = 0, upPitch = 0;
-    float* dInput = nullptr;  // blank warm-up frame; f32 scratch for 8-bit frames at other init radii
-    float* dUp = nullptr;
-    float* dPyr = nullptr;
-    uint2* dCand = nullptr;
-    unsigned capCand = 1u << 20;  // sized to the frame in setup_taps
-    RefKpt* dRef = nullptr;
-    OriKpt* dOri = nullptr;
-    int* dSlot = nullptr;
-    int* dOrder = nullptr;
-    DescJob* dJobs = nullptr;  // per final keypoint, written by k_bucket_rank
-    JobOrder* dJord = nullptr;  // descriptor job order (k_order -> k_rank_final)
-    unsigned* dRange = nullptr;  // 2 * kRangeSlots pixel-range keys (initial blur -> descriptor)
-    unsigned* dBcount = nullptr;
-    unsigned* dBoff = nullptr;
-    uint32_t* dBitmap = nullptr;
-    size_t bitmapWords = 0;
-    Counters* dCtr = nullptr;
-    Counters* hCtr = nullptr;     // kSlots x B pinned host copies of the counters (written by k_descriptor)
-    Counters* hCtrDev = nullptr;  // their device-side address
-    float* dKpts3[kSlots] = {};
-    float* dFeats4[kSlots] = {};
-    uint16_t* dDesc[kSlots] = {};
-    Sidecar dSide[kSlots] = {};
-    int cur = 0, count = 0, prevCount = 0;  // frec(current).slot and the counts of current, current - 1
-    bool countsValid = true;  // count / prevCount / the slot's host counters read after the frame completed
-
-    HeadNode headNode{};
-    bool useGraph = true;
-
-    CopyPool* pool = nullptr;  // staging copies of large host frames (created at the first one)
-    // The most the caller's sift_hip_copy_to_host / sift_hip_results_host
-    // calls took (0 nothing yet, 1 keypoints, 2 keypoints + descriptors):
-    // host-input frames have their descriptor kernel write that much to
-    // pinned host memory (HostOut; a caller that never reads back pays nothing).
-    int hostWant = 0;
-
-    // Stage dumps (sift_hip_set_datagen): directory, and a device copy of the
-    // frame's input as float (the caller's buffer may change before the dump).
-    std::string dgDir;
-    float* dDg = nullptr;
-
-    bool timing = false;
-    int blurReps = 1;  // timing mode: each blur launch repeated back to back inside its event pair
-    std::vector<TimingRec> trecs;
-    std::vector<TimingAgg> tagg;
-    std::vector<hipEvent_t> evPool;
-    size_t evUsed = 0;
-
-    int name_id(const char* n) {
-        for (size_t i = 0; i < tagg.size(); i++)
-            if (tagg[i].name == n) return (int)i;
-        tagg.push_back(TimingAgg{n});
-        return (int)tagg.size() - 1;
-    }
-    hipEvent_t next_event() {
-        if (evUsed == evPool.size()) {
-            hipEvent_t e;
-            (void)hipEventCreate(&e);
-            evPool.push_back(e);
-        }
-        return evPool[evUsed++];
-    }
-    template <class F>
-    void timed(const char* name, double bytes, F&& fn) {
-        if (!timing) {
-            fn();
-            return;
-        }
-        // Blur launches are pure (input plane -> output plane; the first blur's
-        // counter zeroing and range max are idempotent), so they may be
-        // repeated to time them back to back without per-launch event cost.
-        const int reps = strncmp(name, "blur_", 5) == 0 ? blurReps : 1;
-        TimingRec r{name_id(name), next_event(), next_event(), bytes * reps, reps};
-        // A roctx range per stage: rocprofv3
-        // --marker-trace shows the stage spans and the kernels launched in them.
-        roctxRangePushA(name);
-        (void)hipEventRecord(r.e0, stream);
-        for (int i = 0; i < reps; i++) fn();
-        (void)hipEventRecord(r.e1, stream);
-        roctxRangePop();
-        trecs.push_back(r);
-    }
-    void collect_timing() {
-        for (auto& r : trecs) {
-            float ms = 0;
-            (void)hipEventElapsedTime(&ms, r.e0, r.e1);
-            tagg[r.name].ms += ms;
-            tagg[r.name].bytes += r.bytes;
-            tagg[r.name].launches += r.launches;
-        }
-        trecs.clear();
-        evUsed = 0;
-    }
-
-    ~sift_hip_detector() {
-        unregister_sidecars(this);
-        if (allocated) {
-            (void)hipSetDevice(device);
-            for (int k = 0; k < nLanes; k++) {
-                Lane& L = lanes[k];
-                if (L.stream) (void)hipStreamSynchronize(L.stream);
-                for (int b = 0; b < kSlots; b++) {
-                    for (hipGraphExec_t e : {L.exec[b], L.exec1[b], L.execH[b], L.execH1[b]})
-                        if (e) (void)hipGraphExecDestroy(e);
-                    for (hipGraph_t g : {L.graphH[b], L.graphH1[b]})
-                        if (g) (void)hipGraphDestroy(g);
-                    if (L.evFrame[b]) (void)hipEventDestroy(L.evFrame[b]);
-                }
-                if (L.arena) (void)hipFree(L.arena);
-                if (L.mbIn) (void)hipFree(L.mbIn);
-                if (L.hCtr) (void)hipHostFree(L.hCtr);
-                if (L.hRes) (void)hipHostFree(L.hRes);
-                if (L.dHostTab) (void)hipFree(L.dHostTab);
-                for (int k = 0; k < Lane::kInSlots; k++) {
-                    if (L.hStage[k]) (void)hipHostFree(L.hStage[k]);
-                    if (L.dStage[k]) (void)hipFree(L.dStage[k]);
-                    if (L.evRead[k]) (void)hipEventDestroy(L.evRead[k]);
-                }
-                if (L.stream) (void)hipStreamDestroy(L.stream);
-            }
-            if (dDg) (void)hipFree(dDg);
-            for (auto e : evPool) (void)hipEventDestroy(e);
-            if (hstBlock) (void)hipHostFree(hstBlock);
-            for (hipEvent_t e : hstRead) (void)hipEventDestroy(e);
-            if (evIn) (void)hipEventDestroy(evIn);
-            for (hipEvent_t e : evPend)
-                if (e) (void)hipEventDestroy(e);
-            if (evOut) (void)hipEventDestroy(evOut);
-            if (copyStream) (void)hipStreamDestroy(copyStream);
-        }
-        delete pool;
-    }
-};
-
-static_assert(kFrameRing > 2 * kMaxLanes * sift_hip_detector::kMaxMicroBatch + 2 && (kFrameRing & (kFrameRing - 1)) == 0,
-              "frame records outlive every frame in flight");
-
-namespace {
 
 int setup_geometry(sift_hip_detector* d) {
     const sift_hip_config& c = d->cfg;
@@ -624,19 +177,12 @@ void upload_exp_tab() {
     upload_desc_exp_table(tab);
 }
 
-template <class T>
-int dalloc(T** p, size_t count) {
-    if (hipMalloc((void**)p, sizeof(T) * std::max<size_t>(count, 1)) != hipSuccess)
-        return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc failed");
-    return SIFT_HIP_OK;
-}
-
 // Points the handle's buffer views (stream, frame-0 arena pointers, host
 // counters) at lane k.  Every entry point binds the lane it works on: the
 // submitting lane for a new frame (idx 0: launches address frame 0's arena),
 // the current frame's lane and arena for accessors (idx: its arena in a
 // micro-batch, which offsets the results views and host counters).
-void bind_lane(sift_hip_detector* d, int k, int idx = 0) {
+void bind_lane(sift_hip_detector* d, int k, int idx) {
     Lane& L = d->lanes[k];
     const ArenaLayout& a = d->lay;
     char* A = L.arena;
@@ -674,7 +220,7 @@ const uint16_t* frame_desc(const sift_hip_detector* d, long long f) {
     const auto& r = d->frecs[f & (kFrameRing - 1)];
     return reinterpret_cast<const uint16_t*>(d->lanes[r.lane].arena + (size_t)r.idx * d->afs + d->lay.desc[r.slot]);
 }
-const Counters& frame_counters(const sift_hip_detector* d, long long f, int i = 0) {
+const Counters& frame_counters(const sift_hip_detector* d, long long f, int i) {
     const auto& r = d->frecs[f & (kFrameRing - 1)];
     return d->lanes[r.lane].hCtr[(size_t)r.slot * d->B + r.idx + i];
 }
@@ -744,7 +290,6 @@ int allocate(sift_hip_detector* d) {
 }
 
 int build_graphs(sift_hip_detector* d);
-int ensure_host_res(sift_hip_detector* d, Lane& L);
 
 // A new compute lane: stream, zeroed arenas, host counters, events and the
 // captured graphs (bound on return).
@@ -786,7 +331,9 @@ int add_lane(sift_hip_detector* d) {
                              (int)d->kp.capFinal);
     if (d->hostWant)
         if (int rc = ensure_host_res(d, L)) return rc;
-    return build_graphs(d);
+    if (int rc = build_graphs(d)) return rc;
+    L.ready = true;
+    return SIFT_HIP_OK;
 }
 
 // The first kernel reads the caller's image (upload ring slot or a device
@@ -1059,9 +606,6 @@ int build_graphs(sift_hip_detector* d) {
     return SIFT_HIP_OK;
 }
 
-int dump_stage_files(sift_hip_detector* d);
-void complete_counts(sift_hip_detector* d);
-
 bool event_done(hipEvent_t e) {
     const hipError_t r = hipEventQuery(e);
     if (r == hipSuccess) return true;
@@ -1086,44 +630,13 @@ int warm_lane(sift_hip_detector* d) {
     return SIFT_HIP_OK;
 }
 
-// The lane for the next frame, bound on return: the first idle lane (its last
-// frame complete), else a new lane (up to maxLanes), else the busy lane whose
-// last frame is the oldest.  A lane qualifies only if its next results slot
-// holds no frame the caller may still read (current - 1 onwards).
-int pick_lane(sift_hip_detector* d) {
-    auto slot_free = [&](int k) {
-        const Lane& L = d->lanes[k];
-        const int s = (int)(L.launched % d->kSlots);
-        const long long occ = L.slotFrame[s] < 0 ? -1 : L.slotFrame[s] + std::max(L.slotNum[s], 1) - 1;  // its last frame
-        return occ < 0 || occ < d->firstFrame || occ < d->current - 1;
-    };
-    int busy = -1;
-    for (int k = 0; k < d->nLanes; k++) {
-        if (!slot_free(k)) continue;
-        const Lane& L = d->lanes[k];
-        if (L.last < 0 || event_done(L.evFrame[(L.launched + d->kSlots - 1) % d->kSlots])) {
-            bind_lane(d, k);
-            return SIFT_HIP_OK;
-        }
-        if (busy < 0 || L.last < d->lanes[busy].last) busy = k;
-    }
-    if (d->nLanes < d->maxLanes) {  // (lane 0 comes from sift_hip_warmup)
-        if (int rc = add_lane(d)) return rc;
-        return warm_lane(d);
-    }
-    if (busy < 0)
-        return fail(SIFT_HIP_ERR_STATE, "every lane's next results slot is still held: sift_hip_wait first");
-    bind_lane(d, busy);
-    return SIFT_HIP_OK;
-}
-
 // Enqueues launch group d->submitted (nf frames at byte stride sfs) on the
 // bound lane (pick_lane); `consumed` (nullable) is recorded once the input has
 // been read.  A batch (sift_hip_detect_batch_device) is one frame number; a
 // micro-batch (`numbered`) takes nf numbers, frame d->submitted + i in arena i.  With stage dumps on (single frames after warm-up) the frame's
 // input is kept as float, the frame is completed synchronously and dumped.
-int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEvent_t consumed, int nf = 1,
-              long sfs = 0, bool numbered = false) {
+int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEvent_t consumed, int nf, long sfs,
+              bool numbered) {
     const long long f = d->submitted;
     Lane& L = d->lane();
     const int slot = (int)(L.launched % d->kSlots);
@@ -1176,6 +689,7 @@ int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEven
     L.launched++;
     L.last = f + nums - 1;
     for (int i = 0; i < nums; i++) d->frec(f + i) = sift_hip_detector::FrameRec{d->ln, slot, i};
+    for (int i = 0; i < nf; i++) sidecar_refreshed(fptr(d->dDesc[slot], (long)i * d->afs));
     d->submitted = f + nums;
     if (dump) {
         HIPCHK(hipStreamSynchronize(d->stream));
@@ -1227,12 +741,11 @@ int ensure_counts(sift_hip_detector* d) {
 }
 
 int sync_lanes(sift_hip_detector* d) {
-    for (int k = 0; k < d->nLanes; k++) HIPCHK(hipStreamSynchronize(d->lanes[k].stream));
+    for (int k = 0; k < d->nLanes; k++)
+        if (d->lanes[k].ready) HIPCHK(hipStreamSynchronize(d->lanes[k].stream));
     if (d->timing) d->collect_timing();
     return SIFT_HIP_OK;
 }
-
-int run_group(sift_hip_detector* d);
 
 int finish_frame(sift_hip_detector* d) {
     if (int rc = run_group(d)) return rc;
@@ -1244,601 +757,20 @@ int finish_frame(sift_hip_detector* d) {
     return SIFT_HIP_OK;
 }
 
-int copy_stream(sift_hip_detector* d, hipStream_t* s) {
-    if (!d->copyStream) HIPCHK(hipStreamCreateWithFlags(&d->copyStream, hipStreamNonBlocking));
-    *s = d->copyStream;
-    return SIFT_HIP_OK;
-}
+}  // namespace det
+}  // namespace sift_amd
 
-int format_size(int fmt) { return fmt == SIFT_HIP_U8 ? 1 : (fmt == SIFT_HIP_F32 ? 4 : 0); }
+void sift_amd::set_last_error(const std::string& msg) { det::g_err = msg; }
 
-// Frames in flight past `current` (host-input and device submits): at most 2
-// per lane the handle may use.
-int check_in_flight(sift_hip_detector* d) {
-    if (d->submitted + d->npend > d->current + 2LL * d->maxLanes * d->mb)
-        return fail(SIFT_HIP_ERR_STATE, "every lane already has two launch groups in flight past the current frame: sift_hip_wait first");
-    return SIFT_HIP_OK;
-}
-
-// Host results region of a lane slot: kpts3 | feats4 | descriptors at capacity.
-size_t host_res_bytes(const sift_hip_detector* d) {
-    const size_t c = d->kp.capFinal;
-    return ((12 * c + 255) & ~(size_t)255) + 16 * c + 256 * c;
-}
-void host_res(const sift_hip_detector* d, char* base, int region, float** k3, float** f4, uint16_t** desc) {
-    const size_t c = d->kp.capFinal;
-    char* p = base + host_res_bytes(d) * region;
-    *k3 = reinterpret_cast<float*>(p);
-    p += (12 * c + 255) & ~(size_t)255;
-    *f4 = reinterpret_cast<float*>(p);
-    *desc = reinterpret_cast<uint16_t*>(p + 16 * c);
-}
-
-// The lane's pinned results regions (kSlots x B) and the device table that
-// points the descriptor kernel at them (HostOut), set up for every lane once a
-// caller reads results back (sift_hip_copy_to_host / sift_hip_results_host
-// turn hostWant on) and for lanes created after that: a lazy allocation
-// inside a submit stalled it for ~14 ms.  The table goes in on the lane's
-// stream (after its zeroing; frames launched earlier keep a null table).
-int ensure_host_res(sift_hip_detector* d, Lane& L) {
-    if (L.hRes) return SIFT_HIP_OK;
-    const size_t nr = (size_t)d->kSlots * d->B, rb = host_res_bytes(d);
-    HIPCHK(hipHostMalloc((void**)&L.hRes, rb * nr, hipHostMallocMapped | hipHostMallocCoherent));
-    HIPCHK(hipHostGetDevicePointer((void**)&L.hResDev, L.hRes, 0));
-    L.hostTab.resize(nr);
-    for (size_t r = 0; r < nr; r++) L.hostTab[r] = L.hResDev + rb * r;
-    HIPCHK(hipMemcpyAsync(L.dHostTab, L.hostTab.data(), sizeof(char*) * nr, hipMemcpyHostToDevice, L.stream));
-    return SIFT_HIP_OK;
-}
-
-// A host-input frame's results request (the word its staging copy sets:
-// arena i's Counters.pad[1], HostOut): null unless a caller reads results back.
-unsigned* host_request(sift_hip_detector* d, int i, unsigned* val) {
-    *val = (unsigned)d->hostWant << kHostReqShift;
-    return d->hostWant ? &fptr(d->dCtr, (long)i * d->afs)->pad[1] : nullptr;
-}
-
-// After host-input frame f (arena i of its launch group) was launched with a
-// request: its results land in the lane's region slot * B + i.
-void mark_host_results(sift_hip_detector* d, long long f) {
-    if (!d->hostWant) return;
-    const auto& r = d->frec(f);
-    Lane& L = d->lanes[r.lane];
-    const int region = r.slot * d->B + r.idx;
-    L.hostFrame[region] = f;
-    L.hostDesc[region] = d->hostWant > 1;
-}
-
-int run_group(sift_hip_detector* d);
-
-// A host frame on a micro-batching handle: into the next pinned staging slot
-// of the handle's ring (the caller's buffer is free on return), pending until
-// its group runs (run_group copies it to the lane's group input).
-int queue_host(sift_hip_detector* d, const void* img, size_t stride, int fmt, long long* ticket) {
-    const int es = format_size(fmt), H = d->cfg.row_width;
-    const size_t rowB = (size_t)es * d->cfg.col_width, pitchB = (size_t)es * d->inPitch;
-    if (d->npend && d->pend[0].fmt != fmt)
-        if (int rc = run_group(d)) return rc;
-    if (d->hstSlotBytes < pitchB * H) {  // first host frame, or a larger format: (re)allocate the block
-        if (int rc = run_group(d)) return rc;
-        if (int rc = sync_lanes(d)) return rc;  // no copy kernel still reads the old block
-        if (d->hstBlock) HIPCHK(hipHostFree(d->hstBlock));
-        d->hstBlock = nullptr;
-        d->hstSlotBytes = 0;
-        d->hstSlots = (2 * d->maxLanes + 1) * d->mb;  // frames pending or queued on the lanes
-        if (hipHostMalloc((void**)&d->hstBlock, pitchB * H * d->hstSlots, hipHostMallocMapped | hipHostMallocNonCoherent) !=
-            hipSuccess)
-            return fail(SIFT_HIP_ERR_NOMEM, "hipHostMalloc of the micro-batch host staging failed");
-        d->hstSlotBytes = pitchB * H;
-        while ((int)d->hstRead.size() < d->hstSlots) {
-            hipEvent_t e;
-            HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            d->hstRead.push_back(e);
-        }
-    }
-    const int hs = (int)(d->hstNext++ % d->hstSlots);
-    HIPCHK(hipEventSynchronize(d->hstRead[hs]));  // the copy kernel that last read the slot has run
-    char* slot = d->hstBlock + d->hstSlotBytes * hs;
-    if (!d->pool && rowB * H >= (1u << 20)) d->pool = new CopyPool(kCopyWorkers);
-    copy_rows(d->pool, slot, pitchB, (const char*)img, stride, rowB, H);
-    void* dev = nullptr;
-    HIPCHK(hipHostGetDevicePointer(&dev, slot, 0));
-    const int i = d->npend;
-    d->pend[i] = sift_hip_detector::PendingFrame{dev, pitchB, fmt, false, hs};
-    d->npend = i + 1;
-    if (ticket) *ticket = d->submitted + i;
-    return d->npend == d->mb ? run_group(d) : SIFT_HIP_OK;
-}
-
-// Host frame -> the lane's pinned staging (the caller's buffer is free on
-// return) -> device staging by a small-grid copy kernel on the lane's stream
-// -> pipeline on the frame's lane -> results to pinned host memory.  On a
-// micro-batching handle the frame joins the pending group (queue_host).
-int submit_host(sift_hip_detector* d, const void* img, size_t stride, int fmt, long long* ticket) {
-    const int es = format_size(fmt);
-    if (!es) return fail(SIFT_HIP_ERR_INVALID, "unknown pixel format");
-    if (!img) return fail(SIFT_HIP_ERR_INVALID, "null image");
-    const int W = d->cfg.col_width, H = d->cfg.row_width;
-    const size_t rowB = (size_t)es * W, pitchB = (size_t)es * d->inPitch;
-    if (stride == 0) stride = rowB;
-    if (stride < rowB) return fail(SIFT_HIP_ERR_INVALID, "row stride smaller than width");
-    if (int rc = check_in_flight(d)) return rc;
-    if (d->mb > 1 && d->dgDir.empty() && !d->timing) return queue_host(d, img, stride, fmt, ticket);
-    if (int rc = run_group(d)) return rc;  // pending micro-batch frames keep their submission order
-    if (int rc = pick_lane(d)) return rc;
-    Lane& L = d->lane();
-    const int k = (int)(L.uploads & 1);
-    HIPCHK(hipEventSynchronize(L.evRead[k]));  // staging slot k no longer being read (the lane's frame before last)
-    if (!d->pool && rowB * H >= (1u << 20)) d->pool = new CopyPool(kCopyWorkers);
-    copy_rows(d->pool, (char*)L.hStage[k], pitchB, (const char*)img, stride, rowB, H);
-    void* src = nullptr;
-    HIPCHK(hipHostGetDevicePointer(&src, L.hStage[k], 0));
-    const size_t inBytes = sizeof(float) * (size_t)d->inPitch * H;
-    if (!L.dStage[k] && hipMalloc(&L.dStage[k], inBytes) != hipSuccess)
-        return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc of the device staging failed");
-    unsigned req = 0;
-    unsigned* reqAt = d->dgDir.empty() ? host_request(d, 0, &req) : nullptr;
-    launch_copy_rows(src, pitchB, L.dStage[k], pitchB, pitchB, H, kStageWg, d->stream, reqAt, req);
-    HIPCHK(hipEventRecord(L.evRead[k], d->stream));  // host slot k read; device slot k is stream-ordered
-    L.uploads++;
-    d->uploads++;
-    const long long f = d->submitted;
-    if (int rc = run_frame(d, L.dStage[k], d->inPitch, fmt, nullptr)) return rc;
-    if (reqAt) mark_host_results(d, f);
-    if (ticket) *ticket = f;
-    return SIFT_HIP_OK;
-}
-
-// The pending micro-batch frames as one launch group on a lane: each frame's
-// rows are copied (device to device by launch_copy_rows, on the lane's stream after the caller's
-// stream event) into the lane's micro-batch input at a fixed frame stride, and
-// the group runs the B-frame graphs (a partial group: the 1-frame graphs, or
-// the same launches eagerly), frame d->submitted + i in arena i.
-int run_group(sift_hip_detector* d) {
-    const int n = d->npend;
-    if (!n) return SIFT_HIP_OK;
-    if (int rc = pick_lane(d)) return rc;
-    Lane& L = d->lane();
-    const int W = d->cfg.col_width, H = d->cfg.row_width;
-    const size_t fb = sizeof(float) * (size_t)d->inPitch * H;  // one frame of f32 rows (an 8-bit frame uses a quarter)
-    if (!L.mbIn && hipMalloc((void**)&L.mbIn, fb * d->mb) != hipSuccess)
-        return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc of the micro-batch input failed");
-    const int fmt = d->pend[0].fmt, es = format_size(fmt);
-    bool host[sift_hip_detector::kMaxMicroBatch] = {};
-    for (int i = 0; i < n; i++) {
-        const auto& p = d->pend[i];
-        if (p.ordered) HIPCHK(hipStreamWaitEvent(d->stream, d->evPend[i], 0));
-        if (p.hslot >= 0) {  // pinned staging: whole pitch rows over PCIe by a small grid
-            unsigned req;
-            unsigned* reqAt = host_request(d, i, &req);
-            launch_copy_rows(p.img, p.stride, L.mbIn + fb * i, p.stride, p.stride, H, kStageWg, d->stream, reqAt, req);
-            HIPCHK(hipEventRecord(d->hstRead[p.hslot], d->stream));
-            host[i] = reqAt != nullptr;
-        } else {
-            launch_copy_rows(p.img, p.stride, L.mbIn + fb * i, (size_t)es * d->inPitch, (size_t)es * W, H,
-                             kGroupCopyWg, d->stream);
-        }
-    }
-    d->npend = 0;
-    const long long f = d->submitted;
-    if (int rc = run_frame(d, L.mbIn, d->inPitch, fmt, nullptr, n, (long)fb, true)) return rc;
-    for (int i = 0; i < n; i++)
-        if (host[i]) mark_host_results(d, f + i);
-    return SIFT_HIP_OK;
-}
-
-// Device frame (HBM-resident, fp32 or u8) -> the frame's lane; the lane waits
-// for `stream` (the caller's producer) before reading it.  `queue`: a single
-// frame of sift_hip_submit_device on a micro-batching handle joins the pending
-// group instead (one format per group: a frame of the other format flushes it).
-int submit_device(sift_hip_detector* d, const void* img, size_t stride, int fmt, void* stream, int nf, size_t fstride,
-                  long long* ticket, bool queue = false) {
-    hipStream_t ext = (hipStream_t)stream;
-    if (queue && d->mb > 1 && nf == 1 && d->dgDir.empty() && !d->timing) {
-        if (d->npend && d->pend[0].fmt != fmt)
-            if (int rc = run_group(d)) return rc;
-        const int i = d->npend;
-        if (ext) {
-            if (!d->evPend[i]) HIPCHK(hipEventCreateWithFlags(&d->evPend[i], hipEventDisableTiming));
-            HIPCHK(hipEventRecord(d->evPend[i], ext));
-        }
-        d->pend[i] = sift_hip_detector::PendingFrame{img, stride, fmt, ext != nullptr, -1};
-        d->npend = i + 1;
-        if (ticket) *ticket = d->submitted + i;
-        return d->npend == d->mb ? run_group(d) : SIFT_HIP_OK;
-    }
-    if (int rc = run_group(d)) return rc;  // frames are numbered (and launched) in submission order
-    if (int rc = pick_lane(d)) return rc;
-    if (ext) {
-        HIPCHK(hipEventRecord(d->evIn, ext));
-        HIPCHK(hipStreamWaitEvent(d->stream, d->evIn, 0));
-    }
-    const long long f = d->submitted;
-    if (int rc = run_frame(d, img, (int)(stride / format_size(fmt)), fmt, nullptr, nf, (long)fstride)) return rc;
-    if (ticket) *ticket = f;
-    return SIFT_HIP_OK;
-}
-
-int wait_frame(sift_hip_detector* d, long long f) {
-    if (f >= d->submitted && f < d->submitted + d->npend)
-        if (int rc = run_group(d)) return rc;  // a pending micro-batch frame: launch the partial group now
-    if (f < d->firstFrame || f >= d->submitted || f < d->submitted - kFrameRing)
-        return fail(SIFT_HIP_ERR_INVALID, "unknown frame ticket");
-    const auto& r = d->frec(f);
-    Lane& L = d->lanes[r.lane];
-    if (L.slotFrame[r.slot] < 0 || f < L.slotFrame[r.slot] || f >= L.slotFrame[r.slot] + std::max(L.slotNum[r.slot], 1))
-        return fail(SIFT_HIP_ERR_STATE, "frame results already recycled");
-    if (d->timing) {
-        if (int rc = sync_lanes(d)) return rc;
-    } else {
-        HIPCHK(hipEventSynchronize(L.evFrame[r.slot]));
-        if (f - 1 >= d->firstFrame) {  // prev_descriptor may come from another lane
-            const auto& p = d->frec(f - 1);
-            HIPCHK(hipEventSynchronize(d->lanes[p.lane].evFrame[p.slot]));
-        }
-    }
-    make_current(d, f);
-    complete_counts(d);
-    return SIFT_HIP_OK;
-}
-
-// Stage dumps of the current frame (Detector::setDataGen, reference
-// Detector.cu:145-229 / PerfData.cuh): raw little-endian row-major files plus a
-// meta.json describing them; tests/stage_check.py replays them against the CPU
-// oracle (and against this library).
-// mkdir -p
-bool make_dirs(const std::string& path) {
-    for (size_t i = 1; i <= path.size(); i++)
-        if (i == path.size() || path[i] == '/') {
-            const std::string p = path.substr(0, i);
-            if (mkdir(p.c_str(), 0755) != 0 && errno != EEXIST) return false;
-        }
-    return true;
-}
-
-int write_file(const std::string& path, const void* data, size_t bytes) {
-    FILE* fp = fopen(path.c_str(), "wb");
-    if (!fp) return fail(SIFT_HIP_ERR_INVALID, "cannot write " + path);
-    const size_t n = bytes ? fwrite(data, 1, bytes, fp) : 0;
-    fclose(fp);
-    if (n != bytes) return fail(SIFT_HIP_ERR_INVALID, "short write to " + path);
-    return SIFT_HIP_OK;
-}
-
-// Portable descriptor jobs: the plane pointer becomes the plane index
-// o * (L + 3) + layer (the replaying handle has its own arena).
-int job_plane(const sift_hip_detector* d, const float* img) {
-    for (int o = 0; o < d->nOct; o++) {
-        const OctGeom& g = d->pyr.oct[o];
-        for (int l = 0; l < d->L + 3; l++)
-            if (img == g.base + (size_t)l * g.planeStride) return o * (d->L + 3) + l;
-    }
-    return -1;
-}
-
-// refined.rec (RefKpt), oriented.rec (OriKpt slots incl. holes), jobs.rec
-// (DescJob, plane index in place of the pointer), range.u32 (the frame's
-// pixel-range keys), counters.u32 (Counters): frame 0 of the arena, after the
-// frame completed (nothing reuses these buffers before the next frame).
-int dump_records(sift_hip_detector* d, const std::string& dir) {
-    const Counters& c = d->hCtr[(size_t)d->cur * d->B];
-    const size_t nRef = std::min<unsigned>(c.refined, d->kp.capRefined);
-    const size_t nOri = std::min<size_t>(nRef + c.oriented, d->kp.capOriented);
-    const size_t nFin = std::min<unsigned>(c.final_n, d->kp.capFinal);
-    std::vector<RefKpt> ref(nRef);
-    std::vector<OriKpt> ori(nOri);
-    std::vector<DescJob> jobs(nFin);
-    std::vector<unsigned> range(2 * kRangeSlots);
-    if (nRef) HIPCHK(hipMemcpy(ref.data(), d->dRef, sizeof(RefKpt) * nRef, hipMemcpyDeviceToHost));
-    if (nOri) HIPCHK(hipMemcpy(ori.data(), d->dOri, sizeof(OriKpt) * nOri, hipMemcpyDeviceToHost));
-    if (nFin) HIPCHK(hipMemcpy(jobs.data(), d->dJobs, sizeof(DescJob) * nFin, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(range.data(), range_keys(d, d->cur & 1), sizeof(unsigned) * range.size(), hipMemcpyDeviceToHost));
-    for (DescJob& j : jobs) {
-        const long long plane = job_plane(d, j.img);
-        std::memcpy(&j.img, &plane, sizeof plane);
-    }
-    if (int rc = write_file(dir + "/refined.rec", ref.data(), sizeof(RefKpt) * nRef)) return rc;
-    if (int rc = write_file(dir + "/oriented.rec", ori.data(), sizeof(OriKpt) * nOri)) return rc;
-    if (int rc = write_file(dir + "/jobs.rec", jobs.data(), sizeof(DescJob) * nFin)) return rc;
-    if (int rc = write_file(dir + "/range.u32", range.data(), sizeof(unsigned) * range.size())) return rc;
-    return write_file(dir + "/counters.u32", &c, sizeof(Counters));
-}
-
-int dump_stage_files(sift_hip_detector* d) {
-    const std::string& dir = d->dgDir;
-    if (!make_dirs(dir)) return fail(SIFT_HIP_ERR_INVALID, "cannot create " + dir);
-    const int W = d->cfg.col_width, H = d->cfg.row_width;
-    std::vector<float> buf((size_t)W * H);
-    HIPCHK(hipMemcpy(buf.data(), d->dDg, sizeof(float) * buf.size(), hipMemcpyDeviceToHost));
-    if (int rc = write_file(dir + "/input.f32", buf.data(), sizeof(float) * buf.size())) return rc;
-    std::string octs;
-    for (int o = 0; o < d->nOct; o++) {
-        const OctGeom& g = d->pyr.oct[o];
-        std::vector<float> plane((size_t)g.W * g.H);
-        for (int l = 0; l < d->L + 3; l++) {
-            HIPCHK(hipMemcpy2D(plane.data(), sizeof(float) * g.W, g.base + (size_t)l * g.planeStride,
-                               sizeof(float) * g.pitch, sizeof(float) * g.W, g.H, hipMemcpyDeviceToHost));
-            char name[64];
-            snprintf(name, sizeof name, "/gauss_o%d_l%d.f32", o, l);
-            if (int rc = write_file(dir + name, plane.data(), sizeof(float) * plane.size())) return rc;
-        }
-        char e[64];
-        snprintf(e, sizeof e, "%s[%d, %d]", o ? ", " : "", g.W, g.H);
-        octs += e;
-    }
-    const Counters& c = d->hCtr[(size_t)d->cur * d->B];
-    const int nc = (int)std::min<unsigned>(c.cand, d->capCand);
-    std::vector<uint2> cand(nc);
-    std::vector<int> quads(4 * (size_t)nc);
-    if (nc) HIPCHK(hipMemcpy(cand.data(), d->dCand, sizeof(uint2) * nc, hipMemcpyDeviceToHost));
-    for (int i = 0; i < nc; i++) {
-        quads[4 * i] = (int)(cand[i].x >> 8);
-        quads[4 * i + 1] = (int)(cand[i].x & 255);
-        quads[4 * i + 2] = (int)(cand[i].y >> 16);
-        quads[4 * i + 3] = (int)(cand[i].y & 0xffff);
-    }
-    if (int rc = write_file(dir + "/candidates.i32", quads.data(), sizeof(int) * quads.size())) return rc;
-    const int n = d->count;
-    std::vector<float> k3(3 * (size_t)n), f4(4 * (size_t)n);
-    std::vector<uint16_t> desc(128 * (size_t)n);
-    if (n) {
-        HIPCHK(hipMemcpy(k3.data(), d->dKpts3[d->cur], sizeof(float) * k3.size(), hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(f4.data(), d->dFeats4[d->cur], sizeof(float) * f4.size(), hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(desc.data(), d->dDesc[d->cur], sizeof(uint16_t) * desc.size(), hipMemcpyDeviceToHost));
-    }
-    if (int rc = write_file(dir + "/kpts3.f32", k3.data(), sizeof(float) * k3.size())) return rc;
-    if (int rc = write_file(dir + "/feats4.f32", f4.data(), sizeof(float) * f4.size())) return rc;
-    if (int rc = write_file(dir + "/desc.f16", desc.data(), sizeof(uint16_t) * desc.size())) return rc;
-    // The keypoint stages' own device records (inputs of sift_hip_replay_stage).
-    if (int rc = dump_records(d, dir)) return rc;
-    const sift_hip_config& g = d->cfg;
-    char meta[4096];
-    snprintf(meta, sizeof meta,
-             "{\n \"format\": \"sift_hip stage dump 2\",\n \"frame\": %lld,\n \"width\": %d,\n \"height\": %d,\n"
-             " \"config\": {\"numFeatures\": %d, \"numOctaveLayers\": %d, \"contrastThreshould\": %.17g,"
-             " \"edgeThreshould\": %.17g, \"sigma\": %.17g, \"upscale\": %d, \"numOctaves\": %d},\n"
-             " \"octaves\": [%s],\n \"planes_per_octave\": %d,\n \"candidates\": %d,\n \"keypoints\": %d,\n"
-             " \"overflow\": %u,\n"
-             " \"files\": {\"input.f32\": \"float32 [height][width], the frame as the pipeline read it\",\n"
-             "  \"gauss_o<o>_l<l>.f32\": \"float32 [h_o][w_o], Gaussian plane l of octave o\",\n"
-             "  \"candidates.i32\": \"int32 [candidates][4] (octave, layer, row, col) of the 3x3x3 extrema, unordered\",\n"
-             "  \"kpts3.f32\": \"float32 [keypoints][3] {x, y, layer}\",\n"
-             "  \"feats4.f32\": \"float32 [keypoints][4] {packed octave, size, response, angle}\",\n"
-             "  \"desc.f16\": \"float16 [keypoints][128], integers 0..255\",\n"
-             "  \"refined.rec\": \"RefKpt [refined] {f32 x, y, size, response; i32 octave, o, layer, r << 16 | c}\",\n"
-             "  \"oriented.rec\": \"OriKpt [slots] {f32 x, y, size, angle, response; i32 octave, bucket, sub}; "
-             "bucket 0xffffffff = hole\",\n"
-             "  \"jobs.rec\": \"DescJob [keypoints] 64 B {i64 plane o*(L+3)+layer; f32 cos_t, sin_t, angle, hist_width; "
-             "i32 ptx, pty, rows, cols, pitch, radius, out (the output row), pad[3]}; exact mode: largest windows first\",\n"
-             "  \"range.u32\": \"u32 [2][%d] pixel-range keys of the frame\",\n"
-             "  \"counters.u32\": \"u32 [8] {cand, refined, oriented, final, overflow, retainBest threshold bits, "
-             "order entries, 0}\"}\n}\n",
-             d->current - d->firstFrame, g.col_width, g.row_width, g.numFeatures, g.numOctaveLayers,
-             g.contrastThreshould, g.edgeThreshould, g.sigma, g.upscale, d->nOct, octs.c_str(), d->L + 3, nc, n,
-             c.overflow, kRangeSlots);
-    return write_file(dir + "/meta.json", meta, strlen(meta));
-}
-
-// ---------------------------------------------------------------------------
-// Per-stage replay (sift_hip_replay_stage): one stage of the pipeline on a
-// dump's recorded input, as the reference's tool/perf.cu:43-100 runs each
-// HostInterface.hh:11-69 stage on a snapshot.  Runs on frame 0's arena.
-// ---------------------------------------------------------------------------
-template <class T>
-int read_vec(const std::string& path, std::vector<T>& v) {
-    FILE* fp = fopen(path.c_str(), "rb");
-    if (!fp) return fail(SIFT_HIP_ERR_INVALID, "cannot read " + path);
-    fseek(fp, 0, SEEK_END);
-    const long bytes = ftell(fp);
-    fseek(fp, 0, SEEK_SET);
-    if (bytes < 0 || bytes % (long)sizeof(T)) {
-        fclose(fp);
-        return fail(SIFT_HIP_ERR_INVALID, path + ": size is not a whole number of records");
-    }
-    v.resize((size_t)bytes / sizeof(T));
-    const size_t got = bytes ? fread(v.data(), 1, (size_t)bytes, fp) : 0;
-    fclose(fp);
-    if (got != (size_t)bytes) return fail(SIFT_HIP_ERR_INVALID, "short read of " + path);
-    return SIFT_HIP_OK;
-}
-
-int upload_planes(sift_hip_detector* d, const std::string& dir) {
-    for (int o = 0; o < d->nOct; o++) {
-        const OctGeom& g = d->pyr.oct[o];
-        for (int l = 0; l < d->L + 3; l++) {
-            char name[64];
-            snprintf(name, sizeof name, "/gauss_o%d_l%d.f32", o, l);
-            std::vector<float> p;
-            if (int rc = read_vec(dir + name, p)) return rc;
-            if (p.size() != (size_t)g.W * g.H)
-                return fail(SIFT_HIP_ERR_INVALID, dir + name + ": plane size differs from this handle's octave geometry");
-            HIPCHK(hipMemcpy2D(g.base + (size_t)l * g.planeStride, sizeof(float) * g.pitch, p.data(), sizeof(float) * g.W,
-                               sizeof(float) * g.W, g.H, hipMemcpyHostToDevice));
-        }
-    }
-    return SIFT_HIP_OK;
-}
-
-int write_planes(sift_hip_detector* d, const std::string& dir) {
-    for (int o = 0; o < d->nOct; o++) {
-        const OctGeom& g = d->pyr.oct[o];
-        std::vector<float> plane((size_t)g.W * g.H);
-        for (int l = 0; l < d->L + 3; l++) {
-            HIPCHK(hipMemcpy2D(plane.data(), sizeof(float) * g.W, g.base + (size_t)l * g.planeStride,
-                               sizeof(float) * g.pitch, sizeof(float) * g.W, g.H, hipMemcpyDeviceToHost));
-            char name[64];
-            snprintf(name, sizeof name, "/gauss_o%d_l%d.f32", o, l);
-            if (int rc = write_file(dir + name, plane.data(), sizeof(float) * plane.size())) return rc;
-        }
-    }
-    return SIFT_HIP_OK;
-}
-
-// Returns the handle to its post-warm-up state: every scratch invariant the
-// kernels keep (zeroed counters, range keys, dedupe bitmap) restored by one
-// memset of the arenas; the handle has no current frame afterwards.
-int replay_reset(sift_hip_detector* d) {
-    bind_lane(d, 0);
-    HIPCHK(hipMemsetAsync(d->lanes[0].arena, 0, (size_t)d->afs * d->B, d->stream));
-    if (int rc = sync_lanes(d)) return rc;
-    d->firstFrame = d->submitted;
-    d->current = d->submitted - 1;
-    d->curLane = 0;
-    d->curIdx = 0;
-    d->cur = 0;
-    d->count = d->prevCount = 0;
-    d->countsValid = true;
-    return SIFT_HIP_OK;
-}
-
-// The stage itself (replay_stage below owns the handle's state around it:
-// every return from here, error or not, is followed by the restore).
-int replay_stage_body(sift_hip_detector* d, const std::string& in, const std::string& stage, const std::string& out) {
-    std::vector<Counters> dumped;  // the frame's final counters
-    if (stage != "pyramid" && stage != "extrema") {
-        if (int rc = read_vec(in + "/counters.u32", dumped)) return rc;
-        if (dumped.size() != 1) return fail(SIFT_HIP_ERR_INVALID, "counters.u32: expected one Counters record");
-    }
-    Counters c{};
-    int rc = SIFT_HIP_OK;
-    hipStream_t s = d->stream;
-    const int W = d->cfg.col_width, H = d->cfg.row_width;
-    if (stage == "pyramid") {
-        std::vector<float> img;
-        if ((rc = read_vec(in + "/input.f32", img))) return rc;
-        if (img.size() != (size_t)W * H) return fail(SIFT_HIP_ERR_INVALID, "input.f32: size differs from the config");
-        HIPCHK(hipMemcpy2D(d->dInput, sizeof(float) * d->inPitch, img.data(), sizeof(float) * W, sizeof(float) * W, H,
-                           hipMemcpyHostToDevice));
-        enqueue_head(d, d->dInput, d->inPitch, SIFT_HIP_F32, 0, 1, d->afs);
-        enqueue_pyramid(d, 1, 0);
-        HIPCHK(hipStreamSynchronize(s));
-        rc = write_planes(d, out);
-    } else if ((rc = upload_planes(d, in))) {
-        return rc;
-    } else if (stage == "extrema") {
-        enqueue_extrema(d, 1);
-        HIPCHK(hipMemcpyAsync(&c, d->dCtr, sizeof c, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        const int nc = (int)std::min<unsigned>(c.cand, d->capCand);
-        std::vector<uint2> cand(nc);
-        std::vector<int> quads(4 * (size_t)nc);
-        if (nc) HIPCHK(hipMemcpy(cand.data(), d->dCand, sizeof(uint2) * nc, hipMemcpyDeviceToHost));
-        for (int i = 0; i < nc; i++) {
-            quads[4 * i] = (int)(cand[i].x >> 8);
-            quads[4 * i + 1] = (int)(cand[i].x & 255);
-            quads[4 * i + 2] = (int)(cand[i].y >> 16);
-            quads[4 * i + 3] = (int)(cand[i].y & 0xffff);
-        }
-        rc = write_file(out + "/candidates.i32", quads.data(), sizeof(int) * quads.size());
-    } else if (stage == "refine") {
-        std::vector<int> quads;
-        if ((rc = read_vec(in + "/candidates.i32", quads))) return rc;
-        const size_t nc = quads.size() / 4;
-        if (nc > d->capCand) return fail(SIFT_HIP_ERR_INVALID, "candidates.i32: more candidates than the capacity");
-        std::vector<uint2> cand(nc);
-        for (size_t i = 0; i < nc; i++)
-            cand[i] = make_uint2((unsigned)(quads[4 * i] << 8 | quads[4 * i + 1]),
-                                 (unsigned)(quads[4 * i + 2] << 16 | quads[4 * i + 3]));
-        if (nc) HIPCHK(hipMemcpy(d->dCand, cand.data(), sizeof(uint2) * nc, hipMemcpyHostToDevice));
-        c.cand = (unsigned)nc;
-        HIPCHK(hipMemcpy(d->dCtr, &c, sizeof c, hipMemcpyHostToDevice));
-        enqueue_refine(d, 1);
-        HIPCHK(hipMemcpyAsync(&c, d->dCtr, sizeof c, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        const size_t n = std::min<unsigned>(c.refined, d->kp.capRefined);
-        std::vector<RefKpt> ref(n);
-        if (n) HIPCHK(hipMemcpy(ref.data(), d->dRef, sizeof(RefKpt) * n, hipMemcpyDeviceToHost));
-        rc = write_file(out + "/refined.rec", ref.data(), sizeof(RefKpt) * n);
-    } else if (stage == "orientation") {
-        std::vector<RefKpt> ref;
-        if ((rc = read_vec(in + "/refined.rec", ref))) return rc;
-        if (ref.size() > d->kp.capRefined) return fail(SIFT_HIP_ERR_INVALID, "refined.rec: above the capacity");
-        if (!ref.empty()) HIPCHK(hipMemcpy(d->dRef, ref.data(), sizeof(RefKpt) * ref.size(), hipMemcpyHostToDevice));
-        c.cand = dumped[0].cand;
-        c.refined = (unsigned)ref.size();
-        HIPCHK(hipMemcpy(d->dCtr, &c, sizeof c, hipMemcpyHostToDevice));
-        enqueue_orientation(d, 1);
-        HIPCHK(hipMemcpyAsync(&c, d->dCtr, sizeof c, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        const size_t n = std::min<size_t>(ref.size() + c.oriented, d->kp.capOriented);
-        std::vector<OriKpt> ori(n);
-        if (n) HIPCHK(hipMemcpy(ori.data(), d->dOri, sizeof(OriKpt) * n, hipMemcpyDeviceToHost));
-        rc = write_file(out + "/oriented.rec", ori.data(), sizeof(OriKpt) * n);
-    } else if (stage == "order") {
-        std::vector<OriKpt> ori;
-        if ((rc = read_vec(in + "/oriented.rec", ori))) return rc;
-        if (ori.size() > d->kp.capOriented) return fail(SIFT_HIP_ERR_INVALID, "oriented.rec: above the capacity");
-        if (!ori.empty()) HIPCHK(hipMemcpy(d->dOri, ori.data(), sizeof(OriKpt) * ori.size(), hipMemcpyHostToDevice));
-        c.cand = dumped[0].cand;
-        c.refined = dumped[0].refined;
-        c.oriented = dumped[0].oriented;
-        HIPCHK(hipMemcpy(d->dCtr, &c, sizeof c, hipMemcpyHostToDevice));
-        enqueue_order(d, 0, 1);
-        HIPCHK(hipMemcpyAsync(&c, d->dCtr, sizeof c, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        const size_t n = std::min<unsigned>(c.final_n, d->kp.capFinal);
-        std::vector<float> k3(3 * n), f4(4 * n);
-        std::vector<DescJob> jobs(n);
-        if (n) {
-            HIPCHK(hipMemcpy(k3.data(), d->dKpts3[0], sizeof(float) * k3.size(), hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(f4.data(), d->dFeats4[0], sizeof(float) * f4.size(), hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(jobs.data(), d->dJobs, sizeof(DescJob) * n, hipMemcpyDeviceToHost));
-        }
-        for (DescJob& j : jobs) {
-            const long long plane = job_plane(d, j.img);
-            std::memcpy(&j.img, &plane, sizeof plane);
-        }
-        if (!(rc = write_file(out + "/kpts3.f32", k3.data(), sizeof(float) * k3.size())) &&
-            !(rc = write_file(out + "/feats4.f32", f4.data(), sizeof(float) * f4.size())))
-            rc = write_file(out + "/jobs.rec", jobs.data(), sizeof(DescJob) * n);
-    } else {  // descriptor
-        std::vector<DescJob> jobs;
-        std::vector<unsigned> range;
-        if ((rc = read_vec(in + "/jobs.rec", jobs)) || (rc = read_vec(in + "/range.u32", range))) return rc;
-        if (jobs.size() > d->kp.capFinal) return fail(SIFT_HIP_ERR_INVALID, "jobs.rec: above the capacity");
-        if (range.size() != 2 * (size_t)kRangeSlots) return fail(SIFT_HIP_ERR_INVALID, "range.u32: wrong size");
-        for (DescJob& j : jobs) {
-            long long plane;
-            std::memcpy(&plane, &j.img, sizeof plane);
-            if (plane < 0 || plane >= (long long)d->nOct * (d->L + 3))
-                return fail(SIFT_HIP_ERR_INVALID, "jobs.rec: plane index out of range");
-            const OctGeom& g = d->pyr.oct[plane / (d->L + 3)];
-            j.img = g.base + (size_t)(plane % (d->L + 3)) * g.planeStride;
-        }
-        if (!jobs.empty()) HIPCHK(hipMemcpy(d->dJobs, jobs.data(), sizeof(DescJob) * jobs.size(), hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(range_keys(d, 0), range.data(), sizeof(unsigned) * range.size(), hipMemcpyHostToDevice));
-        c = dumped[0];
-        c.final_n = (unsigned)jobs.size();
-        c.pad[1] = 0;  // no host results request (HostOut)
-        HIPCHK(hipMemcpy(d->dCtr, &c, sizeof c, hipMemcpyHostToDevice));
-        enqueue_descriptor(d, 0, 1);
-        HIPCHK(hipStreamSynchronize(s));
-        std::vector<uint16_t> desc(128 * jobs.size());
-        if (!jobs.empty()) HIPCHK(hipMemcpy(desc.data(), d->dDesc[0], sizeof(uint16_t) * desc.size(), hipMemcpyDeviceToHost));
-        rc = write_file(out + "/desc.f16", desc.data(), sizeof(uint16_t) * desc.size());
-    }
-    return rc;
-}
-
-// One cleanup path: once the arenas may have been touched (uploads, kernels),
-// the handle's timing mode and its post-warm-up scratch state (counters, the
-// dedupe bitmap, range keys) are restored on every exit, including a failed
-// read, capacity check, HIP call or output write, so the next frame starts
-// clean.  The first error is the one returned (and kept in last_error).
-int replay_stage(sift_hip_detector* d, const std::string& in, const std::string& stage, const std::string& out) {
-    static const char* kStages[] = {"pyramid", "extrema", "refine", "orientation", "order", "descriptor"};
-    bool known = false;
-    for (const char* k : kStages) known |= stage == k;
-    if (!known) return fail(SIFT_HIP_ERR_INVALID, "unknown stage '" + stage + "'");
-    if (!make_dirs(out)) return fail(SIFT_HIP_ERR_INVALID, "cannot create " + out);
-    HIPCHK(hipStreamSynchronize(d->stream));
-    const bool timing = d->timing;
-    d->timing = false;
-    int rc = replay_reset(d);
-    if (!rc) rc = replay_stage_body(d, in, stage, out);
-    d->timing = timing;
-    const int rc_reset = replay_reset(d);
-    return rc ? rc : rc_reset;
+// Frames the batch accessors expose for the current frame: a batch
+// (sift_hip_detect_batch_device: one frame number, nfOf frames in arenas
+// 0..nfOf-1), or -- for a frame of a micro-batch, which has a frame number of
+// its own and whose views bind_lane already offset to its arena -- that frame
+// alone (index 0).
+int batch_frames_of(sift_hip_detector* d) {
+    if (d->current < d->firstFrame) return 0;
+    const Lane& L = d->lane();
+    return L.slotNum[d->cur] > 1 ? 1 : L.nfOf[d->cur];
 }
 
 // Every entry point starts bound to the current frame's lane (the accessors
@@ -1846,13 +778,11 @@ int replay_stage(sift_hip_detector* d, const std::string& in, const std::string&
 #define CHECK_HANDLE(h)                                                                       \
     do {                                                                                      \
         if (!(h)) return fail(SIFT_HIP_ERR_INVALID, "null handle");                          \
-        if (!(h)->allocated || !(h)->nLanes)                                                  \
+        if (!(h)->allocated || !(h)->lanes[0].ready)                                          \
             return fail(SIFT_HIP_ERR_STATE, "sift_hip_warmup not called");                    \
         HIPCHK(hipSetDevice((h)->device));                                                    \
         bind_lane((h), (h)->curLane, (h)->curIdx);                                            \
     } while (0)
-
-}  // namespace
 
 extern "C" {
 
@@ -1914,7 +844,7 @@ int sift_hip_destroy(sift_hip_t h) {
 
 int sift_hip_warmup(sift_hip_t d) {
     if (!d) return fail(SIFT_HIP_ERR_INVALID, "null handle");
-    if (d->allocated) return d->nLanes ? SIFT_HIP_OK : fail(SIFT_HIP_ERR_STATE, "an earlier warm-up failed");
+    if (d->allocated) return d->lanes[0].ready ? SIFT_HIP_OK : fail(SIFT_HIP_ERR_STATE, "an earlier warm-up failed");
     if (d->mb > 1) {  // a micro-batch runs the lane's B-frame graphs
         if (d->B > 1 && d->B != d->mb)
             return fail(SIFT_HIP_ERR_INVALID, "micro-batch and batch size differ (set one, or both equal)");
@@ -2098,15 +1028,14 @@ int sift_hip_detect_batch_device(sift_hip_t d, const void* frames, int n, size_t
 int sift_hip_batch_frames(sift_hip_t d, int* n) {
     CHECK_HANDLE(d);
     if (!n) return fail(SIFT_HIP_ERR_INVALID, "null argument");
-    *n = d->current < d->firstFrame ? 0 : d->lane().nfOf[d->cur];
+    *n = batch_frames_of(d);
     return SIFT_HIP_OK;
 }
 
 int sift_hip_batch_results_device(sift_hip_t d, int i, int* count, int* overflow, const float** k3,
                                   const float** f4, const uint16_t** desc) {
     CHECK_HANDLE(d);
-    if (d->current < d->firstFrame || i < 0 || i >= d->lane().nfOf[d->cur])
-        return fail(SIFT_HIP_ERR_INVALID, "no such frame in the current batch");
+    if (i < 0 || i >= batch_frames_of(d)) return fail(SIFT_HIP_ERR_INVALID, "no such frame in the current batch");
     if (count || overflow)
         if (int rc = ensure_counts(d)) return rc;
     const Counters& c = d->hCtr[(size_t)d->cur * d->B + i];
@@ -2145,7 +1074,7 @@ int sift_hip_sync(sift_hip_t d) {
 
 int sift_hip_num_keypoints(sift_hip_t d, int* n) {
     if (!d || !n) return fail(SIFT_HIP_ERR_INVALID, "null argument");
-    if (d->allocated && d->nLanes) {
+    if (d->allocated && d->lanes[0].ready) {
         HIPCHK(hipSetDevice(d->device));
         bind_lane(d, d->curLane, d->curIdx);
         if (int rc = ensure_counts(d)) return rc;
@@ -2156,7 +1085,7 @@ int sift_hip_num_keypoints(sift_hip_t d, int* n) {
 
 int sift_hip_overflow_flags(sift_hip_t d, int* flags) {
     if (!d || !flags) return fail(SIFT_HIP_ERR_INVALID, "null argument");
-    if (d->allocated && d->nLanes) {
+    if (d->allocated && d->lanes[0].ready) {
         HIPCHK(hipSetDevice(d->device));
         bind_lane(d, d->curLane, d->curIdx);
         if (int rc = ensure_counts(d)) return rc;
@@ -2195,7 +1124,8 @@ int sift_hip_copy_to_host(sift_hip_t d, float* k3, float* f4, uint16_t* desc, in
     Lane& L = d->lane();
     if (!d->hostWant)
         for (int k = 0; k < d->nLanes; k++)
-            if (int rc = ensure_host_res(d, d->lanes[k])) return rc;
+            if (d->lanes[k].ready)
+                if (int rc = ensure_host_res(d, d->lanes[k])) return rc;
     d->hostWant = std::max(d->hostWant, desc ? 2 : 1);
     const int region = d->cur * d->B + d->curIdx;
     if (L.hRes && L.hostFrame[region] == d->current && d->current >= d->firstFrame && (!desc || L.hostDesc[region])) {
@@ -2240,7 +1170,8 @@ int sift_hip_results_host(sift_hip_t d, const float** k3, const float** f4, cons
     Lane& L = d->lane();
     if (!d->hostWant)
         for (int k = 0; k < d->nLanes; k++)
-            if (int rc = ensure_host_res(d, d->lanes[k])) return rc;
+            if (d->lanes[k].ready)
+                if (int rc = ensure_host_res(d, d->lanes[k])) return rc;
     d->hostWant = std::max(d->hostWant, desc ? 2 : 1);
     const int region = d->cur * d->B + d->curIdx;
     float *hk3, *hf4;
@@ -2266,6 +1197,13 @@ int sift_hip_results_host(sift_hip_t d, const float** k3, const float** f4, cons
     if (f4) *f4 = hf4;
     if (desc) *desc = hdesc;
     if (count) *count = n;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_results_sidecar(sift_hip_t d, const int8_t** codes, const int** keys) {
+    CHECK_HANDLE(d);
+    if (codes) *codes = d->dSide[d->cur].codes;
+    if (keys) *keys = d->dSide[d->cur].keys;
     return SIFT_HIP_OK;
 }
 
@@ -2347,189 +1285,6 @@ int sift_hip_debug_candidates(sift_hip_t d, int* quads, int cap, int* count) {
             quads[4 * i + 3] = (int)(tmp[i].y & 0xffff);
         }
     }
-    return SIFT_HIP_OK;
-}
-
-// ----------------------------------------------------------------------------
-// Matcher
-// ----------------------------------------------------------------------------
-}  // extern "C"
-
-struct sift_hip_matcher {
-    int device = 0;
-    int maxQ = 0, maxT = 0, maxP = 0;
-    unsigned long long* dKeys = nullptr;  // running top-2 keys per (pair, query), all ones between calls
-    unsigned* dDone = nullptr;            // finished splits per (pair, 256-query block), zero between calls
-    int* dMatch = nullptr;
-    int8_t* dCodes = nullptr;             // int8 codes of a call's distinct sets (k_match_prep)
-    int* dRowKeys = nullptr;              // key bias per code row; row codeRows: the zero/padding sentinel
-    unsigned* dFlags = nullptr;           // per set slot: == epoch if the set is not all integers 0..255
-    long codeRows = 0;
-    unsigned epoch = 0;
-    bool sidecars = true;  // single pairs of detector buffers: match their sidecar codes (k_match_direct)
-    ~sift_hip_matcher() {
-        (void)hipSetDevice(device);
-        for (void* p : {(void*)dKeys, (void*)dDone, (void*)dMatch, (void*)dCodes, (void*)dRowKeys, (void*)dFlags})
-            if (p) (void)hipFree(p);
-    }
-};
-
-extern "C" {
-
-int sift_hip_matcher_create(int device, int max_query, int max_train, int max_pairs, sift_hip_matcher_t* out) {
-    if (!out || max_query <= 0 || max_train <= 0 || max_pairs <= 0 || max_pairs > kMaxMatchPairs)
-        return fail(SIFT_HIP_ERR_INVALID, "bad matcher limits");
-    *out = nullptr;
-    auto* m = new sift_hip_matcher();
-    if (device < 0) {
-        if (hipGetDevice(&m->device) != hipSuccess) m->device = 0;
-    } else {
-        m->device = device;
-    }
-    m->maxQ = max_query;
-    m->maxT = max_train;
-    m->maxP = max_pairs;
-    // Distinct sets of a call: at most 2 per pair, each at most max(maxQ, maxT) rows.
-    m->codeRows = 2L * max_pairs * std::max(max_query, max_train);
-    const size_t nkeys = 2 * (size_t)max_pairs * max_query;
-    const size_t nblk = (size_t)max_pairs * ((max_query + kMatchQB - 1) / kMatchQB);
-    if (hipSetDevice(m->device) != hipSuccess ||
-        hipMalloc((void**)&m->dKeys, sizeof(unsigned long long) * nkeys) != hipSuccess ||
-        hipMalloc((void**)&m->dDone, sizeof(unsigned) * nblk) != hipSuccess ||
-        hipMalloc((void**)&m->dMatch, sizeof(int) * (size_t)max_pairs * max_query) != hipSuccess ||
-        hipMalloc((void**)&m->dCodes, (size_t)(m->codeRows + 1) * 128) != hipSuccess ||
-        hipMalloc((void**)&m->dRowKeys, sizeof(int) * (size_t)(m->codeRows + 1)) != hipSuccess ||
-        hipMemset(m->dCodes + (size_t)m->codeRows * 128, 0, 128) != hipSuccess ||
-        hipMemcpy(m->dRowKeys + m->codeRows, &kMatchPadKey, sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMalloc((void**)&m->dFlags, sizeof(unsigned) * 2 * kMaxMatchPairs) != hipSuccess ||
-        hipMemset(m->dKeys, 0xff, sizeof(unsigned long long) * nkeys) != hipSuccess ||
-        hipMemset(m->dDone, 0, sizeof(unsigned) * nblk) != hipSuccess ||
-        hipMemset(m->dFlags, 0, sizeof(unsigned) * 2 * kMaxMatchPairs) != hipSuccess ||
-        hipDeviceSynchronize() != hipSuccess) {
-        delete m;
-        return fail(SIFT_HIP_ERR_NOMEM, "matcher allocation failed");
-    }
-    *out = m;
-    return SIFT_HIP_OK;
-}
-
-int sift_hip_matcher_set_sidecars(sift_hip_matcher_t m, int enable) {
-    if (!m) return fail(SIFT_HIP_ERR_INVALID, "null matcher");
-    m->sidecars = enable != 0;
-    return SIFT_HIP_OK;
-}
-
-int sift_hip_matcher_destroy(sift_hip_matcher_t m) {
-    delete m;
-    return SIFT_HIP_OK;
-}
-
-int sift_hip_match_batched(sift_hip_matcher_t m, int P, const uint16_t* const* q, const int* nq,
-                           const uint16_t* const* t, const int* nt, float ratio, int ratio_on_squared, int* idx2,
-                           float* d2, int* match, void* stream) {
-    if (!m || P <= 0 || P > m->maxP || !q || !nq || !t || !nt) return fail(SIFT_HIP_ERR_INVALID, "bad batch");
-    Sidecar sq{}, st{};
-    if (P == 1 && m->sidecars && nq[0] > 0 && nt[0] > 0 && nq[0] <= m->maxQ && nt[0] <= m->maxT &&
-        find_sidecar(q[0], nq[0], &sq) && find_sidecar(t[0], nt[0], &st)) {
-        // Both sets are detector buffers: their codes are ready (no conversion).
-        HIPCHK(hipSetDevice(m->device));
-        const MatchPair pr{q[0], t[0], nq[0], nt[0], 0, 0, 0, 0, 0, 0};
-        launch_match_direct(pr, sq.codes, sq.keys, st.codes, st.keys, m->dCodes + (size_t)m->codeRows * 128,
-                            m->dRowKeys + m->codeRows, m->dKeys, m->dDone, ratio, ratio_on_squared, idx2, d2, match,
-                            (hipStream_t)stream);
-        HIPCHK(hipGetLastError());
-        return SIFT_HIP_OK;
-    }
-    MatchBatch b{};
-    MatchSets sets{};
-    b.P = P;
-    // Distinct sets by pointer (a set used by several pairs is prepared once).
-    auto set_of = [&](const uint16_t* ptr, int n) {
-        for (int k = 0; k < sets.nsets; k++)
-            if (sets.set[k].src == ptr) {
-                sets.set[k].n = std::max(sets.set[k].n, n);
-                return k;
-            }
-        sets.set[sets.nsets] = MatchSet{ptr, n, 0};
-        return sets.nsets++;
-    };
-    int off = 0, maxq = 1, maxt = 1;
-    for (int p = 0; p < P; p++) {
-        if (nq[p] < 0 || nt[p] < 0 || nq[p] > m->maxQ || nt[p] > m->maxT)
-            return fail(SIFT_HIP_ERR_INVALID, "pair size exceeds matcher limits");
-        if ((nq[p] && !q[p]) || (nt[p] && !t[p])) return fail(SIFT_HIP_ERR_INVALID, "null descriptor pointer");
-        const int qs = set_of(q[p], nq[p]), ts = set_of(t[p], nt[p]);
-        b.pair[p] = MatchPair{q[p], t[p], nq[p], nt[p], off, qs, ts, 0, 0, 0};
-        off += nq[p];
-        maxq = std::max(maxq, nq[p]);
-        maxt = std::max(maxt, nt[p]);
-    }
-    long row = 0;
-    for (int k = 0; k < sets.nsets; k++) {
-        sets.set[k].row0 = (int)row;
-        row += sets.set[k].n;
-        sets.maxn = std::max(sets.maxn, sets.set[k].n);
-    }
-    if (row > m->codeRows) return fail(SIFT_HIP_ERR_INVALID, "descriptor sets exceed the matcher's code buffer");
-    for (int p = 0; p < P; p++) {
-        b.pair[p].qrow0 = sets.set[b.pair[p].qset].row0;
-        b.pair[p].trow0 = sets.set[b.pair[p].tset].row0;
-    }
-    m->epoch = m->epoch + 1 == 0 ? 1 : m->epoch + 1;  // flags from earlier calls never equal it
-    HIPCHK(hipSetDevice(m->device));
-    const MatchPlan plan = match_plan(maxq, maxt, P);
-    launch_match(sets, b, plan, m->maxQ, m->dCodes, m->dRowKeys, (int)m->codeRows, m->dFlags, m->epoch, m->dKeys, m->dDone, ratio,
-                 ratio_on_squared, idx2, d2, match, (hipStream_t)stream);
-    HIPCHK(hipGetLastError());
-    return SIFT_HIP_OK;
-}
-
-int sift_hip_match_device(sift_hip_matcher_t m, const uint16_t* q, int nq, const uint16_t* t, int nt, float ratio,
-                          int ratio_on_squared, int* idx2, float* d2, int* match, void* stream) {
-    return sift_hip_match_batched(m, 1, &q, &nq, &t, &nt, ratio, ratio_on_squared, idx2, d2, match, stream);
-}
-
-int sift_hip_match_plan(int max_query, int max_train, int pairs, int* splits, int* waves) {
-    if (max_query < 0 || max_train < 0 || pairs < 1 || !splits) return fail(SIFT_HIP_ERR_INVALID, "bad match shape");
-    const MatchPlan pl = match_plan(max_query, max_train, pairs);
-    *splits = pl.S;
-    if (waves) *waves = pl.nw;
-    return SIFT_HIP_OK;
-}
-
-int sift_hip_match_host(sift_hip_matcher_t m, const uint16_t* q, int nq, const uint16_t* t, int nt, float ratio,
-                        int ratio_on_squared, int* out) {
-    if (!m || !out) return fail(SIFT_HIP_ERR_INVALID, "null argument");
-    if (nq <= 0) return SIFT_HIP_OK;
-    int rc = sift_hip_match_device(m, q, nq, t, nt, ratio, ratio_on_squared, nullptr, nullptr, m->dMatch, nullptr);
-    if (rc) return rc;
-    HIPCHK(hipMemcpy(out, m->dMatch, sizeof(int) * nq, hipMemcpyDeviceToHost));
-    return SIFT_HIP_OK;
-}
-
-int sift_hip_device_count(int* n) {
-    if (!n) return fail(SIFT_HIP_ERR_INVALID, "null argument");
-    if (hipGetDeviceCount(n) != hipSuccess) *n = 0;
-    return SIFT_HIP_OK;
-}
-int sift_hip_malloc(void** p, size_t bytes) {
-    HIPCHK(hipMalloc(p, bytes));
-    return SIFT_HIP_OK;
-}
-int sift_hip_free(void* p) {
-    HIPCHK(hipFree(p));
-    return SIFT_HIP_OK;
-}
-int sift_hip_memcpy_h2d(void* dst, const void* src, size_t bytes) {
-    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
-    return SIFT_HIP_OK;
-}
-int sift_hip_memcpy_d2h(void* dst, const void* src, size_t bytes) {
-    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
-    return SIFT_HIP_OK;
-}
-int sift_hip_device_sync(void) {
-    HIPCHK(hipDeviceSynchronize());
     return SIFT_HIP_OK;
 }
 

@@ -79,8 +79,10 @@ void Detector::refreshViews() {
     check(sift_hip_results_device(m_handle, &k3, &f4, &desc, &prev, &prevCount, &cap), "results");
     device_kpts = DeviceBuffer<Float3>(reinterpret_cast<Float3*>(const_cast<float*>(k3)), (size_t)cap);
     device_features = DeviceBuffer<Float4>(reinterpret_cast<Float4*>(const_cast<float*>(f4)), (size_t)cap);
-    device_descriptor = DeviceBuffer<Half>(reinterpret_cast<Half*>(const_cast<uint16_t*>(desc)), (size_t)cap * 128);
-    prev_descriptor = DeviceBuffer<Half>(reinterpret_cast<Half*>(const_cast<uint16_t*>(prev)), (size_t)cap * 128);
+    // Writable descriptor views drop the rows' matcher sidecar (sift_hip.h).
+    auto written = [](const void* p) { (void)sift_hip_descriptors_written(static_cast<const uint16_t*>(p)); };
+    device_descriptor = DeviceBuffer<Half>(reinterpret_cast<Half*>(const_cast<uint16_t*>(desc)), (size_t)cap * 128, written);
+    prev_descriptor = DeviceBuffer<Half>(reinterpret_cast<Half*>(const_cast<uint16_t*>(prev)), (size_t)cap * 128, written);
     sift_hip_num_keypoints(m_handle, &total_size);
     warnOverflow();
 }

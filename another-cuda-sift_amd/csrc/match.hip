@@ -610,7 +610,8 @@ __global__ __launch_bounds__(64 * NW, (kMatchWgPerCu * NW) / 4) void k_match_sin
 template <int NW, int QBW>
 __global__ __launch_bounds__(64 * NW, (kMatchBatchWgPerCu * NW) / 4) void k_match_batch(
     MatchBatch batch, int S, int nq_stride, const int8_t* __restrict__ codes, const int* __restrict__ rowkeys,
-    int sentinel, const unsigned* __restrict__ flags, unsigned epoch, unsigned long long* __restrict__ keys,
+    const int8_t* __restrict__ zc, const int* __restrict__ zk, const unsigned* __restrict__ flags, unsigned epoch,
+    unsigned long long* __restrict__ keys,
     unsigned* __restrict__ done, float ratio, int ratio_on_squared, int* __restrict__ idx2, float* __restrict__ d2out,
     int* __restrict__ match) {
     constexpr int QB = 32 * QBW * NW;  // queries per workgroup
@@ -630,15 +631,14 @@ __global__ __launch_bounds__(64 * NW, (kMatchBatchWgPerCu * NW) / 4) void k_matc
     const int tb = min(ntiles, (int)blockIdx.y * tps), te = min(ntiles, tb + tps);
     const int q0w = q0 + 32 * QBW * w;
     Top2 res[QBW];
-    if (flags[pr.qset] != epoch && flags[pr.tset] != epoch) {
-        // ---- integer path ----
+    // flags == nullptr: code sets handed over ready (sift_hip_match_codes_batched), integers by construction.
+    if (!flags || (flags[pr.qset] != epoch && flags[pr.tset] != epoch)) {
+        // ---- integer path (zc / zk: the zero code row and padding key) ----
         const int8_t* __restrict__ tc = codes + (size_t)pr.trow0 * 128;
-        const int* __restrict__ tk = rowkeys + pr.trow0;
-        const int8_t* __restrict__ zc = codes + (size_t)sentinel * 128;  // zero code row (padding)
-        const int* __restrict__ zk = rowkeys + sentinel;
+        const int* __restrict__ tk = rowkeys + pr.tkrow0;
         i32x4 bq[QBW][4];
         int qn[QBW];
-        load_queries<QBW>(codes + (size_t)pr.qrow0 * 128, rowkeys + pr.qrow0, pr.nq, q0w, col, h, bq, qn);
+        load_queries<QBW>(codes + (size_t)pr.qrow0 * 128, rowkeys + pr.qkrow0, pr.nq, q0w, col, h, bq, qn);
         Best best[QBW];
 #pragma unroll
         for (int qb = 0; qb < QBW; qb++) best[qb] = Best{kNone, kNone, kNone, kNone};
@@ -869,7 +869,19 @@ void launch_match(const MatchSets& sets, MatchBatch& batch, const MatchPlan& pla
     for (int p = 0; p < batch.P; p++) max_nq = max(max_nq, batch.pair[p].nq);
     dim3 g((max_nq + kMatchBatchQB - 1) / kMatchBatchQB, plan.S, batch.P);
     hipLaunchKernelGGL((k_match_batch<kMatchBatchNW, kMatchBatchQBW>), g, dim3(64 * kMatchBatchNW), 0, s, batch, plan.S, nq_stride, codes,
-                       rowkeys, sentinel, flags, epoch, keys, done, ratio, ratio_on_squared, idx2, d2, match);
+                       rowkeys, codes + (size_t)sentinel * 128, rowkeys + sentinel, flags, epoch, keys, done, ratio,
+                       ratio_on_squared, idx2, d2, match);
+}
+
+void launch_match_codes(MatchBatch& batch, const MatchPlan& plan, int nq_stride, const int8_t* codes, const int* rowkeys,
+                        const int8_t* zc, const int* zk, unsigned long long* keys, unsigned* done, float ratio,
+                        int ratio_on_squared, int* idx2, float* d2, int* match, hipStream_t s) {
+    int max_nq = 1;
+    for (int p = 0; p < batch.P; p++) max_nq = max(max_nq, batch.pair[p].nq);
+    dim3 g((max_nq + kMatchBatchQB - 1) / kMatchBatchQB, plan.S, batch.P);
+    hipLaunchKernelGGL((k_match_batch<kMatchBatchNW, kMatchBatchQBW>), g, dim3(64 * kMatchBatchNW), 0, s, batch, plan.S,
+                       nq_stride, codes, rowkeys, zc, zk, (const unsigned*)nullptr, 0u, keys, done, ratio, ratio_on_squared,
+                       idx2, d2, match);
 }
 
 }  // namespace sift_amd

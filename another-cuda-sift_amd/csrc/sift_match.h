@@ -19,10 +19,11 @@ struct MatchPair {
     int out_off;        // output row offset of this pair
     int qset, tset;     // this call's prepared sets (k_match_prep) holding q and t
     int qrow0, trow0;   // their first int8 code row
-    int pad;
+    int qkrow0, tkrow0; // their first key bias (prepared sets: = qrow0 / trow0; gathered code buffers may differ)
 };
+static_assert(sizeof(MatchPair) == 56, "kernarg layout");
 
-// Passed by value: lives in the kernarg segment (64 x 48 B = 3 KiB).
+// Passed by value: lives in the kernarg segment (64 x 56 B = 3.5 KiB).
 struct MatchBatch {
     MatchPair pair[kMaxMatchPairs];
     int P;
@@ -66,5 +67,14 @@ void launch_match_direct(const MatchPair& pr, const int8_t* qc, const int* qk, c
                          const int8_t* zc, const int* zk, unsigned long long* keys, unsigned* done, float ratio,
                          int ratio_on_squared, int* idx2, float* d2, int* match, hipStream_t s);
 int match_direct_splits(int nq, int nt);
+
+// Pairs of ready code sets (e.g. the sidecars of every rank all-gathered: C5):
+// k_match_batch on them with no prep launch and no flags (integers by
+// construction); pair p reads code rows qrow0.. / trow0.. of `codes` and key
+// biases qkrow0.. / tkrow0.. of `rowkeys`.  zc / zk: the zero code row and
+// padding key.
+void launch_match_codes(MatchBatch& batch, const MatchPlan& plan, int nq_stride, const int8_t* codes, const int* rowkeys,
+                        const int8_t* zc, const int* zk, unsigned long long* keys, unsigned* done, float ratio,
+                        int ratio_on_squared, int* idx2, float* d2, int* match, hipStream_t s);
 
 }  // namespace sift_amd

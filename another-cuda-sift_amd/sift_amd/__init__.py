@@ -115,6 +115,9 @@ def lib() -> ctypes.CDLL:
         "sift_hip_copy_to_host": (i, [vp, vp, vp, vp, i]),
         "sift_hip_results_host": (i, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), ip]),
         "sift_hip_copy_descriptors_device": (i, [vp, vp, i, vp]),
+        "sift_hip_results_sidecar": (i, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp)]),
+        "sift_hip_descriptors_written": (i, [vp]),
+        "sift_hip_match_codes_batched": (i, [vp, vp, vp, i, vp, vp, vp, vp, vp, vp, f, i, vp, vp, vp, vp]),
         "sift_hip_set_datagen": (i, [vp, ctypes.c_char_p]),
         "sift_hip_replay_stage": (i, [vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]),
         "sift_hip_set_timing": (i, [vp, i]),
@@ -211,12 +214,20 @@ class CudaSiftConfig:
 
 
 class DeviceBuffer:
-    """Non-owning device array view (stands in for thrust::device_vector)."""
+    """Non-owning device array view (stands in for thrust::device_vector).
+    data() is for reading; a caller that writes into a detector's descriptor
+    buffer takes mutable_data(), which drops the buffer's matcher sidecar
+    (sift_hip_descriptors_written) so matches convert the written rows."""
 
-    def __init__(self, ptr: int, size: int):
-        self.ptr, self._size = int(ptr or 0), int(size)
+    def __init__(self, ptr: int, size: int, descriptors: bool = False):
+        self.ptr, self._size, self._desc = int(ptr or 0), int(size), descriptors
 
     def data(self) -> int:
+        return self.ptr
+
+    def mutable_data(self) -> int:
+        if self._desc and self.ptr:
+            _check(lib().sift_hip_descriptors_written(self.ptr), "descriptors_written")
         return self.ptr
 
     def size(self) -> int:
@@ -299,8 +310,8 @@ class Detector:
             self._views = key
             self.device_kpts = DeviceBuffer(k3.value, cap.value)
             self.device_features = DeviceBuffer(f4.value, cap.value)
-            self.device_descriptor = DeviceBuffer(d.value, cap.value * 128)
-            self.prev_descriptor = DeviceBuffer(pd.value, cap.value * 128)
+            self.device_descriptor = DeviceBuffer(d.value, cap.value * 128, descriptors=True)
+            self.prev_descriptor = DeviceBuffer(pd.value, cap.value * 128, descriptors=True)
         self.prev_size = pc.value
         L.sift_hip_num_keypoints(self._h, refs[6])
         self.total_size = n.value
@@ -394,6 +405,13 @@ class Detector:
                "detectBatchDevice")
         if sync:
             self.sync()
+
+    def results_sidecar(self):
+        """(codes, keys) device pointers of the current frame's matcher sidecar (sift_hip_results_sidecar):
+        int8 codes v - 128 per descriptor row (128 B) and int32 key biases -(256 |c|^2 + (row & 255))."""
+        c, k = ctypes.c_void_p(), ctypes.c_void_p()
+        _check(lib().sift_hip_results_sidecar(self._h, ctypes.byref(c), ctypes.byref(k)), "results_sidecar")
+        return c.value, k.value
 
     def batch_frames(self) -> int:
         n = ctypes.c_int()
@@ -552,6 +570,19 @@ class Matcher:
         ma = (ctypes.c_int * P)(*nts)
         _check(lib().sift_hip_match_batched(self._m, P, qa, na, ta, ma, ratio, int(ratio_on_squared),
                                             idx2_ptr or None, d2_ptr or None, match_ptr or None, stream), "match_batched")
+
+    def match_codes_batched(self, codes_ptr: int, keys_ptr: int, pairs: Sequence, ratio: float = 0.8,
+                            ratio_on_squared: bool = False, idx2_ptr: int = 0, d2_ptr: int = 0, match_ptr: int = 0,
+                            stream: Optional[int] = None) -> None:
+        """Pairs (qrow0, qkey0, nq, trow0, tkey0, nt) of ready code sets -- int8 codes (128 B rows from code row
+        qrow0 / trow0) and int32 key biases (from key index qkey0 / tkey0), e.g. every rank's sidecar all-gathered
+        (multi.all_gather_codes / multi.code_pairs) -- in ONE launch, no conversion
+        (sift_hip_match_codes_batched).  Outputs packed per pair as match_batched."""
+        P = len(pairs)
+        qr, qk, nq, tr, tk, nt = ((ctypes.c_int * P)(*[p[k] for p in pairs]) for k in range(6))
+        _check(lib().sift_hip_match_codes_batched(self._m, codes_ptr, keys_ptr, P, qr, qk, nq, tr, tk, nt, ratio,
+                                                  int(ratio_on_squared), idx2_ptr or None, d2_ptr or None,
+                                                  match_ptr or None, stream), "match_codes_batched")
 
     def match_host(self, q_ptr: int, nq: int, t_ptr: int, nt: int, ratio: float = 0.8, ratio_on_squared: bool = True) -> np.ndarray:
         out = np.full(max(nq, 0), -1, np.int32)

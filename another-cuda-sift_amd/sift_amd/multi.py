@@ -66,6 +66,84 @@ def all_gather_sets(local: torch.Tensor, count: int, world: int, group=None) -> 
     return all_gather_rows(local, world, group), counts
 
 
+# ---- C5 exchange of matcher codes instead of fp16 rows ---------------------
+# Every detector frame's descriptor kernel also writes the matcher's int8 code
+# row c = v - 128 (128 B) and key bias -(256 |c|^2 + (row & 255)) (4 B) beside
+# the fp16 row (Detector.results_sidecar): 132 B per row instead of 256, and
+# the receivers match them as they arrive (Matcher.match_codes_batched: no
+# conversion launch).  One collective per exchange: each rank sends one packed
+# block [n_pad code rows | n_pad keys], n_pad = n rounded up to CODE_ROWS so
+# the block is whole 128-B code rows (32 x 132 B = 33 x 128 B).
+CODE_ROWS = 32
+
+
+def codes_from_rows(rows: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(codes int8 (n, 128), keys int32 (n,)) of fp16 descriptor rows holding
+    integers 0..255 -- the sidecar's definition, for rows no detector wrote
+    (padding, foreign sets)."""
+    v = rows.view(torch.float16).to(torch.int32)
+    c = v - 128
+    r = torch.arange(rows.shape[0], dtype=torch.int32, device=rows.device)
+    keys = -(256 * (c * c).sum(dim=1, dtype=torch.int32) + (r & 255))
+    return c.to(torch.int8), keys.to(torch.int32)
+
+
+def code_block_rows(n: int) -> int:
+    return (n + CODE_ROWS - 1) // CODE_ROWS * CODE_ROWS
+
+
+def pack_codes(codes: torch.Tensor, keys: torch.Tensor, n_pad: int) -> torch.Tensor:
+    """One rank's send block: uint8 [n_pad * 132] = n_pad code rows, then n_pad keys."""
+    n = codes.shape[0]
+    blk = torch.zeros(n_pad * 132, dtype=torch.uint8, device=codes.device)
+    blk[: n * 128] = codes.contiguous().view(torch.uint8).reshape(-1)
+    blk[n_pad * 128: n_pad * 128 + n * 4] = keys.contiguous().view(torch.uint8).reshape(-1)
+    return blk
+
+
+def code_set(r: int, n_pad: int) -> Tuple[int, int]:
+    """(first code row, first key index) of rank r's set in a gathered buffer."""
+    return r * n_pad * 132 // 128, (r * n_pad * 132 + n_pad * 128) // 4
+
+
+def all_gather_codes(codes: torch.Tensor, keys: torch.Tensor, world: int, group=None) -> Tuple[torch.Tensor, int]:
+    """All-gather every rank's (n, 128) int8 codes and (n,) int32 keys (same n
+    on all ranks) as ONE collective: returns (the gathered uint8 buffer of
+    world blocks, n_pad); set r's codes start at code row code_set(r)[0] and its
+    keys at key index code_set(r)[1] of that buffer."""
+    n_pad = code_block_rows(codes.shape[0])
+    blk = pack_codes(codes, keys, n_pad)
+    if world == 1 and not dist.is_initialized():
+        return blk, n_pad
+    if dist.get_backend(group) == "nccl":
+        out = torch.empty(world * blk.numel(), dtype=torch.uint8, device=blk.device)
+        dist.all_gather_into_tensor(out, blk, group=group)
+    else:  # gloo (CPU tests)
+        parts = [torch.empty_like(blk) for _ in range(world)]
+        dist.all_gather(parts, blk, group=group)
+        out = torch.cat(parts)
+    return out, n_pad
+
+
+def unpack_codes(buf: torch.Tensor, r: int, n: int, n_pad: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Rank r's (codes, keys) back from a gathered buffer (tests, CPU matchers)."""
+    base = r * n_pad * 132
+    codes = buf[base: base + n * 128].view(torch.int8).reshape(n, 128)
+    keys = buf[base + n_pad * 128: base + n_pad * 128 + n * 4].view(torch.int32)
+    return codes, keys
+
+
+def code_pairs(counts: Sequence[int], rank: int, world: int, n_pad: int) -> List[Tuple[int, int, int, int, int, int]]:
+    """This rank's C5 pairs over a gathered code buffer, as
+    Matcher.match_codes_batched takes them: (qrow0, qkey0, nq, trow0, tkey0, nt)."""
+    q0, qk = code_set(rank, n_pad)
+    out = []
+    for _, j in peer_pairs(rank, world):
+        t0, tk = code_set(j, n_pad)
+        out.append((q0, qk, counts[rank], t0, tk, counts[j]))
+    return out
+
+
 MatchFn = Callable[[Sequence[torch.Tensor], Sequence[int], Sequence[torch.Tensor], Sequence[int]], List[torch.Tensor]]
 
 

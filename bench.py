@@ -76,6 +76,10 @@ def parse():
                          "rocprofv3 --kernel-trace --stats summary is committed beside the roofline numbers")
     ap.add_argument("--traffic-summary", default=os.path.join(ROOT, "profiles", "round5", "pmc_summary.json"),
                     help="PMC summary (tools/pmc_summary.py) with FETCH_SIZE/WRITE_SIZE of this code")
+    ap.add_argument("--cv-traffic-summary",
+                    default=os.path.join(ROOT, "profiles", "round6", "pmc_summary_cvdefault.json"),
+                    help="PMC summary of the OpenCV-default leg (tools/pmc.sh ... --upscale --octaves 0 --features 0)")
+    ap.add_argument("--no-cv-default", action="store_true", help="skip the OpenCV-default configuration leg")
     ap.add_argument("--exact-descriptors", action="store_true",
                     help="run the C2 steps in the exact descriptor mode (SIFT_HIP_DESC_EXACT) instead of the default")
     ap.add_argument("--allow-ab-build", action="store_true",
@@ -463,7 +467,7 @@ def window_bytes(kpts3, feats4, first_octave=0):
     return float(ori.sum()), float(desc.sum()), len(uniq)
 
 
-def kernel_rooflines(det, timing, steps, B, pmc_path):
+def kernel_rooflines(det, timing, steps, B, pmc_path, first_octave=0):
     """Per-kernel roofline entries of the C2 step (eager timing pass, HIP
     events on the detector's stream): algorithmic bytes per launch / average
     launch time against the 8 TB/s HBM peak, with the committed PMC summary's
@@ -472,7 +476,7 @@ def kernel_rooflines(det, timing, steps, B, pmc_path):
     ori_b = desc_b = 0.0
     refined = 0
     for k3, f4, _ in per_frame:
-        o, d, n = window_bytes(k3, f4)
+        o, d, n = window_bytes(k3, f4, first_octave)
         ori_b += o
         desc_b += d
         refined += n
@@ -649,6 +653,53 @@ def main():
                  "note": "same C2 steps with sift_hip_set_descriptor_mode(SIFT_HIP_DESC_EXACT): descriptors "
                          "bit-identical to the oracle (tests/test_gpu_parity.py::test_exact_descriptors_bitexact)"}
     del detx
+
+    # ---- C2 at OpenCV's defaults: upscale (firstOctave -1), numFeatures 0 ----
+    # (SURVEY 8d's secondary C2 row; the configuration the parity bar is defined
+    # on, reference Detector.cu:235-252 / CudaSiftConfig.hh:12-13.)  Same frames,
+    # batches and streams as C2; its own eager stage table and per-kernel
+    # rooflines (a 4x base plane, ~4x the keypoints of the 5000-feature cap).
+    def cv_default_leg():
+        cfgd = make_config(upscale=True, numFeatures=0, numOctaves=0)
+        detd = [sift.Detector(cfgd, device=local, batch=B, lanes=1) for _ in range(nstreams)]
+        for d in detd:
+            d.gpuWarmUpAndAllocate()
+
+        def stepd(s):
+            detd[s % len(detd)].detectBatchDevice(fb.data_ptr(), B, stride, W * H * 4, sync=False)
+
+        for s in range(2 * len(detd)):
+            stepd(s)
+        for d in detd:
+            d.sync()
+        nd = max(a.steps // 4, 1)
+        barrier()
+        t = time.perf_counter()
+        for s in range(nd):
+            stepd(s)
+        for d in detd:
+            d.sync()
+        td = max_over_ranks(time.perf_counter() - t)
+        kpf = detd[0].total_size
+        octs = detd[0].nOctaves
+        rld = measure_roofline(detd[0], frames, stride, a.cv_traffic_summary, nt=6, batch=fb)
+        nt_d = rld["frames"] * B
+        stages_d = stage_table(rld["timing"], nt_d)
+        rk_d = kernel_rooflines(detd[0], rld["timing"], rld["frames"], B, a.cv_traffic_summary, first_octave=-1)
+        return {"value": round(world * nd * B * W * H / 1e6 / td, 2), "unit": "Mpix/s",
+                "ms_per_frame": round(td / (nd * B) * 1e3, 4), "steps": nd, "frames_per_launch": B,
+                "streams": len(detd), "octaves": octs, "keypoints_per_frame": kpf,
+                "stage_us_per_frame_eager": stages_d, "stage_sum_us_eager": round(sum(stages_d.values()), 1),
+                "dominant_stage": next(iter(stages_d)), "roofline_kernels": rk_d,
+                "note": "1920x1200 frames (the C2 batch) with OpenCV's cv::SIFT defaults: upscale=true (2x INTER_LINEAR "
+                        "base, firstOctave -1), numFeatures=0 (keep all), auto octaves; fixed-point descriptors"}
+
+    cv_default = None
+    if not a.no_cv_default:
+        try:
+            cv_default = cv_default_leg()
+        except Exception as e:  # noqa: BLE001 -- side leg: keep the C2 line
+            cv_default = {"error": repr(e)[:300]}
 
     # ---- C4: 256 synthetic 1600x900 frames sharded per image over the ranks -------
     W4, H4, N4 = 1600, 900, 256
@@ -838,12 +889,21 @@ def main():
     # ---- C3: 2000 x 2000 x 128 match -----------------------------------------
     det2 = sift.Detector(make_config(numOctaves=0), device=local)
     det2.gpuWarmUpAndAllocate()
-    sets = []
+    sets, sets_codes = [], []
     # C3 uses sets 0 and 1; C5 uses set k on rank k (world > 1), or all 8 on
-    # one GPU (world == 1 rehearsal).
+    # one GPU (world == 1 rehearsal).  Each set also keeps the detector's
+    # matcher sidecar rows (int8 codes + key biases: what C5 exchanges).
     for i in range(8 if world == 1 else max(2, world)):
         det2.detectAndCompute(sift.synth_frame(77 + i, W, H))
         det2.copyToHost(True)
+        nsc = min(det2.total_size, 2000)
+        cp, kp = det2.results_sidecar()
+        sc = torch.empty((2000, 128), dtype=torch.int8, device=dev)
+        sk = torch.empty(2000, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        if nsc:
+            sift._check(sift.lib().sift_hip_memcpy_d2d(sc.data_ptr(), cp, nsc * 128, None), "sidecar codes")
+            sift._check(sift.lib().sift_hip_memcpy_d2d(sk.data_ptr(), kp, nsc * 4, None), "sidecar keys")
         d = det2.descriptors[:2000]
         if len(d) < 2000:  # pad with seeded SIFT-like rows (normalised, clipped, x512, rounded)
             rng = np.random.default_rng(i)
@@ -853,6 +913,11 @@ def main():
             v = np.round(np.clip(v / np.linalg.norm(v, axis=1, keepdims=True) * 512, 0, 255))
             d = np.concatenate([d.astype(np.float32), v.astype(np.float32)]).astype(np.float16)
         sets.append(torch.from_numpy(np.ascontiguousarray(d).view(np.int16)).to(dev))
+        if nsc < 2000:  # padding rows: their codes as the sidecar defines them
+            pc, pk = multi.codes_from_rows(sets[-1])  # (set-local row indices in the key biases)
+            sc[nsc:], sk[nsc:] = pc[nsc:], pk[nsc:]
+        sets_codes.append((sc, sk))
+    torch.cuda.synchronize()
     nq = 2000
     matcher = sift.Matcher(nq, nq, max_pairs=8, device=local)
     out_idx = torch.empty((nq, 2), dtype=torch.int32, device=dev)
@@ -915,78 +980,97 @@ def main():
                  "matches": int((out_m[:n0d] >= 0).sum().item())}
 
     # ---- C5: 8-way (world-way) all-gather + pairwise match -------------------
+    def time_ms(fn, reps):
+        for _ in range(5):
+            fn()
+        torch.cuda.synchronize()
+        m0, m1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        m0.record()
+        for _ in range(reps):
+            fn()
+        m1.record()
+        torch.cuda.synchronize()
+        return m0.elapsed_time(m1) / reps
+
+    def c5_codes_matcher(buf, pairs, P):
+        bm = sift.Matcher(nq, nq, max_pairs=P, device=local)
+        bi = torch.empty((P * nq, 2), dtype=torch.int32, device=dev)
+        return lambda: bm.match_codes_batched(buf.data_ptr(), buf.data_ptr(), pairs, idx2_ptr=bi.data_ptr(),
+                                              stream=torch.cuda.current_stream().cuda_stream)
+
     def run_c5_single_gpu(K=8):
-        """world == 1: the 8 sets are already on this GPU (no exchange); all
-        K * (K - 1) ordered pairs in ONE batched MFMA launch."""
+        """world == 1: the 8 sets are already on this GPU (no exchange).  The
+        56 ordered pairs of the 8-way match in ONE batched launch (fp16 rows,
+        converted by k_match_prep, and the exchanged codes), and rank 0's share
+        at N = 8 -- its set against the 7 others -- which is what one GPU runs
+        per exchange on the 8-GPU node: the per-GPU C5 figure."""
         pairs = [(i, j) for i in range(K) for j in range(K) if i != j]
         P = len(pairs)
         bm = sift.Matcher(nq, nq, max_pairs=P, device=local)
         bi = torch.empty((P * nq, 2), dtype=torch.int32, device=dev)
 
-        def batched():
-            bm.match_batched([sets[i].data_ptr() for i, _ in pairs], [nq] * P, [sets[j].data_ptr() for _, j in pairs],
-                             [nq] * P, idx2_ptr=bi.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+        def batched(pp):
+            bm.match_batched([sets[i].data_ptr() for i, _ in pp], [nq] * len(pp), [sets[j].data_ptr() for _, j in pp],
+                             [nq] * len(pp), idx2_ptr=bi.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
 
-        for _ in range(5):
-            batched()
-        torch.cuda.synchronize()
-        m0, m1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        reps = 20
-        m0.record()
-        for _ in range(reps):
-            batched()
-        m1.record()
-        torch.cuda.synchronize()
-        ms = m0.elapsed_time(m1) / reps
-        fl = 2.0 * nq * nq * 128 * P
-        return {"virtual_ranks": K, "pairs_per_gpu": P, "batched_match_ms": round(ms, 4), "allgather_us": None,
-                "tops": round(fl / ms / 1e9, 2), "mfma_frac": round(fl / ms / 1e9 / I8_MFMA_PEAK_TOPS, 4),
-                "note": "one-GPU rehearsal of C5: all 8 sets resident, the 56 ordered 2000x2000x128 pairs in one "
-                        "batched launch (no collective on one GPU)"}
+        ms56 = time_ms(lambda: batched(pairs), 20)
+        mine7 = [(0, j) for j in range(1, K)]
+        ms7_f16 = time_ms(lambda: batched(mine7), 50)
+        # The gathered codes buffer as multi.all_gather_codes lays it out (K blocks).
+        n_pad = multi.code_block_rows(nq)
+        buf = torch.cat([multi.pack_codes(c, k, n_pad) for c, k in sets_codes[:K]])
+        counts = [nq] * K
+        code56 = [p for r in range(K) for p in multi.code_pairs(counts, r, K, n_pad)]
+        ms56_codes = time_ms(c5_codes_matcher(buf, code56, P), 20)
+        ms7 = time_ms(c5_codes_matcher(buf, multi.code_pairs(counts, 0, K, n_pad), K - 1), 50)
+        fl, fl7 = 2.0 * nq * nq * 128 * P, 2.0 * nq * nq * 128 * (K - 1)
+        return {"virtual_ranks": K, "pairs_per_gpu": K - 1, "allgather_us": None,
+                "pairs7_ms": round(ms7, 4), "pairs7_tops": round(fl7 / ms7 / 1e9, 2),
+                "pairs7_frac": round(fl7 / ms7 / 1e9 / I8_MFMA_PEAK_TOPS, 4), "pairs7_fp16_prep_ms": round(ms7_f16, 4),
+                "pairs56_ms": round(ms56_codes, 4), "pairs56_frac": round(fl / ms56_codes / 1e9 / I8_MFMA_PEAK_TOPS, 4),
+                "pairs56_fp16_prep_ms": round(ms56, 4),
+                "batched_match_ms": round(ms7, 4), "tops": round(fl7 / ms7 / 1e9, 2),
+                "mfma_frac": round(fl7 / ms7 / 1e9 / I8_MFMA_PEAK_TOPS, 4),
+                "exchange": "int8 codes + key biases (132 B/row, detector sidecars, multi.all_gather_codes layout)",
+                "note": "one-GPU rehearsal of C5: pairs7 = one GPU's share at N = 8 (its set x the 7 gathered ones, "
+                        "sift_hip_match_codes_batched, no conversion), the per-GPU C5 figure; pairs56 = all 56 "
+                        "ordered pairs in one launch; *_fp16_prep = the same pairs from fp16 rows (k_match_prep + "
+                        "k_match_batch)"}
 
     def run_c5():
-        mine = sets[rank].contiguous()
-        counts = multi.all_gather_counts(nq, world, cdev)  # once; the exchange itself is the rows
+        """world > 1: every rank all-gathers the detector's matcher codes (one
+        RCCL all_gather_into_tensor of a 2016 x 132 B block per rank, 266 KB
+        instead of 512 KB of fp16 rows) and matches its set against the
+        world - 1 gathered ones in one launch, no conversion."""
+        mine_c, mine_k = sets_codes[rank]
+        counts = multi.all_gather_counts(nq, world, cdev)  # once; the exchange itself is the block
 
         def gather():
-            return multi.all_gather_rows(mine.to(cdev), world).to(dev)
+            return multi.all_gather_codes(mine_c.to(cdev), mine_k.to(cdev), world)
 
         for _ in range(5):
-            gathered = gather()
+            buf, n_pad = gather()
         torch.cuda.synchronize()
         barrier()
         ag0, ag1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ag0.record()
         for _ in range(20):
-            gathered = gather()
+            buf, n_pad = gather()
         ag1.record()
         torch.cuda.synchronize()
         ag_us = max_over_ranks(ag0.elapsed_time(ag1) / 20 * 1e3)
         assert counts == [nq] * world
-        peers = [j for _, j in multi.peer_pairs(rank, world)]
-        P = len(peers)
-        bi = torch.empty((P * nq, 2), dtype=torch.int32, device=dev)
-        bm = sift.Matcher(nq, nq, max_pairs=P, device=local)
-
-        def batched():
-            bm.match_batched([mine.data_ptr()] * P, [nq] * P, [gathered[j].data_ptr() for j in peers], [nq] * P,
-                             idx2_ptr=bi.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
-
-        for _ in range(10):
-            batched()
-        torch.cuda.synchronize()
-        m0, m1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        m0.record()
-        for _ in range(50):
-            batched()
-        m1.record()
-        torch.cuda.synchronize()
-        bms = max_over_ranks(m0.elapsed_time(m1) / 50)
+        buf = buf.to(dev)
+        pairs = multi.code_pairs(counts, rank, world, n_pad)
+        P = len(pairs)
+        bms = max_over_ranks(time_ms(c5_codes_matcher(buf, pairs, P), 50))
         fl = 2.0 * nq * nq * 128 * P
-        return {"allgather_us": round(ag_us, 2), "allgather_bytes_per_rank": nq * 128 * 2, "pairs_per_gpu": P,
-              "batched_match_ms": round(bms, 4), "tops_per_gpu": round(fl / bms / 1e9, 2),
-              "mfma_frac": round(fl / bms / 1e9 / I8_MFMA_PEAK_TOPS, 4),
-              "collective": f"all_gather ({a.dist_backend}; nccl = RCCL all_gather_into_tensor), sift_amd/multi.py"}
+        return {"allgather_us": round(ag_us, 2), "allgather_bytes_per_rank": n_pad * 132, "pairs_per_gpu": P,
+                "batched_match_ms": round(bms, 4), "tops_per_gpu": round(fl / bms / 1e9, 2),
+                "mfma_frac": round(fl / bms / 1e9 / I8_MFMA_PEAK_TOPS, 4),
+                "exchange": "int8 codes + key biases (132 B/row, detector sidecars)",
+                "collective": f"all_gather ({a.dist_backend}; nccl = RCCL all_gather_into_tensor), "
+                              "sift_amd/multi.py all_gather_codes"}
 
     try:
         c5 = run_c5() if world > 1 else run_c5_single_gpu()
@@ -994,10 +1078,13 @@ def main():
         c5 = {"error": repr(e)[:300]}
     if isinstance(rk, dict) and "batched_match_ms" in c5:
         ops = 2.0 * nq * nq * 128 * c5["pairs_per_gpu"]
-        rk["matcher"] = {"bound": "mfma", "kernel": "k_match_prep + k_match (C5 batched launch)",
+        rk["matcher"] = {"bound": "mfma",
+                         "kernel": "k_match_batch on exchanged codes: one GPU's C5 share (its set x the world - 1 "
+                                   "others, 7 pairs at N = 8), no conversion launch",
                          "algo_ops_per_launch": ops, "avg_launch_us": round(c5["batched_match_ms"] * 1e3, 3),
                          "achieved": round(ops / c5["batched_match_ms"] / 1e9, 1), "peak": I8_MFMA_PEAK_TOPS,
                          "unit": "TOPS", "frac": round(ops / c5["batched_match_ms"] / 1e9 / I8_MFMA_PEAK_TOPS, 4),
+                         "pairs56_frac": c5.get("pairs56_frac"),
                          "c3_single_pair_frac": round(flops / match_ms / 1e9 / I8_MFMA_PEAK_TOPS, 5)}
 
     # ---- CPU baseline: the oracle on the host cores (rank 0, N=1 only) -------
@@ -1044,6 +1131,7 @@ def main():
             "sync_ms_per_frame": round(sync_ms, 4),
             "single_stream": {"value": round(single_value, 2), "ms_per_frame": round(single / n1 * 1e3, 4)},
             "exact_descriptors": exact_leg,
+            "opencv_default_1920x1200": cv_default,
             "host_input": host_input,
             "device_submit": device_submit,
             "stage_us_per_frame_eager": stages,

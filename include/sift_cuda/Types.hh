@@ -44,18 +44,28 @@ struct Half {
 static_assert(sizeof(Float3) == 12 && sizeof(Float4) == 16 && sizeof(Half) == 2, "layout");
 
 // Non-owning view of a device array owned by a Detector (stands in for the
-// reference's thrust::device_vector members; data()/size() as there).
+// reference's thrust::device_vector members, Detector.hh:54-57; data()/size()
+// as there).  data() is read-only: the detector derives data from what it
+// writes (the matcher's int8 sidecar of the descriptor rows), so a caller that
+// writes takes mutable_data(), which tells the detector (for descriptor
+// buffers, sift_hip_descriptors_written: matches then convert those rows).
 template <class T>
 class DeviceBuffer {
 public:
+    using WriteHook = void (*)(const void*);
     DeviceBuffer() = default;
-    DeviceBuffer(T* p, size_t n) : ptr_(p), n_(n) {}
-    T* data() const { return ptr_; }
+    DeviceBuffer(T* p, size_t n, WriteHook on_write = nullptr) : ptr_(p), n_(n), on_write_(on_write) {}
+    const T* data() const { return ptr_; }
+    T* mutable_data() const {
+        if (on_write_ && ptr_) on_write_(ptr_);
+        return ptr_;
+    }
     size_t size() const { return n_; }
 
 private:
     T* ptr_{nullptr};
     size_t n_{0};
+    WriteHook on_write_{nullptr};
 };
 
 }  // namespace sift_cuda

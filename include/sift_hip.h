@@ -236,6 +236,14 @@ int sift_hip_results_host(sift_hip_t h, const float** kpts3, const float** feats
  * `stream`. */
 int sift_hip_copy_descriptors_device(sift_hip_t h, uint16_t* dst, int cap, void* stream);
 
+/* The current frame's matcher sidecar (device pointers, valid as its
+ * descriptor rows): int8 codes v - 128 (128 B per keypoint row) and per row
+ * the key bias -(256 |c|^2 + (row & 255)), written by the descriptor kernel
+ * beside the fp16 rows.  The C5 exchange all-gathers these (132 B per row
+ * instead of 256) and matches them with sift_hip_match_codes_batched.  No
+ * reference counterpart (the reference gathers nothing, Match.cu:8-33). */
+int sift_hip_results_sidecar(sift_hip_t h, const int8_t** codes, const int** keys);
+
 /* Detector::setDataGen(path) (Detector.hh:48-51; the reference dumps each
  * stage's octave-0 inputs/outputs as msgpack+zlib, Detector.cu:145-229,
  * PerfData.cuh:12-155).  With a non-empty dir every following single-frame
@@ -318,6 +326,26 @@ int sift_hip_match_batched(sift_hip_matcher_t m, int P, const uint16_t* const* q
  * identical).  Treat detector buffers as read-only.  enable = 0 turns the
  * lookup off for matcher m (every call converts the fp16 rows). */
 int sift_hip_matcher_set_sidecars(sift_hip_matcher_t m, int enable);
+
+/* The caller wrote into a detector descriptor buffer (a results-slot base as
+ * handed out above; C++: DeviceBuffer::mutable_data, Python:
+ * DeviceBuffer.mutable_data): its sidecar no longer describes the rows, so
+ * matches on that buffer convert the fp16 rows, as for a foreign buffer, until
+ * the detector launches a frame into it again.  Unknown pointers: no-op. */
+int sift_hip_descriptors_written(const uint16_t* desc);
+
+/* Pairs of code sets already in device memory (e.g. every rank's sidecar
+ * all-gathered, C5): int8 codes (128 B rows) and int32 key biases as
+ * sift_hip_results_sidecar lays them out (biases computed with set-local row
+ * indices).  Pair p matches the nq[p] query rows starting at code row qrow0[p]
+ * (their biases from key index qkey0[p]) against the nt[p] train rows starting
+ * at code row trow0[p] (biases from tkey0[p]), all pairs in ONE batched launch
+ * with no conversion (no k_match_prep).  Outputs and the ratio test as
+ * sift_hip_match_batched (packed per pair).  Host arrays of P ints. */
+int sift_hip_match_codes_batched(sift_hip_matcher_t m, const int8_t* codes, const int* keys, int P,
+                                 const int* qrow0, const int* qkey0, const int* nq, const int* trow0,
+                                 const int* tkey0, const int* nt, float ratio, int ratio_on_squared, int* idx2,
+                                 float* d2, int* match, void* stream);
 
 /* matchBruteForce(des, num_des, src, num_src) (Match.cu:8-33): synchronous,
  * result to host memory out[nq]. */

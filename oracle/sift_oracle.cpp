@@ -471,7 +471,7 @@ public:
             double sig_total = sig_prev * k;
             sig[i] = std::sqrt(sig_total * sig_total - sig_prev * sig_prev);
         }
-        pyr.assign(nOctaves * (L + 3), Plane());
+        pyr.resize(nOctaves * (L + 3));  // planes kept from the last call keep their pages (see dogPyramid)
         for (int o = 0; o < nOctaves; o++)
             for (int i = 0; i < L + 3; i++) {
                 Plane& dst = pyr[o * (L + 3) + i];
@@ -492,9 +492,13 @@ public:
 
     // [OpenCV 4.x sift.simd.hpp: buildDoGPyramidComputer] dst = G[i+1] - G[i].
     // Reference: MatOps.cu:10-37.
+    // The planes of `dogpyr` are reused across calls (the caller keeps it):
+    // fresh 9 MB allocations every frame were first touched by the threads of
+    // the loop below, and their concurrent page faults made this stage slower
+    // at 16 threads than at 4 (4.2 -> 5.3 ms per C2 frame, round-5 review).
     void dogPyramid(const std::vector<Plane>& gpyr, std::vector<Plane>& dogpyr) const {
         const int L = P_.L, nOct = (int)gpyr.size() / (L + 3);
-        dogpyr.assign(nOct * (L + 2), Plane());
+        dogpyr.resize(nOct * (L + 2));
         for (int o = 0; o < nOct; o++)
             for (int i = 0; i < L + 2; i++) {
                 const Plane& a = gpyr[o * (L + 3) + i];
@@ -958,7 +962,11 @@ public:
         const int nOct = autoOctaves(img.w, img.h, P_);
         gaussianPyramid(base, nOct, gpyr);
         clk.mark(1);
-        std::vector<Plane> dog;
+        // Reused across calls (dogPyramid).  The parallel loops below must see
+        // the calling thread's planes, so they use this reference, not the
+        // thread_local itself (each OpenMP worker has its own instance).
+        static thread_local std::vector<Plane> dog_tls;
+        std::vector<Plane>& dog = dog_tls;
         dogPyramid(gpyr, dog);
         clk.mark(2);
         std::vector<int> quads;
@@ -1109,7 +1117,7 @@ long sift_oracle_detect_and_compute(const float* img, int w, int h, const sift_o
                                     sift_oracle_kpt* out, float* desc, long cap) {
     Params P = toParams(p);
     Sift s(P, threads);
-    std::vector<Plane> gpyr;
+    static thread_local std::vector<Plane> gpyr;  // reused across calls (pages already mapped)
     std::vector<Keypoint> kpts = s.detect(toPlane(img, w, h), gpyr);
     long n = (long)kpts.size();
     long m = std::min(n, cap);

@@ -48,9 +48,28 @@ def main():
     oi, _ = oracle.knn2(q.astype(np.float32), t.astype(np.float32))
     oi2, _ = oracle.knn2(q.astype(np.float32), t[:400].astype(np.float32))
     ok = bool(np.array_equal(got[0], oi) and np.array_equal(got[1], oi2))
+    # The codes exchange (multi.all_gather_codes: the packed int8 codes + key
+    # biases block, one RCCL all_gather_into_tensor), then the batched matcher
+    # on the gathered buffer (no conversion): q against t and t[:400].
+    qc, qk = multi.codes_from_rows(local.view(torch.int16))
+    buf, n_pad = multi.all_gather_codes(qc, qk, 1)
+    assert buf.numel() == n_pad * 132
+    tc, tk = multi.codes_from_rows(dt.view(torch.int16))
+    tpad = multi.code_block_rows(m)
+    both = torch.cat([buf, multi.pack_codes(tc, tk, tpad)])
+    t0, tk0 = multi.code_set(0, tpad)  # the train block starts after the gathered one
+    t0 += n_pad * 132 // 128
+    tk0 += n_pad * 132 // 4
+    q0, qk0 = multi.code_set(0, n_pad)
+    idx2c = torch.empty((2, n, 2), dtype=torch.int32, device="cuda:0")
+    mt.match_codes_batched(both.data_ptr(), both.data_ptr(), [(q0, qk0, n, t0, tk0, m), (q0, qk0, n, t0, tk0, 400)],
+                           idx2_ptr=idx2c.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    gc = idx2c.cpu().numpy()
+    ok_codes = bool(np.array_equal(gc[0], oi) and np.array_equal(gc[1], oi2))
     dist.destroy_process_group()
-    print(json.dumps({"backend": "nccl", "world": 1, "rows": n, "match_exact": ok}))
-    return 0 if ok else 1
+    print(json.dumps({"backend": "nccl", "world": 1, "rows": n, "match_exact": ok, "codes_match_exact": ok_codes}))
+    return 0 if ok and ok_codes else 1
 
 
 if __name__ == "__main__":

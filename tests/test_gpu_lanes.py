@@ -119,6 +119,29 @@ def test_device_submit_micro_batch_equal_sync(sift, mb, lanes, depth):
     assert_identical(results(det), ref[0])
 
 
+def test_batch_accessors_on_micro_batch_frames(sift):
+    """(Round-5 advisor.)  A waited frame of a micro-batch has its own frame
+    number: the batch accessors expose that frame alone (batch_frames 1, index
+    0 = the frame's own results and counters, index 1 refused), never arenas
+    past the frame's group -- whichever arena of the group it ran in."""
+    frames = [sift.synth_frame(140 + i, W, H) for i in range(8)]
+    ref = sync_reference(sift, frames, numFeatures=2000)
+    dev = [torch.from_numpy(f).cuda() for f in frames]
+    torch.cuda.synchronize()
+    _, det = make_detector(sift, W, H, numFeatures=2000, lanes=2, micro_batch=4)
+    tickets = [det.submitDevice(d.data_ptr(), W * 4) for d in dev]
+    for i, t in enumerate(tickets):
+        det.wait(t)
+        assert det.batch_frames() == 1
+        n, ovf, k3p, f4p, dp = det.batch_results(0)
+        assert n == det.total_size == len(ref[i][0]) and ovf == det.overflow_flags()
+        assert dp == det.device_descriptor.data()
+        k3, f4, d = det.batch_copy_to_host(0)
+        assert np.array_equal(k3, ref[i][0]) and np.array_equal(d.view(np.uint16), ref[i][2])
+        with pytest.raises(RuntimeError):
+            det.batch_results(1)
+
+
 @pytest.mark.parametrize("mb,lanes,depth", [(4, 2, 8), (3, 3, 2)])
 def test_host_submit_micro_batch_equal_sync(sift, mb, lanes, depth):
     """Host frames on a micro-batching handle: staged into the handle's pinned

@@ -105,3 +105,99 @@ def test_sidecar_micro_batch_frames(sift):
         b = run(sift, mc, det.prev_descriptor.data(), n0, det.device_descriptor.data(), n1)
         for x, y in zip(a, b):
             assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), t
+
+
+def test_written_rows_drop_the_sidecar(sift, oracle):
+    """(Round-5 review item 7.)  A caller that writes into a detector's
+    descriptor rows through the writable view (DeviceBuffer.mutable_data ->
+    sift_hip_descriptors_written) gets the converting path's results on those
+    rows -- the stale int8 codes are never matched -- and the sidecar is valid
+    again once the detector writes that buffer with a new frame."""
+    w, h = 752, 480
+    cfg = sift.CudaSiftConfig(col_width=w, row_width=h, numFeatures=2000)
+    det = sift.Detector(cfg, lanes=1)
+    det.gpuWarmUpAndAllocate()
+    det.detectAndCompute(sift.synth_frame(90, w, h))
+    det.detectAndCompute(sift.synth_frame(91, w, h))
+    n0, n1 = det.prev_size, det.total_size
+    q, t = det.prev_descriptor.data(), det.device_descriptor.data()
+    m = sift.Matcher(4096, 4096)
+    mc = sift.Matcher(4096, 4096)
+    mc.set_sidecars(False)
+    before = run(sift, m, q, n0, t, n1)
+    # Overwrite the current frame's rows: new integer descriptors (a permutation
+    # of the rows and a shifted copy), as a caller post-processing them would.
+    rows = host_desc(sift, t, n1)
+    new = np.ascontiguousarray(np.clip(rows[::-1] + 3, 0, 255).astype(np.float16)).view(np.uint16)
+    wp = det.device_descriptor.mutable_data()
+    assert wp == t
+    sift._check(sift.lib().sift_hip_memcpy_h2d(wp, new.ctypes.data, new.nbytes), "h2d")
+    after = run(sift, m, q, n0, t, n1)
+    conv = run(sift, mc, q, n0, t, n1)
+    for x, y in zip(after, conv):
+        assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
+    oi, _ = oracle.knn2(host_desc(sift, q, n0), new.view(np.float16).astype(np.float32))
+    assert np.array_equal(after[0], oi) and not np.array_equal(after[0], before[0])
+    # New frames into the same slots (lanes=1: the four results slots come round) make the
+    # sidecars valid again; the results stay the converting path's.
+    for i in range(4):
+        det.detectAndCompute(sift.synth_frame(92 + i, w, h))
+    n0, n1 = det.prev_size, det.total_size
+    a = run(sift, m, det.prev_descriptor.data(), n0, det.device_descriptor.data(), n1)
+    b = run(sift, mc, det.prev_descriptor.data(), n0, det.device_descriptor.data(), n1)
+    for x, y in zip(a, b):
+        assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
+
+
+def test_codes_batched_from_sidecars(sift, oracle):
+    """sift_hip_match_codes_batched on code sets taken from detector sidecars
+    (results_sidecar) and packed as multi.all_gather_codes lays them out:
+    top-2 indices and d^2 equal the oracle's knn-2 on the fp16 rows; the
+    sidecar codes equal multi.codes_from_rows of the rows."""
+    import torch
+
+    from sift_amd import multi
+
+    w, h = 752, 480
+    cfg = sift.CudaSiftConfig(col_width=w, row_width=h, numFeatures=2000)
+    det = sift.Detector(cfg, lanes=1)
+    det.gpuWarmUpAndAllocate()
+    sets = []
+    for f in (30, 31, 32):
+        det.detectAndCompute(sift.synth_frame(f, w, h))
+        n = det.total_size
+        cp, kp = det.results_sidecar()
+        codes = torch.empty((n, 128), dtype=torch.int8, device="cuda")
+        keys = torch.empty(n, dtype=torch.int32, device="cuda")
+        rows = torch.empty((n, 128), dtype=torch.int16, device="cuda")
+        torch.cuda.synchronize()
+        for dst, src, nb in ((codes, cp, n * 128), (keys, kp, n * 4), (rows, det.device_descriptor.data(), n * 256)):
+            sift._check(sift.lib().sift_hip_memcpy_d2d(dst.data_ptr(), src, nb, None), "d2d")
+        torch.cuda.synchronize()
+        c2, k2 = multi.codes_from_rows(rows)
+        assert torch.equal(c2, codes) and torch.equal(k2, keys)
+        sets.append((codes, keys, rows, n))
+    n_pad = multi.code_block_rows(max(s[3] for s in sets))
+    buf = torch.cat([multi.pack_codes(c, k, n_pad) for c, k, _, _ in sets])
+    pairs = []
+    for a, b in ((0, 1), (1, 2), (2, 0), (0, 2)):
+        qa, qk = multi.code_set(a, n_pad)
+        ta, tk = multi.code_set(b, n_pad)
+        pairs.append((qa, qk, sets[a][3], ta, tk, sets[b][3]))
+    pairs.append(pairs[0][:5] + (300,))  # a ragged train set
+    tot = sum(p[2] for p in pairs)
+    idx2 = torch.empty((tot, 2), dtype=torch.int32, device="cuda")
+    d2 = torch.empty((tot, 2), dtype=torch.float32, device="cuda")
+    m = sift.Matcher(4096, 4096, max_pairs=8)
+    m.match_codes_batched(buf.data_ptr(), buf.data_ptr(), pairs, idx2_ptr=idx2.data_ptr(), d2_ptr=d2.data_ptr())
+    torch.cuda.synchronize()
+    gi, gd = idx2.cpu().numpy(), d2.cpu().numpy()
+    off = 0
+    for (a, b), p in zip(((0, 1), (1, 2), (2, 0), (0, 2), (0, 1)), pairs):
+        fq = sets[a][2].cpu().numpy().view(np.float16).astype(np.float32)
+        ft = sets[b][2].cpu().numpy().view(np.float16).astype(np.float32)[: p[5]]
+        oi, od = oracle.knn2(fq, ft)
+        assert np.array_equal(gi[off: off + p[2]], oi), (a, b)
+        valid = oi >= 0
+        assert np.array_equal(np.sqrt(gd[off: off + p[2]][valid]).astype(np.float32), od[valid]), (a, b)
+        off += p[2]

@@ -4,8 +4,9 @@ the first 8-GPU run does not also debug dlopen / ncclCommInitAll:
   * C ABI: sift_hip_comm_create(1, {0}) + sift_hip_comm_allgather moves the
     bytes (RCCL loaded with dlopen inside libsift_hip.so).
   * Python: torch.distributed "nccl" (= RCCL) at world size 1 through
-    sift_amd.multi.all_gather_sets -> Matcher.match_batched, exact vs the
-    oracle (fresh child process: tests/nccl_world1_child.py).
+    sift_amd.multi.all_gather_sets -> Matcher.match_batched, and the codes
+    exchange multi.all_gather_codes -> Matcher.match_codes_batched, both exact
+    vs the oracle (fresh child process: tests/nccl_world1_child.py).
   * C++: tools/multi_gpu_example --rccl (sift_cuda::rcclAllGather) on one GPU.
 """
 import ctypes
@@ -49,7 +50,7 @@ def test_torch_nccl_world1_exchange_and_match():
                        text=True, timeout=240, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
-    assert out["backend"] == "nccl" and out["match_exact"]
+    assert out["backend"] == "nccl" and out["match_exact"] and out["codes_match_exact"]
 
 
 def test_multi_gpu_example_rccl_one_gpu():

@@ -3,7 +3,9 @@
 
 Checks the frame sharding (C4: frame i -> rank i mod world, no collective) and
 the C5 exchange (all-gather of every rank's descriptor set, each rank matching
-its own set against every peer) against a single-process computation.
+its own set against every peer) against a single-process computation -- both
+exchange formats: fp16 rows, and the matcher codes + key biases (one packed
+block per rank, multi.all_gather_codes) that the GPU ranks send.
 """
 import os
 import socket
@@ -70,8 +72,20 @@ def _run(rank, world, n_frames, q, torch, dist, multi):
         return [torch.from_numpy(_ratio_match(a.numpy(), x, b.numpy(), y)) for a, x, b, y in zip(qs, nqs, ts, nts)]
 
     res = multi.cross_match(gathered, counts, rank, world, match_batched)
+    # The codes exchange: one packed block per rank, then this rank's pairs
+    # over the gathered buffer (a CPU matcher on the decoded codes v = c + 128).
+    codes, keys = multi.codes_from_rows(torch.from_numpy(own))
+    buf, n_pad = multi.all_gather_codes(codes, keys, world)
+    got = {}
+    for (q0, qk, nq, t0, tk, nt) in multi.code_pairs(counts, rank, world, n_pad):
+        j = [jj for jj in range(world) if multi.code_set(jj, n_pad)[0] == t0][0]
+        qc = buf[q0 * 128: (q0 + nq) * 128].view(torch.int8).reshape(nq, 128).to(torch.int32) + 128
+        tc = buf[t0 * 128: (t0 + nt) * 128].view(torch.int8).reshape(nt, 128).to(torch.int32) + 128
+        assert torch.equal(buf[4 * qk: 4 * (qk + nq)].view(torch.int32), keys[:nq])
+        got[j] = _ratio_match(qc.to(torch.float16).numpy().view(np.int16), nq, tc.to(torch.float16).numpy().view(np.int16), nt)
+    codes_sets = [tuple(x.numpy() for x in multi.unpack_codes(buf, j, NSET, n_pad)) for j in range(world)]
     out = [None] * world
-    dist.all_gather_object(out, {"frames": frames, "counts": counts,
+    dist.all_gather_object(out, {"frames": frames, "counts": counts, "codes_sets": codes_sets, "code_matches": got,
                                  "gathered": gathered.numpy(), "matches": {j: r.numpy() for j, r in res.items()}})
     if rank == 0:
         q.put(out)
@@ -106,6 +120,12 @@ def test_two_rank_shard_gather_match():
         for j in peers:
             exp = _ratio_match(sets[r][0], sets[r][1], sets[j][0], sets[j][1])
             assert np.array_equal(out[r]["matches"][j], exp)
+            assert np.array_equal(out[r]["code_matches"][j], exp)
+        for j in range(world):  # every rank received every rank's codes and key biases
+            v = sets[j][0].view(np.float16).astype(np.int32)
+            c = v - 128
+            assert np.array_equal(out[r]["codes_sets"][j][0], c.astype(np.int8))
+            assert np.array_equal(out[r]["codes_sets"][j][1], -(256 * (c * c).sum(1) + (np.arange(NSET) & 255)))
     assert sets[0][1] > 20
 
 
@@ -122,3 +142,12 @@ def test_single_rank_helpers():
     g, c = multi.all_gather_sets(t, 3, 1)
     assert g.shape == (1, 4, 128) and c == [3]
     assert multi.cross_match(g, c, 0, 1, None) == {}
+    # Packed code blocks: whole 128-B code rows per rank, keys after the codes.
+    assert multi.code_block_rows(2000) == 2016 and multi.code_set(1, 2016) == (2079, 66528 + 64512)
+    rows = torch.from_numpy(np.arange(3 * 128, dtype=np.float16).reshape(3, 128) % 256).view(torch.int16)
+    codes, keys = multi.codes_from_rows(rows)
+    buf, n_pad = multi.all_gather_codes(codes, keys, 1)
+    assert n_pad == 32 and buf.numel() == 32 * 132
+    c2, k2 = multi.unpack_codes(buf, 0, 3, n_pad)
+    assert torch.equal(c2, codes) and torch.equal(k2, keys)
+    assert multi.code_pairs([3], 0, 1, n_pad) == []

@@ -1,4 +1,5 @@
-"""Run the C2 workload for a few frames (no torch) -- a small target for rocprofv3."""
+"""Run the C2 workload (or another configuration: --upscale --octaves 0 --features 0 is
+OpenCV's default) for a few frames (no torch) -- a small target for rocprofv3."""
 import argparse
 import os
 import sys
@@ -14,11 +15,13 @@ ap.add_argument("--width", type=int, default=1920)
 ap.add_argument("--height", type=int, default=1200)
 ap.add_argument("--octaves", type=int, default=3)
 ap.add_argument("--upscale", action="store_true")
+ap.add_argument("--features", type=int, default=5000, help="numFeatures (0: keep all, OpenCV's default)")
 ap.add_argument("--eager", action="store_true", help="timing mode: un-graphed launches")
 ap.add_argument("--batch", type=int, default=1, help="frames per launch (sift_hip_set_batch)")
 ap.add_argument("--exact", action="store_true", help="exact descriptor mode (SIFT_HIP_DESC_EXACT)")
 a = ap.parse_args()
-cfg = sift.CudaSiftConfig(col_width=a.width, row_width=a.height, numOctaves=a.octaves, upscale=a.upscale)
+cfg = sift.CudaSiftConfig(col_width=a.width, row_width=a.height, numOctaves=a.octaves, upscale=a.upscale,
+                          numFeatures=a.features)
 det = sift.Detector(cfg, device=0, batch=a.batch, exact_descriptors=a.exact)
 det.gpuWarmUpAndAllocate()
 det.set_timing(a.eager)
