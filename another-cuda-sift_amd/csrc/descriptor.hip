@@ -186,6 +186,16 @@ struct JobWords {
 // Minimum waves per SIMD (VGPR budget <= 80): 198 us vs 208 (5) and 211 (8)
 // per 8-frame launch; re-swept in round 3 (5 / 7: 337 / 331 vs 334 us).
 constexpr int kDescWaves = 6;
+// Sum over the 64 lanes, returned to every lane (DPP, as wave_max).
+__device__ __forceinline__ float wave_sum(float x) {
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x111, 0xf, 0xf, false));
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x112, 0xf, 0xf, false));
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x114, 0xf, 0xf, false));
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x118, 0xf, 0xf, false));
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x142, 0xa, 0xf, false));
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x143, 0xc, 0xf, false));
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+}
 template <int kDT>
 __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* __restrict__ jobs, const Counters* __restrict__ ctr,
                                                    const unsigned* __restrict__ range_keys,
@@ -198,7 +208,6 @@ __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* _
     // (slot 9 = orientation 8, wrapped into 0 at the end).  The per-keypoint
     // scale keeps every bin below 2^31, so no carry crosses the word boundary.
     __shared__ __attribute__((aligned(16))) unsigned histE[kCopies * kHistWords];  // copy c at c * kHistWords
-    __shared__ __attribute__((aligned(16))) float sq[128];
     __shared__ int rowpre[kMaxRows + 4], rowlo[kMaxRows], rowln[kMaxRows];
     __shared__ float s_norm[12];
     __shared__ int s_cn[2];  // |codes|^2 of the keypoint's two halves (sidecar key bias)
@@ -458,7 +467,7 @@ __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* _
         }
         lds_barrier();
 
-        // Wrap, L2 norm (8 fma lanes, then v_reduce_sum's pairing), 0.2 clip.
+        // Wrap, L2 norm, 0.2 clip, renormalisation, x512 rounding.
         const float inv = ldexpf(1.f, -S);
         float val[kPer];
 #pragma unroll
@@ -475,39 +484,25 @@ __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* _
                 if (kk == 0) hv += hO[cell * kCellW + 9];
             }
             val[h] = (float)((double)hv * (double)inv);
-            if (tid + kDT * h < 128) sq[t] = val[h];
         }
+        // Both norms as wave sums (DPP) of the entries' squares, one partial
+        // per wave through LDS: two barriers instead of four and no serial
+        // 128-term sum (thread 0 alone, OpenCV's order: 347.8 vs 336.9 us per
+        // serialised 16-frame launch, round 6).  The float order is not
+        // OpenCV's, so the scale can differ by an ulp -- inside the default
+        // mode's +-1 bar (its histogram is summed in another order already;
+        // the exact mode keeps OpenCV's order).
+        static_assert(kPer == 1, "one entry per thread");
+        const bool own = tid < 128;
+        const float w1 = wave_sum(own ? val[0] * val[0] : 0.f);
+        if (lane == 0) s_norm[tid >> 6] = w1;
         lds_barrier();
-        if (tid < 8) {
-            float a = 0.f;
-#pragma unroll
-            for (int q = 0; q < 16; q++) a = __fmaf_rn(sq[tid + 8 * q], sq[tid + 8 * q], a);
-            s_norm[tid] = a;
-        }
+        const float thr = __builtin_sqrtf(s_norm[0] + s_norm[1]) * 0.2f;
+        val[0] = fminf(val[0], thr);
+        const float w2 = wave_sum(own ? val[0] * val[0] : 0.f);
+        if (lane == 0) s_norm[4 + (tid >> 6)] = w2;
         lds_barrier();
-        const float t0 = s_norm[0] + s_norm[4], t1 = s_norm[1] + s_norm[5], t2 = s_norm[2] + s_norm[6],
-                    t3 = s_norm[3] + s_norm[7];
-        const float thr = __builtin_sqrtf((t0 + t2) + (t1 + t3)) * 0.2f;
-#pragma unroll
-        for (int h = 0; h < kPer; h++) {
-            val[h] = fminf(val[h], thr);
-            if (tid + kDT * h < 128) sq[tid + kDT * h] = val[h] * val[h];
-        }
-        lds_barrier();
-        if (tid == 0) {
-            float nrm2 = 0.f;  // sequential over k = 0..127, the oracle's order
-#pragma unroll 4
-            for (int q = 0; q < 128; q += 4) {
-                const float4 s4 = *reinterpret_cast<const float4*>(sq + q);
-                nrm2 = nrm2 + s4.x;
-                nrm2 = nrm2 + s4.y;
-                nrm2 = nrm2 + s4.z;
-                nrm2 = nrm2 + s4.w;
-            }
-            s_norm[8] = 512.f / fmaxf(__builtin_sqrtf(nrm2), FLT_EPSILON);
-        }
-        lds_barrier();
-        const float scale = s_norm[8];
+        const float scale = 512.f / fmaxf(__builtin_sqrtf(s_norm[4] + s_norm[5]), FLT_EPSILON);
         const unsigned po = (unsigned)jb.out;  // output row (the job order may differ: JobOrder)
         int c2 = 0;  // this thread's share of |codes|^2
 #pragma unroll
@@ -539,36 +534,37 @@ __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* _
 // contributions sequentially in raster order of the window; float addition is
 // not associative, so the fixed-point histogram above can land one byte off.
 // Here every bin has ONE owner lane that adds its contributions in that order:
-//   * one wave per keypoint; the enumerated samples are taken in chunks of 64
-//     consecutive samples (raster order), one per lane;
-//   * phase 1: each lane computes its sample with the oracle's correctly
-//     rounded math (cv_exp32f table exp, fastAtan2 with IEEE division,
-//     magnitude with IEEE sqrt), writes per target cell the float4 its owner
-//     lanes add ({P, S}, below) and a 16-bit (record base, o0 >> 1) word to
-//     LDS, and 12 ballots give, per interior cell row, cell column and
-//     orientation pair, the samples that touch it;
-//   * phase 2: lane = (cell 0..15, orientation pair g 0..3) ANDs its three
-//     masks and walks the set bits in ascending order (= raster order), adding
-//     into its bins 2g, 2g+1 (and bin 8 for g = 0, wrapped into bin 0 at the
-//     end as OpenCV does).  A sample touching the lane only through one bin
-//     adds an exact +0 to the other (every contribution is >= +0, so x + 0 = x).
-// Measured cost: DESIGN.md section 2.
-// Waves per workgroup, each on its own keypoints with private LDS (no
-// workgroup barrier inside the keypoint loop).
+//   * one wave per keypoint (four independent waves per workgroup, private
+//     LDS, no workgroup barrier inside the keypoint loop); the enumerated
+//     samples are taken in chunks of 64 consecutive samples (raster order),
+//     one per lane, their gradient loads two chunks ahead;
+//   * each lane computes its sample with the oracle's correctly rounded math
+//     (cv_exp32f table exp, fastAtan2 with IEEE division, magnitude with IEEE
+//     sqrt) and OpenCV's trilinear split into 8 contributions;
+//   * owners: lane = (cell 0..15, orientation pair g 0..3) adds bins 2g,
+//     2g + 1; bin 8 (o0 = 7's upper bin, wrapped into bin 0 at the end as
+//     OpenCV does) has its own run per cell, added by the cell's g = 0 lane;
+//   * packed runs (round 6): per chunk each owner takes the popcount of its
+//     ballot mask (the samples touching its cell row, column and orientation
+//     pair), one wave scan of the counts gives every owner a contiguous run in
+//     LDS and a table row {mask, run start}, and each sample writes, for every
+//     owner it touches, the float2 that owner adds at run start + rank (rank =
+//     v_mbcnt of the owner's mask below the sample); then each owner adds its
+//     run in order, four entries per step.  Entries are {into bin 2g, into
+//     bin 2g + 1}: even o0 writes (v_o0, v_o0+1) to pair o0 / 2, odd o0 writes
+//     (+0, v_o0) to pair (o0 - 1) / 2 and (v_o0+1, +0) to pair (o0 + 1) / 2
+//     (bin 8's run for o0 = 7, whose adds read the x halves only).  Runs are
+//     padded to four entries with zeros: every contribution is >= +0, so
+//     x + 0 = x exactly.  A sample's targets outside the 4x4 interior read a
+//     null row (mask 0) whose rank lands on a trash entry.
+// The walk's length is still the busiest owner's hits in the chunk (64
+// consecutive samples are a thin band of the window), but a hit costs ~2.5
+// instructions instead of the ~15 of the round-4 mask walk (owners pulling
+// their hits by bit scans and decoding per-sample records; 1585 -> 1275 us per
+// serialised 16-frame launch).
+// ---------------------------------------------------------------------------
 constexpr int kExactWaves = 4;
-// Hits per walk step (their LDS reads in flight together): 2, 3, 4 measured
-// 0.158 / 0.157 / 0.160 ms per frame (profiles/round4/exact_ab_hits*.jsonl).
-constexpr int kExactHits = 2;
-// Floats per sample record (its 4 float4s).  The walk's record reads run at
-// LDS bank conflicts ~1.1x their active cycles (tools/exact_pmc.sh); padded
-// strides 20 / 24: 0.157 / 0.158 vs 0.159 ms per frame, within box noise.
-constexpr int kRecStride = 16;
-static_assert(kRecStride % 4 == 0 && 64 * kRecStride + 64 < (1 << 14), "record bases in 14 bits, float4-aligned");
-constexpr int kZeroRec = 40;  // zero floats after the 64 records (absent second hit of a walk step)
 constexpr int kExactWG = 64 * kExactWaves;
-// Orders one wave's LDS writes before its later LDS reads by other lanes (LDS
-// executes a wave's instructions in order; the fences keep the compiler from
-// moving accesses across).
 // Inclusive prefix maximum over the 64 lanes (non-negative values; DPP as
 // wave_incl_scan).
 __device__ __forceinline__ int wave_incl_max(int x) {
@@ -580,6 +576,9 @@ __device__ __forceinline__ int wave_incl_max(int x) {
     x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false));
     return x;
 }
+// Orders one wave's LDS writes before its later LDS reads by other lanes (LDS
+// executes a wave's instructions in order; the fences keep the compiler from
+// moving accesses across).
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
     __builtin_amdgcn_wave_barrier();
@@ -590,373 +589,14 @@ void upload_desc_exp_table(const float* tab64) {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(c_desc_exptab), tab64, 64 * sizeof(float));
 }
 
-__global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __restrict__ jobs,
-                                                               const Counters* __restrict__ ctr,
-                                                               uint16_t* __restrict__ desc, Sidecar sidecar,
-                                                               Counters* __restrict__ host_ctr, HostOut host, long fs,
-                                                               unsigned nf) {
-    __shared__ float s_tab[64];
-    // Chunk sample s: per target cell (dr, dc) one float4 {P.x, P.y, S.x, S.y}
-    // (below), at s*16 + (dr*2 + dc)*4; then a zero record for absent hits.
-    __shared__ __attribute__((aligned(16))) float s_rec[kExactWaves][64 * kRecStride + kZeroRec];
-    // 16-bit / 8-bit tables and the epilogue's raw[] and fetch's row map
-    // inside the records (dead at those points): 4.8 KB per wave, 8 waves/SIMD.
-    __shared__ unsigned short s_meta[kExactWaves][65];  // record base | (o0 >> 1) << 14 (below); [64]: the zero record
-    __shared__ unsigned short s_rowpre[kExactWaves][kMaxRows + 1];  // <= 128^2 samples
-    __shared__ signed char s_rowlo[kExactWaves][kMaxRows];           // |j| <= radius + 2 <= 66
-    __shared__ float s_nrm[kExactWaves][12];
-
-    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    float* rec = s_rec[w];
-    unsigned short* meta = s_meta[w];
-    unsigned short* rowpre = s_rowpre[w];
-    signed char* rowlo = s_rowlo[w];
-    float* raw = rec;  // after the chunk loop
-    float* s_norm = s_nrm[w];
-    int* rowmap = reinterpret_cast<int*>(rec);  // inside fetch(), between a chunk's walk and the next chunk's records
-    const unsigned frame = blockIdx.x % nf, wg = blockIdx.x / nf, nwg = gridDim.x / nf;
-    const long foff = frame * fs;
-    jobs = fptr(jobs, foff);
-    ctr = fptr(ctr, foff);
-    desc = fptr(desc, foff);
-    sidecar.codes = fptr(sidecar.codes, foff);
-    sidecar.keys = fptr(sidecar.keys, foff);
-    host_ctr += frame;
-    const unsigned n = ctr->final_n;
-    static_assert(sizeof(Counters) <= 4 * kExactWG, "counters handed over by one workgroup");
-    if (wg == 0 && threadIdx.x < sizeof(Counters) / 4)
-        reinterpret_cast<unsigned*>(host_ctr)[threadIdx.x] = reinterpret_cast<const unsigned*>(ctr)[threadIdx.x];
-    if (wg * kExactWaves >= n) return;  // workgroup-uniform
-    if (w == 0) s_tab[lane] = c_desc_exptab[lane];
-    if (lane < kZeroRec) rec[64 * kRecStride + lane] = 0.f;
-    if (lane == 0) meta[64] = 64 * kRecStride + 64;  // + any lane offset (-64 .. -28) lands in the zero floats
-    lds_barrier();
-    const float bins_per_rad = kN / 360.f;
-    const float exp_scale = -1.f / (kD * kD * 0.5f);
-    // This lane's bins: interior cell (ci, cj), orientations 2g and 2g + 1.
-    const int cell = lane >> 2, g = lane & 3, ci = cell >> 2, cj = cell & 3;
-
-    for (unsigned p = wg * kExactWaves + w; p < n; p += nwg * kExactWaves) {
-        // The job through SGPRs: a VGPR copy of jb.img would put every buffer
-        // load of the chunk loop in a waterfall loop.
-        JobWords jwd;
-        const unsigned* __restrict__ jw = reinterpret_cast<const unsigned*>(jobs + p);
-#pragma unroll
-        for (int q = 0; q < 16; q++) jwd.w[q >> 2][q & 3] = __builtin_amdgcn_readfirstlane(jw[q]);
-        const DescJob jb = __builtin_bit_cast(DescJob, jwd);
-        DescGeom G;
-        G.cos_t = jb.cos_t;
-        G.sin_t = jb.sin_t;
-        G.exp_scale = exp_scale;
-        G.ptx = jb.ptx;
-        G.pty = jb.pty;
-        G.rows = jb.rows;
-        G.cols = jb.cols;
-        const int radius = jb.radius, side = 2 * radius + 1;
-        const bool enumerated = side <= kMaxRows;
-        const __amdgpu_buffer_rsrc_t rsrc =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(jb.img), 0, jb.rows * jb.pitch * 4, 0x00020000);
-        int N;
-        if (enumerated) {
-            // Per-row j-intervals (supersets of the in-square samples, clipped
-            // to the image interior) and their prefix sum: two rows per lane.
-            const float inv_sin = __builtin_amdgcn_rcpf(G.sin_t), inv_cos = __builtin_amdgcn_rcpf(G.cos_t);
-            int len2[2];
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int t = 2 * lane + h, i = t - radius, r = G.pty + i;
-                int lo = max(-radius, 1 - G.ptx), hi = min(radius, G.cols - 2 - G.ptx);
-                if (r <= 0 || r >= G.rows - 1 || t >= side) hi = lo - 1;
-                clip_interval(lo, hi, G.sin_t, inv_sin, (float)i * G.cos_t + (kD / 2 - 0.5f), radius);
-                clip_interval(lo, hi, G.cos_t, inv_cos, -(float)i * G.sin_t + (kD / 2 - 0.5f), radius);
-                len2[h] = max(hi - lo + 1, 0);
-                if (t < side) rowlo[t] = lo;
-            }
-            const int sum = wave_incl_scan(len2[0] + len2[1]);
-            if (2 * lane + 1 <= side) rowpre[2 * lane + 1] = sum - len2[1];
-            if (2 * lane + 2 <= side) rowpre[2 * lane + 2] = sum;
-            if (lane == 0) rowpre[0] = 0;
-            N = __builtin_amdgcn_readlane(sum, 63);
-        } else {
-            N = side * side;  // huge window: the full raster, the oracle's test per sample
-        }
-        wave_lds_sync();
-
-        // Window sample k -> (i, j): row by binary search over the prefix sums.
-        // Enumerated sample k -> its row: binary search over the prefix sums.
-        auto row_search = [&](int k) {
-            int lo = 0, hi = side - 1;  // last row with rowpre[row] <= k
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (rowpre[mid] <= k) lo = mid;
-                else hi = mid - 1;
-            }
-            return lo;
-        };
-        auto gload = [&](unsigned o) {
-            return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o, 0, 0));
-        };
-        const unsigned pitch4 = 4u * jb.pitch;
-        // Gradient loads run two chunks ahead of the math and walk
-        // (unconditionally: past the end they re-read an in-buffer address),
-        // so their latency hides behind two chunks' work.
-        struct Fetch {
-            int i, j;
-            float l, r, u, d;
-        };
-        // Rows of a chunk [kf, kf + 64) without a per-lane search: frb is the
-        // row of sample kf; rows frb+1 .. frb+64 that start inside the chunk
-        // mark their start position (ds_max: of several rows starting at one
-        // position -- empty rows -- the last is the non-empty one) and a wave
-        // prefix maximum gives every position its row.  Non-empty rows are
-        // contiguous, so 64 rows cover the chunk; if not, the search.
-        int frb = N > 0 ? __builtin_amdgcn_readfirstlane(enumerated ? row_search(0) : 0) : 0;
-        auto fetch = [&](int kf) {
-            Fetch f;
-            if (enumerated) {
-                int row;
-                const bool covered = rowpre[min(frb + 65, side)] >= min(kf + 64, N);  // uniform
-                if (covered) {
-                    rowmap[lane] = frb;
-                    wave_lds_sync();
-                    const int r = frb + 1 + lane;
-                    if (r < side) {
-                        const int st = rowpre[r] - kf;
-                        if (st >= 0 && st < 64) atomicMax(&rowmap[st], r);
-                    }
-                    wave_lds_sync();
-                    row = wave_incl_max(rowmap[lane]);
-                    // rowmap aliases the float records of rec[]: keep the
-                    // record stores that follow from being scheduled above
-                    // this int read (TBAA would allow it).
-                    wave_lds_sync();
-                } else {
-                    row = row_search(min(kf + lane, N - 1));
-                }
-                frb = __builtin_amdgcn_readlane(row, 63);
-                f.i = row - radius;
-                f.j = rowlo[row] + (kf + lane - rowpre[row]);
-            } else {
-                const int k = min(kf + lane, N - 1);
-                f.i = k / side - radius;
-                f.j = k % side - radius;
-            }
-            const unsigned o = (unsigned)((G.pty + f.i) * jb.pitch + G.ptx + f.j) * 4u;
-            f.l = gload(o - 4u);
-            f.r = gload(o + 4u);
-            f.u = gload(o - pitch4);
-            f.d = gload(o + pitch4);
-            return f;
-        };
-        Fetch f1 = fetch(0), f2 = fetch(64);
-        // Walk constants: pair address = meta's base + this lane's cell offset.
-        const int lane_off = ci * 8 + cj * 4 - 64;
-        unsigned sel_ci[kD], sel_cj[kD], sel_g[kD];  // all ones where this lane's index is q
-#pragma unroll
-        for (int q = 0; q < kD; q++) {
-            sel_ci[q] = ci == q ? ~0u : 0u;
-            sel_cj[q] = cj == q ? ~0u : 0u;
-            sel_g[q] = g == q ? ~0u : 0u;
-        }
-        float accA = 0.f, accB = 0.f, accW = 0.f;  // bins 2g, 2g + 1, and 8 (g = 0)
-        for (int k0 = 0; k0 < N; k0 += 64) {
-            // ---- phase 1: sample k0 + lane ----
-            const int i = f1.i, j = f1.j;
-            const float l = f1.l, r = f1.r, u = f1.u, d = f1.d;
-            f1 = f2;
-            f2 = fetch(k0 + 128);
-            float rbin, cbin, c_rot, r_rot;
-            const bool valid = desc_sample(G, i, j, rbin, cbin, c_rot, r_rot) && k0 + lane < N;
-            const float dx = r - l, dy = u - d;
-            const float wgt = cv_exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, s_tab);
-            const float gori = cv_fast_atan2(dy, dx);
-            const float gmag = cv_magnitude(dx, dy);
-            float obin = (gori - jb.angle) * bins_per_rad;
-            const float mag = gmag * wgt;
-            const int r0 = cv_floor(rbin), c0 = cv_floor(cbin);
-            int o0 = cv_floor(obin);
-            rbin -= (float)r0;
-            cbin -= (float)c0;
-            obin -= (float)o0;
-            if (o0 < 0) o0 += kN;
-            if (o0 >= kN) o0 -= kN;
-            float v[8];
-            trilinear(mag, rbin, cbin, obin, v);
-            // Per target cell (dr, dc) the values its owner lanes add, arranged
-            // by orientation so the walk needs no case analysis.  The primary
-            // owner (pair g = o0 >> 1) adds P to bins (2g, 2g + 1); for odd o0
-            // the secondary owner (g = (o0 + 1) >> 1 mod 4) adds S.x to bin 2g
-            // and S.y to bin 8:
-            //   o0 even:   P = (v_o0, v_o0+1), S = (0, 0)
-            //   o0 odd:    P = (0, v_o0),      S = (v_o0+1, 0)
-            //   o0 = 7:    P = (0, v_7),       S = (0, v_8)   (bin 8: g = 0's third bin)
-            const bool odd = o0 & 1, seven = o0 == kN - 1;
-            float4* rp = reinterpret_cast<float4*>(rec + lane * kRecStride);
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const float x = v[2 * q], y = v[2 * q + 1];
-                rp[q] = make_float4(odd ? 0.f : x, odd ? x : y, odd && !seven ? y : 0.f, seven ? y : 0.f);
-            }
-            // Owner lane (ci, cj) reads the float4 of (dr, dc) = (ci - r0, cj - c0)
-            // at lane*16 + dr*8 + dc*4 = base - 64 + ci*8 + cj*4 (base >= 28 for
-            // valid samples: r0, c0 <= 3); o0 >> 1 in bits 14-15.
-            meta[lane] = (unsigned short)((lane * kRecStride + 64 - r0 * 8 - c0 * 4) | (o0 >> 1) << 14);
-            // Samples touching interior cell row / column q (r0 in {q - 1, q})
-            // and orientation pair q (o0 in {2q - 1 mod 8, 2q, 2q + 1}).
-            // Plain compares (an invalid sample's row 64 touches no cell), so
-            // each ballot is one v_cmp into an SGPR pair.
-            const int r0v = valid ? r0 : 64;
-            unsigned long long RR[kD], CC[kD], OO[kD];
-#pragma unroll
-            for (int q = 0; q < kD; q++) {
-                RR[q] = __builtin_amdgcn_ballot_w64((unsigned)(r0v - q + 1) < 2u);
-                CC[q] = __builtin_amdgcn_ballot_w64((unsigned)(c0 - q + 1) < 2u);
-                OO[q] = __builtin_amdgcn_ballot_w64((unsigned)((o0 - 2 * q + 1) & (kN - 1)) < 3u);
-            }
-            // This lane's three masks by bitfield inserts with lane-constant
-            // selectors (no branches).
-            auto pick = [](const unsigned long long (&X)[kD], const unsigned (&sel)[kD]) {
-                unsigned lo = (unsigned)X[0], hi = (unsigned)(X[0] >> 32);
-#pragma unroll
-                for (int q = 1; q < kD; q++) {
-                    lo = ((unsigned)X[q] & sel[q]) | (lo & ~sel[q]);
-                    hi = ((unsigned)(X[q] >> 32) & sel[q]) | (hi & ~sel[q]);
-                }
-                return (unsigned long long)hi << 32 | lo;
-            };
-            unsigned long long M = pick(RR, sel_ci) & pick(CC, sel_cj) & pick(OO, sel_g);
-            // rec / meta writes of every lane before any lane reads them (one
-            // wave: LDS executes its instructions in order; this keeps the
-            // compiler from moving the reads up).
-            wave_lds_sync();
-            // ---- phase 2: this lane's samples in ascending (raster) order,
-            // two per iteration (their LDS reads in flight together) ----
-            auto add = [&](int mt, float4 pv) {
-                const bool prim = (mt >> 14) == g;  // else this lane is the secondary owner (o0 = 2g - 1)
-                accA = accA + (prim ? pv.x : pv.z);
-                accB = accB + (prim ? pv.y : 0.f);
-                accW = accW + (prim ? 0.f : pv.w);
-            };
-            // 32-bit halves (samples 0-31, then 32-63: raster order kept), so
-            // the bit scans and clears are single VALU ops; a missing second
-            // hit reads the zero record (adds +0).
-            auto walk = [&](unsigned m, int base) {
-                while (m) {
-                    int sx[kExactHits];
-#pragma unroll
-                    for (int h = 0; h < kExactHits; h++) {
-                        sx[h] = m ? base + __builtin_ctz(m) : 64;
-                        m &= m - 1;
-                    }
-                    int mt[kExactHits];
-#pragma unroll
-                    for (int h = 0; h < kExactHits; h++) mt[h] = meta[sx[h]];
-                    float4 pv[kExactHits];
-#pragma unroll
-                    for (int h = 0; h < kExactHits; h++)
-                        pv[h] = *reinterpret_cast<const float4*>(rec + (mt[h] & 0x3fff) + lane_off);
-#pragma unroll
-                    for (int h = 0; h < kExactHits; h++) add(mt[h], pv[h]);
-                }
-            };
-            walk((unsigned)M, 0);
-            walk((unsigned)(M >> 32), 32);
-            wave_lds_sync();
-        }
-        // OpenCV's wrap: hist[0] += hist[8] (hist[1] += hist[9] adds +0).
-        raw[cell * kN + 2 * g] = g == 0 ? accA + accW : accA;
-        raw[cell * kN + 2 * g + 1] = accB;
-        wave_lds_sync();
-        // L2 norm (8 fma lanes, v_reduce_sum's pairing), 0.2 clip, sequential
-        // renorm, x512 rounding: the oracle's float operations.
-        if (lane < 8) {
-            float a = 0.f;
-#pragma unroll
-            for (int q = 0; q < 16; q++) a = __fmaf_rn(raw[lane + 8 * q], raw[lane + 8 * q], a);
-            s_norm[lane] = a;
-        }
-        wave_lds_sync();
-        const float t0 = s_norm[0] + s_norm[4], t1 = s_norm[1] + s_norm[5], t2 = s_norm[2] + s_norm[6],
-                    t3 = s_norm[3] + s_norm[7];
-        const float thr = __builtin_sqrtf((t0 + t2) + (t1 + t3)) * 0.2f;
-        const float v0 = fminf(raw[2 * lane], thr), v1 = fminf(raw[2 * lane + 1], thr);
-        wave_lds_sync();
-        raw[2 * lane] = v0;
-        raw[2 * lane + 1] = v1;
-        wave_lds_sync();
-        if (lane == 0) {
-            float nrm2 = 0.f;
-            for (int q = 0; q < 128; q++) nrm2 = nrm2 + raw[q] * raw[q];
-            s_norm[8] = 512.f / fmaxf(__builtin_sqrtf(nrm2), FLT_EPSILON);
-        }
-        wave_lds_sync();
-        const float scale = s_norm[8];
-        int b0 = cv_round(v0 * scale), b1 = cv_round(v1 * scale);
-        b0 = b0 < 0 ? 0 : (b0 > 255 ? 255 : b0);
-        b1 = b1 < 0 ? 0 : (b1 > 255 ? 255 : b1);
-        const _Float16 h0 = (_Float16)(float)b0, h1 = (_Float16)(float)b1;
-        const unsigned po = (unsigned)jb.out;  // output row (jobs run longest first, JobOrder)
-        const unsigned pair = (unsigned)__builtin_bit_cast(uint16_t, h0) | (unsigned)__builtin_bit_cast(uint16_t, h1) << 16;
-        reinterpret_cast<unsigned*>(desc + (size_t)po * 128)[lane] = pair;
-        // Host rows looked up here, not kept across the keypoint loop (VGPRs:
-        // 73 vs 62, one wave per SIMD less).
-        HostOut hf = host;
-        const HostRows hr = host_rows(hf, ctr, frame, foff);
-        if (hr.desc) reinterpret_cast<unsigned*>(hr.desc + (size_t)po * 128)[lane] = pair;
-        if (hr.k3 && lane < 7) host_row(hr, hf, po, lane);
-        // Matcher sidecar: int8 codes and the key bias (k_descriptor's epilogue).
-        reinterpret_cast<unsigned short*>(sidecar.codes + (size_t)po * 128)[lane] =
-            (unsigned short)((b0 - 128) & 255) | (unsigned short)(((b1 - 128) & 255) << 8);
-        const int c2 = __builtin_amdgcn_readlane(wave_incl_scan((b0 - 128) * (b0 - 128) + (b1 - 128) * (b1 - 128)), 63);
-        if (lane == 0) sidecar.keys[po] = -(256 * c2 + (int)(po & 255));
-        wave_lds_sync();  // rowpre / raw / s_norm are rewritten by the next keypoint
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Exact mode, packed owner runs (round 6).  Same owners and the same
-// per-bin raster order as k_descriptor_exact above, but a chunk's hits are
-// pushed to their owners instead of pulled: each owner lane (cell, pair g)
-// counts its hits (popcount of its ballot mask), a wave scan of the counts
-// gives every owner a contiguous run in LDS, and each sample writes, for every
-// owner it touches, the two floats that owner adds at position run start +
-// rank, rank = the number of earlier samples of the chunk in the owner's mask
-// (v_mbcnt).  The walk is then a straight read of the owner's run, four
-// entries per step with no bit scans, record decoding or selects; its length
-// is still the busiest owner's hit count (a 64-sample chunk is a thin band of
-// the window), but each hit costs ~2.5 instructions instead of ~15.
-//   * owners: lane = (cell 0..15, orientation pair g 0..3) adds bins 2g, 2g+1;
-//     bin 8 (o0 = 7's upper bin) has its own run per cell (row g = 4), walked
-//     by the cell's g = 0 lane into its third accumulator;
-//   * entries are float2 {into bin 2g, into bin 2g + 1}: even o0 writes
-//     (v_o0, v_o0+1) to pair o0 / 2; odd o0 writes (+0, v_o0) to pair
-//     (o0 - 1) / 2 and (v_o0+1, +0) to pair (o0 + 1) / 2 (bin 8's run for
-//     o0 = 7, whose walk reads the x halves only).  Runs are padded to four
-//     entries with zeros; every contribution is >= +0, so x + 0 = x exactly;
-//   * a sample's targets outside the 4x4 interior read a null row (mask 0,
-//     start = a trash entry).
-// ---------------------------------------------------------------------------
-#ifndef SIFT_DBG_BFI
-#define SIFT_DBG_BFI 0
-#endif
-#ifndef SIFT_DBG_DPP
-#define SIFT_DBG_DPP 0
-#endif
-#ifndef SIFT_DBG_PADS
-#define SIFT_DBG_PADS 0
-#endif
 constexpr int kRunRows = 16 * 5;               // (cell, g): g = 0..3 pairs, g = 4 bin 8
 constexpr int kNullRow = kRunRows;             // invalid targets
 constexpr int kPoolEntries = 64 * 8 + 80 * 3;  // <= 8 entries per sample + padding of 80 runs to multiples of 4
 constexpr int kTrash = kPoolEntries;           // 4 entries: invalid targets, and the zeroing of empty runs
-// Bitfield select d = (sel & s) | (~sel & v) with the SGPR operand in place:
-// one v_bfi_b32 (the compiler's form of the pick moved every ballot half to a
-// VGPR and used two instructions per step).
-__device__ __forceinline__ unsigned bfi_sv(unsigned sel, unsigned s, unsigned v) {
-    unsigned d;
-    asm volatile("v_bfi_b32 %0, %1, %2, %3" : "=v"(d) : "v"(sel), "s"(s), "v"(v));
-    return d;
-}
+// (Measured and dropped: the masks' picks as inline-asm v_bfi_b32 with the
+// ballot SGPR as an operand -- 60 fewer VALU per chunk than the compiler's
+// v_mov + v_cndmask, but descriptors went wrong on the GPU (an SGPR hazard the
+// compiler cannot see inside inline asm; tests/test_gpu_batch.py).)
 // Inclusive wave prefix sum with the DPP row shifts / broadcasts applied to
 // the adds themselves (no zero-initialised copies): wave_incl_scan's result.
 // Rows outside row_mask are not written and keep their sum.
@@ -972,7 +612,7 @@ __device__ __forceinline__ int wave_incl_scan_dpp(int x) {
         : "+v"(x));
     return x;
 }
-__global__ __launch_bounds__(kExactWG) void k_descriptor_exact_runs(const DescJob* __restrict__ jobs,
+__global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __restrict__ jobs,
                                                                     const Counters* __restrict__ ctr,
                                                                     uint16_t* __restrict__ desc, Sidecar sidecar,
                                                                     Counters* __restrict__ host_ctr, HostOut host,
@@ -1072,8 +712,14 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact_runs(const DescJo
             int i, j;
             float l, r, u, d;
         };
-        // As k_descriptor_exact's fetch: gradient loads two chunks ahead, rows
-        // of a chunk by a ds_max scatter of row starts + a DPP prefix maximum.
+        // Gradient loads two chunks ahead of the math (unconditionally: past
+        // the end they re-read an in-buffer address).  Rows of a chunk [kf, kf
+        // + 64) without a per-lane search: frb is the row of sample kf; rows
+        // frb+1 .. frb+64 that start inside the chunk mark their start (ds_max:
+        // of several rows starting at one position -- empty rows -- the last
+        // is the non-empty one) and a wave prefix maximum gives every position
+        // its row.  Non-empty rows are contiguous, so 64 rows cover the chunk;
+        // if not, the binary search.
         int frb = N > 0 ? __builtin_amdgcn_readfirstlane(enumerated ? row_search(0) : 0) : 0;
         auto fetch = [&](int kf) {
             Fetch f;
@@ -1119,7 +765,7 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact_runs(const DescJo
         }
         float accA = 0.f, accB = 0.f, accW = 0.f;  // bins 2g, 2g + 1, and 8 (g = 0)
         for (int k0 = 0; k0 < N; k0 += 64) {
-            // ---- sample k0 + lane: the oracle's math (as k_descriptor_exact) ----
+            // ---- sample k0 + lane: the oracle's math ----
             const int i = f1.i, j = f1.j;
             const float l = f1.l, r = f1.r, u = f1.u, d = f1.d;
             f1 = f2;
@@ -1158,13 +804,8 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact_runs(const DescJo
                 unsigned lo = (unsigned)X[0], hi = (unsigned)(X[0] >> 32);
 #pragma unroll
                 for (int q = 1; q < kD; q++) {
-#if SIFT_DBG_BFI
-                    lo = bfi_sv(sel[q], (unsigned)X[q], lo);
-                    hi = bfi_sv(sel[q], (unsigned)(X[q] >> 32), hi);
-#else
                     lo = ((unsigned)X[q] & sel[q]) | (lo & ~sel[q]);
                     hi = ((unsigned)(X[q] >> 32) & sel[q]) | (hi & ~sel[q]);
-#endif
                 }
                 return (unsigned long long)hi << 32 | lo;
             };
@@ -1175,31 +816,19 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact_runs(const DescJo
             const int c4 = (cnt + 3) & ~3, w4 = (cntw + 3) & ~3;
             // Runs: every pair run, then every bin-8 run (16-bit halves of one scan).
             const int packed = c4 | w4 << 16;
-#if SIFT_DBG_DPP
             const int incl = wave_incl_scan_dpp(packed), excl = incl - packed;
-#else
-            const int incl = wave_incl_scan(packed), excl = incl - packed;
-#endif
             const int start = excl & 0xffff, startw = (__builtin_amdgcn_readlane(incl, 63) & 0xffff) + (excl >> 16);
             tbl[cell * 5 + g] = make_uint4((unsigned)M, (unsigned)(M >> 32), (unsigned)start, 0u);
             if (g == 0) tbl[cell * 5 + 4] = make_uint4((unsigned)Mw, (unsigned)(Mw >> 32), (unsigned)startw, 0u);
             // Padding: the run's last four entries are zeroed unconditionally
             // (the samples' writes below land on the real ones afterwards); an
             // empty run zeroes the trash entries instead.
-#if !SIFT_DBG_PADS
-#pragma unroll
-            for (int t = 1; t < 4; t++) {  // zero padding up to four entries
-                if (cnt + t <= c4 && (cnt & 3)) pool[start + c4 - t] = make_float2(0.f, 0.f);
-                if (cntw + t <= w4 && (cntw & 3)) pool[startw + w4 - t] = make_float2(0.f, 0.f);
-            }
-#else
             {
                 float4* zp = reinterpret_cast<float4*>(pool + (c4 ? start + c4 - 4 : kTrash));
                 zp[0] = zp[1] = make_float4(0.f, 0.f, 0.f, 0.f);
                 float4* zw = reinterpret_cast<float4*>(pool + (w4 ? startw + w4 - 4 : kTrash));
                 zw[0] = zw[1] = make_float4(0.f, 0.f, 0.f, 0.f);
             }
-#endif
             wave_lds_sync();
             // ---- samples: push each contribution pair to its owner's run ----
             const bool odd = o0 & 1;
@@ -1285,17 +914,13 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact_runs(const DescJo
     }
 }
 
-#ifndef SIFT_EXACT_RUNS
-#define SIFT_EXACT_RUNS 1  // A/B: 0 = the mask walk (k_descriptor_exact)
-#endif
-
 void launch_descriptor(const DescJob* jobs, const Counters* ctr, const unsigned* range_keys, uint16_t* desc,
                        Sidecar sidecar, Counters* host_ctr, HostOut host, const KeypointParams& kp, const Frames& fr,
                        hipStream_t s) {
     if (kp.descExact) {
         // One wave per keypoint; each workgroup loops over keypoints.
         const int per = fr.nf <= 1 ? 2048 : std::max(512, 8192 / fr.nf);
-        hipLaunchKernelGGL(SIFT_EXACT_RUNS ? k_descriptor_exact_runs : k_descriptor_exact, dim3(per * fr.nf),
+        hipLaunchKernelGGL(k_descriptor_exact, dim3(per * fr.nf),
                            dim3(kExactWG), 0, s, jobs, ctr, desc, sidecar, host_ctr, host, fr.stride, (unsigned)fr.nf);
         return;
     }
