@@ -590,9 +590,7 @@ void upload_desc_exp_table(const float* tab64) {
 }
 
 constexpr int kRunRows = 16 * 5;               // (cell, g): g = 0..3 pairs, g = 4 bin 8
-constexpr int kNullRow = kRunRows;             // invalid targets
 constexpr int kPoolEntries = 64 * 8 + 80 * 3;  // <= 8 entries per sample + padding of 80 runs to multiples of 4
-constexpr int kTrash = kPoolEntries;           // 4 entries: invalid targets, and the zeroing of empty runs
 // (Measured and dropped: the masks' picks as inline-asm v_bfi_b32 with the
 // ballot SGPR as an operand -- 60 fewer VALU per chunk than the compiler's
 // v_mov + v_cndmask, but descriptors went wrong on the GPU (an SGPR hazard the
@@ -618,8 +616,8 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
                                                                     Counters* __restrict__ host_ctr, HostOut host,
                                                                     long fs, unsigned nf) {
     __shared__ float s_tab[64];
-    __shared__ __attribute__((aligned(16))) float2 s_pool[kExactWaves][kPoolEntries + 4];  // + the trash entries
-    __shared__ __attribute__((aligned(16))) uint4 s_tbl[kExactWaves][kRunRows + 1];        // {mask lo, hi, start, -}
+    __shared__ __attribute__((aligned(16))) float2 s_pool[kExactWaves][kPoolEntries];
+    __shared__ __attribute__((aligned(16))) uint4 s_tbl[kExactWaves][kRunRows];            // {mask lo, hi, start, -}
     __shared__ unsigned short s_rowpre[kExactWaves][kMaxRows + 1];
     __shared__ signed char s_rowlo[kExactWaves][kMaxRows];
     __shared__ float s_nrm[kExactWaves][12];
@@ -646,7 +644,6 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
         reinterpret_cast<unsigned*>(host_ctr)[threadIdx.x] = reinterpret_cast<const unsigned*>(ctr)[threadIdx.x];
     if (wg * kExactWaves >= n) return;  // workgroup-uniform
     if (w == 0) s_tab[lane] = c_desc_exptab[lane];
-    if (lane == 0) tbl[kNullRow] = make_uint4(0u, 0u, (unsigned)kTrash, 0u);
     lds_barrier();
     const float bins_per_rad = kN / 360.f;
     const float exp_scale = -1.f / (kD * kD * 0.5f);
@@ -820,13 +817,15 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
             const int start = excl & 0xffff, startw = (__builtin_amdgcn_readlane(incl, 63) & 0xffff) + (excl >> 16);
             tbl[cell * 5 + g] = make_uint4((unsigned)M, (unsigned)(M >> 32), (unsigned)start, 0u);
             if (g == 0) tbl[cell * 5 + 4] = make_uint4((unsigned)Mw, (unsigned)(Mw >> 32), (unsigned)startw, 0u);
-            // Padding: the run's last four entries are zeroed unconditionally
-            // (the samples' writes below land on the real ones afterwards); an
-            // empty run zeroes the trash entries instead.
-            {
-                float4* zp = reinterpret_cast<float4*>(pool + (c4 ? start + c4 - 4 : kTrash));
+            // Padding: a run whose count is not a multiple of four has its last
+            // four entries zeroed first (the samples' writes below land on the
+            // real ones afterwards).
+            if (cnt & 3) {
+                float4* zp = reinterpret_cast<float4*>(pool + start + c4 - 4);
                 zp[0] = zp[1] = make_float4(0.f, 0.f, 0.f, 0.f);
-                float4* zw = reinterpret_cast<float4*>(pool + (w4 ? startw + w4 - 4 : kTrash));
+            }
+            if (cntw & 3) {
+                float4* zw = reinterpret_cast<float4*>(pool + startw + w4 - 4);
                 zw[0] = zw[1] = make_float4(0.f, 0.f, 0.f, 0.f);
             }
             wave_lds_sync();
@@ -835,15 +834,17 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 const int tci = r0 + (q >> 1), tcj = c0 + (q & 1);
-                const bool ok = valid && (unsigned)tci < (unsigned)kD && (unsigned)tcj < (unsigned)kD;
-                const int rp = ok ? (tci * kD + tcj) * 5 + (o0 >> 1) : kNullRow;
-                const int rs = ok && odd ? rp + 1 : kNullRow;
-                const uint4 tp = tbl[rp], ts = tbl[rs];
-                const unsigned ip = __builtin_amdgcn_mbcnt_hi(tp.y, __builtin_amdgcn_mbcnt_lo(tp.x, tp.z));
-                const unsigned is = __builtin_amdgcn_mbcnt_hi(ts.y, __builtin_amdgcn_mbcnt_lo(ts.x, ts.z));
-                const float lo = v[2 * q], hi = v[2 * q + 1];
-                pool[ip] = make_float2(odd ? 0.f : lo, odd ? lo : hi);
-                pool[is] = make_float2(hi, 0.f);
+                if (valid && (unsigned)tci < (unsigned)kD && (unsigned)tcj < (unsigned)kD) {
+                    const int rp = (tci * kD + tcj) * 5 + (o0 >> 1);
+                    const float lo = v[2 * q], hi = v[2 * q + 1];
+                    const uint3 tp = *reinterpret_cast<const uint3*>(&tbl[rp]);
+                    pool[__builtin_amdgcn_mbcnt_hi(tp.y, __builtin_amdgcn_mbcnt_lo(tp.x, tp.z))] =
+                        make_float2(odd ? 0.f : lo, odd ? lo : hi);
+                    if (odd) {
+                        const uint3 ts = *reinterpret_cast<const uint3*>(&tbl[rp + 1]);
+                        pool[__builtin_amdgcn_mbcnt_hi(ts.y, __builtin_amdgcn_mbcnt_lo(ts.x, ts.z))] = make_float2(hi, 0.f);
+                    }
+                }
             }
             wave_lds_sync();
             // ---- owners: add the runs in order ----

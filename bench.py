@@ -74,7 +74,7 @@ def parse():
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the eager per-kernel timing pass (every launch event-bracketed): the command whose "
                          "rocprofv3 --kernel-trace --stats summary is committed beside the roofline numbers")
-    ap.add_argument("--traffic-summary", default=os.path.join(ROOT, "profiles", "round5", "pmc_summary.json"),
+    ap.add_argument("--traffic-summary", default=os.path.join(ROOT, "profiles", "round6", "pmc_summary.json"),
                     help="PMC summary (tools/pmc_summary.py) with FETCH_SIZE/WRITE_SIZE of this code")
     ap.add_argument("--cv-traffic-summary",
                     default=os.path.join(ROOT, "profiles", "round6", "pmc_summary_cvdefault.json"),
