@@ -30,56 +30,145 @@ __device__ __forceinline__ void up_coeff(int d, int slen, int& s, float& a0, flo
     a1 = f;
 }
 
-// Four adjacent outputs of one row per thread, one 16-byte store (rows are
-// 256-B aligned, so x0 = 4 q is): a quarter of the threads and stores of a
-// thread per output, whose 2.3 M waves per 16-frame 1920x1200 launch ran at
-// 1.9 TB/s (24.8 us per frame, round-6 bench `opencv_default` stage table).
+__device__ __forceinline__ float dpp_left_or(float own, float v) {  // lane i <- lane i-1, lane 0 <- own
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own), __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float dpp_right_or(float own, float v) {  // lane i <- lane i+1, lane 63 <- own
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own), __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
+
+// One wave per 256 source columns and a run of source rows (rows per wave =
+// H / (4 gridDim.y), rounded up): lane l holds columns c, c + 1 for c = base +
+// 2l and c = base + 128 + 2l -- one 8-byte load per row and half, 512 B
+// contiguous per wave -- and takes its neighbours c - 1, c + 2 from lanes l - 1
+// / l + 1 by DPP (lanes 0 / 63 from the other half or one extra load per row).
+// Each source row's horizontal interpolation is formed once and kept in a
+// 3-row ring; rows 2m, 2m + 1 are then one 16-byte store per half whose 64
+// lanes cover 1 KB contiguously.  Away from the left and right borders every
+// horizontal output takes the fixed weights (0.25, 0.75) / (0.75, 0.25) --
+// up_coeff's values there, in the same operation order; border lanes and every
+// vertical step take up_coeff.  (Measured, round 6, per 16-frame 1920x1200
+// launch: one output per thread 408 us (1.8 TB/s); 16 outputs per thread with
+// two 16-byte stores 32 B apart 330; one wave per row with contiguous stores
+// and three loads per window 242 -- 167 of it with the loads removed.)
 template <typename T>
 __global__ __launch_bounds__(256) void k_upsample2x(const T* __restrict__ src, int spitch, int W, int H,
                                                     float* __restrict__ dst, int dpitch, long sfs, long dfs) {
     src = fptr(src, blockIdx.z * sfs);  // frame blockIdx.z
     dst = fptr(dst, blockIdx.z * dfs);
-    const int x0 = 4 * (blockIdx.x * 64 + (threadIdx.x & 63));
-    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (x0 >= 2 * W || y >= 2 * H) return;
-    int sy;
-    float ay0, ay1;
-    up_coeff(y, H, sy, ay0, ay1);
-    const int sy1 = min(sy + 1, H - 1);
-    const T* r0 = src + (size_t)sy * spitch;
-    const T* r1 = src + (size_t)sy1 * spitch;
-    float o[4];
+    const int per = (H + 4 * (int)gridDim.y - 1) / (4 * (int)gridDim.y);  // source rows per wave
+    const int m0 = (blockIdx.y * 4 + (threadIdx.x >> 6)) * per;
+    if (m0 >= H) return;  // wave-uniform
+    const int mEnd = min(m0 + per, H);
+    const int lane = threadIdx.x & 63, base = blockIdx.x * 256;
+    const int c[2] = {base + 2 * lane, base + 128 + 2 * lane};
+    const int xe = lane == 0 ? max(base - 1, 0) : min(base + 256, W - 1);  // lanes 0 / 63: outer columns
+    const bool vec = sizeof(T) == 4 && (reinterpret_cast<uintptr_t>(src) & 7) == 0 && (spitch & 1) == 0;
+    struct Raw {
+        float v[2][2], e;
+    };
+    // Source row y (clamped), columns clamped to the row: every lane's window
+    // is src[clamp(c - 1 .. c + 2)].
+    auto load = [&](int y, Raw& r) {
+        const T* row = src + (size_t)min(max(y, 0), H - 1) * spitch;
 #pragma unroll
-    for (int t = 0; t < 4; t++) {
-        const int x = min(x0 + t, 2 * W - 1);  // past the row end: a duplicate, never stored
-        int sx;
-        float ax0, ax1;
-        up_coeff(x, W, sx, ax0, ax1);
-        const int sx1 = min(sx + 1, W - 1);
-        const float h0 = (float)r0[sx] * ax0 + (float)r0[sx1] * ax1;
-        const float h1 = (float)r1[sx] * ax0 + (float)r1[sx1] * ax1;
-        o[t] = h0 * ay0 + h1 * ay1;
-    }
-    float* d = dst + (size_t)y * dpitch + x0;
-    if (x0 + 4 <= 2 * W) {
-        *reinterpret_cast<float4*>(d) = make_float4(o[0], o[1], o[2], o[3]);
-    } else {
+        for (int h = 0; h < 2; h++) {
+            if (vec && c[h] + 1 < W) {
+                const float2 q = *reinterpret_cast<const float2*>(row + c[h]);
+                r.v[h][0] = q.x;
+                r.v[h][1] = q.y;
+            } else {
+                r.v[h][0] = (float)row[min(c[h], W - 1)];
+                r.v[h][1] = (float)row[min(c[h] + 1, W - 1)];
+            }
+        }
+        r.e = (float)row[xe];
+    };
+    auto horiz = [&](const Raw& r, float (&hh)[8]) {
+        float w[2][4];
+        const float a1_63 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r.v[0][1]), 63));
+        const float b0_0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r.v[1][0]), 0));
+        w[0][0] = dpp_left_or(r.e, r.v[0][1]);
+        w[0][3] = dpp_right_or(b0_0, r.v[0][0]);
+        w[1][0] = dpp_left_or(a1_63, r.v[1][1]);
+        w[1][3] = dpp_right_or(r.e, r.v[1][0]);
 #pragma unroll
-        for (int t = 0; t < 4; t++)
-            if (x0 + t < 2 * W) d[t] = o[t];
+        for (int h = 0; h < 2; h++) {
+            w[h][1] = r.v[h][0];
+            w[h][2] = r.v[h][1];
+            if (c[h] >= 1 && c[h] + 2 < W) {
+                hh[4 * h] = w[h][0] * 0.25f + w[h][1] * 0.75f;
+                hh[4 * h + 1] = w[h][1] * 0.75f + w[h][2] * 0.25f;
+                hh[4 * h + 2] = w[h][1] * 0.25f + w[h][2] * 0.75f;
+                hh[4 * h + 3] = w[h][2] * 0.75f + w[h][3] * 0.25f;
+            } else {
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    int sx;
+                    float ax0, ax1;
+                    up_coeff(min(2 * c[h] + t, 2 * W - 1), W, sx, ax0, ax1);
+                    const int k0 = min(max(sx - c[h] + 1, 0), 3), k1 = min(max(min(sx + 1, W - 1) - c[h] + 1, 0), 3);
+                    const float s0 = k0 == 0 ? w[h][0] : (k0 == 1 ? w[h][1] : (k0 == 2 ? w[h][2] : w[h][3]));
+                    const float s1 = k1 == 0 ? w[h][0] : (k1 == 1 ? w[h][1] : (k1 == 2 ? w[h][2] : w[h][3]));
+                    hh[4 * h + t] = s0 * ax0 + s1 * ax1;
+                }
+            }
+        }
+    };
+    Raw rr;
+    float hp[8], hc[8], hn[8];
+    load(m0 - 1, rr);
+    horiz(rr, hp);
+    load(m0, rr);
+    horiz(rr, hc);
+    load(m0 + 1, rr);
+    for (int m = m0; m < mEnd; m++) {
+        horiz(rr, hn);                  // source row m + 1
+        if (m + 1 < mEnd) load(m + 2, rr);  // one row ahead of the stores
+#pragma unroll
+        for (int v = 0; v < 2; v++) {
+            int sy;
+            float ay0, ay1;
+            up_coeff(2 * m + v, H, sy, ay0, ay1);  // sy in {m - 1, m}, its successor in {m, m + 1}
+            const bool r0c = sy == m, r1c = min(sy + 1, H - 1) == m;
+            float o[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) o[i] = (r0c ? hc[i] : hp[i]) * ay0 + (r1c ? hc[i] : hn[i]) * ay1;
+            float* d = dst + (size_t)(2 * m + v) * dpitch;
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                if (c[h] + 2 <= W) {
+                    *reinterpret_cast<float4*>(d + 2 * c[h]) = make_float4(o[4 * h], o[4 * h + 1], o[4 * h + 2], o[4 * h + 3]);
+                } else if (c[h] < W) {  // W odd: the row's last two outputs
+                    d[2 * c[h]] = o[4 * h];
+                    d[2 * c[h] + 1] = o[4 * h + 1];
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            hp[i] = hc[i];
+            hc[i] = hn[i];
+        }
     }
+}
+
+// Source rows per wave: 8 for frame batches (fewer, longer-lived waves), 2
+// for a single frame (more waves in flight).
+dim3 up_grid(int W, int H, int nf) {
+    const int per = nf > 1 ? 8 : 2;
+    return dim3((W + 255) / 256, (H + 4 * per - 1) / (4 * per), nf);
 }
 
 void launch_upsample2x(const float* src, int spitch, int W, int H, float* dst, int dpitch, const Frames& fr, long sfs,
                        hipStream_t s) {
-    dim3 grid((2 * W + 255) / 256, (2 * H + 3) / 4, fr.nf);
-    hipLaunchKernelGGL(k_upsample2x<float>, grid, dim3(256), 0, s, src, spitch, W, H, dst, dpitch, sfs, fr.stride);
+    hipLaunchKernelGGL(k_upsample2x<float>, up_grid(W, H, fr.nf), dim3(256), 0, s, src, spitch, W, H, dst, dpitch, sfs,
+                       fr.stride);
 }
 
 void launch_upsample2x_u8(const uint8_t* src, int spitch, int W, int H, float* dst, int dpitch, const Frames& fr,
                           long sfs, hipStream_t s) {
-    dim3 grid((2 * W + 255) / 256, (2 * H + 3) / 4, fr.nf);
-    hipLaunchKernelGGL(k_upsample2x<uint8_t>, grid, dim3(256), 0, s, src, spitch, W, H, dst, dpitch, sfs, fr.stride);
+    hipLaunchKernelGGL(k_upsample2x<uint8_t>, up_grid(W, H, fr.nf), dim3(256), 0, s, src, spitch, W, H, dst, dpitch, sfs, fr.stride);
 }
 
 // ---------------------------------------------------------------------------
@@ -718,7 +807,7 @@ void head_upsample_node(HeadNode& h, const float* src, int spitch, int W, int H,
     put(7, &fr.stride, sizeof fr.stride);
     h.p = hipKernelNodeParams{};
     h.p.func = reinterpret_cast<void*>(&k_upsample2x<float>);
-    h.p.gridDim = dim3((2 * W + 255) / 256, (2 * H + 3) / 4, fr.nf);
+    h.p.gridDim = up_grid(W, H, fr.nf);
     h.p.blockDim = dim3(256);
     h.p.sharedMemBytes = 0;
     h.p.kernelParams = h.argv;
@@ -1165,13 +1254,6 @@ constexpr int EX4_LIST = 2048;  // per-workgroup candidate list (LDS): a 256 x 3
 // 16-frame launch.)
 constexpr int kExCpl = 4;
 constexpr int EX4_COLS = 64 * kExCpl;  // columns per wave
-
-__device__ __forceinline__ float dpp_left_or(float own, float v) {  // lane i <- lane i-1, lane 0 <- own
-    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own), __float_as_int(v), 0x138, 0xf, 0xf, false));
-}
-__device__ __forceinline__ float dpp_right_or(float own, float v) {  // lane i <- lane i+1, lane 63 <- own
-    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own), __float_as_int(v), 0x130, 0xf, 0xf, false));
-}
 
 // One workgroup = 4 waves stacked vertically over a 256-column strip: block
 // `tile` of the octave (strips across; the caller picks the XCD order).
