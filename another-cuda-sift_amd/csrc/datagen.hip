@@ -53,7 +53,7 @@ int job_plane(const sift_hip_detector* d, const float* img) {
 // pixel-range keys), counters.u32 (Counters): frame 0 of the arena, after the
 // frame completed (nothing reuses these buffers before the next frame).
 int dump_records(sift_hip_detector* d, const std::string& dir) {
-    const Counters& c = d->hCtr[(size_t)d->cur * d->B];
+    const Counters& c = d->hCtr[(size_t)d->cur * d->lane().B];
     const size_t nRef = std::min<unsigned>(c.refined, d->kp.capRefined);
     const size_t nOri = std::min<size_t>(nRef + c.oriented, d->kp.capOriented);
     const size_t nFin = std::min<unsigned>(c.final_n, d->kp.capFinal);
@@ -98,7 +98,7 @@ int dump_stage_files(sift_hip_detector* d) {
         snprintf(e, sizeof e, "%s[%d, %d]", o ? ", " : "", g.W, g.H);
         octs += e;
     }
-    const Counters& c = d->hCtr[(size_t)d->cur * d->B];
+    const Counters& c = d->hCtr[(size_t)d->cur * d->lane().B];
     const int nc = (int)std::min<unsigned>(c.cand, d->capCand);
     std::vector<uint2> cand(nc);
     std::vector<int> quads(4 * (size_t)nc);
@@ -211,7 +211,7 @@ int write_planes(sift_hip_detector* d, const std::string& dir) {
 // memset of the arenas; the handle has no current frame afterwards.
 int replay_reset(sift_hip_detector* d) {
     bind_lane(d, 0);
-    HIPCHK(hipMemsetAsync(d->lanes[0].arena, 0, (size_t)d->afs * d->B, d->stream));
+    HIPCHK(hipMemsetAsync(d->lanes[0].arena, 0, (size_t)d->afs * d->lanes[0].B, d->stream));
     if (int rc = sync_lanes(d)) return rc;
     d->firstFrame = d->submitted;
     d->current = d->submitted - 1;

@@ -222,7 +222,7 @@ const uint16_t* frame_desc(const sift_hip_detector* d, long long f) {
 }
 const Counters& frame_counters(const sift_hip_detector* d, long long f, int i) {
     const auto& r = d->frecs[f & (kFrameRing - 1)];
-    return d->lanes[r.lane].hCtr[(size_t)r.slot * d->B + r.idx + i];
+    return d->lanes[r.lane].hCtr[(size_t)r.slot * d->lanes[r.lane].B + r.idx + i];
 }
 
 // Per-handle allocations shared by the lanes: the upload ring and the frame
@@ -293,16 +293,17 @@ int build_graphs(sift_hip_detector* d);
 
 // A new compute lane: stream, zeroed arenas, host counters, events and the
 // captured graphs (bound on return).
-int add_lane(sift_hip_detector* d) {
+int add_lane(sift_hip_detector* d, int B) {
     if (d->nLanes >= kMaxLanes) return fail(SIFT_HIP_ERR_STATE, "no lane left");
     const int k = d->nLanes;
     Lane& L = d->lanes[k];
     d->nLanes++;  // from here the destructor releases what the lane holds
+    L.B = B;
     HIPCHK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
-    if (hipMalloc((void**)&L.arena, (size_t)d->afs * d->B) != hipSuccess)
+    if (hipMalloc((void**)&L.arena, (size_t)d->afs * B) != hipSuccess)
         return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc of the frame arenas failed");
-    HIPCHK(hipMemsetAsync(L.arena, 0, (size_t)d->afs * d->B, L.stream));
-    const size_t nh = (size_t)d->kSlots * d->B;
+    HIPCHK(hipMemsetAsync(L.arena, 0, (size_t)d->afs * B, L.stream));
+    const size_t nh = (size_t)d->kSlots * B;
     HIPCHK(hipHostMalloc((void**)&L.hCtr, sizeof(Counters) * nh, hipHostMallocMapped | hipHostMallocCoherent));
     memset(L.hCtr, 0, sizeof(Counters) * nh);
     HIPCHK(hipHostGetDevicePointer((void**)&L.hCtrDev, L.hCtr, 0));
@@ -324,7 +325,7 @@ int add_lane(sift_hip_detector* d) {
         HIPCHK(hipEventRecord(L.evRead[i], L.stream));
     }
     bind_lane(d, k);
-    for (int i = 0; i < d->B; i++)
+    for (int i = 0; i < B; i++)
         for (int b = 0; b < d->kSlots; b++)
             register_sidecar(d, fptr(d->dDesc[b], (long)i * d->afs),
                              Sidecar{fptr(d->dSide[b].codes, (long)i * d->afs), fptr(d->dSide[b].keys, (long)i * d->afs)},
@@ -533,8 +534,8 @@ void enqueue_descriptor(sift_hip_detector* d, int slot, int nf) {
     const Frames fr{nf, d->afs};
     d->timed("descriptor", 0, [&] {
         launch_descriptor(d->dJobs, d->dCtr, range_keys(d, slot & 1), d->dDesc[slot], d->dSide[slot],
-                          d->hCtrDev + (size_t)slot * d->B,
-                          HostOut{d->lanes[d->ln].dHostTab + (size_t)slot * d->B, d->dKpts3[slot], d->dFeats4[slot],
+                          d->hCtrDev + (size_t)slot * d->lane().B,
+                          HostOut{d->lane().dHostTab + (size_t)slot * d->lane().B, d->dKpts3[slot], d->dFeats4[slot],
                                   d->kp.capFinal},
                           d->kp, fr, d->stream);
     });
@@ -594,10 +595,10 @@ int capture_with_head(sift_hip_detector* d, int slot, int nf, hipGraphExec_t* ou
 int build_graphs(sift_hip_detector* d) {
     Lane& L = d->lane();
     for (int b = 0; b < d->kSlots; b++) {
-        if (int rc = capture(d, b, d->B, &L.exec[b])) return rc;
-        if (int rc = capture_with_head(d, b, d->B, &L.execH[b], &L.graphH[b], &L.headH[b])) return rc;
+        if (int rc = capture(d, b, L.B, &L.exec[b])) return rc;
+        if (int rc = capture_with_head(d, b, L.B, &L.execH[b], &L.graphH[b], &L.headH[b])) return rc;
         L.headIn[b][0] = Lane::HeadIn{d->dInput, d->inPitch, d->afs};
-        if (d->B > 1) {
+        if (L.B > 1) {
             if (int rc = capture(d, b, 1, &L.exec1[b])) return rc;
             if (int rc = capture_with_head(d, b, 1, &L.execH1[b], &L.graphH1[b], &L.headH1[b])) return rc;
             L.headIn[b][1] = Lane::HeadIn{d->dInput, d->inPitch, d->afs};
@@ -619,12 +620,12 @@ bool event_done(hipEvent_t e) {
 // range-key parity alternating, and the lane's next frame takes slot 0.
 int warm_lane(sift_hip_detector* d) {
     Lane& L = d->lane();
-    const int nb = d->B > 1 ? 2 : 1;
+    const int nb = L.B > 1 ? 2 : 1;
     for (int r = 0; r < nb; r++)
         for (int b = 0; b < d->kSlots; b++) {
             HIPCHK(hipGraphLaunch(r == 0 ? L.execH[b] : L.execH1[b], L.stream));
             HIPCHK(hipEventRecord(L.evFrame[b], L.stream));
-            L.nfOf[b] = r == 0 ? d->B : 1;
+            L.nfOf[b] = r == 0 ? L.B : 1;
         }
     L.launched = (long long)nb * d->kSlots;
     return SIFT_HIP_OK;
@@ -653,7 +654,7 @@ int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEven
     }
     const bool graphs = d->useGraph && !d->timing;
     hipGraphExec_t gh = !graphs || consumed || fmt != SIFT_HIP_F32 ? nullptr
-                        : nf == d->B                                 ? L.execH[slot]
+                        : nf == L.B                                  ? L.execH[slot]
                         : nf == 1                                    ? L.execH1[slot]
                                                                      : nullptr;
     // The head node of execH[slot] is re-pointed only once that exec's last
@@ -663,18 +664,18 @@ int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEven
     if (gh && !event_done(L.evFrame[slot])) gh = nullptr;
     if (gh) {  // device f32 input: one launch for the whole frame, the head re-pointed at img
         const Lane::HeadIn in{img, pitch, sfs};
-        Lane::HeadIn& cur = L.headIn[slot][nf == d->B ? 0 : 1];
+        Lane::HeadIn& cur = L.headIn[slot][nf == L.B ? 0 : 1];
         if (!(cur == in)) {
             HeadNode& h = d->headNode;
             head_node(d, h, static_cast<const float*>(img), pitch, slot & 1, nf, sfs);
-            HIPCHK(hipGraphExecKernelNodeSetParams(gh, nf == d->B ? L.headH[slot] : L.headH1[slot], &h.p));
+            HIPCHK(hipGraphExecKernelNodeSetParams(gh, nf == L.B ? L.headH[slot] : L.headH1[slot], &h.p));
             cur = in;
         }
         HIPCHK(hipGraphLaunch(gh, d->stream));
     } else {
         enqueue_head(d, img, pitch, fmt, slot & 1, nf, sfs);
         if (consumed) HIPCHK(hipEventRecord(consumed, d->stream));
-        hipGraphExec_t g = nf == d->B ? L.exec[slot] : (nf == 1 ? L.exec1[slot] : nullptr);
+        hipGraphExec_t g = nf == L.B ? L.exec[slot] : (nf == 1 ? L.exec1[slot] : nullptr);
         if (graphs && g) {
             HIPCHK(hipGraphLaunch(g, d->stream));
         } else {  // timing mode, or a partial batch: the same launches, eagerly
@@ -852,7 +853,7 @@ int sift_hip_warmup(sift_hip_t d) {
     }
     int rc = allocate(d);
     if (rc) return rc;
-    rc = add_lane(d);  // lane 0; more lanes on demand (pick_lane)
+    rc = add_lane(d, d->B);  // lane 0; more lanes on demand (pick_lane)
     if (rc) return rc;
     // One blank frame (batch) through each graph: first-touch, code-object load.
     for (int i = 0; i < d->kSlots * (d->B > 1 ? 2 : 1); i++) {
@@ -973,6 +974,21 @@ int sift_hip_micro_batch(sift_hip_t d, int* frames) {
     return SIFT_HIP_OK;
 }
 
+int sift_hip_set_auto_micro_batch(sift_hip_t d, int frames) {
+    if (!d) return fail(SIFT_HIP_ERR_INVALID, "null handle");
+    if (frames < 0 || frames > sift_hip_detector::kMaxMicroBatch)
+        return fail(SIFT_HIP_ERR_INVALID, "automatic micro-batch out of range (0..16)");
+    if (d->allocated) return fail(SIFT_HIP_ERR_STATE, "sift_hip_set_auto_micro_batch after sift_hip_warmup");
+    d->autoMb = frames;
+    return SIFT_HIP_OK;
+}
+
+int sift_hip_auto_micro_batch(sift_hip_t d, int* frames) {
+    if (!d || !frames) return fail(SIFT_HIP_ERR_INVALID, "null argument");
+    *frames = auto_groups(d) ? d->autoMb : 0;
+    return SIFT_HIP_OK;
+}
+
 int sift_hip_lanes(sift_hip_t d, int* max_lanes, int* created) {
     if (!d) return fail(SIFT_HIP_ERR_INVALID, "null handle");
     if (max_lanes) *max_lanes = d->maxLanes;
@@ -1038,7 +1054,7 @@ int sift_hip_batch_results_device(sift_hip_t d, int i, int* count, int* overflow
     if (i < 0 || i >= batch_frames_of(d)) return fail(SIFT_HIP_ERR_INVALID, "no such frame in the current batch");
     if (count || overflow)
         if (int rc = ensure_counts(d)) return rc;
-    const Counters& c = d->hCtr[(size_t)d->cur * d->B + i];
+    const Counters& c = d->hCtr[(size_t)d->cur * d->lane().B + i];
     const long o = (long)i * d->afs;
     if (count) *count = (int)std::min<unsigned>(c.final_n, d->kp.capFinal);
     if (overflow) *overflow = (int)c.overflow;
@@ -1090,7 +1106,7 @@ int sift_hip_overflow_flags(sift_hip_t d, int* flags) {
         bind_lane(d, d->curLane, d->curIdx);
         if (int rc = ensure_counts(d)) return rc;
     }
-    *flags = d->hCtr ? (int)d->hCtr[(size_t)d->cur * d->B].overflow : 0;
+    *flags = d->hCtr ? (int)d->hCtr[(size_t)d->cur * d->lane().B].overflow : 0;
     return SIFT_HIP_OK;
 }
 
@@ -1127,7 +1143,7 @@ int sift_hip_copy_to_host(sift_hip_t d, float* k3, float* f4, uint16_t* desc, in
             if (d->lanes[k].ready)
                 if (int rc = ensure_host_res(d, d->lanes[k])) return rc;
     d->hostWant = std::max(d->hostWant, desc ? 2 : 1);
-    const int region = d->cur * d->B + d->curIdx;
+    const int region = d->cur * d->lane().B + d->curIdx;
     if (L.hRes && L.hostFrame[region] == d->current && d->current >= d->firstFrame && (!desc || L.hostDesc[region])) {
         // A host-input frame: its descriptor kernel wrote them to pinned host memory.
         HIPCHK(hipEventSynchronize(L.evFrame[d->cur]));
@@ -1173,7 +1189,7 @@ int sift_hip_results_host(sift_hip_t d, const float** k3, const float** f4, cons
             if (d->lanes[k].ready)
                 if (int rc = ensure_host_res(d, d->lanes[k])) return rc;
     d->hostWant = std::max(d->hostWant, desc ? 2 : 1);
-    const int region = d->cur * d->B + d->curIdx;
+    const int region = d->cur * d->lane().B + d->curIdx;
     float *hk3, *hf4;
     uint16_t* hdesc;
     host_res(d, L.hRes, region, &hk3, &hf4, &hdesc);
@@ -1271,7 +1287,7 @@ int sift_hip_debug_gaussian(sift_hip_t d, int o, int layer, float* out) {
 int sift_hip_debug_candidates(sift_hip_t d, int* quads, int cap, int* count) {
     CHECK_HANDLE(d);
     if (int rc = ensure_counts(d)) return rc;
-    const Counters& c = d->hCtr[(size_t)d->cur * d->B];
+    const Counters& c = d->hCtr[(size_t)d->cur * d->lane().B];
     const int n = (int)std::min<unsigned>(c.cand, d->capCand);
     if (count) *count = (int)c.cand;
     const int m = std::min(n, cap);

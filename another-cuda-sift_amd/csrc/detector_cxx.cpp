@@ -160,6 +160,9 @@ void Detector::setLanes(int lanes) {
     if (m_handle) check(sift_hip_set_lanes(m_handle, lanes), "setLanes");
 }
 
+void Detector::setAutoMicroBatch(int frames) {
+    if (m_handle) check(sift_hip_set_auto_micro_batch(m_handle, frames), "setAutoMicroBatch");
+}
 void Detector::setMicroBatch(int frames) {
     if (m_handle) check(sift_hip_set_micro_batch(m_handle, frames), "setMicroBatch");
 }

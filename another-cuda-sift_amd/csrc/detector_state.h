@@ -134,6 +134,10 @@ constexpr int kFrameRing = 256;  // per-frame (lane, slot, arena) records: > 2 x
 // different lanes run concurrently ("Frames in flight").
 struct Lane {
     hipStream_t stream = nullptr;
+    // Frame arenas of this lane (launch groups of up to B frames): the handle's
+    // batch size, or its automatic group size for the lanes created after lane
+    // 0 (sift_hip_set_auto_micro_batch).
+    int B = 1;
     // Set once add_lane completed (stream, arenas, host counters, graphs): a
     // lane whose creation failed part-way is never picked, synchronised or
     // handed host regions (its partial allocations wait for the destructor).
@@ -250,6 +254,13 @@ struct sift_hip_detector {
     // by the frames pending.
     static constexpr int kMaxMicroBatch = 16;
     int mb = 1;
+    // Automatic launch groups (sift_hip_set_auto_micro_batch, default 8) on a
+    // handle with neither a batch nor a micro-batch set: a submitted frame runs
+    // at once while a lane is free; once every lane is busy, frames queue and
+    // the queue runs as one launch group when a lane frees or when it holds
+    // autoMb frames.  Lane 0 keeps one arena (the synchronous path's memory);
+    // lanes created later hold autoMb.
+    int autoMb = 8;
     struct PendingFrame {
         const void* img;  // device frame, or the device address of a host frame's pinned staging
         size_t stride;
@@ -442,7 +453,7 @@ int allocate(sift_hip_detector* d);
 void bind_lane(sift_hip_detector* d, int k, int idx = 0);
 const uint16_t* frame_desc(const sift_hip_detector* d, long long f);
 const Counters& frame_counters(const sift_hip_detector* d, long long f, int i = 0);
-int add_lane(sift_hip_detector* d);
+int add_lane(sift_hip_detector* d, int B);
 int warm_lane(sift_hip_detector* d);
 unsigned* range_keys(sift_hip_detector* d, int p);
 void enqueue_head(sift_hip_detector* d, const void* img, int pitch, int fmt, int parity, int nf, long sfs);
@@ -462,7 +473,10 @@ int sync_lanes(sift_hip_detector* d);
 int finish_frame(sift_hip_detector* d);
 
 // ---- lanes.hip ----
-int pick_lane(sift_hip_detector* d);
+int group_cap(const sift_hip_detector* d);
+bool auto_groups(const sift_hip_detector* d);
+bool lane_available(sift_hip_detector* d, int nf);
+int pick_lane(sift_hip_detector* d, int nf = 1);
 int copy_stream(sift_hip_detector* d, hipStream_t* s);
 int format_size(int fmt);
 int check_in_flight(sift_hip_detector* d);

@@ -31,29 +31,68 @@ void copy_rows(CopyPool* pool, char* dst, size_t dpitch, const char* src, size_t
     pool->run([&](int k) { part((int)((long)rows * k / P), (int)((long)rows * (k + 1) / P)); });
 }
 
-// The lane for the next frame, bound on return: the first idle lane (its last
-// frame complete), else a new lane (up to maxLanes), else the busy lane whose
-// last frame is the oldest.  A lane qualifies only if its next results slot
-// holds no frame the caller may still read (current - 1 onwards).
-int pick_lane(sift_hip_detector* d) {
-    auto slot_free = [&](int k) {
-        const Lane& L = d->lanes[k];
-        const int s = (int)(L.launched % d->kSlots);
-        const long long occ = L.slotFrame[s] < 0 ? -1 : L.slotFrame[s] + std::max(L.slotNum[s], 1) - 1;  // its last frame
-        return occ < 0 || occ < d->firstFrame || occ < d->current - 1;
-    };
+// Launch-group size of a submitted frame's queue: the micro-batch, else the
+// automatic group size (a handle without a batch, with a second lane to run
+// groups on), else 1 (no queue).
+bool auto_groups(const sift_hip_detector* d) { return d->mb == 1 && d->B == 1 && d->autoMb > 1 && d->maxLanes > 1; }
+int group_cap(const sift_hip_detector* d) { return d->mb > 1 ? d->mb : (auto_groups(d) ? d->autoMb : 1); }
+
+namespace {
+// Automatic groups: frames past the current one (queued ones included).  Up
+// to 2 per lane run as single frames (the unbatched regime); past that, a
+// queue launches early only with at least half a group, so every results slot
+// of a group lane holds >= that many frames and the frames the caller may
+// still read fit in the slots (in_flight_limit).
+long long past_current(const sift_hip_detector* d) { return d->submitted + d->npend - std::max(d->current, d->firstFrame - 1); }
+int auto_min_group(const sift_hip_detector* d) { return std::max(2, d->autoMb / 2); }
+long long in_flight_limit(const sift_hip_detector* d) {
+    if (!auto_groups(d)) return 2LL * d->maxLanes * group_cap(d);
+    return std::max(2LL * d->maxLanes, (long long)(d->maxLanes - 1) * (d->kSlots - 1) * auto_min_group(d));
+}
+}  // namespace
+
+namespace {
+// A lane qualifies for a launch group of nf frames if it has the arenas and
+// its next results slot holds no frame the caller may still read (current - 1
+// onwards); it is idle once its last launch group completed.
+bool lane_fits(const sift_hip_detector* d, int k, int nf) {
+    const Lane& L = d->lanes[k];
+    if (!L.ready || L.B < nf) return false;
+    const int s = (int)(L.launched % d->kSlots);
+    const long long occ = L.slotFrame[s] < 0 ? -1 : L.slotFrame[s] + std::max(L.slotNum[s], 1) - 1;  // its last frame
+    return occ < 0 || occ < d->firstFrame || occ < d->current - 1;
+}
+bool lane_idle(const sift_hip_detector* d, int k) {
+    const Lane& L = d->lanes[k];
+    return L.last < 0 || event_done(L.evFrame[(L.launched + d->kSlots - 1) % d->kSlots]);
+}
+// Arenas of a lane created now: the handle's batch, or the automatic group size.
+int new_lane_frames(const sift_hip_detector* d) { return auto_groups(d) ? d->autoMb : d->B; }
+}  // namespace
+
+// Whether a launch group of nf frames would start at once: an idle lane that
+// fits it, or a lane still to be created.
+bool lane_available(sift_hip_detector* d, int nf) {
+    for (int k = 0; k < d->nLanes; k++)
+        if (lane_fits(d, k, nf) && lane_idle(d, k)) return true;
+    return d->nLanes < d->maxLanes && new_lane_frames(d) >= nf;
+}
+
+// The lane for the next launch group (nf frames), bound on return: the first
+// idle lane that fits it, else a new lane (up to maxLanes), else the busy lane
+// that fits it whose last frame is the oldest.
+int pick_lane(sift_hip_detector* d, int nf) {
     int busy = -1;
     for (int k = 0; k < d->nLanes; k++) {
-        if (!d->lanes[k].ready || !slot_free(k)) continue;
-        const Lane& L = d->lanes[k];
-        if (L.last < 0 || event_done(L.evFrame[(L.launched + d->kSlots - 1) % d->kSlots])) {
+        if (!lane_fits(d, k, nf)) continue;
+        if (lane_idle(d, k)) {
             bind_lane(d, k);
             return SIFT_HIP_OK;
         }
-        if (busy < 0 || L.last < d->lanes[busy].last) busy = k;
+        if (busy < 0 || d->lanes[k].last < d->lanes[busy].last) busy = k;
     }
-    if (d->nLanes < d->maxLanes) {  // (lane 0 comes from sift_hip_warmup)
-        if (int rc = add_lane(d)) return rc;
+    if (d->nLanes < d->maxLanes && new_lane_frames(d) >= nf) {  // (lane 0 comes from sift_hip_warmup)
+        if (int rc = add_lane(d, new_lane_frames(d))) return rc;
         return warm_lane(d);
     }
     if (busy < 0)
@@ -73,8 +112,8 @@ int format_size(int fmt) { return fmt == SIFT_HIP_U8 ? 1 : (fmt == SIFT_HIP_F32 
 // Frames in flight past `current` (host-input and device submits): at most 2
 // per lane the handle may use.
 int check_in_flight(sift_hip_detector* d) {
-    if (d->submitted + d->npend > d->current + 2LL * d->maxLanes * d->mb)
-        return fail(SIFT_HIP_ERR_STATE, "every lane already has two launch groups in flight past the current frame: sift_hip_wait first");
+    if (d->submitted + d->npend > d->current + in_flight_limit(d))
+        return fail(SIFT_HIP_ERR_STATE, "the frames in flight past the current frame reach the handle's limit: sift_hip_wait first");
     return SIFT_HIP_OK;
 }
 
@@ -100,7 +139,7 @@ void host_res(const sift_hip_detector* d, char* base, int region, float** k3, fl
 // stream (after its zeroing; frames launched earlier keep a null table).
 int ensure_host_res(sift_hip_detector* d, Lane& L) {
     if (L.hRes) return SIFT_HIP_OK;
-    const size_t nr = (size_t)d->kSlots * d->B, rb = host_res_bytes(d);
+    const size_t nr = (size_t)d->kSlots * L.B, rb = host_res_bytes(d);
     HIPCHK(hipHostMalloc((void**)&L.hRes, rb * nr, hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(hipHostGetDevicePointer((void**)&L.hResDev, L.hRes, 0));
     L.hostTab.resize(nr);
@@ -122,9 +161,30 @@ void mark_host_results(sift_hip_detector* d, long long f) {
     if (!d->hostWant) return;
     const auto& r = d->frec(f);
     Lane& L = d->lanes[r.lane];
-    const int region = r.slot * d->B + r.idx;
+    const int region = r.slot * L.B + r.idx;
     L.hostFrame[region] = f;
     L.hostDesc[region] = d->hostWant > 1;
+}
+
+// Whether a submitted frame joins the pending queue: always with a micro-batch;
+// with automatic groups once frames are pending or the frame would be the
+// third in flight per lane (up to that it is launched at once, on a busy lane
+// if none is free, as without groups: its stream starts it as soon as the
+// lane frees, where a queue waits for the next call).  Stage dumps and the
+// timing mode run frames one at a time.
+bool queue_frame(sift_hip_detector* d) {
+    if (!d->dgDir.empty() || d->timing) return false;
+    if (d->mb > 1) return true;
+    return auto_groups(d) && (d->npend > 0 || past_current(d) + 1 > 2LL * d->maxLanes);
+}
+// Whether the pending queue runs now: it holds a full group, or (automatic
+// groups) a lane that fits it has become free and the queue holds half a
+// group (any count while the frames in flight stay within 2 per lane).
+bool launch_now(sift_hip_detector* d) {
+    if (d->npend >= group_cap(d)) return true;
+    if (d->mb > 1) return false;
+    const bool shallow = past_current(d) <= 2LL * d->maxLanes;
+    return (shallow || d->npend >= auto_min_group(d)) && lane_available(d, d->npend);
 }
 
 // A host frame on a micro-batching handle: into the next pinned staging slot
@@ -133,15 +193,13 @@ void mark_host_results(sift_hip_detector* d, long long f) {
 int queue_host(sift_hip_detector* d, const void* img, size_t stride, int fmt, long long* ticket) {
     const int es = format_size(fmt), H = d->cfg.row_width;
     const size_t rowB = (size_t)es * d->cfg.col_width, pitchB = (size_t)es * d->inPitch;
-    if (d->npend && d->pend[0].fmt != fmt)
-        if (int rc = run_group(d)) return rc;
     if (d->hstSlotBytes < pitchB * H) {  // first host frame, or a larger format: (re)allocate the block
         if (int rc = run_group(d)) return rc;
         if (int rc = sync_lanes(d)) return rc;  // no copy kernel still reads the old block
         if (d->hstBlock) HIPCHK(hipHostFree(d->hstBlock));
         d->hstBlock = nullptr;
         d->hstSlotBytes = 0;
-        d->hstSlots = (2 * d->maxLanes + 1) * d->mb;  // frames pending or queued on the lanes
+        d->hstSlots = (2 * d->maxLanes + 1) * group_cap(d);  // frames pending or queued on the lanes
         if (hipHostMalloc((void**)&d->hstBlock, pitchB * H * d->hstSlots, hipHostMallocMapped | hipHostMallocNonCoherent) !=
             hipSuccess)
             return fail(SIFT_HIP_ERR_NOMEM, "hipHostMalloc of the micro-batch host staging failed");
@@ -163,7 +221,7 @@ int queue_host(sift_hip_detector* d, const void* img, size_t stride, int fmt, lo
     d->pend[i] = sift_hip_detector::PendingFrame{dev, pitchB, fmt, false, hs};
     d->npend = i + 1;
     if (ticket) *ticket = d->submitted + i;
-    if (d->npend < d->mb) return SIFT_HIP_OK;
+    if (!launch_now(d)) return SIFT_HIP_OK;
     const int rc = run_group(d);
     if (rc && d->npend == i + 1) {  // the group did not launch: this call's frame is not queued either
         d->npend = i;
@@ -185,7 +243,7 @@ int submit_host(sift_hip_detector* d, const void* img, size_t stride, int fmt, l
     if (stride == 0) stride = rowB;
     if (stride < rowB) return fail(SIFT_HIP_ERR_INVALID, "row stride smaller than width");
     if (int rc = check_in_flight(d)) return rc;
-    if (d->mb > 1 && d->dgDir.empty() && !d->timing) return queue_host(d, img, stride, fmt, ticket);
+    if (queue_frame(d)) return queue_host(d, img, stride, fmt, ticket);
     if (int rc = run_group(d)) return rc;  // pending micro-batch frames keep their submission order
     if (int rc = pick_lane(d)) return rc;
     Lane& L = d->lane();
@@ -219,26 +277,48 @@ int submit_host(sift_hip_detector* d, const void* img, size_t stride, int fmt, l
 int run_group(sift_hip_detector* d) {
     const int n = d->npend;
     if (!n) return SIFT_HIP_OK;
-    if (int rc = pick_lane(d)) return rc;
+    if (int rc = pick_lane(d, n)) return rc;
     Lane& L = d->lane();
     const int W = d->cfg.col_width, H = d->cfg.row_width;
+    if (n == 1 && d->pend[0].hslot < 0) {  // one device frame: straight from the caller's buffer
+        const auto& p = d->pend[0];
+        if (p.ordered) HIPCHK(hipStreamWaitEvent(d->stream, d->evPend[0], 0));
+        d->npend = 0;
+        return run_frame(d, p.img, (int)(p.stride / format_size(p.fmt)), p.fmt, nullptr);
+    }
+    // One format per launch group: the frames' own, or f32 when they mix (an
+    // 8-bit frame converted exactly, as the 8-bit head does).
+    int fmt = d->pend[0].fmt;
+    for (int i = 1; i < n; i++)
+        if (d->pend[i].fmt != fmt) fmt = SIFT_HIP_F32;
+    const int es = format_size(fmt);
     const size_t fb = sizeof(float) * (size_t)d->inPitch * H;  // one frame of f32 rows (an 8-bit frame uses a quarter)
-    if (!L.mbIn && hipMalloc((void**)&L.mbIn, fb * d->mb) != hipSuccess)
+    if (!L.mbIn && hipMalloc((void**)&L.mbIn, fb * L.B) != hipSuccess)
         return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc of the micro-batch input failed");
-    const int fmt = d->pend[0].fmt, es = format_size(fmt);
     bool host[sift_hip_detector::kMaxMicroBatch] = {};
     for (int i = 0; i < n; i++) {
         const auto& p = d->pend[i];
         if (p.ordered) HIPCHK(hipStreamWaitEvent(d->stream, d->evPend[i], 0));
+        char* dst = L.mbIn + fb * i;
+        const bool convert = p.fmt != fmt;  // an 8-bit frame in an f32 group
         if (p.hslot >= 0) {  // pinned staging: whole pitch rows over PCIe by a small grid
             unsigned req;
             unsigned* reqAt = host_request(d, i, &req);
-            launch_copy_rows(p.img, p.stride, L.mbIn + fb * i, p.stride, p.stride, H, kStageWg, d->stream, reqAt, req);
+            if (convert && !L.dStage[0] && hipMalloc(&L.dStage[0], fb) != hipSuccess)
+                return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc of the device staging failed");
+            // (the lane's host staging slot 0 as scratch: stream-ordered with its other users)
+            char* to = convert ? static_cast<char*>(L.dStage[0]) : dst;
+            launch_copy_rows(p.img, p.stride, to, p.stride, p.stride, H, kStageWg, d->stream, reqAt, req);
             HIPCHK(hipEventRecord(d->hstRead[p.hslot], d->stream));
+            if (convert)
+                launch_u8_to_f32((const uint8_t*)to, (int)p.stride, W, H, (float*)dst, d->inPitch, Frames{1, 0}, 0,
+                                 d->stream);
             host[i] = reqAt != nullptr;
+        } else if (convert) {
+            launch_u8_to_f32((const uint8_t*)p.img, (int)p.stride, W, H, (float*)dst, d->inPitch, Frames{1, 0}, 0,
+                             d->stream);
         } else {
-            launch_copy_rows(p.img, p.stride, L.mbIn + fb * i, (size_t)es * d->inPitch, (size_t)es * W, H,
-                             kGroupCopyWg, d->stream);
+            launch_copy_rows(p.img, p.stride, dst, (size_t)es * d->inPitch, (size_t)es * W, H, kGroupCopyWg, d->stream);
         }
     }
     d->npend = 0;
@@ -252,13 +332,11 @@ int run_group(sift_hip_detector* d) {
 // Device frame (HBM-resident, fp32 or u8) -> the frame's lane; the lane waits
 // for `stream` (the caller's producer) before reading it.  `queue`: a single
 // frame of sift_hip_submit_device on a micro-batching handle joins the pending
-// group instead (one format per group: a frame of the other format flushes it).
+// group instead.
 int submit_device(sift_hip_detector* d, const void* img, size_t stride, int fmt, void* stream, int nf, size_t fstride,
                   long long* ticket, bool queue) {
     hipStream_t ext = (hipStream_t)stream;
-    if (queue && d->mb > 1 && nf == 1 && d->dgDir.empty() && !d->timing) {
-        if (d->npend && d->pend[0].fmt != fmt)
-            if (int rc = run_group(d)) return rc;
+    if (queue && nf == 1 && queue_frame(d)) {
         const int i = d->npend;
         if (ext) {
             if (!d->evPend[i]) HIPCHK(hipEventCreateWithFlags(&d->evPend[i], hipEventDisableTiming));
@@ -267,13 +345,13 @@ int submit_device(sift_hip_detector* d, const void* img, size_t stride, int fmt,
         d->pend[i] = sift_hip_detector::PendingFrame{img, stride, fmt, ext != nullptr, -1};
         d->npend = i + 1;
         if (ticket) *ticket = d->submitted + i;
-        if (d->npend < d->mb) return SIFT_HIP_OK;
+        if (!launch_now(d)) return SIFT_HIP_OK;
         const int rc = run_group(d);
         if (rc && d->npend == i + 1) d->npend = i;  // the group did not launch: this call's frame is not queued
         return rc;
     }
     if (int rc = run_group(d)) return rc;  // frames are numbered (and launched) in submission order
-    if (int rc = pick_lane(d)) return rc;
+    if (int rc = pick_lane(d, nf)) return rc;
     if (ext) {
         HIPCHK(hipEventRecord(d->evIn, ext));
         HIPCHK(hipStreamWaitEvent(d->stream, d->evIn, 0));

@@ -99,6 +99,8 @@ def lib() -> ctypes.CDLL:
         "sift_hip_lanes": (i, [vp, ip, ip]),
         "sift_hip_set_micro_batch": (i, [vp, i]),
         "sift_hip_micro_batch": (i, [vp, ip]),
+        "sift_hip_set_auto_micro_batch": (i, [vp, i]),
+        "sift_hip_auto_micro_batch": (i, [vp, ip]),
         "sift_hip_sync": (i, [vp]),
         "sift_hip_set_batch": (i, [vp, i]),
         "sift_hip_batch_capacity": (i, [vp, ip]),
@@ -238,7 +240,7 @@ class Detector:
     """sift_cuda::Detector (Detector.hh:24-96) over the C ABI."""
 
     def __init__(self, config: CudaSiftConfig, device: int = -1, batch: int = 1, exact_descriptors: bool = False,
-                 lanes: Optional[int] = None, micro_batch: int = 1):
+                 lanes: Optional[int] = None, micro_batch: int = 1, auto_micro_batch: Optional[int] = None):
         """batch > 1: frame-batch handle (sift_hip_set_batch): detectBatchDevice runs up to `batch`
         frames per launch; the single-frame methods keep working (frame 0's arena).
         exact_descriptors: OpenCV's sequential float histogram (SIFT_HIP_DESC_EXACT), descriptors
@@ -246,7 +248,9 @@ class Detector:
         lanes: compute lanes for frames in flight (sift_hip_set_lanes, 1..4, library default 2):
         frames submitted before the previous one completes run concurrently on another lane.
         micro_batch > 1: frames of submitDevice queue until that many run as one launch group on a
-        lane (sift_hip_set_micro_batch; a wait on a queued frame launches the partial group)."""
+        lane (sift_hip_set_micro_batch; a wait on a queued frame launches the partial group).
+        auto_micro_batch: automatic launch groups of up to that many frames once every lane is busy
+        (sift_hip_set_auto_micro_batch; library default 8, 0 = off)."""
         self.config = config
         self.batch = int(batch)
         self.exact_descriptors = bool(exact_descriptors)
@@ -258,6 +262,8 @@ class Detector:
             _check(lib().sift_hip_set_lanes(self._h, int(lanes)), "set_lanes")
         if micro_batch != 1:
             _check(lib().sift_hip_set_micro_batch(self._h, int(micro_batch)), "set_micro_batch")
+        if auto_micro_batch is not None:
+            _check(lib().sift_hip_set_auto_micro_batch(self._h, int(auto_micro_batch)), "set_auto_micro_batch")
         if self.exact_descriptors:
             _check(lib().sift_hip_set_descriptor_mode(self._h, SIFT_HIP_DESC_EXACT), "set_descriptor_mode")
         n = ctypes.c_int()
@@ -376,6 +382,12 @@ class Detector:
         """Frames per submitDevice launch group (sift_hip_micro_batch)."""
         m = ctypes.c_int()
         _check(lib().sift_hip_micro_batch(self._h, ctypes.byref(m)), "micro_batch")
+        return m.value
+
+    def auto_micro_batch(self) -> int:
+        """Largest automatic launch group (sift_hip_auto_micro_batch; 0: automatic groups off)."""
+        m = ctypes.c_int()
+        _check(lib().sift_hip_auto_micro_batch(self._h, ctypes.byref(m)), "auto_micro_batch")
         return m.value
 
     def wait(self, ticket: int) -> None:

@@ -54,6 +54,10 @@ public:
     // Extra: submitDevice frames run in launch groups of `frames`
     // (sift_hip_set_micro_batch, 1..16); before gpuWarmUpAndAllocate.
     void setMicroBatch(int frames);
+    // Extra: automatic launch groups of up to `frames` once every lane is
+    // busy (sift_hip_set_auto_micro_batch; default 8, 0 = off); before
+    // gpuWarmUpAndAllocate.
+    void setAutoMicroBatch(int frames);
     // Extra: image already in device memory (fp32, row stride in bytes).
     void detectAndComputeDevice(const float* device_image, size_t row_stride_bytes, void* hip_stream = nullptr);
 

@@ -191,6 +191,26 @@ int sift_hip_submit_device(sift_hip_t h, const void* dev_img, size_t row_stride_
 int sift_hip_set_micro_batch(sift_hip_t h, int frames);
 int sift_hip_micro_batch(sift_hip_t h, int* frames);
 
+/* Automatic launch groups (the default, frames = 8; before sift_hip_warmup;
+ * 0 or 1 turns them off) on a handle without a batch or micro-batch and with
+ * more than one lane.  Frames of sift_hip_submit / sift_hip_submit_device run
+ * as single frames while at most 2 per lane are in flight past the last
+ * waited one (exactly as without groups); past that they queue, and the queue
+ * runs as ONE launch group (as with a micro-batch) when it holds `frames`
+ * frames, or -- checked at each submit -- when a lane that can take it is
+ * free and it holds frames / 2, or at a wait on a queued frame /
+ * sift_hip_sync / any other detect.  So a caller keeping many frames in
+ * flight gets micro-batched launches with no extra call, and a synchronous or
+ * shallow caller runs unchanged.  Lane 0 keeps one frame arena; lanes created
+ * later hold `frames` arenas.  Each results slot of a group lane then holds at
+ * least frames / 2 frames, which bounds the frames in flight past the last
+ * waited one at max(2 x lanes, (lanes - 1) x 3 x frames / 2) (24 for 3 lanes
+ * and the default 8).  A group of 8-bit and f32 frames runs as f32 (8-bit
+ * frames converted exactly).  Results, tickets and prev_descriptor are per
+ * frame and identical to unbatched submission. */
+int sift_hip_set_auto_micro_batch(sift_hip_t h, int frames);
+int sift_hip_auto_micro_batch(sift_hip_t h, int* frames);
+
 /* Detector::total_size (Detector.hh:62, Detector.cu:584-604). */
 int sift_hip_num_keypoints(sift_hip_t h, int* n);
 /* Capacities of the handle's per-frame buffers (host-only, valid right after

@@ -104,7 +104,7 @@ def test_device_submit_micro_batch_equal_sync(sift, mb, lanes, depth):
     assert det.micro_batch() == mb
 
     def submit(s):
-        if s % 5 == 3:  # a u8 frame inside a group of f32 frames: the group is flushed first
+        if s % 5 == 3:  # a u8 frame inside a group of f32 frames: converted, the group runs as f32
             return det.submitDevice(u8[s].data_ptr(), W, u8=True)
         if s % 4 == 1:
             return det.submitDevice(dev[s].data_ptr(), W * 4, stream=stream.cuda_stream)
@@ -269,7 +269,8 @@ def test_sync_caller_keeps_one_lane(sift):
 
 def test_lane_limits(sift):
     img = sift.synth_frame(1, 128, 96)
-    _, det = make_detector(sift, 128, 96, lanes=2)
+    _, det = make_detector(sift, 128, 96, lanes=2, auto_micro_batch=0)  # unbatched: 2 frames per lane
+    assert det.auto_micro_batch() == 0
     t = [det.submit(img) for _ in range(4)]  # two per lane past the current frame
     with pytest.raises(sift.SiftHipError):
         det.submit(img)
@@ -280,6 +281,59 @@ def test_lane_limits(sift):
         det.wait(x)
     with pytest.raises(sift.SiftHipError):
         sift.Detector(sift.CudaSiftConfig(col_width=128, row_width=96), lanes=5)
+
+
+@pytest.mark.parametrize("lanes,depth,n", [(3, 12, 26), (3, 24, 40), (2, 12, 30), (4, 36, 50)])
+def test_device_submit_auto_groups_equal_sync(sift, lanes, depth, n):
+    """Automatic launch groups (the default: sift_hip_set_auto_micro_batch 8):
+    a caller keeping `depth` device frames in flight with no micro-batch call
+    gets its frames queued once every lane is busy and run in groups of up to
+    8 on the lanes created after lane 0; every waited frame and
+    prev_descriptor equal the synchronous path, u8 frames and frames ordered
+    after the caller's stream included."""
+    frames = [sift.synth_frame(300 + i % 13, W, H) for i in range(n)]
+    ref13 = sync_reference(sift, frames[:13], numFeatures=2000)
+    ref = [ref13[i % 13] for i in range(n)]
+    dev = [torch.from_numpy(f).cuda() for f in frames[:13]]
+    u8 = [torch.from_numpy(f.astype(np.uint8)).cuda() for f in frames[:13]]
+    stream = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    _, det = make_detector(sift, W, H, numFeatures=2000, lanes=lanes)
+    assert det.auto_micro_batch() == 8 and det.micro_batch() == 1
+
+    def submit(s):
+        if s % 7 == 5:
+            return det.submitDevice(u8[s % 13].data_ptr(), W, u8=True)
+        if s % 4 == 1:
+            return det.submitDevice(dev[s % 13].data_ptr(), W * 4, stream=stream.cuda_stream)
+        return det.submitDevice(dev[s % 13].data_ptr(), W * 4)
+
+    # frame i's reference predecessor is frame i - 1 of the same sequence (ref[i - 1])
+    run_pipelined(sift, det, frames, ref, depth, submit)
+    assert det.lanes()[1] >= 2
+    # the in-flight limit, max(2 x lanes, (lanes - 1) x 3 x 4) frames past the current one, and not
+    # a submit earlier (every frame up to it finds a results slot)
+    limit, ok = max(2 * lanes, (lanes - 1) * 12), 0
+    with pytest.raises(sift.SiftHipError, match="in flight"):
+        for _ in range(limit + 1):
+            det.submitDevice(dev[0].data_ptr(), W * 4)
+            ok += 1
+    assert ok == limit
+    det.sync()
+    # a synchronous detect after the stream: lane 0, one frame
+    det.detectAndComputeDevice(dev[2].data_ptr(), W * 4, sync=True)
+    assert_identical(results(det), ref13[2])
+
+
+@pytest.mark.parametrize("depth", [6, 20])
+def test_host_submit_auto_groups_equal_sync(sift, depth):
+    """Host frames (f32 and u8) under automatic launch groups: staged into the
+    pinned ring once queued, results read back after every wait."""
+    frames = [sift.synth_frame(330 + i, W, H) for i in range(24)]
+    ref = sync_reference(sift, frames, numFeatures=2000)
+    _, det = make_detector(sift, W, H, numFeatures=2000, lanes=3)
+    run_pipelined(sift, det, frames, ref, depth,
+                  lambda s: det.submit(frames[s].astype(np.uint8) if s % 3 == 1 else frames[s]))
 
 
 class _Cai:

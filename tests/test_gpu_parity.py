@@ -19,9 +19,10 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def make_detector(sift, w, h, exact_descriptors=False, lanes=None, micro_batch=1, **kw):
+def make_detector(sift, w, h, exact_descriptors=False, lanes=None, micro_batch=1, auto_micro_batch=None, **kw):
     cfg = sift.CudaSiftConfig(col_width=w, row_width=h, **kw)
-    det = sift.Detector(cfg, exact_descriptors=exact_descriptors, lanes=lanes, micro_batch=micro_batch)
+    det = sift.Detector(cfg, exact_descriptors=exact_descriptors, lanes=lanes, micro_batch=micro_batch,
+                        auto_micro_batch=auto_micro_batch)
     det.gpuWarmUpAndAllocate()
     return cfg, det
 
@@ -442,6 +443,13 @@ def test_cpp_tools(sift):
                         timeout=300)
     assert m.returncode == 0 and r7.returncode == 0, m.stdout + m.stderr + r7.stderr
     assert m.stdout == r7.stdout
+    # ... and 10 frames ahead on the default handle: automatic launch groups, the same lines
+    a = subprocess.run([os.path.join(lib, "extract_and_match_example"), "--frames", "14", "--pipelined", "--ahead", "10"],
+                       capture_output=True, text=True, timeout=300)
+    r14 = subprocess.run([os.path.join(lib, "extract_and_match_example"), "--frames", "14"], capture_output=True,
+                         text=True, timeout=300)
+    assert a.returncode == 0 and r14.returncode == 0, a.stdout + a.stderr + r14.stderr
+    assert a.stdout == r14.stdout
     # the exact descriptor mode through the C++ surface (setExactDescriptors)
     x = subprocess.run([os.path.join(lib, "extract_and_match_example"), "--frames", "3", "--exact"],
                        capture_output=True, text=True, timeout=300)

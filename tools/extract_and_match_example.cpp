@@ -8,6 +8,9 @@
 // (OpenCV's descriptor bytes, sift_hip_set_descriptor_mode).  --micro-batch N
 // (with --pipelined): Detector::setMicroBatch(N) on 2 lanes, 2N frames
 // submitted ahead, so frames run in N-frame launch groups; same lines.
+// --ahead N (with --pipelined): N frames submitted past the one waited for
+// (default 1, or 2N with --micro-batch); past 2 per lane the default handle
+// runs them in automatic launch groups (sift_hip_set_auto_micro_batch).
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -19,7 +22,7 @@
 int main(int argc, char** argv) {
     int W = 752, H = 480, frames = 4, dx = 3, dy = 2;
     bool pipelined = false, exact = false;
-    int micro = 1;
+    int micro = 1, ahead_arg = 0;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         if (a == "--pipelined") pipelined = true;
@@ -28,6 +31,7 @@ int main(int argc, char** argv) {
         else if (a == "--height" && i + 1 < argc) H = std::atoi(argv[++i]);
         else if (a == "--frames" && i + 1 < argc) frames = std::atoi(argv[++i]);
         else if (a == "--micro-batch" && i + 1 < argc) micro = std::atoi(argv[++i]);
+        else if (a == "--ahead" && i + 1 < argc) ahead_arg = std::atoi(argv[++i]);
     }
     const int PW = W + frames * dx, PH = H + frames * dy;
     std::vector<float> big((size_t)PW * PH);
@@ -58,7 +62,7 @@ int main(int argc, char** argv) {
         frame(f, img);
         ticket[f] = detector.submit(img);
     };
-    const int ahead = micro > 1 ? 2 * micro : 1;  // frames submitted past the one being waited for
+    const int ahead = ahead_arg > 0 ? ahead_arg : (micro > 1 ? 2 * micro : 1);  // frames past the one waited for
     if (pipelined)
         for (int f = 0; f < ahead && f < frames; f++) submit(f);
     for (int f = 0; f < frames; f++) {
