@@ -43,7 +43,9 @@ namespace {
 // queue launches early only with at least half a group, so every results slot
 // of a group lane holds >= that many frames and the frames the caller may
 // still read fit in the slots (in_flight_limit).
-long long past_current(const sift_hip_detector* d) { return d->submitted + d->npend - std::max(d->current, d->firstFrame - 1); }
+long long past_current(const sift_hip_detector* d) {
+    return d->submitted + d->npend - 1 - std::max(d->current, d->firstFrame - 1);
+}
 int auto_min_group(const sift_hip_detector* d) { return std::max(2, d->autoMb / 2); }
 long long in_flight_limit(const sift_hip_detector* d) {
     if (!auto_groups(d)) return 2LL * d->maxLanes * group_cap(d);
