@@ -590,7 +590,7 @@ void upload_desc_exp_table(const float* tab64) {
 }
 
 constexpr int kRunRows = 16 * 5;               // (cell, g): g = 0..3 pairs, g = 4 bin 8
-constexpr int kPoolEntries = 64 * 8 + 80 * 3;  // <= 8 entries per sample + padding of 80 runs to multiples of 4
+constexpr int kPoolEntries = 64 * 8 + 80;  // <= 8 entries per sample + padding of 80 runs to even counts
 // (Measured and dropped: the masks' picks as inline-asm v_bfi_b32 with the
 // ballot SGPR as an operand -- 60 fewer VALU per chunk than the compiler's
 // v_mov + v_cndmask, but descriptors went wrong on the GPU (an SGPR hazard the
@@ -810,24 +810,16 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
             const unsigned long long M = RC & pick(OO, sel_g);
             const unsigned long long Mw = g == 0 ? RC & O7 : 0ull;
             const int cnt = __builtin_popcountll(M), cntw = __builtin_popcountll(Mw);
-            const int c4 = (cnt + 3) & ~3, w4 = (cntw + 3) & ~3;
+            const int c2 = (cnt + 1) & ~1, w2 = (cntw + 1) & ~1;
             // Runs: every pair run, then every bin-8 run (16-bit halves of one scan).
-            const int packed = c4 | w4 << 16;
+            const int packed = c2 | w2 << 16;
             const int incl = wave_incl_scan_dpp(packed), excl = incl - packed;
             const int start = excl & 0xffff, startw = (__builtin_amdgcn_readlane(incl, 63) & 0xffff) + (excl >> 16);
             tbl[cell * 5 + g] = make_uint4((unsigned)M, (unsigned)(M >> 32), (unsigned)start, 0u);
             if (g == 0) tbl[cell * 5 + 4] = make_uint4((unsigned)Mw, (unsigned)(Mw >> 32), (unsigned)startw, 0u);
-            // Padding: a run whose count is not a multiple of four has its last
-            // four entries zeroed first (the samples' writes below land on the
-            // real ones afterwards).
-            if (cnt & 3) {
-                float4* zp = reinterpret_cast<float4*>(pool + start + c4 - 4);
-                zp[0] = zp[1] = make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-            if (cntw & 3) {
-                float4* zw = reinterpret_cast<float4*>(pool + startw + w4 - 4);
-                zw[0] = zw[1] = make_float4(0.f, 0.f, 0.f, 0.f);
-            }
+            // Padding: a run of odd count ends in a zero entry.
+            if (cnt & 1) pool[start + c2 - 1] = make_float2(0.f, 0.f);
+            if (cntw & 1) pool[startw + w2 - 1] = make_float2(0.f, 0.f);
             wave_lds_sync();
             // ---- samples: push each contribution pair to its owner's run ----
             const bool odd = o0 & 1;
@@ -848,8 +840,9 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
             }
             wave_lds_sync();
             // ---- owners: add the runs in order ----
-            const float4* run = reinterpret_cast<const float4*>(pool + start);
-            for (int k = 0; k < c4 / 2; k += 2) {
+            const float4* run = reinterpret_cast<const float4*>(pool + start);  // (start even: 16-byte aligned)
+            int k = 0;
+            for (; k + 1 < c2 / 2; k += 2) {
                 const float4 e0 = run[k], e1 = run[k + 1];
                 accA = accA + e0.x;
                 accB = accB + e0.y;
@@ -860,13 +853,18 @@ __global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __
                 accA = accA + e1.z;
                 accB = accB + e1.w;
             }
+            if (k < c2 / 2) {
+                const float4 e0 = run[k];
+                accA = accA + e0.x;
+                accB = accB + e0.y;
+                accA = accA + e0.z;
+                accB = accB + e0.w;
+            }
             const float4* runw = reinterpret_cast<const float4*>(pool + startw);
-            for (int k = 0; k < w4 / 2; k += 2) {  // g = 0 lanes (w4 = 0 elsewhere)
-                const float4 e0 = runw[k], e1 = runw[k + 1];
+            for (k = 0; k < w2 / 2; k++) {  // g = 0 lanes (w2 = 0 elsewhere)
+                const float4 e0 = runw[k];
                 accW = accW + e0.x;
                 accW = accW + e0.z;
-                accW = accW + e1.x;
-                accW = accW + e1.z;
             }
             wave_lds_sync();
         }
