@@ -293,17 +293,18 @@ int build_graphs(sift_hip_detector* d);
 
 // A new compute lane: stream, zeroed arenas, host counters, events and the
 // captured graphs (bound on return).
-int add_lane(sift_hip_detector* d, int B) {
+int add_lane(sift_hip_detector* d, int B, int nslots) {
     if (d->nLanes >= kMaxLanes) return fail(SIFT_HIP_ERR_STATE, "no lane left");
     const int k = d->nLanes;
     Lane& L = d->lanes[k];
     d->nLanes++;  // from here the destructor releases what the lane holds
     L.B = B;
+    L.nslots = nslots;
     HIPCHK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
     if (hipMalloc((void**)&L.arena, (size_t)d->afs * B) != hipSuccess)
         return fail(SIFT_HIP_ERR_NOMEM, "hipMalloc of the frame arenas failed");
     HIPCHK(hipMemsetAsync(L.arena, 0, (size_t)d->afs * B, L.stream));
-    const size_t nh = (size_t)d->kSlots * B;
+    const size_t nh = (size_t)nslots * B;
     HIPCHK(hipHostMalloc((void**)&L.hCtr, sizeof(Counters) * nh, hipHostMallocMapped | hipHostMallocCoherent));
     memset(L.hCtr, 0, sizeof(Counters) * nh);
     HIPCHK(hipHostGetDevicePointer((void**)&L.hCtrDev, L.hCtr, 0));
@@ -594,7 +595,7 @@ int capture_with_head(sift_hip_detector* d, int slot, int nf, hipGraphExec_t* ou
 
 int build_graphs(sift_hip_detector* d) {
     Lane& L = d->lane();
-    for (int b = 0; b < d->kSlots; b++) {
+    for (int b = 0; b < L.nslots; b++) {
         if (int rc = capture(d, b, L.B, &L.exec[b])) return rc;
         if (int rc = capture_with_head(d, b, L.B, &L.execH[b], &L.graphH[b], &L.headH[b])) return rc;
         L.headIn[b][0] = Lane::HeadIn{d->dInput, d->inPitch, d->afs};
@@ -622,12 +623,12 @@ int warm_lane(sift_hip_detector* d) {
     Lane& L = d->lane();
     const int nb = L.B > 1 ? 2 : 1;
     for (int r = 0; r < nb; r++)
-        for (int b = 0; b < d->kSlots; b++) {
+        for (int b = 0; b < L.nslots; b++) {
             HIPCHK(hipGraphLaunch(r == 0 ? L.execH[b] : L.execH1[b], L.stream));
             HIPCHK(hipEventRecord(L.evFrame[b], L.stream));
             L.nfOf[b] = r == 0 ? L.B : 1;
         }
-    L.launched = (long long)nb * d->kSlots;
+    L.launched = (long long)nb * L.nslots;
     return SIFT_HIP_OK;
 }
 
@@ -640,7 +641,7 @@ int run_frame(sift_hip_detector* d, const void* img, int pitch, int fmt, hipEven
               bool numbered) {
     const long long f = d->submitted;
     Lane& L = d->lane();
-    const int slot = (int)(L.launched % d->kSlots);
+    const int slot = (int)(L.launched % L.nslots);
     const bool dump = !d->dgDir.empty() && nf == 1 && d->firstFrame > 0;
     const int W = d->cfg.col_width, H = d->cfg.row_width;
     if (dump) {
@@ -856,8 +857,9 @@ int sift_hip_warmup(sift_hip_t d) {
     rc = add_lane(d, d->B);  // lane 0; more lanes on demand (pick_lane)
     if (rc) return rc;
     // One blank frame (batch) through each graph: first-touch, code-object load.
-    for (int i = 0; i < d->kSlots * (d->B > 1 ? 2 : 1); i++) {
-        const int nf = i < d->kSlots ? d->B : 1;
+    const int ns = d->lanes[0].nslots;
+    for (int i = 0; i < ns * (d->B > 1 ? 2 : 1); i++) {
+        const int nf = i < ns ? d->B : 1;
         if ((rc = run_frame(d, d->dInput, d->inPitch, SIFT_HIP_F32, nullptr, nf, d->afs))) return rc;
         if ((rc = finish_frame(d))) return rc;
     }
@@ -1127,7 +1129,7 @@ int sift_hip_results_device(sift_hip_t d, const float** k3, const float** f4, co
     if (k3) *k3 = d->dKpts3[d->cur];
     if (f4) *f4 = d->dFeats4[d->cur];
     if (desc) *desc = d->dDesc[d->cur];
-    if (prev) *prev = d->current - 1 >= d->firstFrame ? frame_desc(d, d->current - 1) : d->dDesc[(d->cur + d->kSlots - 1) % d->kSlots];
+    if (prev) *prev = d->current - 1 >= d->firstFrame ? frame_desc(d, d->current - 1) : d->dDesc[(d->cur + d->lane().nslots - 1) % d->lane().nslots];
     if (prevCount) *prevCount = d->prevCount;
     if (capacity) *capacity = (int)d->kp.capFinal;
     return SIFT_HIP_OK;

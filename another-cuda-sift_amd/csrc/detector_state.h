@@ -123,8 +123,12 @@ bool find_sidecar(const uint16_t* desc, int n, Sidecar* out);
 bool sidecar_written(const uint16_t* desc);     // the caller wrote the rows: drop the sidecar
 void sidecar_refreshed(const uint16_t* desc);   // a frame is launched into the buffer: valid again
 
-// Results slots per compute lane: frames f-1 .. f+2 of a lane never share one.
-constexpr int kResultSlots = 4;
+// Results slots per compute lane (Lane::nslots): 4 -- frames f-1 .. f+2 of a
+// lane never share one -- and 8 on the lanes of automatic launch groups, whose
+// launch groups vary in size (a lane's slots then hold at least 8 launches'
+// frames before one is reused).  The arena layout holds kResultSlots.
+constexpr int kResultSlots = 8;
+constexpr int kLaneSlots = 4;
 constexpr int kMaxLanes = 4;
 constexpr int kFrameRing = 256;  // per-frame (lane, slot, arena) records: > 2 x kMaxLanes x kMaxMicroBatch (frames in flight) + the two readable
 
@@ -138,6 +142,7 @@ struct Lane {
     // batch size, or its automatic group size for the lanes created after lane
     // 0 (sift_hip_set_auto_micro_batch).
     int B = 1;
+    int nslots = kLaneSlots;  // results slots in use (even: slot parity = launch parity)
     // Set once add_lane completed (stream, arenas, host counters, graphs): a
     // lane whose creation failed part-way is never picked, synchronised or
     // handed host regions (its partial allocations wait for the destructor).
@@ -166,7 +171,7 @@ struct Lane {
     };
     HeadIn headIn[kResultSlots][2];
     int nfOf[kResultSlots] = {};  // frames of the launch group that wrote each slot
-    long long slotFrame[kResultSlots] = {-1, -1, -1, -1};  // the (first) frame whose results each slot holds
+    long long slotFrame[kResultSlots] = {-1, -1, -1, -1, -1, -1, -1, -1};  // the (first) frame whose results each slot holds
     int slotNum[kResultSlots] = {};  // frame numbers in that slot (> 1: a micro-batch, frame slotFrame + i in arena i)
     long long launched = 0;  // launch groups run on this lane; the next takes slot launched % kResultSlots
     long long last = -1;     // the last frame launched here (-1: none since warm-up)
@@ -453,7 +458,7 @@ int allocate(sift_hip_detector* d);
 void bind_lane(sift_hip_detector* d, int k, int idx = 0);
 const uint16_t* frame_desc(const sift_hip_detector* d, long long f);
 const Counters& frame_counters(const sift_hip_detector* d, long long f, int i = 0);
-int add_lane(sift_hip_detector* d, int B);
+int add_lane(sift_hip_detector* d, int B, int nslots = kLaneSlots);
 int warm_lane(sift_hip_detector* d);
 unsigned* range_keys(sift_hip_detector* d, int p);
 void enqueue_head(sift_hip_detector* d, const void* img, int pitch, int fmt, int parity, int nf, long sfs);

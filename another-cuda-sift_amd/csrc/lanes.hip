@@ -49,7 +49,7 @@ long long past_current(const sift_hip_detector* d) {
 int auto_min_group(const sift_hip_detector* d) { return std::max(2, d->autoMb / 2); }
 long long in_flight_limit(const sift_hip_detector* d) {
     if (!auto_groups(d)) return 2LL * d->maxLanes * group_cap(d);
-    return std::max(2LL * d->maxLanes, (long long)(d->maxLanes - 1) * (d->kSlots - 1) * auto_min_group(d));
+    return std::max(2LL * d->maxLanes, (long long)(d->maxLanes - 1) * 3 * auto_min_group(d));
 }
 }  // namespace
 
@@ -60,13 +60,13 @@ namespace {
 bool lane_fits(const sift_hip_detector* d, int k, int nf) {
     const Lane& L = d->lanes[k];
     if (!L.ready || L.B < nf) return false;
-    const int s = (int)(L.launched % d->kSlots);
+    const int s = (int)(L.launched % L.nslots);
     const long long occ = L.slotFrame[s] < 0 ? -1 : L.slotFrame[s] + std::max(L.slotNum[s], 1) - 1;  // its last frame
     return occ < 0 || occ < d->firstFrame || occ < d->current - 1;
 }
 bool lane_idle(const sift_hip_detector* d, int k) {
     const Lane& L = d->lanes[k];
-    return L.last < 0 || event_done(L.evFrame[(L.launched + d->kSlots - 1) % d->kSlots]);
+    return L.last < 0 || event_done(L.evFrame[(L.launched + L.nslots - 1) % L.nslots]);
 }
 // Arenas of a lane created now: the handle's batch, or the automatic group size.
 int new_lane_frames(const sift_hip_detector* d) { return auto_groups(d) ? d->autoMb : d->B; }
@@ -94,7 +94,7 @@ int pick_lane(sift_hip_detector* d, int nf) {
         if (busy < 0 || d->lanes[k].last < d->lanes[busy].last) busy = k;
     }
     if (d->nLanes < d->maxLanes && new_lane_frames(d) >= nf) {  // (lane 0 comes from sift_hip_warmup)
-        if (int rc = add_lane(d, new_lane_frames(d))) return rc;
+        if (int rc = add_lane(d, new_lane_frames(d), auto_groups(d) ? kResultSlots : kLaneSlots)) return rc;
         return warm_lane(d);
     }
     if (busy < 0)
@@ -141,7 +141,7 @@ void host_res(const sift_hip_detector* d, char* base, int region, float** k3, fl
 // stream (after its zeroing; frames launched earlier keep a null table).
 int ensure_host_res(sift_hip_detector* d, Lane& L) {
     if (L.hRes) return SIFT_HIP_OK;
-    const size_t nr = (size_t)d->kSlots * L.B, rb = host_res_bytes(d);
+    const size_t nr = (size_t)L.nslots * L.B, rb = host_res_bytes(d);
     HIPCHK(hipHostMalloc((void**)&L.hRes, rb * nr, hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(hipHostGetDevicePointer((void**)&L.hResDev, L.hRes, 0));
     L.hostTab.resize(nr);

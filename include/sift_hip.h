@@ -202,8 +202,8 @@ int sift_hip_micro_batch(sift_hip_t h, int* frames);
  * sift_hip_sync / any other detect.  So a caller keeping many frames in
  * flight gets micro-batched launches with no extra call, and a synchronous or
  * shallow caller runs unchanged.  Lane 0 keeps one frame arena; lanes created
- * later hold `frames` arenas.  Each results slot of a group lane then holds at
- * least frames / 2 frames, which bounds the frames in flight past the last
+ * later hold `frames` arenas and 8 results slots.  Each results slot of a
+ * group lane then holds at least frames / 2 frames, which bounds the frames in flight past the last
  * waited one at max(2 x lanes, (lanes - 1) x 3 x frames / 2) (24 for 3 lanes
  * and the default 8).  A group of 8-bit and f32 frames runs as f32 (8-bit
  * frames converted exactly).  Queued host frames go through a pinned staging

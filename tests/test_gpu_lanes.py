@@ -40,8 +40,9 @@ def prev_rows(sift, det, n):
     return prev
 
 
-def run_pipelined(sift, det, frames, ref, depth, submit):
-    """Keeps `depth` frames in flight; each waited frame must equal the synchronous path."""
+def run_pipelined(sift, det, frames, ref, depth, submit, prev0=None):
+    """Keeps `depth` frames in flight; each waited frame must equal the synchronous path
+    (prev0: the reference of the frame before the first one, None for none)."""
     queue, i = [], 0
 
     def drain_one():
@@ -49,9 +50,10 @@ def run_pipelined(sift, det, frames, ref, depth, submit):
         t = queue.pop(0)
         det.wait(t)
         assert_identical(results(det), ref[i])
-        if i:
-            assert det.prev_size == len(ref[i - 1][0])
-            assert np.array_equal(prev_rows(sift, det, det.prev_size), ref[i - 1][2])
+        before = ref[i - 1] if i else prev0
+        if before is not None:
+            assert det.prev_size == len(before[0])
+            assert np.array_equal(prev_rows(sift, det, det.prev_size), before[2])
         else:
             assert det.prev_size == 0
         i += 1
@@ -325,15 +327,20 @@ def test_device_submit_auto_groups_equal_sync(sift, lanes, depth, n):
     assert_identical(results(det), ref13[2])
 
 
-@pytest.mark.parametrize("depth", [6, 20])
+@pytest.mark.parametrize("depth", [6, 20, 24])
 def test_host_submit_auto_groups_equal_sync(sift, depth):
     """Host frames (f32 and u8) under automatic launch groups: staged into the
-    pinned ring once queued, results read back after every wait."""
-    frames = [sift.synth_frame(330 + i, W, H) for i in range(24)]
+    pinned ring once queued, results read back after every wait.  Three passes
+    on one handle: each restarts from a drained pipeline (single frames, then
+    groups), the transition that once left group lanes' results slots holding
+    single frames still readable (round 6: 8 slots on those lanes)."""
+    frames = [sift.synth_frame(330 + i, W, H) for i in range(30)]
     ref = sync_reference(sift, frames, numFeatures=2000)
     _, det = make_detector(sift, W, H, numFeatures=2000, lanes=3)
-    run_pipelined(sift, det, frames, ref, depth,
-                  lambda s: det.submit(frames[s].astype(np.uint8) if s % 3 == 1 else frames[s]))
+    for p in range(3):
+        run_pipelined(sift, det, frames, ref, depth,
+                      lambda s: det.submit(frames[s].astype(np.uint8) if s % 3 == 1 else frames[s]),
+                      prev0=ref[-1] if p else None)
 
 
 class _Cai:
