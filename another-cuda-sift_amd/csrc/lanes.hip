@@ -51,9 +51,7 @@ long long in_flight_limit(const sift_hip_detector* d) {
     if (!auto_groups(d)) return 2LL * d->maxLanes * group_cap(d);
     return std::max(2LL * d->maxLanes, (long long)(d->maxLanes - 1) * 3 * auto_min_group(d));
 }
-}  // namespace
 
-namespace {
 // A lane qualifies for a launch group of nf frames if it has the arenas and
 // its next results slot holds no frame the caller may still read (current - 1
 // onwards); it is idle once its last launch group completed.
@@ -111,8 +109,10 @@ int copy_stream(sift_hip_detector* d, hipStream_t* s) {
 
 int format_size(int fmt) { return fmt == SIFT_HIP_U8 ? 1 : (fmt == SIFT_HIP_F32 ? 4 : 0); }
 
-// Frames in flight past `current` (host-input and device submits): at most 2
-// per lane the handle may use.
+// Frames in flight past `current` (host-input and device submits, queued ones
+// included): at most in_flight_limit -- 2 per lane unbatched, 2 groups per
+// lane with a micro-batch, max(2 x lanes, (lanes - 1) x 3 x frames / 2) with
+// automatic groups.
 int check_in_flight(sift_hip_detector* d) {
     if (d->submitted + d->npend > d->current + in_flight_limit(d))
         return fail(SIFT_HIP_ERR_STATE, "the frames in flight past the current frame reach the handle's limit: sift_hip_wait first");
@@ -133,7 +133,7 @@ void host_res(const sift_hip_detector* d, char* base, int region, float** k3, fl
     *desc = reinterpret_cast<uint16_t*>(p + 16 * c);
 }
 
-// The lane's pinned results regions (kSlots x B) and the device table that
+// The lane's pinned results regions (nslots x B) and the device table that
 // points the descriptor kernel at them (HostOut), set up for every lane once a
 // caller reads results back (sift_hip_copy_to_host / sift_hip_results_host
 // turn hostWant on) and for lanes created after that: a lazy allocation
