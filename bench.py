@@ -817,14 +817,9 @@ def main():
         torch.cuda.synchronize()
         t_dev = pipelined(lambda s: detp.submitDevice(frames[s % nframes].data_ptr(), stride), None)
         t_dev8 = pipelined(lambda s: detp.submitDevice(dev_u8[s % nframes].data_ptr(), W, u8=True), None)
-        host_input = {
-            "sync_f32": {"value": round(world * nh * W * H / 1e6 / t_sync, 2), "ms_per_frame": round(t_sync / nh * 1e3, 4)},
-            "pipelined_u8": {"value": round(world * nh * W * H / 1e6 / t_pipe, 2), "ms_per_frame": round(t_pipe / nh * 1e3, 4),
-                             "lanes": PIPE_LANES, "in_flight": PIPE_DEPTH, "lanes_created": detp.lanes()[1]},
-            "unit": "Mpix/s",
-            "note": "PCIe-inclusive, host frame -> results in host memory (copyToHost with descriptors), one detector; "
-                    f"pipelined: submit/wait with {PIPE_DEPTH} frames in flight on {PIPE_LANES} compute lanes",
-        }
+        shallow_u8 = {"value": round(world * nh * W * H / 1e6 / t_pipe, 2), "ms_per_frame": round(t_pipe / nh * 1e3, 4),
+                      "lanes": PIPE_LANES, "in_flight": PIPE_DEPTH,
+                      "note": f"the same loop with {PIPE_DEPTH} frames in flight (2 per lane: every frame launched alone)"}
         # The same default handle (no micro-batch call) with AUTO_DEPTH frames in
         # flight: past 2 frames per lane the submitted frames queue and run as
         # automatic launch groups of up to 8 (sift_hip_set_auto_micro_batch).
@@ -835,18 +830,25 @@ def main():
         t_ad = pipelined(lambda s: detp.submitDevice(frames[s % nframes].data_ptr(), stride), None)
         t_ad8 = pipelined(lambda s: detp.submitDevice(dev_u8[s % nframes].data_ptr(), W, u8=True), None)
         PIPE_DEPTH = PIPE_DEPTH_SAVED
-        auto_note = (f"default handle ({PIPE_LANES} lanes, no micro-batch call), {AUTO_DEPTH} frames in flight: "
-                     f"automatic launch groups of up to {detp.auto_micro_batch()} frames once every lane is busy")
-        host_input["pipelined_u8_auto_groups"] = {
-            "value": round(world * nh * W * H / 1e6 / t_ah, 2), "ms_per_frame": round(t_ah / nh * 1e3, 4),
-            "lanes": PIPE_LANES, "in_flight": AUTO_DEPTH, "note": auto_note}
-        host_input["pipelined_u8_auto_groups_views"] = {
-            "value": round(world * nh * W * H / 1e6 / t_av, 2), "ms_per_frame": round(t_av / nh * 1e3, 4),
-            "lanes": PIPE_LANES, "in_flight": AUTO_DEPTH, "note": auto_note + "; results_host(True) after every wait"}
-        auto_dev = {
-            "f32": {"value": round(world * nh * W * H / 1e6 / t_ad, 2), "ms_per_frame": round(t_ad / nh * 1e3, 4)},
-            "u8": {"value": round(world * nh * W * H / 1e6 / t_ad8, 2), "ms_per_frame": round(t_ad8 / nh * 1e3, 4)},
-            "lanes": PIPE_LANES, "in_flight": AUTO_DEPTH, "note": auto_note}
+        auto_note = (f"default handle ({PIPE_LANES} lanes, no micro-batch call), {AUTO_DEPTH} frames in flight: past 2 "
+                     f"per lane they run as automatic launch groups of up to {detp.auto_micro_batch()} frames")
+        host_input = {
+            "sync_f32": {"value": round(world * nh * W * H / 1e6 / t_sync, 2), "ms_per_frame": round(t_sync / nh * 1e3, 4)},
+            "pipelined_u8": {"value": round(world * nh * W * H / 1e6 / t_ah, 2), "ms_per_frame": round(t_ah / nh * 1e3, 4),
+                             "lanes": PIPE_LANES, "in_flight": AUTO_DEPTH, "lanes_created": detp.lanes()[1]},
+            "pipelined_u8_views": {"value": round(world * nh * W * H / 1e6 / t_av, 2),
+                                   "ms_per_frame": round(t_av / nh * 1e3, 4), "lanes": PIPE_LANES, "in_flight": AUTO_DEPTH,
+                                   "note": "results_host(True) after every wait instead of copyToHost(True)"},
+            "pipelined_u8_in_flight_6": shallow_u8,
+            "unit": "Mpix/s",
+            "note": "PCIe-inclusive, host frame -> results in host memory (copyToHost with descriptors), one detector; "
+                    f"pipelined: submit/wait on a {auto_note}",
+        }
+        shallow_dev = {
+            "f32": {"value": round(world * nh * W * H / 1e6 / t_dev, 2), "ms_per_frame": round(t_dev / nh * 1e3, 4)},
+            "u8": {"value": round(world * nh * W * H / 1e6 / t_dev8, 2), "ms_per_frame": round(t_dev8 / nh * 1e3, 4)},
+            "lanes": PIPE_LANES, "in_flight": PIPE_DEPTH,
+            "note": f"the same loop with {PIPE_DEPTH} frames in flight (2 per lane: every frame launched alone)"}
         del detp
         # The same loop on a micro-batching handle (sift_hip_set_micro_batch):
         # submitted frames run MB at a time as one launch group per lane.
@@ -875,13 +877,12 @@ def main():
         t_mb8 = pipelined(lambda s: detp.submitDevice(dev_u8[s % nframes].data_ptr(), W, u8=True), None)
         PIPE_DEPTH = PIPE_DEPTH_SAVED
         device_submit = {
-            "f32": {"value": round(world * nh * W * H / 1e6 / t_dev, 2), "ms_per_frame": round(t_dev / nh * 1e3, 4)},
-            "u8": {"value": round(world * nh * W * H / 1e6 / t_dev8, 2), "ms_per_frame": round(t_dev8 / nh * 1e3, 4)},
-            "unit": "Mpix/s", "lanes": PIPE_LANES, "in_flight": PIPE_DEPTH,
-            "note": "HBM-resident single frames through submitDevice/wait (sift_hip_submit_device), one detector, "
-                    f"{PIPE_DEPTH} frames in flight on {PIPE_LANES} compute lanes (2 per lane: every frame launched "
-                    "alone); results stay on the device",
-            "auto_groups": auto_dev,
+            "f32": {"value": round(world * nh * W * H / 1e6 / t_ad, 2), "ms_per_frame": round(t_ad / nh * 1e3, 4)},
+            "u8": {"value": round(world * nh * W * H / 1e6 / t_ad8, 2), "ms_per_frame": round(t_ad8 / nh * 1e3, 4)},
+            "unit": "Mpix/s", "lanes": PIPE_LANES, "in_flight": AUTO_DEPTH,
+            "note": "HBM-resident single frames through submitDevice/wait (sift_hip_submit_device) on a "
+                    f"{auto_note}; results stay on the device",
+            "in_flight_6": shallow_dev,
             "micro_batch": {
                 "f32": {"value": round(world * nh * W * H / 1e6 / t_mb, 2), "ms_per_frame": round(t_mb / nh * 1e3, 4)},
                 "u8": {"value": round(world * nh * W * H / 1e6 / t_mb8, 2), "ms_per_frame": round(t_mb8 / nh * 1e3, 4)},
