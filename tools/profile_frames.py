@@ -19,6 +19,7 @@ ap.add_argument("--features", type=int, default=5000, help="numFeatures (0: keep
 ap.add_argument("--eager", action="store_true", help="timing mode: un-graphed launches")
 ap.add_argument("--batch", type=int, default=1, help="frames per launch (sift_hip_set_batch)")
 ap.add_argument("--exact", action="store_true", help="exact descriptor mode (SIFT_HIP_DESC_EXACT)")
+ap.add_argument("--hash", action="store_true", help="print a digest of every frame's results (A/B builds must agree)")
 a = ap.parse_args()
 cfg = sift.CudaSiftConfig(col_width=a.width, row_width=a.height, numOctaves=a.octaves, upscale=a.upscale,
                           numFeatures=a.features)
@@ -34,6 +35,15 @@ for _ in range(a.frames):
     else:
         det.detectAndCompute(img)
 print("keypoints", det.total_size)
+if a.hash:
+    import hashlib
+    h = hashlib.sha256()
+    for i in range(det.batch_frames() if a.batch > 1 else 1):
+        k3, f4, d = det.batch_copy_to_host(i) if a.batch > 1 else (det.copyToHost(), det.final_kpts, det.final_features,
+                                                                   det.descriptors)[1:]
+        for x in (k3, f4, d):
+            h.update(np.ascontiguousarray(x).tobytes())
+    print("results sha256", h.hexdigest()[:16])
 if a.eager:
     for k, v in sorted(det.timing().items(), key=lambda kv: -kv[1]["ms"]):
         print(f"{k:16s} {v['ms'] / a.frames * 1e3:9.2f} us/frame  launches/frame {v['launches'] / a.frames:.0f}")
