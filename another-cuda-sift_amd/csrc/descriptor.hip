@@ -564,6 +564,10 @@ __global__ __launch_bounds__(kDT, kDescWaves) void k_descriptor(const DescJob* _
 // serialised 16-frame launch).
 // ---------------------------------------------------------------------------
 constexpr int kExactWaves = 4;
+// Minimum waves per SIMD: 6 (78 VGPRs, a 12-byte spill) -- the LDS limit of
+// the 4-wave workgroups; the unconstrained build took 83 VGPRs, 5 waves/SIMD:
+// 923-929 vs 977-989 us per 16-frame launch (profiles/round6/exact_waves_ab.txt).
+constexpr int kExactMinWaves = 6;
 constexpr int kExactWG = 64 * kExactWaves;
 // Inclusive prefix maximum over the 64 lanes (non-negative values; DPP as
 // wave_incl_scan).
@@ -610,7 +614,7 @@ __device__ __forceinline__ int wave_incl_scan_dpp(int x) {
         : "+v"(x));
     return x;
 }
-__global__ __launch_bounds__(kExactWG) void k_descriptor_exact(const DescJob* __restrict__ jobs,
+__global__ __launch_bounds__(kExactWG, kExactMinWaves) void k_descriptor_exact(const DescJob* __restrict__ jobs,
                                                                     const Counters* __restrict__ ctr,
                                                                     uint16_t* __restrict__ desc, Sidecar sidecar,
                                                                     Counters* __restrict__ host_ctr, HostOut host,
