@@ -20,13 +20,16 @@ ap.add_argument("--frames", type=int, default=400, help="frames timed per combin
 ap.add_argument("--width", type=int, default=1920)
 ap.add_argument("--height", type=int, default=1200)
 ap.add_argument("--octaves", type=int, default=3)
+ap.add_argument("--exact", action="store_true", help="exact descriptor mode (SIFT_HIP_DESC_EXACT)")
+ap.add_argument("--lanes", type=int, default=0, help="lanes per detector (0: the handle default; bench.py uses 1)")
 a = ap.parse_args()
 W, H = a.width, a.height
 cfg = sift.CudaSiftConfig(col_width=W, row_width=H, numFeatures=5000, numOctaves=a.octaves)
 for B in [int(x) for x in a.batches.split(",")]:
     fb = torch.from_numpy(np.stack([sift.synth_frame(i, W, H) for i in range(B)])).cuda()
     for S in [int(x) for x in a.streams.split(",")]:
-        dets = [sift.Detector(cfg, device=0, batch=B) for _ in range(S)]
+        kw = {"lanes": a.lanes} if a.lanes else {}
+        dets = [sift.Detector(cfg, device=0, batch=B, exact_descriptors=a.exact, **kw) for _ in range(S)]
         for d in dets:
             d.gpuWarmUpAndAllocate()
 
